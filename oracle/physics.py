@@ -1,0 +1,177 @@
+"""ORACLE (test infrastructure only): ctypes wrapper of csrc/physics_oracle.c.
+
+Restates MCMC/energy_calculator.py:121-203, MCMC/potential.py:3-29,55-116,
+MCMC/simulation_box.py:31-65 and MCMC/monte_carlo.py:264-301 (see the C file
+header for the evaluation-order details).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libphysics_oracle.so")
+_lib = None
+
+
+class Phys(ctypes.Structure):
+    """Physics constants (main_algorithm_1.py:40-53, energy_calculator.py:79-80)."""
+
+    _fields_ = [
+        ("Lx", ctypes.c_double),
+        ("Ly", ctypes.c_double),
+        ("V0", ctypes.c_double * 2),
+        ("r0", ctypes.c_double),
+        ("k", ctypes.c_double),
+        ("num_wells", ctypes.c_int),
+        ("r_cut", ctypes.c_double),
+        ("r_core", ctypes.c_double),
+    ]
+
+
+def make_phys(N, rho=0.03, aspect=1.0, V0=(-10.0, -10.5), r0=1.2, k=15.0, num_wells=2):
+    """Box from initialise_fcc (initialise.py:27-31): L = sqrt(N/rho)."""
+    area = N / rho
+    Lx = float(np.sqrt(area * aspect))
+    Ly = float(np.sqrt(area / aspect))
+    p = Phys()
+    p.Lx, p.Ly = Lx, Ly
+    p.V0[0], p.V0[1] = V0
+    p.r0, p.k, p.num_wells = r0, k, num_wells
+    p.r_cut, p.r_core = 2.5, 0.5
+    return p
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_total_energy.restype = ctypes.c_int
+        L.oracle_total_energy.argtypes = [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(Phys),
+            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.c_void_p]
+        L.oracle_total_energy_batch.restype = None
+        L.oracle_total_energy_batch.argtypes = [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.POINTER(Phys),
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_min_image_dist.restype = ctypes.c_double
+        L.oracle_min_image_dist.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_double, ctypes.c_double]
+        L.oracle_pcg64_seed.restype = None
+        L.oracle_pcg64_seed.argtypes = [ctypes.c_uint64, ctypes.c_void_p]
+        L.oracle_pcg64_next_double.restype = ctypes.c_double
+        L.oracle_pcg64_next_double.argtypes = [ctypes.c_void_p]
+        L.oracle_mh_accept.restype = None
+        L.oracle_mh_accept.argtypes = [
+            ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_double, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_pairwise_sum.restype = ctypes.c_double
+        L.oracle_pairwise_sum.argtypes = [ctypes.c_void_p, ctypes.c_long]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def total_energy(pos, phys, with_cutoff=False):
+    """One chain, pos (N,2) float32/float64 -> (E, W, overlap[, cutoff bool (N,N)])."""
+    pos = np.ascontiguousarray(pos)
+    assert pos.dtype in (np.float32, np.float64) and pos.ndim == 2 and pos.shape[1] == 2
+    N = pos.shape[0]
+    E = ctypes.c_double()
+    W = ctypes.c_double()
+    bits = np.zeros((N * N + 63) // 64, dtype=np.uint64) if with_cutoff else None
+    hit = lib().oracle_total_energy(_ptr(pos), int(pos.dtype == np.float32), N, ctypes.byref(phys),
+                                    ctypes.byref(E), ctypes.byref(W),
+                                    _ptr(bits) if with_cutoff else None)
+    if with_cutoff:
+        flat = np.unpackbits(bits.view(np.uint8), bitorder="little")[: N * N].astype(bool)
+        return E.value, W.value, bool(hit), flat.reshape(N, N)
+    return E.value, W.value, bool(hit)
+
+
+def total_energy_batch(pos, phys):
+    """pos (C,N,2) -> E (C,) f64, W (C,) f64, overlap (C,) u8."""
+    pos = np.ascontiguousarray(pos)
+    C, N, _ = pos.shape
+    E = np.empty(C, np.float64)
+    W = np.empty(C, np.float64)
+    ov = np.empty(C, np.uint8)
+    lib().oracle_total_energy_batch(_ptr(pos), int(pos.dtype == np.float32), C, N,
+                                    ctypes.byref(phys), _ptr(E), _ptr(W), _ptr(ov))
+    return E, W, ov
+
+
+def min_image_dist(pos, i, j, phys):
+    pos = np.ascontiguousarray(pos)
+    return lib().oracle_min_image_dist(_ptr(pos), int(pos.dtype == np.float32), i, j,
+                                       phys.Lx, phys.Ly)
+
+
+def pcg64_seed(seed):
+    """default_rng(seed) state as u64[4] = state_hi, state_lo, inc_hi, inc_lo."""
+    out = np.zeros(4, np.uint64)
+    lib().oracle_pcg64_seed(int(seed), _ptr(out))
+    return out
+
+
+def pcg64_seed_many(seeds):
+    return np.stack([pcg64_seed(s) for s in seeds]) if len(seeds) else np.zeros((0, 4), np.uint64)
+
+
+def pcg64_next_double(state):
+    """Advance state (u64[4], modified in place) and return Generator.random()."""
+    assert state.dtype == np.uint64 and state.flags.c_contiguous
+    return lib().oracle_pcg64_next_double(_ptr(state))
+
+
+def mh_accept(E_old, E_new, nll_old, nll_new, pcg, beta=1.0, correct_sign=False):
+    """Batched reference acceptance (monte_carlo.py:264-301); pcg (C,4) u64 advanced in place."""
+    E_old = np.ascontiguousarray(E_old, np.float64)
+    E_new = np.ascontiguousarray(E_new, np.float64)
+    nll_old = np.ascontiguousarray(nll_old, np.float64)
+    nll_new = np.ascontiguousarray(nll_new, np.float64)
+    assert pcg.dtype == np.uint64 and pcg.flags.c_contiguous
+    C = E_old.shape[0]
+    acc = np.empty(C, np.uint8)
+    u = np.empty(C, np.float64)
+    lib().oracle_mh_accept(C, _ptr(E_old), _ptr(E_new), _ptr(nll_old), _ptr(nll_new), beta,
+                           _ptr(pcg), int(bool(correct_sign)), _ptr(acc), _ptr(u))
+    return acc, u
+
+
+def pairwise_sum(a):
+    a = np.ascontiguousarray(a, np.float64)
+    return lib().oracle_pairwise_sum(_ptr(a), a.shape[0])
+
+
+def fcc_lattice(N, rho=0.03, aspect=1.0):
+    """Restatement of initialise_fcc (MCMC/initialise.py:8-116): float64 (N,2)."""
+    import math
+    area = N / rho
+    bx = np.sqrt(area * aspect)
+    by = np.sqrt(area / aspect)
+    nx = math.ceil(np.sqrt(N / 2 * aspect))
+    ny = math.ceil(N / (2 * nx))
+    dx = bx / (nx - 0.5)
+    dy = by / (ny - 0.5)
+    cand = []
+    for i in range(nx):
+        for j in range(ny):
+            a = np.array([i * dx, j * dy])
+            cand.append(np.array([a[0] % bx, a[1] % by]))
+            b = np.array([(i + 0.5) * dx, (j + 0.5) * dy])
+            cand.append(np.array([b[0] % bx, b[1] % by]))
+    cand = np.array(cand)
+    center = np.array([bx / 2, by / 2])
+    d2 = np.sum((cand - center) ** 2, axis=1)
+    return cand[np.argsort(d2)[:N]]

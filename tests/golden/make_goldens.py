@@ -1,0 +1,278 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
+
+Container-only: imports /root/reference (read-only) through the recipe of
+SURVEY.md §8(c) and never ships it anywhere; only the produced vectors
+(inputs + outputs, *.npz) are committed.  Re-run with
+
+    python tests/golden/make_goldens.py
+
+Fixtures:
+  flow_<case>.npz   reference NormalizingFlow.log_prob / sampling-direction
+                    outputs (+ per-layer z, spline bins) for seeded weights
+                    from oracle.flow.random_state_dict (weights stored for the
+                    small cases, seed + checksum for the N=64 case)
+  spline.npz        reference unconstrained_rational_quadratic_spline I/O
+  energy.npz        reference EnergyCalculator totals, overlap flags and
+                    r<=2.5 neighbour masks (float32 and float64 states,
+                    N = 3, 16, 64, with overlap / exact-cutoff / PBC-straddling pairs)
+  mh_trace.npz      reference MonteCarlo.nf_big_move traces (accept mask,
+                    energies, NLLs, final PCG64 state) for given proposals
+  pcg64.npz         numpy default_rng(seed) states and first draws, seeds 42..105
+"""
+import contextlib
+import hashlib
+import io
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+REF = "/root/reference"
+LINK = "/tmp/oracle_ref/flow_state"  # get_project_root() needs a dir named flow_state
+
+
+def import_reference():
+    os.makedirs(os.path.dirname(LINK), exist_ok=True)
+    if not os.path.islink(LINK):
+        os.symlink(REF, LINK)
+    os.environ.setdefault("MPLBACKEND", "Agg")
+    sys.dont_write_bytecode = True
+    for p in (LINK, os.path.join(LINK, "MCMC"), os.path.join(LINK, "NF")):
+        sys.path.insert(0, p)
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        import normflows as NF  # noqa
+        import MCMC as MC  # noqa
+        import energy_calculator  # noqa  (module-level names used by MonteCarlo)
+        from simulation_box import SimulationBox  # noqa
+    return NF, MC, SimulationBox
+
+
+def sd_checksum(sd):
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(sd[k].detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+def build_ref_model(NF, dims):
+    layers = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        for _ in range(dims.L):
+            layers.append(NF.flows.CircularCoupledRationalQuadraticSpline(
+                dims.D, dims.nb, dims.H, range(dims.D), num_bins=dims.K, tail_bound=dims.B))
+    base = NF.Energy.UniformParticle(dims.N, 2, dims.B)
+    return NF.NormalizingFlow(base, layers)
+
+
+def flow_case(NF, name, dims, seed, nbatch, store_weights):
+    from oracle import flow as OF
+    sd = OF.random_state_dict(dims, seed=seed)
+    model = build_ref_model(NF, dims)
+    model.load_state_dict(sd, strict=True)  # pins the reference key set
+    model.eval()
+    g = torch.Generator().manual_seed(seed + 100)
+    B = dims.B
+    # density-direction inputs: uniform in the box, plus exact edges and outside points
+    x = (torch.rand((nbatch, dims.D), generator=g) * 2 - 1) * B
+    x[0, :] = B
+    x[1, :] = -B
+    x[2, 0] = B * 1.0001  # outside the tail bound -> identity tail, base -inf
+    with torch.no_grad():
+        lp = model.log_prob(x.clone())
+        zs = []
+        z = x.clone()
+        for i in range(dims.L - 1, -1, -1):
+            z, _ = model.flows[i].inverse(z)
+            zs.append(z.clone())
+        # sampling direction from supplied base draws (NormalizingFlow.sample body, core.py:192-193)
+        zb = (torch.rand((nbatch, dims.D), generator=g) * 2 - 1) * B
+        xs = zb.clone()
+        ld_s = torch.zeros(nbatch)
+        for f in model.flows:
+            xs, ld = f(xs)
+            ld_s += ld
+    out = dict(N=dims.N, L=dims.L, H=dims.H, nb=dims.nb, K=dims.K, B=B, seed=seed,
+               checksum=np.frombuffer(bytes.fromhex(sd_checksum(sd)), dtype=np.uint8),
+               x=x.numpy(), log_prob=lp.numpy(), z_layers=np.stack([t.numpy() for t in zs]),
+               z_base=zb.numpy(), x_sample=xs.numpy(), logdet_sample=ld_s.numpy())
+    if store_weights:
+        for k, v in sd.items():
+            out["sd/" + k] = v.numpy()
+    np.savez_compressed(os.path.join(HERE, f"flow_{name}.npz"), **out)
+    print(f"flow_{name}: log_prob[:4]={lp[:4].tolist()}")
+
+
+def spline_case():
+    from normflows.utils import splines as S  # reference module
+    rng = np.random.default_rng(7)
+    rows = {}
+    for K in (5, 8, 32):
+        n = 257
+        B = 11.547005383792516
+        x = ((rng.random(n) * 2 - 1) * B * 1.02).astype(np.float32)
+        x[0], x[1] = np.float32(B), np.float32(-B)
+        uw = (rng.standard_normal((n, K)) * 0.7).astype(np.float32)
+        uh = (rng.standard_normal((n, K)) * 0.7).astype(np.float32)
+        ud = (rng.standard_normal((n, K + 1)) * 0.9 + 0.54).astype(np.float32)
+        for inv in (False, True):
+            o, l = S.unconstrained_rational_quadratic_spline(
+                torch.from_numpy(x), torch.from_numpy(uw), torch.from_numpy(uh), torch.from_numpy(ud),
+                inverse=inv, tails=["circular"] * n, tail_bound=B)
+            rows[f"K{K}_{'inv' if inv else 'fwd'}_out"] = o.numpy()
+            rows[f"K{K}_{'inv' if inv else 'fwd'}_lad"] = l.numpy()
+        rows[f"K{K}_x"], rows[f"K{K}_uw"], rows[f"K{K}_uh"], rows[f"K{K}_ud"] = x, uw, uh, ud
+        rows[f"K{K}_B"] = np.float64(B)
+    np.savez_compressed(os.path.join(HERE, "spline.npz"), **rows)
+    print("spline: ok")
+
+
+def energy_case(MC, SimulationBox):
+    from energy_calculator import EnergyCalculator
+    from oracle.physics import fcc_lattice
+    rng = np.random.default_rng(11)
+    out = {}
+    idx = 0
+    for N in (3, 16, 64):
+        L = float(np.sqrt(N / 0.03))
+        box = SimulationBox(np.sqrt(N / 0.03 * 1.0), np.sqrt(N / 0.03 / 1.0))
+        confs = []
+        base = fcc_lattice(N) if N > 3 else np.array([[2.0, 5.0], [4.0, 5.0], [3.0, 7.0]])
+        confs.append(base.copy())
+        for t in range(6):
+            confs.append(base + rng.normal(0, 0.3, base.shape))
+        for t in range(3):
+            confs.append(rng.random((N, 2)) * L)  # uniform: often overlapping
+        c = base.copy()
+        c[1] = c[0] + np.array([2.5, 0.0])  # exact cutoff pair (r == 2.5)
+        confs.append(c)
+        c = base.copy()
+        c[0] = np.array([0.1, 3.0])
+        c[1] = np.array([L - 0.9, 3.0])  # PBC-straddling pair at r ~ 1.0
+        confs.append(c)
+        c = base.copy()
+        c[-1] = c[0] + np.array([0.3, 0.2])  # hard-core overlap late in the row loop
+        confs.append(c)
+        for ci, conf in enumerate(confs):
+            conf = np.mod(conf, L)
+            for dt in (np.float64, np.float32):
+                pos = conf.astype(dt)
+                with contextlib.redirect_stdout(io.StringIO()):
+                    ec = EnergyCalculator(N, pos, box, num_wells=2, V0_list=[-10.0, -10.5], r0=1.2,
+                                          k=15, timing=False, checking=False)
+                E, W = ec.total_energy, ec.total_virial
+                # neighbour mask: r <= 2.5 over i<j from the reference's own distance routine
+                nb = np.zeros((N, N), bool)
+                for i in range(N - 1):
+                    r = box.compute_distances(pos[i], pos[i + 1:])
+                    nb[i, i + 1:] = r <= 2.5
+                out[f"c{idx}_pos"] = pos
+                out[f"c{idx}_E"] = np.float64(E)
+                out[f"c{idx}_W"] = np.float64(W)
+                out[f"c{idx}_nbr"] = np.packbits(nb, bitorder="little")
+                out[f"c{idx}_N"] = np.int64(N)
+                idx += 1
+    out["count"] = np.int64(idx)
+    np.savez_compressed(os.path.join(HERE, "energy.npz"), **out)
+    print(f"energy: {idx} configs")
+
+
+def mh_trace_case(NF, MC, SimulationBox):
+    from oracle import flow as OF
+    from oracle.physics import fcc_lattice
+    out = {}
+    for N, chains, steps in ((16, 4, 40), (64, 2, 20)):
+        dims = OF.FlowDims(N=N, L=2, H=32, nb=1, K=8, B=OF.half_box(N))
+        sd = OF.random_state_dict(dims, seed=5 + N)
+        model = build_ref_model(NF, dims)
+        model.load_state_dict(sd, strict=True)
+        model.eval()
+        HB = OF.half_box(N)
+        rng = np.random.default_rng(123 + N)
+        for c in range(chains):
+            particles, box = None, None
+            with contextlib.redirect_stdout(io.StringIO()):
+                particles, box = MC.initialise_fcc(num_particles=N, rho=0.03, aspect_ratio=1.0)
+                mc = MC.MonteCarlo(particles=particles, sim_box=box, temperature=1.0, num_particles=N,
+                                   num_wells=2, V0_list=[-10.0, -10.5], r0=1.2, k=15,
+                                   initial_max_displacement=0.65, target_acceptance=0.5,
+                                   timing=False, checking=False, logger=None, seed=42 + c,
+                                   device=torch.device("cpu"))
+                mc.set_nf_model(model)
+            props, acc, E, nll_o, nll_n = [], [], [], [], []
+            for t in range(steps):
+                if t % 3 == 0:
+                    # flow proposal exactly as main_algorithm_1.py:340-343 (float32 + HALF_BOX)
+                    z = (torch.rand((1, dims.D), generator=torch.Generator().manual_seed(1000 * c + t)) * 2 - 1) * HB
+                    with torch.no_grad():
+                        for f in model.flows:
+                            z, _ = f(z)
+                    cfg = z.reshape(N, 2).numpy() + HB
+                else:
+                    # local perturbation of the current state so acceptances happen
+                    cfg = (np.asarray(mc.particles, np.float64) + rng.normal(0, 0.05, (N, 2)))
+                    cfg = np.mod(cfg, 2 * HB).astype(np.float32)
+                cfg = np.asarray(cfg, np.float32)
+                old = mc.particles - np.array([mc.half_width, mc.half_width])
+                old_nll = -model.log_prob(torch.tensor(old.reshape(1, -1), dtype=torch.float)).item()
+                new_c = cfg - np.array([mc.half_width, mc.half_width])
+                new_nll = -model.log_prob(torch.tensor(new_c.reshape(1, -1), dtype=torch.float)).item()
+                with contextlib.redirect_stdout(io.StringIO()):
+                    a = mc.nf_big_move(cfg)
+                props.append(cfg)
+                acc.append(bool(a))
+                E.append(mc.energy_calculator.total_energy)
+                nll_o.append(old_nll)
+                nll_n.append(new_nll)
+            st = mc.rng.bit_generator.state["state"]
+            key = f"N{N}_c{c}"
+            out[key + "_init"] = np.asarray(particles, np.float64)
+            out[key + "_props"] = np.stack(props)
+            out[key + "_accept"] = np.array(acc)
+            out[key + "_E"] = np.array(E)
+            out[key + "_nll_old"] = np.array(nll_o)
+            out[key + "_nll_new"] = np.array(nll_n)
+            out[key + "_final"] = np.asarray(mc.particles)
+            out[key + "_pcg_state"] = np.array([st["state"] >> 64, st["state"] & (2**64 - 1),
+                                                st["inc"] >> 64, st["inc"] & (2**64 - 1)], np.uint64)
+            out[key + "_seed"] = np.int64(42 + c)
+            print(f"mh {key}: accepts {sum(acc)}/{steps}")
+        out[f"N{N}_flow_seed"] = np.int64(5 + N)
+        out[f"N{N}_checksum"] = np.frombuffer(bytes.fromhex(sd_checksum(sd)), dtype=np.uint8)
+        out[f"N{N}_chains"] = np.int64(chains)
+    np.savez_compressed(os.path.join(HERE, "mh_trace.npz"), **out)
+
+
+def pcg_case():
+    seeds = np.arange(42, 42 + 64)
+    st = np.zeros((64, 4), np.uint64)
+    draws = np.zeros((64, 8))
+    for i, s in enumerate(seeds):
+        g = np.random.default_rng(int(s))
+        d = g.bit_generator.state["state"]
+        st[i] = [d["state"] >> 64, d["state"] & (2**64 - 1), d["inc"] >> 64, d["inc"] & (2**64 - 1)]
+        draws[i] = g.random(8)
+    np.savez_compressed(os.path.join(HERE, "pcg64.npz"), seeds=seeds, state=st, draws=draws)
+    print("pcg64: ok")
+
+
+def main():
+    NF, MC, SimulationBox = import_reference()
+    from oracle import flow as OF
+    torch.set_num_threads(1)
+    flow_case(NF, "tiny", OF.FlowDims(N=4, L=2, H=32, nb=1, K=5, B=OF.half_box(4)), 1, 64, True)
+    flow_case(NF, "n16", OF.FlowDims(N=16, L=3, H=64, nb=2, K=8, B=OF.half_box(16)), 2, 48, False)
+    flow_case(NF, "n64", OF.FlowDims(N=64, L=2, H=128, nb=2, K=32, B=OF.half_box(64)), 3, 16, False)
+    spline_case()
+    energy_case(MC, SimulationBox)
+    mh_trace_case(NF, MC, SimulationBox)
+    pcg_case()
+
+
+if __name__ == "__main__":
+    main()
