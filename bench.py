@@ -1,0 +1,263 @@
+"""Benchmark: NF-proposed MH steps/sec, N=64 2D LJ, 65536 chains per GPU (BASELINE.json).
+
+One "step" = one fused NF-MH step of every chain (Algorithm-1 flow, A1
+hyper-parameters L=15, H=256, 32 residual blocks, K=32 bins, N=64 particles):
+  proposal sampling pass (in-kernel U(-B,B) base draws -> 15 sampling-direction
+  couplings -> box coordinates) -> log q(x') density pass (15 couplings + base)
+  -> LJ + double-well energy of x' -> reference-sign MH accept with per-chain
+  PCG64 streams -> state / energy / NLL update.
+The kernel sequence is exactly fs_nf_mh_step's; the pieces are launched through
+the C ABI one by one so HIP events on the launch stream time each kernel over the
+timed region.  Multi-GPU: one process per GPU (torchrun), chains sharded (global
+chain index -> PCG64 seed 42+g and proposal-stream row), no per-step collective;
+the final density histogram and well-occupancy counters are all-reduced (RCCL).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "flow-state_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+from flowstate import _lib  # noqa: E402
+from flowstate.MCMC import BatchedMonteCarlo, Physics, initialise_fcc  # noqa: E402
+from flowstate.models import A1, build_flow, half_box  # noqa: E402
+
+PEAK_F32_TFLOPS = 157.3  # MI355X dense FP32 (MFMA = vector rate), MI355X_MICROARCH.md
+
+
+def flops_per_pass(N, L, H, nb, K):
+    """Conditioner GEMM FLOP per chain per pass."""
+    return 2 * L * (2 * N * H + 2 * nb * H * H + H * N * (3 * K + 1))
+
+
+def synthetic_model(N, device):
+    """Random-init A1 flow (no checkpoint exists offline): reference init order under
+    torch.manual_seed(0), then final layers N(0, 0.01) and unconditional spline
+    logits N(0, 0.3) so log q is not the identity-init constant."""
+    torch.manual_seed(0)
+    m = build_flow(N, **A1)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for f in m.flows:
+            f.prqct.transform_net.final_layer.weight.copy_(
+                torch.randn(f.prqct.transform_net.final_layer.weight.shape, generator=g) * 0.01)
+            u = f.prqct.unconditional_transform
+            u.unnormalized_widths.copy_(torch.randn(u.unnormalized_widths.shape, generator=g) * 0.3)
+            u.unnormalized_heights.copy_(torch.randn(u.unnormalized_heights.shape, generator=g) * 0.3)
+    return m.to(device).eval()
+
+
+def synthetic_states(N, C, c0, seed=7):
+    """FCC lattice (initialise.py:8-116) + small per-chain jitter, float64 box coords."""
+    base, box = initialise_fcc(num_particles=N, rho=0.03, aspect_ratio=1.0)
+    rng = np.random.default_rng(seed + c0)
+    L = float(box.box_size_x)
+    return np.mod(base[None] + rng.normal(0, 0.05, (C, N, 2)), L), L
+
+
+class Stepper:
+    """The fs_nf_mh_step kernel sequence, launched piecewise with HIP events."""
+
+    def __init__(self, bmc):
+        self.b = bmc
+        self.L = _lib.load()
+        self.dims = bmc.model.dims()
+        self.packed = bmc.model.packed()
+        C, D = bmc.C, 2 * bmc.N
+        dev = bmc.device
+        self.config = torch.empty((C, D), dtype=torch.float32, device=dev)
+        self.centered = torch.empty_like(self.config)
+        self.log_q = torch.empty(C, dtype=torch.float32, device=dev)
+        self.E_new = torch.empty(C, dtype=torch.float64, device=dev)
+        self.W_new = torch.empty_like(self.E_new)
+        self.events = []
+        self.t = np.zeros(4)  # propose, log_prob, energy, accept (ms, summed over timed steps)
+
+    def step(self, timed):
+        b, L, st = self.b, self.L, _lib.stream_ptr()
+        p = _lib.ptr
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if timed else None
+        if timed:
+            self.events.append(ev)
+            ev[0].record()
+        _lib.check(L.fs_flow_propose(self.dims, p(self.packed), b.C, b.proposal_seed, b.step_count, b.chain_offset,
+                                     b.phys.half_width, p(self.config), p(self.centered), None, p(b.err), st))
+        if timed:
+            ev[1].record()
+        _lib.check(L.fs_flow_log_prob(self.dims, p(self.packed), p(self.centered), b.C, p(self.log_q), None,
+                                      p(b.err), st))
+        if timed:
+            ev[2].record()
+        _lib.check(L.fs_energy_lj_dw(b.phys.c, p(self.config), 1, b.C, b.N, p(self.E_new), p(self.W_new), None, None,
+                                     st))
+        if timed:
+            ev[3].record()
+        _lib.check(L.fs_mh_accept(b.phys.c, b.C, b.N, p(b.E_old), p(b.W_old), p(b.nll_old), p(self.E_new),
+                                  p(self.W_new), p(self.log_q), p(b.pcg), p(b.state), p(b.state_is_f32),
+                                  p(self.config), p(b.accept), p(b.attempts), p(b.accepted), p(b.n_accept), b.flags,
+                                  st))
+        if timed:
+            ev[4].record()
+        b.step_count += 1
+
+    def harvest(self):
+        for ev in self.events:
+            for i in range(4):
+                self.t[i] += ev[i].elapsed_time(ev[i + 1])
+        self.events = []
+
+
+def cpu_baseline(N, budget_s=15.0):
+    """The oracle's restatement of the reference CPU path, per chain, on the host
+    cores: proposals generated in a batch (as main_algorithm_1.py:340-343 does)
+    then, per chain, nf_big_move semantics (monte_carlo.py:235-303): total energy
+    of the proposal (reference pair loop order), batch-1 log_prob of old AND new,
+    PCG64 accept, energy recompute on reject."""
+    from oracle import flow as OF
+    from oracle import physics as OP
+
+    threads = torch.get_num_threads()  # honours OMP_NUM_THREADS (the box's CPU share)
+    dims = OF.FlowDims(N=N, B=half_box(N), **A1)
+    sd = {k: v.detach().cpu() for k, v in synthetic_model(N, "cpu").state_dict().items()}
+    init, L = synthetic_states(N, 4, 0)
+    phys = OP.make_phys(N)
+    hw = L / 2
+    chains = [dict(state=init[c].copy(), pcg=OP.pcg64_seed(42 + c)[None].copy()) for c in range(4)]
+    for ch in chains:
+        ch["E"] = OP.total_energy(ch["state"], phys)[0]
+    t0 = time.perf_counter()
+    g = torch.Generator().manual_seed(1234)
+    z = (torch.rand((16, dims.D), generator=g) * 2 - 1) * dims.B
+    props = (OF.sample_from(sd, z, dims).numpy() + np.float32(dims.B)).astype(np.float32)
+    steps = 0
+    k = 0
+    while time.perf_counter() - t0 < budget_s or steps == 0:
+        ch = chains[steps % len(chains)]
+        cfg = props[k % len(props)].reshape(N, 2)
+        k += 1
+        E_new = OP.total_energy(cfg, phys)[0]
+        old = torch.tensor((ch["state"] - np.array([hw, hw])).reshape(1, -1), dtype=torch.float)
+        new = torch.tensor((cfg - np.array([hw, hw])).reshape(1, -1), dtype=torch.float)
+        nll_o = -OF.log_prob(sd, old, dims).item()
+        nll_n = -OF.log_prob(sd, new, dims).item()
+        acc, _ = OP.mh_accept([ch["E"]], [E_new], [nll_o], [nll_n], ch["pcg"])
+        if acc[0]:
+            ch["state"], ch["E"] = cfg, E_new
+        else:
+            ch["E"] = OP.total_energy(ch["state"], phys)[0]
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} nf_big_move steps (A1 flow, N={N}) over 4 chains incl. batched generation of "
+                      f"16 proposals, {dt:.1f} s wall on {threads} host threads ({os.cpu_count()} visible CPUs)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--chains", type=int, default=65536, help="chains per GPU")
+    ap.add_argument("--particles", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    N, C = args.particles, args.chains
+    c0 = rank * C
+    model = synthetic_model(N, dev)
+    init, L = synthetic_states(N, C, c0)
+    phys = Physics(L, L, temperature=1.0, num_wells=2, V0_list=(-10.0, -10.5), r0=1.2, k=15)
+    bmc = BatchedMonteCarlo(model, init, phys, np.arange(42 + c0, 42 + c0 + C, dtype=np.uint64), device=dev,
+                            chain_offset=c0)
+    stepper = Stepper(bmc)
+    for _ in range(args.warmup):
+        stepper.step(timed=False)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    acc0 = int(bmc.n_accept.item())
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        stepper.step(timed=True)
+    # final reduction: density histogram + well occupancy of the current states
+    hist = bmc.histogram2d(100)
+    wells = bmc.well_counts().sum(dim=0)
+    if dist:
+        dist.all_reduce(hist)
+        dist.all_reduce(wells)
+    torch.cuda.synchronize()
+    stepper.harvest()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    bmc.check_errors()
+    n_acc = torch.tensor([int(bmc.n_accept.item()) - acc0], dtype=torch.int64, device=dev)
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(n_acc)
+    elapsed = float(t_max.item())
+
+    total_steps = C * world * args.steps
+    value = total_steps / elapsed
+    fpp = flops_per_pass(N, **A1)
+    t_prop, t_lp, t_en, t_acc = (stepper.t / args.steps)  # ms per launch
+    achieved = 2 * fpp * C / ((t_prop + t_lp) * 1e-3) / 1e12  # both flow passes (same kernel template)
+    out = {
+        "metric": "NF-proposed MH steps/sec, N=64 2D LJ, 65536 chains; acceptance-rate match",
+        "value": value,
+        "unit": "steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (FCC+jitter states, random-init A1 flow with perturbed final layers)",
+        "config": {"workload": f"Algorithm-1 NF-proposed MH step, N={N}, {C} chains per GPU",
+                   "particles": N, "chains_per_gpu": C, "flow": "A1: L=15 H=256 blocks=32 K=32",
+                   "parallelism": f"dp{world} (chains sharded, RCCL all-reduce of final histogram)"},
+        "acceptance_rate": n_acc.item() / total_steps,
+        "kernel_ms": {"flow_propose": t_prop, "flow_log_prob": t_lp, "energy": t_en, "mh_accept": t_acc},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_F32_TFLOPS, "traffic": None,
+                     "kernel": "flow_pass_kernel<256,32,*> (propose + log_prob)",
+                     "algorithmic_flop_per_launch": fpp * C},
+    }
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,198 @@
+// extern "C" boundary of libflowstate (include/flowstate.h): argument checks,
+// dispatch to the HIP launchers, thread-local error strings.  No exception
+// crosses the ABI; no call synchronises the device.
+#include <stdarg.h>
+
+#include "fs_internal.h"
+#include "flow_layout.h"
+
+hipError_t fs_pcg64_seed_impl(const uint64_t *seeds, int64_t C, uint64_t *state, hipStream_t st);
+hipError_t fs_pcg64_random_impl(uint64_t *state, int64_t C, double *out, hipStream_t st);
+hipError_t fs_hist2d_impl(const double *pos, int64_t C, int N, double shift, const double *edges, int nb,
+                          int64_t *hist, hipStream_t st);
+hipError_t fs_well_stats_impl(const fs_phys *p, const double *pos, int64_t C, int N, int64_t *counts,
+                              hipStream_t st);
+
+static thread_local char g_err[512] = "";
+
+void fs_set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+static int hip_rc(hipError_t e, const char *where) {
+    if (e == hipSuccess) return FS_OK;
+    fs_set_error("%s: %s", where, hipGetErrorString(e));
+    return (int)e > 0 ? (int)e : 1;
+}
+
+#define REQUIRE(cond, ...)              \
+    do {                                \
+        if (!(cond)) {                  \
+            fs_set_error(__VA_ARGS__);  \
+            return FS_EINVAL;           \
+        }                               \
+    } while (0)
+
+static int check_dims(const fs_flow_dims *d) {
+    char why[256];
+    REQUIRE(d != nullptr, "dims is NULL");
+    if (!fs_flow_supported(d, why, sizeof(why))) {
+        fs_set_error("%s", why);
+        return FS_EUNSUPPORTED;
+    }
+    return FS_OK;
+}
+
+extern "C" {
+
+const char *fs_last_error(void) { return g_err; }
+
+int fs_version(void) { return 10000; }
+
+int64_t fs_flow_raw_floats(const fs_flow_dims *d) {
+    if (check_dims(d) != FS_OK) return -1;
+    return fs_flow_raw_floats_impl(d);
+}
+
+int64_t fs_flow_packed_bytes(const fs_flow_dims *d) {
+    if (check_dims(d) != FS_OK) return -1;
+    return fs_flow_packed_bytes_impl(d);
+}
+
+int fs_flow_pack(const fs_flow_dims *d, const float *raw, void *packed, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    REQUIRE(raw && packed, "fs_flow_pack: NULL buffer");
+    REQUIRE(((uintptr_t)packed & 15) == 0, "fs_flow_pack: packed must be 16-byte aligned");
+    return hip_rc(fs_flow_pack_impl(d, raw, (float *)packed, (hipStream_t)stream), "fs_flow_pack");
+}
+
+int fs_flow_log_prob(const fs_flow_dims *d, const void *packed, const float *x, int64_t B, float *log_q,
+                     float *z_out, int32_t *err, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    REQUIRE(packed && x && log_q && B >= 0, "fs_flow_log_prob: invalid arguments");
+    return hip_rc(fs_flow_pass_impl(d, packed, 0, x, B, z_out, log_q, 1, nullptr, nullptr, 0, 0, 0, 0.0, err,
+                                    (hipStream_t)stream),
+                  "fs_flow_log_prob");
+}
+
+int fs_flow_inverse(const fs_flow_dims *d, const void *packed, const float *x, int64_t B, float *z_out,
+                    float *log_det, int32_t *err, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    REQUIRE(packed && x && (z_out || log_det) && B >= 0, "fs_flow_inverse: invalid arguments");
+    return hip_rc(fs_flow_pass_impl(d, packed, 0, x, B, z_out, log_det, 0, nullptr, nullptr, 0, 0, 0, 0.0, err,
+                                    (hipStream_t)stream),
+                  "fs_flow_inverse");
+}
+
+int fs_flow_forward(const fs_flow_dims *d, const void *packed, const float *z, int64_t B, float *x_out,
+                    float *log_det, int32_t *err, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    REQUIRE(packed && z && (x_out || log_det) && B >= 0, "fs_flow_forward: invalid arguments");
+    return hip_rc(fs_flow_pass_impl(d, packed, 1, z, B, x_out, log_det, 0, nullptr, nullptr, 0, 0, 0, 0.0, err,
+                                    (hipStream_t)stream),
+                  "fs_flow_forward");
+}
+
+int fs_flow_propose(const fs_flow_dims *d, const void *packed, int64_t B, uint64_t seed, uint64_t counter,
+                    int64_t row_offset, double half_width, float *config, float *centered, float *x_out,
+                    int32_t *err, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    REQUIRE(packed && B >= 0 && (config || centered || x_out), "fs_flow_propose: invalid arguments");
+    return hip_rc(fs_flow_pass_impl(d, packed, 2, nullptr, B, x_out, nullptr, 0, config, centered, seed, counter,
+                                    row_offset, half_width, err, (hipStream_t)stream),
+                  "fs_flow_propose");
+}
+
+int fs_energy_lj_dw(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int32_t N, double *E, double *W,
+                    uint8_t *overlap, uint64_t *nbr, void *stream) {
+    REQUIRE(p && pos && E && C >= 0, "fs_energy_lj_dw: invalid arguments");
+    REQUIRE(N >= 1 && N <= fs::kMaxN, "fs_energy_lj_dw: N=%d outside [1, %d]", N, fs::kMaxN);
+    REQUIRE(p->Lx > 0 && p->Ly > 0, "fs_energy_lj_dw: box must be positive");
+    return hip_rc(fs_energy_impl(p, pos, pos_is_f32, C, N, E, W, overlap, nbr, (hipStream_t)stream),
+                  "fs_energy_lj_dw");
+}
+
+int fs_pcg64_seed(const uint64_t *seeds, int64_t C, uint64_t *state, void *stream) {
+    REQUIRE(seeds && state && C >= 0, "fs_pcg64_seed: invalid arguments");
+    return hip_rc(fs_pcg64_seed_impl(seeds, C, state, (hipStream_t)stream), "fs_pcg64_seed");
+}
+
+int fs_pcg64_random(uint64_t *state, int64_t C, double *out, void *stream) {
+    REQUIRE(state && out && C >= 0, "fs_pcg64_random: invalid arguments");
+    return hip_rc(fs_pcg64_random_impl(state, C, out, (hipStream_t)stream), "fs_pcg64_random");
+}
+
+int fs_mh_accept(const fs_phys *p, int64_t C, int32_t N, double *E_old, double *W_old, double *nll_old,
+                 const double *E_new, const double *W_new, const float *log_q_new, uint64_t *pcg, double *state,
+                 uint8_t *state_is_f32, const float *config, uint8_t *accept, int64_t *attempts, int64_t *accepted,
+                 unsigned long long *n_accept, int flags, void *stream) {
+    REQUIRE(p && E_old && nll_old && E_new && log_q_new && pcg && accept && C >= 0,
+            "fs_mh_accept: invalid arguments");
+    REQUIRE(N >= 1 && N <= fs::kMaxN, "fs_mh_accept: N=%d outside [1, %d]", N, fs::kMaxN);
+    REQUIRE((state == nullptr) == (config == nullptr), "fs_mh_accept: state and config go together");
+    return hip_rc(fs_mh_accept_impl(p, C, N, E_old, W_old, nll_old, E_new, W_new, log_q_new, pcg, state,
+                                    state_is_f32, config, accept, attempts, accepted, n_accept, flags,
+                                    (hipStream_t)stream),
+                  "fs_mh_accept");
+}
+
+int64_t fs_nf_mh_step_ws_bytes(const fs_flow_dims *d, int64_t C) {
+    if (check_dims(d) != FS_OK || C < 0) return -1;
+    const int64_t D = 2 * d->N;
+    // config f32 [C][D] | centered f32 [C][D] | log_q f32 [C] | E_new f64 [C] | W_new f64 [C]
+    return fs::rup(C * D * 4, 256) * 2 + fs::rup(C * 4, 256) + fs::rup(C * 8, 256) * 2;
+}
+
+int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C, uint64_t seed,
+                  uint64_t step, int64_t chain_offset, double *E_old, double *W_old, double *nll_old, uint64_t *pcg, double *state,
+                  uint8_t *state_is_f32, uint8_t *accept, int64_t *attempts, int64_t *accepted,
+                  unsigned long long *n_accept, int32_t *err, int flags, void *ws, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    REQUIRE(packed && p && E_old && nll_old && pcg && accept && ws && C >= 0, "fs_nf_mh_step: invalid arguments");
+    REQUIRE(((uintptr_t)ws & 255) == 0, "fs_nf_mh_step: workspace must be 256-byte aligned");
+    const int64_t D = 2 * d->N;
+    char *w = (char *)ws;
+    float *config = (float *)w;
+    w += fs::rup(C * D * 4, 256);
+    float *centered = (float *)w;
+    w += fs::rup(C * D * 4, 256);
+    float *log_q = (float *)w;
+    w += fs::rup(C * 4, 256);
+    double *E_new = (double *)w;
+    w += fs::rup(C * 8, 256);
+    double *W_new = (double *)w;
+    hipStream_t st = (hipStream_t)stream;
+    const double half_width = p->Lx / 2.0;  // MonteCarlo.half_width (monte_carlo.py:66)
+    hipError_t e = fs_flow_pass_impl(d, packed, 2, nullptr, C, nullptr, nullptr, 0, config, centered, seed, step,
+                                     chain_offset, half_width, err, st);
+    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/propose");
+    e = fs_flow_pass_impl(d, packed, 0, centered, C, nullptr, log_q, 1, nullptr, nullptr, 0, 0, 0, 0.0, err, st);
+    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/log_prob");
+    e = fs_energy_impl(p, config, 1, C, d->N, E_new, W_new, nullptr, nullptr, st);
+    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/energy");
+    e = fs_mh_accept_impl(p, C, d->N, E_old, W_old, nll_old, E_new, W_new, log_q, pcg, state, state_is_f32,
+                          state ? config : nullptr, accept, attempts, accepted, n_accept, flags, st);
+    return hip_rc(e, "fs_nf_mh_step/accept");
+}
+
+int fs_hist2d(const double *pos, int64_t C, int32_t N, double shift, const double *edges, int32_t nbins,
+              int64_t *hist, void *stream) {
+    REQUIRE(pos && edges && hist && C >= 0 && N >= 1 && nbins >= 1, "fs_hist2d: invalid arguments");
+    return hip_rc(fs_hist2d_impl(pos, C, N, shift, edges, nbins, hist, (hipStream_t)stream), "fs_hist2d");
+}
+
+int fs_well_stats(const fs_phys *p, const double *pos, int64_t C, int32_t N, int64_t *counts, void *stream) {
+    REQUIRE(p && pos && counts && C >= 0 && N >= 1, "fs_well_stats: invalid arguments");
+    return hip_rc(fs_well_stats_impl(p, pos, C, N, counts, (hipStream_t)stream), "fs_well_stats");
+}
+
+}  // extern "C"

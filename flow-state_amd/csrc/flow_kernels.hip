@@ -1,0 +1,765 @@
+// MI355X (gfx950) kernels for the circular rational-quadratic-spline coupling
+// flow of the NF-proposed MH hot path.
+//
+// One workgroup = 4 waves = 64 chains (rows) carried through ALL L coupling
+// layers of a pass without touching HBM between layers:
+//   * the chain coordinates live in LDS (CO), the roll of every coupling
+//     (coupling.py:100-101, :113-114) is an index offset, never a copy;
+//   * the conditioner ResidualNet (resnet.py:53-104) runs as v_mfma_f32_32x32x2_f32
+//     GEMMs: activations X [64 x H] in LDS (16-byte-slot XOR swizzle, conflict-free
+//     ds_read_b128 A fragments), weights streamed from L2 as pre-packed 1 KiB
+//     fragments (one dwordx4 per lane feeds 4 MFMAs), the residual stream h in
+//     the accumulator registers of the wave that owns its columns;
+//   * bias / eval-BatchNorm / ReLU / residual add are fused GEMM epilogues;
+//   * the final layer is computed feature by feature (3 x 32 columns: widths,
+//     heights, derivatives d_0..d_{K-1}; d_K of every feature in a separate
+//     "tail" GEMM) and fed straight into the spline through a per-wave LDS
+//     transpose: one lane = one chain for softmax / cumsum / bin search /
+//     rational-quadratic map / log-det (splines.py:16-222);
+//   * the unconditional spline (coupling.py:176-265) uses knots precomputed at
+//     pack time (they are batch independent).
+// Reference sign/shape quirks are kept: circular-tail derivative pad that ties
+// nothing (splines.py:35-37), searchsorted eps on the last knot, the /sqrt(H)
+// scaling of widths and heights (coupling.py:340-342), -D*log(2B) base density.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "flow_layout.h"
+#include "fs_internal.h"
+
+namespace fs {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr float kMinW = 1e-3f;  // splines.py:6-8
+constexpr float kMinH = 1e-3f;
+constexpr float kMinD = 1e-3f;
+
+enum { MODE_DENSITY = 0, MODE_SAMPLE = 1, MODE_PROPOSE = 2 };
+
+// (H, K) instantiations: A1 of main_algorithm_1.py:59-67 (H=256, K=32), A2 of
+// main_algorithm_2.py:43-51 (H=128, K=15), and the small test/golden shapes.
+#define FS_FLOW_INSTANCES \
+    FS_CASE(256, 32) FS_CASE(256, 15) FS_CASE(128, 32) FS_CASE(128, 15) FS_CASE(64, 8) FS_CASE(32, 5) FS_CASE(32, 8)
+
+struct FlowArgs {
+    const float *packed;
+    const float *in;      // [B][D] (density / sample); unused by propose
+    float *out;           // [B][D] logical-order result, nullable
+    float *scalar_out;    // [B] log_q (density + base) or log_det, nullable
+    float *config;        // propose: fl32(x + B) box coordinates, nullable
+    float *centered;      // propose: fl32(config - half_width), nullable
+    int32_t *err;         // bit0: NaN discriminant, nullable
+    int64_t nrows;
+    uint64_t seed, counter;
+    int64_t row_offset;   // global index of row 0 (multi-GPU sharding of the proposal stream)
+    double half_width;
+    int N, L, nb, K;
+    int add_base;
+    float B, twoB, negB;  // fl32(tail_bound), fl32(2*tail_bound), -fl32(tail_bound)
+    float scale_pf;       // fl32(pi / tail_bound)          (wrapper.py:151-154, nn.py:125-126)
+    float sqrtH;          // fl32(sqrt(H))                 (coupling.py:340-342)
+    float base_lp;        // fl32(-D * log(fl32(2B)))      (Uniform.py:70)
+};
+
+__device__ __forceinline__ int swz(int row, int col) {
+    return (((col >> 2) ^ (row & 15)) << 2) | (col & 3);
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---------------------------------------------------------------------------
+// GEMM: acc[rt][ct] (32x32 tiles, rows 32*rt.., cols 32*(tile0+ct)..) =
+//       X[64 x 8*kg] . Bpacked[tiles tile0..tile0+CT-1]
+// ---------------------------------------------------------------------------
+template <int CT>
+__device__ __forceinline__ void gemm64(const float *__restrict__ X, int xw,
+                                       const f32x4 *__restrict__ Bp, int kg, int tile0,
+                                       f32x16 (&acc)[2][CT]) {
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, r = lane & 31, sw = r & 15;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[rt][ct][i] = 0.f;
+    const float *xa0 = X + r * xw;
+    const float *xa1 = X + (32 + r) * xw;
+    const f32x4 *bp = Bp + (size_t)tile0 * kg * 64 + lane;
+    f32x4 a0 = *(const f32x4 *)(xa0 + ((h ^ sw) << 2));
+    f32x4 a1 = *(const f32x4 *)(xa1 + ((h ^ sw) << 2));
+    f32x4 b[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) b[ct] = bp[(size_t)ct * kg * 64];
+    for (int g = 0; g < kg; ++g) {
+        // prefetch next k-group while the MFMAs of this one run
+        const int gn = (g + 1 < kg) ? g + 1 : g;
+        const int sn = ((2 * gn + h) ^ sw) << 2;
+        f32x4 na0 = *(const f32x4 *)(xa0 + sn);
+        f32x4 na1 = *(const f32x4 *)(xa1 + sn);
+        f32x4 nb[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) nb[ct] = bp[((size_t)ct * kg + gn) * 64];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                acc[0][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[j], b[ct][j], acc[0][ct], 0, 0, 0);
+                acc[1][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[j], b[ct][j], acc[1][ct], 0, 0, 0);
+            }
+        }
+        a0 = na0;
+        a1 = na1;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) b[ct] = nb[ct];
+    }
+}
+
+// accumulator element i of tile rt -> row
+__device__ __forceinline__ int acc_row(int rt, int i, int h) {
+    return 32 * rt + 8 * (i >> 2) + 4 * h + (i & 3);
+}
+
+// ---------------------------------------------------------------------------
+// Spline pieces (float32, no contraction: each torch op rounds separately)
+// ---------------------------------------------------------------------------
+#pragma clang fp contract(off)
+
+__device__ __forceinline__ float softplus_t(float x) {  // F.softplus(beta=1, threshold=20)
+    return x > 20.f ? x : log1pf(expf(x));
+}
+
+// softmax -> min-width affine -> cumsum (double accumulation, torch CPU) ->
+// scale to [-B, B] with pinned ends (splines.py:117-127 / :131-143).  K is a
+// compile-time constant so every array below stays in registers.
+template <int K>
+__device__ __forceinline__ void knots_from_logits(const float (&u)[K], float (&kn)[K + 1], float minb,
+                                                  float twoB, float negB, float B) {
+    float m = u[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) m = fmaxf(m, u[k]);
+    float e[K];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        e[k] = expf(u[k] - m);
+        s += e[k];
+    }
+    const float inv = 1.f / s;
+    const float c1 = (float)(1.0 - 1e-3 * (double)K);
+    double cs = 0.0;
+    kn[0] = negB;
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) {
+        const float w = minb + c1 * (e[k] * inv);
+        cs += (double)w;
+        kn[k + 1] = twoB * (float)cs + negB;
+    }
+    kn[K] = B;
+}
+
+// rational_quadratic_spline forward (splines.py:202-222) / inverse (:162-201)
+template <bool INV>
+__device__ __forceinline__ void rqs_eval(float x, float icw, float ibw, float ich, float ih, float d0,
+                                         float d1, float &y, float &lad, bool &nan_disc) {
+    const float idl = ih / ibw;
+    const float sdd = (d0 + d1) - 2.f * idl;
+    if (INV) {
+        const float xm = x - ich;
+        const float a = xm * sdd + ih * (idl - d0);
+        const float b = ih * d0 - xm * sdd;
+        const float c = -idl * xm;
+        const float disc = fabsf(b * b - (4.f * a) * c);
+        nan_disc = disc != disc;
+        const float root = (2.f * c) / (-b - sqrtf(disc));
+        y = root * ibw + icw;
+        const float tomt = root * (1.f - root);
+        const float den = idl + sdd * tomt;
+        const float omr = 1.f - root;
+        const float dnum = (idl * idl) * ((d1 * (root * root) + (2.f * idl) * tomt) + d0 * (omr * omr));
+        lad = -(logf(dnum) - 2.f * logf(den));
+    } else {
+        const float theta = (x - icw) / ibw;
+        const float tomt = theta * (1.f - theta);
+        const float num = ih * (idl * (theta * theta) + d0 * tomt);
+        const float den = idl + sdd * tomt;
+        y = ich + num / den;
+        const float omt = 1.f - theta;
+        const float dnum = (idl * idl) * ((d1 * (theta * theta) + (2.f * idl) * tomt) + d0 * (omt * omt));
+        lad = logf(dnum) - 2.f * logf(den);
+        nan_disc = false;
+    }
+}
+
+// Unconditional spline over this wave's identity features (lane = chain).
+template <int K, bool INV>
+__device__ __forceinline__ float uncond_spline(const float *__restrict__ U, float *CO, int cs, int N,
+                                               int D, int off, const FlowArgs &a, bool &nan_any) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int K1 = K + 1;
+    float ld = 0.f;
+    for (int f = wid; f < N; f += kWaves) {
+        const float *T = U + (size_t)f * 3 * K1;
+        const int p = (2 * f + off) % D;
+        const float x = CO[lane * cs + p];
+        const bool inside = (x >= a.negB) && (x <= a.B);
+        const float *kn = INV ? T + K1 : T;
+        int bin = -1;
+#pragma unroll
+        for (int k = 0; k < K; ++k) bin += (x >= kn[k]) ? 1 : 0;
+        bin = bin < 0 ? 0 : (bin > K - 1 ? K - 1 : bin);
+        const float icw = T[bin], cw1 = T[bin + 1];
+        const float ich = T[K1 + bin], ch1 = T[K1 + bin + 1];
+        const float d0 = T[2 * K1 + bin], d1 = T[2 * K1 + bin + 1];
+        float y, l;
+        bool nd;
+        rqs_eval<INV>(x, icw, cw1 - icw, ich, ch1 - ich, d0, d1, y, l, nd);
+        if (inside) {
+            CO[lane * cs + p] = y;
+            ld += l;
+            nan_any |= nd;
+        }
+    }
+    return ld;
+}
+
+// Stage one 32-column accumulator tile (64 rows) + column bias into the
+// wave's [64][33] LDS buffer so that lane r can read chain r's row.
+__device__ __forceinline__ void stage_tile(float *STG, const f32x16 &t0, const f32x16 &t1, float bias) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        STG[acc_row(0, i, h) * 33 + r] = t0[i] + bias;
+        STG[acc_row(1, i, h) * 33 + r] = t1[i] + bias;
+    }
+}
+
+// Final layer + conditional spline of transform feature j for the 64 chains
+// of the wave: three single-tile GEMMs (widths, heights, derivatives), each
+// staged through the wave's LDS transpose buffer right away so that only one
+// 32x64 accumulator pair is live at a time.
+template <int K, bool INV>
+__device__ __forceinline__ float cond_spline(const float *__restrict__ X, int xw, const f32x4 *__restrict__ Wf,
+                                             int kg, const float *__restrict__ bf, float *STG, const float *TL,
+                                             int tstride, float *CO, int cs, int p, int j, const FlowArgs &a,
+                                             bool &nan_any) {
+    const int lane = threadIdx.x & 63, r = lane & 31;
+    float cw[K + 1], ch[K + 1];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        f32x16 acc[2][1];
+        gemm64<1>(X, xw, Wf, kg, 3 * j + t, acc);
+        stage_tile(STG, acc[0][0], acc[1][0], bf[32 * t + r]);
+        wave_lds_sync();
+        if (t < 2) {
+            float u[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) u[k] = STG[lane * 33 + k] / a.sqrtH;
+            if (t == 0)
+                knots_from_logits<K>(u, cw, kMinW, a.twoB, a.negB, a.B);
+            else
+                knots_from_logits<K>(u, ch, kMinH, a.twoB, a.negB, a.B);
+            wave_lds_sync();
+        }
+    }
+    const float x = CO[lane * cs + p];
+    const bool inside = (x >= a.negB) && (x <= a.B);
+    // searchsorted (splines.py:11-13): knots are non-decreasing, so the last k
+    // with x >= knot[k] is the bin; carry the gathered values along the scan
+    // (register-resident, no dynamically indexed array)
+    int bin = 0;
+    float icw = cw[0], cw1 = cw[1], ich = ch[0], ch1 = ch[1];
+#pragma unroll
+    for (int k = 1; k < K; ++k) {
+        if (x >= (INV ? ch[k] : cw[k])) {
+            bin = k;
+            icw = cw[k];
+            cw1 = cw[k + 1];
+            ich = ch[k];
+            ch1 = ch[k + 1];
+        }
+    }
+    const float ud0 = STG[lane * 33 + bin];
+    const float ud1 = (bin + 1 < K) ? STG[lane * 33 + bin + 1] : TL[lane * tstride + j];
+    const float d0 = kMinD + softplus_t(ud0);
+    const float d1 = kMinD + softplus_t(ud1);
+    float y, l;
+    bool nd;
+    rqs_eval<INV>(x, icw, cw1 - icw, ich, ch1 - ich, d0, d1, y, l, nd);
+    wave_lds_sync();  // STG reads done before the next feature restages
+    if (inside) {
+        CO[lane * cs + p] = y;
+        nan_any |= nd;
+        return l;
+    }
+    return 0.f;
+}
+
+#pragma clang fp contract(on)
+
+// Counter-based uniform draws for the base distribution (UniformParticle.sample,
+// Energy/Uniform.py:20-36): Philox4x32-10 keyed by seed, counter (row, step, i/4).
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// ---------------------------------------------------------------------------
+// The pass kernel (K = spline bins, compile time).
+// ---------------------------------------------------------------------------
+template <int H, int K, int MODE>
+__global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
+    constexpr int NT = H / 32;
+    constexpr int CTW = (NT + kWaves - 1) / kWaves;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int N = a.N, D = 2 * N;
+    const LdsLayout LL = lds_layout(N, H);
+    const PackLayout PL = pack_layout(N, H, a.nb, a.K);
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    const int h = lane >> 5, r = lane & 31;
+    float *X = (float *)(smem + LL.x);
+    float *CO = (float *)(smem + LL.coord);
+    float *STG = (float *)(smem + LL.stg) + wid * kRows * 33;
+    float *TL = (float *)(smem + LL.tail);
+    float *LDP = (float *)(smem + LL.ld);
+    const int xw = LL.xw, cs = LL.cstride, ts = LL.tstride;
+    const int64_t row0 = (int64_t)blockIdx.x * kRows;
+    const bool row_valid = row0 + lane < a.nrows;
+
+    // ---- inputs -> CO (logical order == physical order at offset 0)
+    if (MODE == MODE_PROPOSE) {
+        const int nq = (D + 3) / 4;
+        for (int e = tid; e < kRows * nq; e += kThreads) {
+            const int rr = e / nq, q = e - rr * nq;
+            const uint64_t gr = (uint64_t)(a.row_offset + row0 + rr);
+            uint4 c = make_uint4((uint32_t)gr, (uint32_t)(gr >> 32) ^ (uint32_t)(a.counter >> 32),
+                                 (uint32_t)a.counter, (uint32_t)q);
+            uint4 o = philox4x32(c, make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32)));
+            const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int i = 4 * q + t;
+                if (i < D) {
+                    const float u = (float)(w[t] >> 8) * 5.9604644775390625e-08f;  // [0,1)
+                    CO[rr * cs + i] = u * a.twoB + a.negB;
+                }
+            }
+        }
+    } else {
+        for (int e = tid; e < kRows * D; e += kThreads) {
+            const int rr = e / D, i = e - rr * D;
+            const int64_t gr = row0 + rr;
+            CO[rr * cs + i] = (gr < a.nrows) ? a.in[gr * D + i] : 0.f;
+        }
+    }
+    float ld = 0.f;
+    bool nan_any = false;
+    int off = 0;
+    const int tile0 = wid * CTW;
+    const bool act = tile0 < NT;
+    __syncthreads();
+
+    for (int s = 0; s < a.L; ++s) {
+        const int layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
+        const float *P = a.packed + (int64_t)layer * PL.stride;
+        const float *V = P + PL.vec;
+        if (MODE != MODE_DENSITY) {
+            off = (off + N) % D;  // Coupling.inverse rolls first (coupling.py:113-114)
+            ld += uncond_spline<K, true>(P + PL.unc, CO, cs, N, D, off, a, nan_any);
+            __syncthreads();
+        }
+        // periodic features [cos(s x_id) | sin(s x_id)] (nn.py:120-137) -> X
+        for (int f = wid; f < N; f += kWaves) {
+            const float v = CO[lane * cs + (2 * f + off) % D];
+            const float sv = a.scale_pf * v;
+            X[lane * xw + swz(lane, f)] = cosf(sv);
+            X[lane * xw + swz(lane, N + f)] = sinf(sv);
+        }
+        for (int c = D + wid; c < 8 * PL.kg_in; c += kWaves) X[lane * xw + swz(lane, c)] = 0.f;
+        __syncthreads();
+
+        f32x16 hr[2][CTW], acc[2][CTW];
+        if (act) {  // initial_layer
+            gemm64<CTW>(X, xw, (const f32x4 *)(P + PL.win), PL.kg_in, tile0, acc);
+#pragma unroll
+            for (int ct = 0; ct < CTW; ++ct) {
+                const float bb = V[32 * (tile0 + ct) + r];
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) hr[rt][ct][i] = acc[rt][ct][i] + bb;
+            }
+        }
+        for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
+            const float *VB = V + PL.v_blocks + (int64_t)6 * H * jb;
+            const f32x4 *W0 = (const f32x4 *)(P + PL.blocks + jb * PL.block_stride);
+            const f32x4 *W1 = W0 + PL.block_stride / 8;
+            __syncthreads();
+            if (act) {
+#pragma unroll
+                for (int ct = 0; ct < CTW; ++ct) {
+                    const int col = 32 * (tile0 + ct) + r;
+                    const float al = VB[col], be = VB[H + col];
+#pragma unroll
+                    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const int R = acc_row(rt, i, h);
+                            X[R * xw + swz(R, col)] = fmaxf(hr[rt][ct][i] * al + be, 0.f);
+                        }
+                }
+            }
+            __syncthreads();
+            if (act) gemm64<CTW>(X, xw, W0, PL.kg_h, tile0, acc);
+            __syncthreads();
+            if (act) {
+#pragma unroll
+                for (int ct = 0; ct < CTW; ++ct) {
+                    const int col = 32 * (tile0 + ct) + r;
+                    const float b0 = VB[2 * H + col], al = VB[3 * H + col], be = VB[4 * H + col];
+#pragma unroll
+                    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const int R = acc_row(rt, i, h);
+                            X[R * xw + swz(R, col)] = fmaxf((acc[rt][ct][i] + b0) * al + be, 0.f);
+                        }
+                }
+            }
+            __syncthreads();
+            if (act) {
+                gemm64<CTW>(X, xw, W1, PL.kg_h, tile0, acc);
+#pragma unroll
+                for (int ct = 0; ct < CTW; ++ct) {
+                    const float b1 = VB[5 * H + 32 * (tile0 + ct) + r];
+#pragma unroll
+                    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) hr[rt][ct][i] = hr[rt][ct][i] + (acc[rt][ct][i] + b1);
+                }
+            }
+        }
+        __syncthreads();
+        if (act) {  // X <- h for the final layer
+#pragma unroll
+            for (int ct = 0; ct < CTW; ++ct) {
+                const int col = 32 * (tile0 + ct) + r;
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int R = acc_row(rt, i, h);
+                        X[R * xw + swz(R, col)] = hr[rt][ct][i];
+                    }
+            }
+        }
+        __syncthreads();
+        // tail block: d_K of every transform feature -> TL[row][feature]
+        for (int q = wid; q < PL.ntt; q += kWaves) {
+            f32x16 t[2][1];
+            gemm64<1>(X, xw, (const f32x4 *)(P + PL.wt), PL.kg_h, q, t);
+            const float bt = V[PL.v_bt + 32 * q + r];
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) TL[acc_row(rt, i, h) * ts + 32 * q + r] = t[rt][0][i] + bt;
+        }
+        __syncthreads();
+        // final layer + conditional spline, feature by feature
+        for (int j = wid; j < N; j += kWaves) {
+            const int p = (2 * j + 1 + off) % D;
+            ld += cond_spline<K, MODE != MODE_DENSITY>(X, xw, (const f32x4 *)(P + PL.wf), PL.kg_h,
+                                                        V + PL.v_bf + 96 * j, STG, TL, ts, CO, cs, p, j, a,
+                                                        nan_any);
+        }
+        if (MODE == MODE_DENSITY) {
+            ld += uncond_spline<K, false>(P + PL.unc, CO, cs, N, D, off, a, nan_any);
+            off = (off + N) % D;  // Coupling.forward rolls last (coupling.py:100-101)
+        }
+        __syncthreads();
+    }
+
+    // ---- outputs
+    LDP[wid * kRows + lane] = ld;
+    if (nan_any && row_valid && a.err) atomicOr(a.err, 1);
+    __syncthreads();
+    if (wid == 0) {
+        const float tot = ((LDP[lane] + LDP[kRows + lane]) + LDP[2 * kRows + lane]) + LDP[3 * kRows + lane];
+        float outv = tot;
+        if (MODE == MODE_DENSITY && a.add_base) {
+            bool inb = true;
+            for (int i = 0; i < D; ++i) {
+                const float z = CO[lane * cs + i];
+                inb = inb && (z >= a.negB) && (z <= a.B);
+            }
+            outv = tot + (inb ? a.base_lp : -INFINITY);
+        }
+        if (row_valid && a.scalar_out) a.scalar_out[row0 + lane] = outv;
+    }
+    for (int e = tid; e < kRows * D; e += kThreads) {
+        const int rr = e / D, i = e - rr * D;
+        const int64_t gr = row0 + rr;
+        if (gr >= a.nrows) continue;
+        const float v = CO[rr * cs + (i + off) % D];
+        if (a.out) a.out[gr * D + i] = v;
+        if (MODE == MODE_PROPOSE) {
+            const float cfg = __fadd_rn(v, a.B);  // a_ + HALF_BOX in float32 (main_algorithm_1.py:343)
+            if (a.config) a.config[gr * D + i] = cfg;
+            if (a.centered) a.centered[gr * D + i] = (float)((double)cfg - a.half_width);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Packing kernels
+// ---------------------------------------------------------------------------
+// kind 0: plain linear W[nout][kin];  kind 1: final layer main (feature tiles);
+// kind 2: final layer tail (d_K per feature)
+__global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restrict__ src, int kin, int kg,
+                                   int ntiles, int nout, int kind, int K) {
+    const int64_t total = (int64_t)ntiles * kg * 256;
+    const int P = 3 * K + 1;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int j = idx & 3;
+        const int lane = (idx >> 2) & 63;
+        const int64_t tg = idx >> 8;
+        const int g = (int)(tg % kg);
+        const int tile = (int)(tg / kg);
+        const int k = 8 * g + 4 * (lane >> 5) + j;
+        const int c = lane & 31;
+        int64_t row = -1;
+        if (kind == 0) {
+            const int col = 32 * tile + c;
+            row = col < nout ? col : -1;
+        } else if (kind == 1) {
+            const int feat = tile / 3, t = tile % 3;
+            if (c < K) row = (int64_t)feat * P + t * K + c;
+        } else {
+            const int feat = 32 * tile + c;
+            if (feat < nout) row = (int64_t)feat * P + 3 * K;
+        }
+        dst[idx] = (row >= 0 && k < kin) ? src[row * kin + k] : 0.f;
+    }
+}
+
+#pragma clang fp contract(off)
+// vectors: biases, folded eval BatchNorm (alpha = w / sqrt(var + eps), beta = b - mean*alpha),
+// final-layer biases in packed column order, unconditional-spline knots.
+__global__ void pack_vec_kernel(float *__restrict__ dst, const float *__restrict__ src, int N, int H, int nb,
+                                int K, double tail_bound) {
+    const RawLayout R = raw_layout(N, H, nb, K);
+    const PackLayout PL = pack_layout(N, H, nb, K);
+    float *V = dst + PL.vec;
+    const int P = 3 * K + 1;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nthr = gridDim.x * blockDim.x;
+    for (int i = tid; i < H; i += nthr) V[i] = src[R.bin + i];
+    const float eps = 1e-3f;
+    for (int i = tid; i < nb * H; i += nthr) {
+        const int jb = i / H, c = i % H;
+        const float *B = src + R.blocks + (int64_t)jb * R.block_stride;
+        float *VB = V + PL.v_blocks + (int64_t)6 * H * jb;
+        {
+            const float w = B[c], b = B[H + c], m = B[2 * H + c], v = B[3 * H + c];
+            const float inv = 1.f / sqrtf(v + eps);
+            const float al = inv * w;
+            VB[c] = al;
+            VB[H + c] = b - m * al;
+        }
+        VB[2 * H + c] = B[RawLayout::b0(H) + c];
+        {
+            const float *B1 = B + RawLayout::bn1(H);
+            const float w = B1[c], b = B1[H + c], m = B1[2 * H + c], v = B1[3 * H + c];
+            const float inv = 1.f / sqrtf(v + eps);
+            const float al = inv * w;
+            VB[3 * H + c] = al;
+            VB[4 * H + c] = b - m * al;
+        }
+        VB[5 * H + c] = B[RawLayout::b1(H) + c];
+    }
+    for (int i = tid; i < N * 96; i += nthr) {
+        const int feat = i / 96, t = (i % 96) / 32, c = i % 32;
+        V[PL.v_bf + i] = (c < K) ? src[R.bf + (int64_t)feat * P + t * K + c] : 0.f;
+    }
+    for (int i = tid; i < PL.ntt * 32; i += nthr) V[PL.v_bt + i] = (i < N) ? src[R.bf + (int64_t)i * P + 3 * K] : 0.f;
+    // unconditional knots (PiecewiseRationalQuadraticCDF, coupling.py:227-259): batch independent
+    const float B = (float)tail_bound, twoB = (float)(2.0 * tail_bound), negB = (float)(-tail_bound);
+    const int K1 = K + 1;
+    for (int f = tid; f < N; f += nthr) {
+        float *T = dst + PL.unc + (int64_t)f * 3 * K1;
+        for (int which = 0; which < 2; ++which) {
+            const float *u = src + (which == 0 ? R.uw : R.uh) + (int64_t)f * K;
+            float m = u[0];
+            for (int k = 1; k < K; ++k) m = fmaxf(m, u[k]);
+            float s = 0.f;
+            for (int k = 0; k < K; ++k) s += expf(u[k] - m);
+            const float inv = 1.f / s;
+            const float c1 = (float)(1.0 - 1e-3 * (double)K);
+            double cum = 0.0;
+            float *kn = T + which * K1;
+            kn[0] = negB;
+            for (int k = 0; k < K; ++k) {
+                const float p = expf(u[k] - m) * inv;
+                const float w = (which == 0 ? kMinW : kMinH) + c1 * p;
+                cum += (double)w;
+                kn[k + 1] = twoB * (float)cum + negB;
+            }
+            kn[K] = B;
+        }
+        const float *ud = src + R.ud + (int64_t)f * K1;
+        for (int k = 0; k < K1; ++k) {
+            const float x = ud[k];
+            T[2 * K1 + k] = kMinD + (x > 20.f ? x : log1pf(expf(x)));
+        }
+    }
+}
+#pragma clang fp contract(on)
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+// ---------------------------------------------------------------------------
+template <int H, int K, int MODE>
+static hipError_t launch_pass_t(const FlowArgs &a, int N, hipStream_t st) {
+    const LdsLayout LL = lds_layout(N, H);
+    auto kfn = flow_pass_kernel<H, K, MODE>;
+    static bool attr_set = false;  // per instantiation
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const int64_t blocks = (a.nrows + kRows - 1) / kRows;
+    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kThreads), LL.total, st, a);
+    return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_pass_mode(const FlowArgs &a, int N, int H, int K, hipStream_t st) {
+#define FS_CASE(HH, KK) \
+    if (H == HH && K == KK) return launch_pass_t<HH, KK, MODE>(a, N, st);
+    FS_FLOW_INSTANCES
+#undef FS_CASE
+    return hipErrorInvalidValue;
+}
+
+}  // namespace fs
+
+using namespace fs;
+
+bool fs_flow_supported(const fs_flow_dims *d, char *why, size_t n) {
+    if (!d) return false;
+    bool ok_hk = false;
+#define FS_CASE(HH, KK) ok_hk |= (d->H == HH && d->K == KK);
+    FS_FLOW_INSTANCES
+#undef FS_CASE
+    if (!ok_hk) {
+        snprintf(why, n, "unsupported (H=%d, K=%d): instantiated (H, K) pairs are listed in FS_FLOW_INSTANCES "
+                 "(flow_kernels.hip)", d->H, d->K);
+        return false;
+    }
+    if (d->N < 1 || d->N > kMaxN || d->L < 1 || d->nb < 0 || d->K < 1 || d->K > kMaxK || !(d->tail_bound > 0)) {
+        snprintf(why, n, "invalid dims N=%d L=%d nb=%d K=%d B=%g (N<=%d, K<=%d)", d->N, d->L, d->nb, d->K,
+                 d->tail_bound, kMaxN, kMaxK);
+        return false;
+    }
+    if (lds_layout(d->N, d->H).total > 163840) {
+        snprintf(why, n, "LDS budget exceeded for N=%d H=%d", d->N, d->H);
+        return false;
+    }
+    return true;
+}
+
+int64_t fs_flow_raw_floats_impl(const fs_flow_dims *d) {
+    return raw_layout(d->N, d->H, d->nb, d->K).stride * d->L;
+}
+
+int64_t fs_flow_packed_bytes_impl(const fs_flow_dims *d) {
+    return pack_layout(d->N, d->H, d->nb, d->K).stride * d->L * 4;
+}
+
+hipError_t fs_flow_pack_impl(const fs_flow_dims *d, const float *raw, float *packed, hipStream_t st) {
+    const int N = d->N, H = d->H, nb = d->nb, K = d->K;
+    const RawLayout R = raw_layout(N, H, nb, K);
+    const PackLayout PL = pack_layout(N, H, nb, K);
+    hipError_t e = hipMemsetAsync(packed, 0, (size_t)PL.stride * d->L * 4, st);
+    if (e != hipSuccess) return e;
+    for (int l = 0; l < d->L; ++l) {
+        const float *src = raw + (int64_t)l * R.stride;
+        float *dst = packed + (int64_t)l * PL.stride;
+        auto lin = [&](float *o, const float *w, int kin, int kg, int ntiles, int nout, int kind) {
+            int64_t tot = (int64_t)ntiles * kg * 256;
+            int blocks = (int)((tot + 255) / 256);
+            if (blocks > 4096) blocks = 4096;
+            hipLaunchKernelGGL(pack_linear_kernel, dim3(blocks), dim3(256), 0, st, o, w, kin, kg, ntiles, nout,
+                               kind, K);
+        };
+        lin(dst + PL.win, src + R.win, 2 * N, PL.kg_in, H / 32, H, 0);
+        for (int jb = 0; jb < nb; ++jb) {
+            const float *B = src + R.blocks + (int64_t)jb * R.block_stride;
+            float *o = dst + PL.blocks + (int64_t)jb * PL.block_stride;
+            lin(o, B + RawLayout::w0(H), H, PL.kg_h, H / 32, H, 0);
+            lin(o + PL.block_stride / 2, B + RawLayout::w1(H), H, PL.kg_h, H / 32, H, 0);
+        }
+        lin(dst + PL.wf, src + R.wf, H, PL.kg_h, 3 * N, 0, 1);
+        lin(dst + PL.wt, src + R.wf, H, PL.kg_h, PL.ntt, N, 2);
+        hipLaunchKernelGGL(pack_vec_kernel, dim3(16), dim3(256), 0, st, dst, src, N, H, nb, K, d->tail_bound);
+    }
+    return hipGetLastError();
+}
+
+static void fill_args(FlowArgs &a, const fs_flow_dims *d, const void *packed, int64_t B) {
+    memset(&a, 0, sizeof(a));
+    a.packed = (const float *)packed;
+    a.nrows = B;
+    a.N = d->N;
+    a.L = d->L;
+    a.nb = d->nb;
+    a.K = d->K;
+    const double tb = d->tail_bound;
+    a.B = (float)tb;
+    a.twoB = (float)(2.0 * tb);
+    a.negB = (float)(-tb);
+    a.scale_pf = (float)(M_PI / tb);
+    a.sqrtH = (float)sqrt((double)d->H);
+    // UniformParticle.log_prob: -D * torch.log(torch.tensor(2*B)) in float32
+    const float lg = logf((float)(2.0 * tb));
+    a.base_lp = (float)(-2 * d->N) * lg;
+}
+
+hipError_t fs_flow_pass_impl(const fs_flow_dims *d, const void *packed, int mode, const float *in, int64_t B,
+                             float *out, float *scalar, int add_base, float *config, float *centered,
+                             uint64_t seed, uint64_t counter, int64_t row_offset, double half_width,
+                             int32_t *err, hipStream_t st) {
+    if (B <= 0) return hipSuccess;
+    FlowArgs a;
+    fill_args(a, d, packed, B);
+    a.in = in;
+    a.out = out;
+    a.scalar_out = scalar;
+    a.add_base = add_base;
+    a.config = config;
+    a.centered = centered;
+    a.seed = seed;
+    a.counter = counter;
+    a.row_offset = row_offset;
+    a.half_width = half_width;
+    a.err = err;
+    if (mode == MODE_DENSITY) return launch_pass_mode<MODE_DENSITY>(a, d->N, d->H, d->K, st);
+    if (mode == MODE_SAMPLE) return launch_pass_mode<MODE_SAMPLE>(a, d->N, d->H, d->K, st);
+    return launch_pass_mode<MODE_PROPOSE>(a, d->N, d->H, d->K, st);
+}

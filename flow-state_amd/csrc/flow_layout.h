@@ -1,0 +1,117 @@
+// Raw (state_dict order) and packed (MFMA-fragment) parameter layouts of one
+// circular-RQS coupling layer.  Shared by the host C-ABI and the device code.
+#pragma once
+#include <stdint.h>
+#ifdef __HIPCC__
+#include <hip/hip_runtime.h>
+#endif
+
+#ifdef __HIPCC__
+#define FS_HD __host__ __device__ __forceinline__
+#else
+#define FS_HD inline
+#endif
+
+namespace fs {
+
+constexpr int kRows = 64;     // chains per workgroup (= lanes of a wave: lane-per-chain spline)
+constexpr int kWaves = 4;     // waves per workgroup
+constexpr int kThreads = kRows * kWaves;
+constexpr int kMaxN = 64;     // particles (energy kernel: lane-per-particle, nbr mask in one u64)
+constexpr int kMaxK = 32;     // spline bins (one 32-column MFMA tile per parameter group)
+
+FS_HD int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+struct RawLayout {  // offsets in floats within one layer of the raw buffer
+    int64_t win, bin, blocks, block_stride, wf, bf, uw, uh, ud, stride;
+    // within a block
+    static constexpr int64_t bn0 = 0;  // + H*{0: weight, 1: bias, 2: mean, 3: var}
+    FS_HD static int64_t w0(int64_t H) { return 4 * H; }
+    FS_HD static int64_t b0(int64_t H) { return 4 * H + H * H; }
+    FS_HD static int64_t bn1(int64_t H) { return 5 * H + H * H; }
+    FS_HD static int64_t w1(int64_t H) { return 9 * H + H * H; }
+    FS_HD static int64_t b1(int64_t H) { return 9 * H + 2 * H * H; }
+};
+
+FS_HD RawLayout raw_layout(int N, int H, int nb, int K) {
+    RawLayout r;
+    const int64_t D = 2 * N, P = 3 * K + 1;
+    r.win = 0;
+    r.bin = H * D;
+    r.blocks = r.bin + H;
+    r.block_stride = 2 * (int64_t)H * H + 10 * (int64_t)H;
+    r.wf = r.blocks + nb * r.block_stride;
+    r.bf = r.wf + N * P * H;
+    r.uw = r.bf + N * P;
+    r.uh = r.uw + (int64_t)N * K;
+    r.ud = r.uh + (int64_t)N * K;
+    r.stride = r.ud + (int64_t)N * (K + 1);
+    return r;
+}
+
+// Packed layout of one layer (offsets in floats, every section 64-float aligned).
+// GEMM B operands are stored as [tile][k-group][lane][4]: tile = 32 output
+// columns, k-group = 8 reduction indices; lane l (h = l>>5, c = l&31) holds
+// W[col = 32*tile + c][k = 8*g + 4*h + j] for j = 0..3 -> one 16-byte load per
+// lane feeds four v_mfma_f32_32x32x2_f32 steps (k = 8g+j and 8g+4+j).
+struct PackLayout {
+    int kg_in;       // k-groups of the initial layer (ceil(2N/8))
+    int kg_h;        // k-groups of an H-input layer (H/8)
+    int ntt;         // tail tiles (ceil(N/32)): the last derivative d_K of every feature
+    int64_t win;     // [H/32][kg_in][64][4]
+    int64_t blocks;  // nb x { W0 [H/32][kg_h][64][4], W1 [...] }
+    int64_t block_stride;
+    int64_t wf;      // final layer, per feature j: 3 tiles (widths, heights, d_0..d_{K-1})
+    int64_t wt;      // tail block: column n = d_K of feature n
+    int64_t vec;     // b_in[H]; nb x {a0,c0,b0,a1,c1,b1}[H]; bf[N][3][32]; bt[ntt*32]
+    int64_t v_blocks, v_bf, v_bt;
+    int64_t unc;     // unconditional knots: [N][3][K+1] = cumwidths, cumheights, derivatives
+    int64_t stride;
+};
+
+FS_HD PackLayout pack_layout(int N, int H, int nb, int K) {
+    PackLayout p;
+    p.kg_in = (int)((2 * N + 7) / 8);
+    p.kg_h = H / 8;
+    p.ntt = (N + 31) / 32;
+    const int64_t tiles_h = H / 32;
+    p.win = 0;
+    p.blocks = rup(p.win + tiles_h * p.kg_in * 256, 64);
+    p.block_stride = 2 * tiles_h * p.kg_h * 256;
+    p.wf = rup(p.blocks + nb * p.block_stride, 64);
+    p.wt = rup(p.wf + (int64_t)N * 3 * p.kg_h * 256, 64);
+    p.vec = rup(p.wt + (int64_t)p.ntt * p.kg_h * 256, 64);
+    p.v_blocks = H;
+    p.v_bf = p.v_blocks + 6 * (int64_t)H * nb;
+    p.v_bt = p.v_bf + (int64_t)N * 96;
+    p.unc = rup(p.vec + p.v_bt + p.ntt * 32, 64);
+    p.stride = rup(p.unc + (int64_t)N * 3 * (K + 1), 64);
+    return p;
+}
+
+// LDS bytes of the flow-pass kernel.
+FS_HD int flow_xw(int N, int H) {  // X row width in floats: holds H hidden or 2N inputs, 16-slot swizzle groups
+    int w = H > 2 * N ? H : 2 * N;
+    return (int)rup(w, 64);
+}
+
+struct LdsLayout {
+    int x, coord, stg, tail, ld, total;  // byte offsets
+    int xw, cstride, tstride;
+};
+
+FS_HD LdsLayout lds_layout(int N, int H) {
+    LdsLayout l;
+    l.xw = flow_xw(N, H);
+    l.cstride = 2 * N + 1;                 // odd stride: lane-per-row reads are conflict-free
+    l.tstride = ((N + 31) / 32) * 32 + 1;
+    l.x = 0;
+    l.coord = l.x + kRows * l.xw * 4;
+    l.stg = (int)rup(l.coord + kRows * l.cstride * 4, 16);
+    l.tail = l.stg + kWaves * kRows * 33 * 4;
+    l.ld = (int)rup(l.tail + kRows * l.tstride * 4, 16);
+    l.total = l.ld + kWaves * kRows * 4 + 16;
+    return l;
+}
+
+}  // namespace fs

@@ -1,0 +1,29 @@
+// Internal declarations shared by the HIP translation units of libflowstate.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/flowstate.h"
+
+bool fs_flow_supported(const fs_flow_dims *d, char *why, size_t n);
+int64_t fs_flow_raw_floats_impl(const fs_flow_dims *d);
+int64_t fs_flow_packed_bytes_impl(const fs_flow_dims *d);
+hipError_t fs_flow_pack_impl(const fs_flow_dims *d, const float *raw, float *packed, hipStream_t st);
+// mode: 0 density (Coupling.forward stack, layers L-1..0), 1 sample (Coupling.inverse stack,
+// layers 0..L-1, base draws supplied), 2 propose (sample with in-kernel base draws + box coords)
+hipError_t fs_flow_pass_impl(const fs_flow_dims *d, const void *packed, int mode, const float *in, int64_t B,
+                             float *out, float *scalar, int add_base, float *config, float *centered,
+                             uint64_t seed, uint64_t counter, int64_t row_offset, double half_width,
+                             int32_t *err, hipStream_t st);
+
+hipError_t fs_energy_impl(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int N, double *E,
+                          double *W, uint8_t *overlap, uint64_t *nbr, hipStream_t st);
+hipError_t fs_mh_accept_impl(const fs_phys *p, int64_t C, int N, double *E_old, double *W_old, double *nll_old,
+                             const double *E_new, const double *W_new, const float *log_q_new, uint64_t *pcg,
+                             double *state, uint8_t *state_is_f32, const float *config, uint8_t *accept,
+                             int64_t *attempts, int64_t *accepted, unsigned long long *n_accept, int flags,
+                             hipStream_t st);
+
+void fs_set_error(const char *fmt, ...);

@@ -1,0 +1,428 @@
+// MI355X kernels for the physics / acceptance side of the NF-MH step:
+//   * LJ + double-well total energy (energy_calculator.py:121-203) — one wave per
+//     chain, lane i = particle i = pair-row i, coordinates staged in LDS, fp64
+//     pair arithmetic in the reference's evaluation order (numpy pairwise row
+//     sums, Python-float row accumulation) so results track numpy to the ulp;
+//     hard-core flag by wave ballot; optional r <= r_cut neighbour masks;
+//   * numpy SeedSequence + PCG64 (monte_carlo.py:92-95) and Generator.random();
+//   * the nf_big_move accept / reject + state update (monte_carlo.py:235-303)
+//     with a wave ballot / popcount accept counter and a ballot-driven
+//     wave-cooperative copy of the accepted configurations;
+//   * histogram2d / well-occupancy reductions (hybrid_NF_MCMC/utils.py:61-141, 488-495).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "flow_layout.h"
+#include "fs_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace fs {
+
+// ---------------------------------------------------------------- energy
+// minimum-image distance (simulation_box.py:31-56) with numpy's promotion rules
+__device__ __forceinline__ double dist_f32(float ax, float ay, float bx, float by, double Lx, double Ly) {
+    const float d0 = __fsub_rn(ax, bx), d1 = __fsub_rn(ay, by);
+    const double w0 = (double)d0 - Lx * rint((double)d0 / Lx);
+    const double w1 = (double)d1 - Ly * rint((double)d1 / Ly);
+    const float t0 = (float)w0, t1 = (float)w1;
+    const float s = __fadd_rn(__fmul_rn(t0, t0), __fmul_rn(t1, t1));  // OpenBLAS sdot
+    return (double)__fsqrt_rn(s);
+}
+
+__device__ __forceinline__ double dist_f64(double ax, double ay, double bx, double by, double Lx, double Ly) {
+    const double d0 = ax - bx, d1 = ay - by;
+    const double t0 = d0 - Lx * rint(d0 / Lx);
+    const double t1 = d1 - Ly * rint(d1 / Ly);
+    return __dsqrt_rn(fma(t1, t1, __dmul_rn(t0, t0)));  // OpenBLAS ddot (FMA kernel)
+}
+
+// x^6 rounded once from a double-double product (tracks the correctly rounded pow)
+__device__ __forceinline__ double pow6(double x) {
+    const double x2 = x * x, x2e = fma(x, x, -x2);
+    const double x3 = x2 * x, x3e = fma(x2, x, -x3) + x2e * x;
+    const double x6 = x3 * x3, x6e = fma(x3, x3, -x6) + 2.0 * x3 * x3e;
+    return x6 + x6e;
+}
+
+__device__ __forceinline__ void lj_pair(double r, double r_cut, double e_cut, double &e, double &w) {
+    if (r <= r_cut) {  // potential.py:11 inclusive
+        const double sr6 = pow6(1.0 / r);
+        const double sr12 = sr6 * sr6;
+        e = 4.0 * (sr12 - sr6) - e_cut;
+        w = 48.0 * (sr12 - 0.5 * sr6);
+    } else {
+        e = 0.0;
+        w = 0.0;
+    }
+}
+
+// numpy pairwise sum of n <= 128 values held in LDS (serial, one lane)
+__device__ double pairwise_lds(const double *a, int n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int i = 0; i < n; ++i) res += a[i];
+        return res;
+    }
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+        for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+}
+
+template <bool F32>
+__global__ void __launch_bounds__(256) energy_kernel(fs_phys p, const void *__restrict__ pos, int64_t C, int N,
+                                                     double *__restrict__ E, double *__restrict__ W,
+                                                     uint8_t *__restrict__ ov, uint64_t *__restrict__ nbr) {
+    __shared__ double sx[4][64], sy[4][64], se[4][64], sw[4][64], sv[4][64];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t c = (int64_t)blockIdx.x * 4 + wid;
+    if (c >= C) return;  // whole wave leaves; no block-level barrier below
+    if (lane < N) {
+        if (F32) {
+            const float *q = (const float *)pos + c * 2 * N;
+            sx[wid][lane] = q[2 * lane];
+            sy[wid][lane] = q[2 * lane + 1];
+        } else {
+            const double *q = (const double *)pos + c * 2 * N;
+            sx[wid][lane] = q[2 * lane];
+            sy[wid][lane] = q[2 * lane + 1];
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const double sr6c = pow6(1.0 / p.r_cut);
+    const double e_cut = 4.0 * (sr6c * sr6c - sr6c);
+    const int i = lane;
+    const int n = (i < N - 1) ? N - 1 - i : 0;
+    const double xi = sx[wid][i < N ? i : 0], yi = sy[wid][i < N ? i : 0];
+    bool hit = false;
+    uint64_t mask = 0;
+    auto pair = [&](int t, double &e, double &w) {
+        const int j = i + 1 + t;
+        const double r = F32 ? dist_f32((float)xi, (float)yi, (float)sx[wid][j], (float)sy[wid][j], p.Lx, p.Ly)
+                             : dist_f64(xi, yi, sx[wid][j], sy[wid][j], p.Lx, p.Ly);
+        hit |= r < p.r_core;
+        if (r <= p.r_cut) mask |= (uint64_t)1 << j;
+        lj_pair(r, p.r_cut, e_cut, e, w);
+    };
+    // row sum in numpy's pairwise order (loops_utils.h pairwise_sum, n <= 128)
+    double re = 0.0, rw = 0.0;
+    if (n < 8) {
+        for (int t = 0; t < n; ++t) {
+            double e, w;
+            pair(t, e, w);
+            re += e;
+            rw += w;
+        }
+    } else {
+        double ae[8], aw[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pair(j, ae[j], aw[j]);
+        const int nfull = n - (n % 8);
+        for (int t0 = 8; t0 < nfull; t0 += 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                double e, w;
+                pair(t0 + j, e, w);
+                ae[j] += e;
+                aw[j] += w;
+            }
+        }
+        re = ((ae[0] + ae[1]) + (ae[2] + ae[3])) + ((ae[4] + ae[5]) + (ae[6] + ae[7]));
+        rw = ((aw[0] + aw[1]) + (aw[2] + aw[3])) + ((aw[4] + aw[5]) + (aw[6] + aw[7]));
+        for (int t = nfull; t < n; ++t) {
+            double e, w;
+            pair(t, e, w);
+            re += e;
+            rw += w;
+        }
+    }
+    // external double well per particle (potential.py:89-112)
+    double v = 0.0;
+    if (lane < N) {
+        const double cy = p.Ly / 2.0;
+        for (int k = 0; k < p.num_wells && k < 2; ++k) {
+            const double cx = (k == 0) ? p.Lx / 4.0 : 3.0 * p.Lx / 4.0;
+            double dx = xi - cx, dy = yi - cy;
+            dx -= p.Lx * rint(dx / p.Lx);
+            dy -= p.Ly * rint(dy / p.Ly);
+            const double r = sqrt(dx * dx + dy * dy);
+            const double tr = 0.5 * (1.0 + tanh(p.k * (r - p.r0)));
+            v += p.V0[k] * (1.0 - tr);
+        }
+    }
+    se[wid][lane] = re;
+    sw[wid][lane] = rw;
+    sv[wid][lane] = v;
+    if (nbr && lane < N) nbr[c * N + lane] = mask;
+    const bool any_hit = __ballot(hit) != 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+        double te = 0.0, tw = 0.0;
+        for (int k = 0; k < N - 1; ++k) {  // Python-float accumulation over rows
+            te += se[wid][k];
+            tw += sw[wid][k];
+        }
+        if (p.num_wells > 0) te += pairwise_lds(sv[wid], N);
+        if (any_hit) {
+            te = INFINITY;
+            tw = INFINITY;
+        }
+        E[c] = te;
+        if (W) W[c] = tw;
+        if (ov) ov[c] = any_hit ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------- PCG64
+struct u128 {
+    uint64_t hi, lo;
+};
+
+__device__ __forceinline__ u128 mul_add(u128 a, u128 m, u128 inc) {
+    u128 r;
+    r.lo = a.lo * m.lo;
+    r.hi = __umul64hi(a.lo, m.lo) + a.lo * m.hi + a.hi * m.lo;
+    const uint64_t lo = r.lo + inc.lo;
+    r.hi += inc.hi + (lo < r.lo ? 1 : 0);
+    r.lo = lo;
+    return r;
+}
+
+__device__ __forceinline__ double pcg64_next_double(uint64_t *s) {
+    const u128 M = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull};
+    u128 st = {s[0], s[1]}, inc = {s[2], s[3]};
+    st = mul_add(st, M, inc);
+    s[0] = st.hi;
+    s[1] = st.lo;
+    const uint64_t x = st.hi ^ st.lo;
+    const unsigned rot = (unsigned)(st.hi >> 58);
+    const uint64_t out = (x >> rot) | (x << ((64 - rot) & 63));
+    return (double)(out >> 11) * (1.0 / 9007199254740992.0);
+}
+
+__device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t &hc) {
+    v ^= hc;
+    hc *= 0x931e8875u;
+    v *= hc;
+    v ^= v >> 16;
+    return v;
+}
+
+__device__ __forceinline__ uint32_t ss_mix(uint32_t x, uint32_t y) {
+    uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y;
+    r ^= r >> 16;
+    return r;
+}
+
+// numpy SeedSequence(seed).generate_state(4, uint64) -> pcg64_set_seed
+__global__ void pcg64_seed_kernel(const uint64_t *__restrict__ seeds, int64_t C, uint64_t *__restrict__ state) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    uint64_t seed = seeds[c];
+    uint32_t ent[2] = {0u, 0u};
+    int n_ent = 0;
+    if (seed == 0) ent[n_ent++] = 0;
+    while (seed) {
+        ent[n_ent++] = (uint32_t)seed;
+        seed >>= 32;
+    }
+    uint32_t pool[4];
+    uint32_t hc = 0x43b0d7e5u;
+    for (int i = 0; i < 4; ++i) pool[i] = ss_hashmix(i < n_ent ? ent[i] : 0u, hc);
+    for (int s = 0; s < 4; ++s)
+        for (int d = 0; d < 4; ++d)
+            if (s != d) pool[d] = ss_mix(pool[d], ss_hashmix(pool[s], hc));
+    uint32_t w[8];
+    uint32_t hb = 0x8b51f9ddu;
+    for (int i = 0; i < 8; ++i) {
+        uint32_t v = pool[i & 3];
+        v ^= hb;
+        hb *= 0x58f38dedu;
+        v *= hb;
+        v ^= v >> 16;
+        w[i] = v;
+    }
+    uint64_t val[4];
+    for (int i = 0; i < 4; ++i) val[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+    const u128 M = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull};
+    const u128 initstate = {val[0], val[1]};
+    u128 inc = {(val[2] << 1) | (val[3] >> 63), (val[3] << 1) | 1ull};
+    u128 st = {0, 0};
+    st = mul_add(st, M, inc);
+    const uint64_t lo = st.lo + initstate.lo;
+    st.hi += initstate.hi + (lo < st.lo ? 1 : 0);
+    st.lo = lo;
+    st = mul_add(st, M, inc);
+    state[4 * c + 0] = st.hi;
+    state[4 * c + 1] = st.lo;
+    state[4 * c + 2] = inc.hi;
+    state[4 * c + 3] = inc.lo;
+}
+
+__global__ void pcg64_random_kernel(uint64_t *__restrict__ state, int64_t C, double *__restrict__ out) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    out[c] = pcg64_next_double(state + 4 * c);
+}
+
+// ---------------------------------------------------------------- MH accept
+__global__ void __launch_bounds__(256) mh_accept_kernel(fs_phys p, int64_t C, int N, double *E_old, double *W_old,
+                                                        double *nll_old, const double *E_new, const double *W_new,
+                                                        const float *log_q_new, uint64_t *pcg, double *state,
+                                                        uint8_t *state_is_f32, const float *config,
+                                                        uint8_t *accept, int64_t *attempts, int64_t *accepted,
+                                                        unsigned long long *n_accept, int flags) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool valid = c < C;
+    int acc = 0;
+    if (valid) {
+        const double en = E_new[c];
+        const double nll_new = -(double)log_q_new[c];  // - log_prob(new).item()
+        const double dE = en - E_old[c];
+        const double dN = nll_new - nll_old[c];
+        const double ratio_log = (flags & FS_MH_CORRECT_SIGN) ? (-p.beta * dE + dN) : (-p.beta * dE - dN);
+        const double ratio = exp(ratio_log);
+        if (ratio >= 1.0) {
+            acc = 1;
+        } else {
+            const double u = pcg64_next_double(pcg + 4 * c);
+            acc = u < ratio ? 1 : 0;  // NaN ratio -> draw and reject
+        }
+        accept[c] = (uint8_t)acc;
+        if (attempts) attempts[c] += 1;
+        if (acc) {
+            E_old[c] = en;
+            if (W_old && W_new) W_old[c] = W_new[c];
+            nll_old[c] = nll_new;
+            if (accepted) accepted[c] += 1;
+            if (state_is_f32) state_is_f32[c] = 1;
+        }
+    }
+    uint64_t m = __ballot(acc);
+    if (lane == 0 && n_accept && m) atomicAdd(n_accept, (unsigned long long)__popcll(m));
+    if (state && config) {  // wave-cooperative coalesced copy of each accepted configuration
+        const int64_t base = c - lane;
+        const int D = 2 * N;
+        while (m) {
+            const int b = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            const int64_t cc = base + b;
+            for (int t = lane; t < D; t += 64) state[cc * D + t] = (double)config[cc * D + t];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- reductions
+__global__ void hist2d_kernel(const double *__restrict__ pos, int64_t C, int N, double shift,
+                              const double *__restrict__ edges, int nb, unsigned long long *__restrict__ hist) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= C * N) return;
+    const double x = pos[2 * t] - shift, y = pos[2 * t + 1] - shift;
+    // np.searchsorted(edges, v, side='right'), right edge folded into the last bin
+    auto bin_of = [&](double v) {
+        int lo = 0, hi = nb + 1;  // edges has nb+1 entries
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (edges[mid] <= v) lo = mid + 1;
+            else hi = mid;
+        }
+        int b = lo;  // in [0, nb+1]
+        if (v == edges[nb]) b -= 1;
+        return b - 1;  // -1 or nb => outlier
+    };
+    const int bx = bin_of(x), by = bin_of(y);
+    if (bx < 0 || bx >= nb || by < 0 || by >= nb) return;
+    atomicAdd(&hist[bx * nb + by], 1ull);
+}
+
+__global__ void well_stats_kernel(fs_phys p, const double *__restrict__ pos, int64_t C, int N,
+                                  long long *__restrict__ counts) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double bx = p.Lx, by = p.Ly;
+    const double rad = p.r0 * 1.1, rad2 = rad * rad;
+    bool allA = true, allB = true;
+    for (int i = 0; i < N; ++i) {
+        const double x = pos[(c * N + i) * 2], y = pos[(c * N + i) * 2 + 1];
+        auto in = [&](double cx, double cy) {
+            double dx = x - cx, dy = y - cy;
+            dx -= bx * rint(dx / bx);
+            dy -= by * rint(dy / by);
+            return (dx * dx + dy * dy) <= rad2;
+        };
+        const bool inA = in(bx / 4, by / 2);
+        const bool inB = !inA && in(3 * bx / 4, by / 2);
+        allA &= inA;
+        allB &= inB;
+    }
+    counts[3 * c] += allA;
+    counts[3 * c + 1] += (!allA && allB);
+    counts[3 * c + 2] += 1;
+}
+
+}  // namespace fs
+
+using namespace fs;
+
+hipError_t fs_energy_impl(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int N, double *E,
+                          double *W, uint8_t *overlap, uint64_t *nbr, hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((C + 3) / 4));
+    if (pos_is_f32)
+        hipLaunchKernelGGL(energy_kernel<true>, grid, dim3(256), 0, st, *p, pos, C, N, E, W, overlap, nbr);
+    else
+        hipLaunchKernelGGL(energy_kernel<false>, grid, dim3(256), 0, st, *p, pos, C, N, E, W, overlap, nbr);
+    return hipGetLastError();
+}
+
+hipError_t fs_mh_accept_impl(const fs_phys *p, int64_t C, int N, double *E_old, double *W_old, double *nll_old,
+                             const double *E_new, const double *W_new, const float *log_q_new, uint64_t *pcg,
+                             double *state, uint8_t *state_is_f32, const float *config, uint8_t *accept,
+                             int64_t *attempts, int64_t *accepted, unsigned long long *n_accept, int flags,
+                             hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mh_accept_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, *p, C, N, E_old,
+                       W_old, nll_old, E_new, W_new, log_q_new, pcg, state, state_is_f32, config, accept,
+                       attempts, accepted, n_accept, flags);
+    return hipGetLastError();
+}
+
+hipError_t fs_pcg64_seed_impl(const uint64_t *seeds, int64_t C, uint64_t *state, hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pcg64_seed_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, seeds, C, state);
+    return hipGetLastError();
+}
+
+hipError_t fs_pcg64_random_impl(uint64_t *state, int64_t C, double *out, hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pcg64_random_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, state, C, out);
+    return hipGetLastError();
+}
+
+hipError_t fs_hist2d_impl(const double *pos, int64_t C, int N, double shift, const double *edges, int nb,
+                          int64_t *hist, hipStream_t st) {
+    const int64_t n = C * N;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(hist2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pos, C, N, shift,
+                       edges, nb, (unsigned long long *)hist);
+    return hipGetLastError();
+}
+
+hipError_t fs_well_stats_impl(const fs_phys *p, const double *pos, int64_t C, int N, int64_t *counts,
+                              hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    hipLaunchKernelGGL(well_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, *p, pos, C, N,
+                       (long long *)counts);
+    return hipGetLastError();
+}

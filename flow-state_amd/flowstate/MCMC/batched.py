@@ -1,0 +1,167 @@
+"""BatchedMonteCarlo — C independent chains, one NF-proposed MH step per call.
+
+The reference runs chains in a Python loop, one ``MonteCarlo.nf_big_move``
+per chain (main_algorithm_1.py:381-395, monte_carlo.py:235-303).  Here all C
+chains live on the device:
+
+  state        (C, N, 2) float64  box coordinates (holds the reference's float64
+                                   initial state and the float32 values it
+                                   switches to after an accepted big move)
+  state_is_f32 (C,) u8            the reference dtype of each chain's state
+  E_old, W_old (C,) float64       cached total energy / virial (energy_calculator.py:46)
+  nll_old      (C,) float64       cached -log q(state) (float32 value, exact on replay)
+  pcg          (C, 4) u64         numpy PCG64 state, seeded like default_rng(seed_c)
+  attempts, accepted (C,) int64   monte_carlo.py:80-81 counters
+
+``step()`` = fs_nf_mh_step: proposal sampling pass (base draws in-kernel) ->
+density pass on the proposals -> energies -> accept/update.  ``nf_big_move``
+takes externally supplied proposals (the reference's pre-generated configs).
+"""
+import numpy as np
+import torch
+
+from .. import _lib
+from .energy_calculator import make_phys, total_energy
+
+
+class Physics:
+    """Physics constants of the driver (main_algorithm_1.py:40-53)."""
+
+    def __init__(self, box_x, box_y=None, temperature=1.0, num_wells=2, V0_list=(-10.0, -10.5), r0=1.2, k=15):
+        self.box_x = float(box_x)
+        self.box_y = float(box_x if box_y is None else box_y)
+        self.beta = 1.0 / temperature
+        self.num_wells, self.V0_list, self.r0, self.k = num_wells, tuple(V0_list), r0, k
+        self.c = make_phys(self.box_x, self.box_y, num_wells, V0_list, r0, k, self.beta)
+
+    @property
+    def half_width(self):
+        return self.box_x / 2  # MonteCarlo.half_width (monte_carlo.py:66)
+
+
+class BatchedMonteCarlo:
+    def __init__(self, model, particles, physics, seeds, device=None, proposal_seed=1234,
+                 correct_sign=False, state_is_f32=None, chain_offset=0):
+        self.model = model
+        self.phys = physics
+        dev = torch.device(device) if device is not None else next(model.parameters()).device
+        _lib.require_device(torch.empty(0, device=dev))
+        self.device = dev
+        p = torch.as_tensor(np.asarray(particles) if not torch.is_tensor(particles) else particles)
+        if p.dim() == 2:
+            p = p[None]
+        self.C, self.N = int(p.shape[0]), int(p.shape[1])
+        if 2 * self.N != model.flows[0].num_input_channels:
+            raise ValueError("particles do not match the flow dimension")
+        if state_is_f32 is None:
+            state_is_f32 = p.dtype == torch.float32
+        self.state = p.to(device=dev, dtype=torch.float64).contiguous()
+        self.state_is_f32 = torch.full((self.C,), int(bool(state_is_f32)), dtype=torch.uint8, device=dev)
+        self.correct_sign = bool(correct_sign)
+        self.flags = _lib.FS_MH_CORRECT_SIGN if correct_sign else 0
+        self.proposal_seed = int(proposal_seed)
+        self.chain_offset = int(chain_offset)
+        self.step_count = 0
+        seeds = torch.as_tensor(np.asarray(seeds, dtype=np.uint64).view(np.int64), device=dev)
+        if seeds.numel() != self.C:
+            raise ValueError("one seed per chain")
+        self.pcg = torch.empty((self.C, 4), dtype=torch.int64, device=dev)
+        L = _lib.load()
+        _lib.check(L.fs_pcg64_seed(_lib.ptr(seeds), self.C, _lib.ptr(self.pcg), _lib.stream_ptr()), "fs_pcg64_seed")
+        self.attempts = torch.zeros(self.C, dtype=torch.int64, device=dev)
+        self.accepted = torch.zeros(self.C, dtype=torch.int64, device=dev)
+        self.n_accept = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.accept = torch.zeros(self.C, dtype=torch.uint8, device=dev)
+        self.E_old, self.W_old, self.nll_old = self._initial_energy_and_nll()
+        self._ws = None
+
+    # ------------------------------------------------------------------
+    def _centered_f32(self, pos, is_f32_mask=None):
+        """fl32(pos - half_width) as nf_big_move feeds the flow (monte_carlo.py:251-258)."""
+        return (pos - self.phys.half_width).to(torch.float32).reshape(pos.shape[0], -1).contiguous()
+
+    def _initial_energy_and_nll(self):
+        # energies in the reference dtype of each chain's state
+        E = torch.empty(self.C, dtype=torch.float64, device=self.device)
+        W = torch.empty_like(E)
+        f32 = self.state_is_f32.bool()
+        for mask, dt in ((f32, torch.float32), (~f32, torch.float64)):
+            idx = mask.nonzero().flatten()
+            if idx.numel():
+                e, w, _ = total_energy(self.state[idx].to(dt), self.phys.c)
+                E[idx], W[idx] = e, w
+        lq = self.model.log_prob(self._centered_f32(self.state))
+        return E, W, -(lq.to(torch.float64))
+
+    def _workspace(self):
+        if self._ws is None:
+            n = _lib.load().fs_nf_mh_step_ws_bytes(self.model.dims(), self.C)
+            _lib.check(0 if n >= 0 else -1, "fs_nf_mh_step_ws_bytes")
+            self._ws = torch.empty((n + 255) // 256 * 64, dtype=torch.float32, device=self.device)
+        return self._ws
+
+    # ------------------------------------------------------------------
+    def step(self, n=1):
+        """n fused NF-MH steps for all chains (stream-ordered, no host sync)."""
+        L = _lib.load()
+        packed = self.model.packed()
+        dims = self.model.dims()
+        ws = self._workspace()
+        st = _lib.stream_ptr()
+        for _ in range(n):
+            _lib.check(L.fs_nf_mh_step(dims, _lib.ptr(packed), self.phys.c, self.C, self.proposal_seed,
+                                       self.step_count, self.chain_offset, _lib.ptr(self.E_old), _lib.ptr(self.W_old),
+                                       _lib.ptr(self.nll_old), _lib.ptr(self.pcg), _lib.ptr(self.state),
+                                       _lib.ptr(self.state_is_f32), _lib.ptr(self.accept),
+                                       _lib.ptr(self.attempts), _lib.ptr(self.accepted), _lib.ptr(self.n_accept),
+                                       _lib.ptr(self.err), self.flags, _lib.ptr(ws), st), "fs_nf_mh_step")
+            self.step_count += 1
+        return self.accept
+
+    def check_errors(self):
+        if int(self.err.item()) & 1:
+            raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
+
+    def nf_big_move(self, configs):
+        """Batched nf_big_move with supplied proposals (C, N, 2) float32 box coords."""
+        cfg = torch.as_tensor(configs, device=self.device)
+        if cfg.dtype != torch.float32:
+            raise ValueError("proposals are float32 (main_algorithm_1.py:340-343)")
+        cfg = cfg.reshape(self.C, self.N, 2).contiguous()
+        E_new, W_new, _ = total_energy(cfg, self.phys.c)
+        lq = self.model.log_prob(self._centered_f32(cfg.to(torch.float64)))
+        L = _lib.load()
+        _lib.check(L.fs_mh_accept(self.phys.c, self.C, self.N, _lib.ptr(self.E_old), _lib.ptr(self.W_old),
+                                  _lib.ptr(self.nll_old), _lib.ptr(E_new), _lib.ptr(W_new), _lib.ptr(lq),
+                                  _lib.ptr(self.pcg), _lib.ptr(self.state), _lib.ptr(self.state_is_f32),
+                                  _lib.ptr(cfg), _lib.ptr(self.accept), _lib.ptr(self.attempts),
+                                  _lib.ptr(self.accepted), _lib.ptr(self.n_accept), self.flags,
+                                  _lib.stream_ptr()), "fs_mh_accept")
+        return self.accept
+
+    # ------------------------------------------------------------------
+    def particles(self):
+        """State in each chain's reference dtype, host numpy (C, N, 2)."""
+        return self.state.cpu().numpy()
+
+    def acceptance_rate(self):
+        a = self.attempts.sum().item()
+        return self.accepted.sum().item() / a if a else 0.0
+
+    def histogram2d(self, bins=100):
+        """Density histogram of the current states (utils.py:488-495): counts (bins-1, bins-1)."""
+        B = self.phys.half_width
+        edges = torch.as_tensor(np.linspace(-B, B, bins), device=self.device)
+        hist = torch.zeros((bins - 1) * (bins - 1), dtype=torch.int64, device=self.device)
+        _lib.check(_lib.load().fs_hist2d(_lib.ptr(self.state), self.C, self.N, B, _lib.ptr(edges), bins - 1,
+                                         _lib.ptr(hist), _lib.stream_ptr()), "fs_hist2d")
+        return hist.reshape(bins - 1, bins - 1)
+
+    def well_counts(self, counts=None):
+        """(C, 3) int64: all-in-A, all-in-B, samples (utils.py:61-141) accumulated into counts."""
+        if counts is None:
+            counts = torch.zeros((self.C, 3), dtype=torch.int64, device=self.device)
+        _lib.check(_lib.load().fs_well_stats(self.phys.c, _lib.ptr(self.state), self.C, self.N, _lib.ptr(counts),
+                                             _lib.stream_ptr()), "fs_well_stats")
+        return counts

@@ -1,0 +1,184 @@
+"""NormalizingFlow drop-in (reference: NF/normflows/core.py:10-230).
+
+Same constructor and method names/semantics as the reference fork:
+``forward`` / ``forward_and_log_det`` (sampling direction), ``inverse`` /
+``inverse_and_log_det`` (density direction), ``log_prob`` (density direction +
+UniformParticle base term), ``sample(n)`` returning the tensor only (the fork's
+change, core.py:178-196), ``save`` / ``load``.  Every pass runs as ONE
+libflowstate launch over the whole coupling stack (fs_flow_*), reading a packed
+copy of the parameters that is rebuilt on the device whenever a parameter or
+BatchNorm buffer changes (eval-mode BatchNorm is folded at pack time).
+
+Training (forward_kld / reverse_kld with autograd) is not part of the
+inference hot path this build covers; those methods raise.
+"""
+import torch
+import torch.nn as nn
+
+from .. import _lib
+from .Energy import UniformParticle
+
+
+def _tensor_key(ts):
+    return tuple((t.data_ptr(), t._version, str(t.device)) for t in ts)
+
+
+class _PackCache:
+    """Device-resident packed parameter image of a list of identical-shape layers."""
+
+    def __init__(self):
+        self.key = None
+        self.packed = None
+        self.raw = None
+
+    def get(self, layers):
+        tensors = [t for layer in layers for t in layer.raw_param_tensors()]
+        key = _tensor_key(tensors)
+        if key == self.key:
+            return self.packed
+        dev = tensors[0].device
+        _lib.require_device(tensors[0])
+        dims = layers[0].dims(L=len(layers))
+        L = _lib.load()
+        nraw = L.fs_flow_raw_floats(dims)
+        nbytes = L.fs_flow_packed_bytes(dims)
+        if nraw < 0 or nbytes < 0:
+            _lib.check(-1, "flow dims")
+        with torch.no_grad():
+            raw = torch.cat([t.detach().reshape(-1).to(torch.float32) for t in tensors])
+        if raw.numel() != nraw:
+            raise _lib.FlowStateError(f"raw parameter count {raw.numel()} != expected {nraw}")
+        packed = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+        _lib.check(L.fs_flow_pack(dims, _lib.ptr(raw), _lib.ptr(packed), _lib.stream_ptr()), "fs_flow_pack")
+        self.raw, self.packed, self.key = raw, packed, key
+        return packed
+
+
+def _check_stack(layers):
+    if not layers:
+        raise ValueError("empty flow stack")
+    for l in layers[1:]:
+        if not layers[0].same_shape(l):
+            raise _lib.FlowStateError("all coupling layers of a stack must share hyper-parameters")
+    for l in layers:
+        if l.training and any(m.training for m in l.modules() if isinstance(m, nn.BatchNorm1d)):
+            raise _lib.FlowStateError(
+                "flowstate runs the flow in eval mode (BatchNorm running statistics, as the reference's "
+                "hot path does after model.eval(), main_algorithm_1.py:331); call .eval() first")
+
+
+def _prepare_input(x, D):
+    _lib.require_device(x)
+    if x.dim() != 2 or x.shape[1] != D:
+        raise ValueError(f"Expected input of shape (B, {D}), got {tuple(x.shape)}")
+    return x.detach().to(torch.float32).contiguous()
+
+
+def _raise_on_nan(err):
+    if int(err.item()) & 1:
+        raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
+
+
+def _run_stack(layers, x, direction, cache=None, base_log_prob=None):
+    """Run the coupling stack in one launch.  direction: 'forward' (sampling,
+    layers 0..L-1) or 'inverse' (density, layers L-1..0).  Returns (out, log_det)."""
+    _check_stack(layers)
+    cache = cache or getattr(layers[0], "_fs_cache", None)
+    if cache is None:
+        cache = _PackCache()
+        layers[0]._fs_cache = cache
+    D = layers[0].num_input_channels
+    x = _prepare_input(x, D)
+    packed = cache.get(layers)
+    dims = layers[0].dims(L=len(layers))
+    B = x.shape[0]
+    out = torch.empty_like(x)
+    ld = torch.empty(B, dtype=torch.float32, device=x.device)
+    err = torch.zeros(1, dtype=torch.int32, device=x.device)
+    L = _lib.load()
+    st = _lib.stream_ptr()
+    if direction == "forward":
+        _lib.check(L.fs_flow_forward(dims, _lib.ptr(packed), _lib.ptr(x), B, _lib.ptr(out), _lib.ptr(ld),
+                                     _lib.ptr(err), st), "fs_flow_forward")
+        _raise_on_nan(err)
+    elif base_log_prob:
+        _lib.check(L.fs_flow_log_prob(dims, _lib.ptr(packed), _lib.ptr(x), B, _lib.ptr(ld), _lib.ptr(out),
+                                      _lib.ptr(err), st), "fs_flow_log_prob")
+    else:
+        _lib.check(L.fs_flow_inverse(dims, _lib.ptr(packed), _lib.ptr(x), B, _lib.ptr(out), _lib.ptr(ld),
+                                     _lib.ptr(err), st), "fs_flow_inverse")
+    return out, ld
+
+
+class NormalizingFlow(nn.Module):
+    """Normalizing flow (core.py:10-230) over CircularCoupledRationalQuadraticSpline layers."""
+
+    def __init__(self, q0, flows, p=None):
+        super().__init__()
+        self.q0 = q0
+        self.flows = nn.ModuleList(flows)
+        self.p = p
+        self._cache = _PackCache()
+
+    def _layers(self):
+        return list(self.flows)
+
+    def _base_check(self):
+        if not isinstance(self.q0, UniformParticle):
+            raise NotImplementedError("the fused base density is UniformParticle (main_algorithm_1.py:277)")
+        b = float(self.q0.bound)
+        if any(abs(f.tail_bound - b) > 0 for f in self.flows):
+            raise NotImplementedError("q0.bound must equal the layers' tail_bound (main_algorithm_1.py:276-283)")
+
+    def packed(self):
+        """Device packed parameter image (rebuilt when parameters/buffers change)."""
+        return self._cache.get(self._layers())
+
+    def dims(self):
+        return self.flows[0].dims(L=len(self.flows))
+
+    @torch.no_grad()
+    def forward(self, z):
+        """core.py:28-39: latent z -> x (sampling direction)."""
+        return _run_stack(self._layers(), z, "forward", self._cache)[0]
+
+    @torch.no_grad()
+    def forward_and_log_det(self, z):
+        """core.py:41-56."""
+        return _run_stack(self._layers(), z, "forward", self._cache)
+
+    @torch.no_grad()
+    def inverse(self, x):
+        """core.py:58-69: x -> latent z (density direction)."""
+        return _run_stack(self._layers(), x, "inverse", self._cache)[0]
+
+    @torch.no_grad()
+    def inverse_and_log_det(self, x):
+        """core.py:71-86."""
+        return _run_stack(self._layers(), x, "inverse", self._cache)
+
+    @torch.no_grad()
+    def log_prob(self, x):
+        """core.py:198-214: sum of layer log-dets + UniformParticle.log_prob, in x.dtype."""
+        self._base_check()
+        _, lq = _run_stack(self._layers(), x, "inverse", self._cache, base_log_prob=True)
+        return lq.to(x.dtype)
+
+    @torch.no_grad()
+    def sample(self, num_samples=1):
+        """core.py:178-196 (fork): returns the samples only."""
+        z = self.q0(num_samples)
+        dev = next(self.parameters()).device
+        return self.forward(z.to(dev))
+
+    def forward_kld(self, x):
+        raise NotImplementedError("training (core.py:88-103) is outside the inference hot path (SURVEY §8(f))")
+
+    def reverse_kld(self, num_samples=1, beta=1.0, score_fn=True):
+        raise NotImplementedError("training (core.py:105-142) is outside the inference hot path (SURVEY §8(f))")
+
+    def save(self, path):
+        torch.save(self.state_dict(), path)
+
+    def load(self, path):
+        self.load_state_dict(torch.load(path, weights_only=True))

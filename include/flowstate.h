@@ -1,0 +1,188 @@
+/*
+ * flowstate.h — C ABI of the MI355X-native NF-proposed Metropolis–Hastings
+ * hot path (libflowstate.so, built for gfx950).
+ *
+ * The reference (Inesalmansa/flow-state) is pure Python and has no FFI; the
+ * boundary it exposes is the Python API that hybrid_NF_MCMC/main_algorithm_1.py
+ * calls.  Each entry point below replaces one reference function (cited as
+ * path:line in the reference tree); INTEGRATION.md shows the ctypes binding
+ * the reference side would add, and flow-state_amd/flowstate/ is that binding
+ * plus the drop-in NormalizingFlow / MonteCarlo classes.
+ *
+ * Conventions
+ *   - every tensor argument is a DEVICE pointer owned by the caller;
+ *   - `stream` is a hipStream_t passed as void* (no HIP types in the ABI);
+ *   - calls are stream-ordered and never synchronise the device;
+ *   - return 0 on success, <0 for an invalid argument, >0 for a HIP error
+ *     code; fs_last_error() returns a thread-local message for the last
+ *     failure of the calling thread.  No C++ exception crosses the ABI.
+ */
+#ifndef FLOWSTATE_H
+#define FLOWSTATE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FS_OK 0
+#define FS_EINVAL (-1)
+#define FS_EUNSUPPORTED (-2)
+
+/* Flow hyper-parameters.  Mirrors the CircularCoupledRationalQuadraticSpline
+ * stack built by main_algorithm_1.py:280-284 (wrapper.py:103-119):
+ * N particles (D = 2N), L layers, H hidden units, nb residual blocks,
+ * K spline bins, tail_bound = HALF_BOX. */
+typedef struct {
+    int32_t N;
+    int32_t L;
+    int32_t H;
+    int32_t nb;
+    int32_t K;
+    int32_t reserved;
+    double tail_bound;
+} fs_flow_dims;
+
+/* Physics of the 2D NVT LJ double-well system (main_algorithm_1.py:40-53,
+ * energy_calculator.py:79-80, monte_carlo.py:66-67). */
+typedef struct {
+    double Lx, Ly;        /* SimulationBox.box_size_x / _y                 */
+    double V0[2];         /* V0_list                                       */
+    double r0, k;         /* well radius, steepness                        */
+    int32_t num_wells;    /* 0, 1, 2                                       */
+    int32_t reserved;
+    double r_cut;         /* 2.5 (inclusive)                               */
+    double r_core;        /* 0.5 hard core                                 */
+    double beta;          /* 1 / temperature                               */
+} fs_phys;
+
+const char *fs_last_error(void);
+int fs_version(void);
+
+/* ------------------------------------------------------------------ */
+/* Normalizing flow (NF/normflows)                                     */
+/* ------------------------------------------------------------------ */
+
+/* Number of floats of the canonical raw parameter buffer: for each layer
+ * i = 0..L-1, in this order (all float32, row-major as in the state_dict):
+ *   initial_layer.weight [H][2N], initial_layer.bias [H],
+ *   for each block j: batch_norm_layers.0.{weight,bias,running_mean,running_var} [H] x4,
+ *                     linear_layers.0.{weight [H][H], bias [H]},
+ *                     batch_norm_layers.1.{weight,bias,running_mean,running_var} [H] x4,
+ *                     linear_layers.1.{weight [H][H], bias [H]},
+ *   final_layer.weight [N(3K+1)][H], final_layer.bias [N(3K+1)],
+ *   unconditional_transform.unnormalized_{widths [N][K], heights [N][K],
+ *                                         derivatives [N][K+1]}.
+ * Keys are those of flows.{i}.prqct.transform_net.* (wrapper.py:168-185,
+ * resnet.py:53-104) and flows.{i}.prqct.unconditional_transform.* (coupling.py:176-221). */
+int64_t fs_flow_raw_floats(const fs_flow_dims *d);
+
+/* Bytes of the packed (MFMA-fragment-ordered, BatchNorm-folded, unconditional
+ * spline knots precomputed) parameter image. */
+int64_t fs_flow_packed_bytes(const fs_flow_dims *d);
+
+/* Pack raw -> packed on the device.  Must be re-run after any weight update
+ * (eval-mode BatchNorm statistics are folded here, resnet.py:37-50). */
+int fs_flow_pack(const fs_flow_dims *d, const float *raw, void *packed, void *stream);
+
+/* NormalizingFlow.log_prob (NF/normflows/core.py:198-214): layers L-1..0 in
+ * the density direction (CircularCoupled...inverse = Coupling.forward,
+ * wrapper.py:273-275, coupling.py:71-102) + UniformParticle.log_prob
+ * (Energy/Uniform.py:50-74).  x, z_out: [B][2N] float32 (z_out nullable);
+ * log_q: [B].  err (nullable, device int32): bit0 set on a NaN discriminant. */
+int fs_flow_log_prob(const fs_flow_dims *d, const void *packed, const float *x, int64_t B,
+                     float *log_q, float *z_out, int32_t *err, void *stream);
+
+/* NormalizingFlow.inverse_and_log_det without the base term (core.py:71-86). */
+int fs_flow_inverse(const fs_flow_dims *d, const void *packed, const float *x, int64_t B,
+                    float *z_out, float *log_det, int32_t *err, void *stream);
+
+/* NormalizingFlow.forward_and_log_det / sample body (core.py:41-56, 178-196):
+ * layers 0..L-1 in the sampling direction (CircularCoupled...forward =
+ * Coupling.inverse, wrapper.py:269-271, coupling.py:104-134) from supplied
+ * base draws z [B][2N] -> x [B][2N]; log_det nullable.  err bit0: NaN
+ * discriminant (the reference raises ValueError, splines.py:176-183). */
+int fs_flow_forward(const fs_flow_dims *d, const void *packed, const float *z, int64_t B,
+                    float *x_out, float *log_det, int32_t *err, void *stream);
+
+/* Proposal generation for the batched MH step (utils.py:422-450 +
+ * main_algorithm_1.py:340-343): base draws z ~ U(-B, B) from a counter-based
+ * generator keyed (seed, counter, row_offset + row), sampling pass, then
+ *   config   = fl32(x + fl32(tail_bound))         box coordinates [B][N][2]
+ *   centered = fl32((double)config - half_width)   the NF input of nf_big_move
+ *                                                   (monte_carlo.py:251-258).
+ * x_out (centered model-space sample) and centered are nullable. */
+int fs_flow_propose(const fs_flow_dims *d, const void *packed, int64_t B, uint64_t seed,
+                    uint64_t counter, int64_t row_offset, double half_width, float *config,
+                    float *centered, float *x_out, int32_t *err, void *stream);
+
+/* ------------------------------------------------------------------ */
+/* Physics (MCMC/)                                                     */
+/* ------------------------------------------------------------------ */
+
+/* EnergyCalculator.calculate_total_energy_virial (energy_calculator.py:121-203)
+ * for C chains: pos [C][N][2], float32 (pos_is_f32=1) or float64.
+ * E, W: [C] float64 (+inf on a hard-core overlap, the reference's early return);
+ * overlap [C] u8 nullable; nbr nullable: [C][N] u64, bit j of word i set iff
+ * i<j and r_ij <= r_cut (the neighbour mask of potential.py:11).  N <= 64. */
+int fs_energy_lj_dw(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int32_t N,
+                    double *E, double *W, uint8_t *overlap, uint64_t *nbr, void *stream);
+
+/* np.random.default_rng(seed) (SeedSequence + PCG64 init, monte_carlo.py:92-95)
+ * for C seeds -> state [C][4] u64 = {state_hi, state_lo, inc_hi, inc_lo}. */
+int fs_pcg64_seed(const uint64_t *seeds, int64_t C, uint64_t *state, void *stream);
+
+/* C x Generator.random() draws, advancing each state once. */
+int fs_pcg64_random(uint64_t *state, int64_t C, double *out, void *stream);
+
+/* MonteCarlo.nf_big_move decision + update (monte_carlo.py:235-303), batched:
+ *   ratio = exp(-beta*(E_new - E_old) - (nll_new - nll_old))   (reference sign;
+ *           flags bit0 FS_MH_CORRECT_SIGN uses +(nll_new - nll_old))
+ *   accept iff ratio >= 1 (no draw) or Generator.random() < ratio.
+ * On accept: state[c] <- config[c] (float32 values, state_is_f32[c] <- 1),
+ * E_old/W_old/nll_old <- new values, accepted[c]++.  attempts[c]++ always
+ * (monte_carlo.py:240).  accept [C] u8 out; n_accept (nullable) += accepts
+ * (wave ballot + popcount, one atomic per wave). */
+#define FS_MH_CORRECT_SIGN 1
+int fs_mh_accept(const fs_phys *p, int64_t C, int32_t N, double *E_old, double *W_old,
+                 double *nll_old, const double *E_new, const double *W_new, const float *log_q_new,
+                 uint64_t *pcg, double *state, uint8_t *state_is_f32, const float *config,
+                 uint8_t *accept, int64_t *attempts, int64_t *accepted,
+                 unsigned long long *n_accept, int flags, void *stream);
+
+/* Fused batched NF-MH step over C chains: fs_flow_propose -> fs_flow_log_prob
+ * (density pass on `centered`) -> fs_energy_lj_dw (config, float32) ->
+ * fs_mh_accept.  chain_offset: global index of chain 0 (proposal stream row), so a
+ * chain's trajectory does not depend on how chains are sharded over GPUs.
+ * ws: caller workspace of fs_nf_mh_step_ws_bytes() bytes (256-byte aligned):
+ * config f32 [C][2N] | centered f32 [C][2N] | log_q f32 [C] | E_new f64 [C] |
+ * W_new f64 [C], each section padded to 256 bytes. */
+int64_t fs_nf_mh_step_ws_bytes(const fs_flow_dims *d, int64_t C);
+int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C,
+                  uint64_t seed, uint64_t step, int64_t chain_offset, double *E_old, double *W_old, double *nll_old,
+                  uint64_t *pcg, double *state, uint8_t *state_is_f32, uint8_t *accept,
+                  int64_t *attempts, int64_t *accepted, unsigned long long *n_accept,
+                  int32_t *err, int flags, void *ws, void *stream);
+
+/* ------------------------------------------------------------------ */
+/* Analysis reductions (hybrid_NF_MCMC/utils.py)                       */
+/* ------------------------------------------------------------------ */
+
+/* np.histogram2d over centered coordinates with the given edges
+ * (utils.py:488-495: edges = linspace(-B, B, nb+1) per axis, last bin
+ * right-inclusive).  pos [C][N][2] float64 box coords minus `shift`;
+ * hist [nb][nb] int64 accumulated (+=). */
+int fs_hist2d(const double *pos, int64_t C, int32_t N, double shift, const double *edges,
+              int32_t nbins, int64_t *hist, void *stream);
+
+/* classify_particles / calculate_well_statistics (utils.py:61-141): for each
+ * chain, all particles within 1.1*r0 of the left well (A) or all within the
+ * right well (B); counts[c][0] += all_A, counts[c][1] += all_B, counts[c][2] += 1. */
+int fs_well_stats(const fs_phys *p, const double *pos, int64_t C, int32_t N, int64_t *counts,
+                  void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLOWSTATE_H */

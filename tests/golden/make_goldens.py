@@ -248,6 +248,20 @@ def mh_trace_case(NF, MC, SimulationBox):
     np.savez_compressed(os.path.join(HERE, "mh_trace.npz"), **out)
 
 
+def init_case(NF):
+    """Reference module-construction RNG order: state_dict right after
+    torch.manual_seed(seed) + construction (wrapper.py:98-275, resnet.py:53-104)."""
+    from oracle import flow as OF
+    dims = OF.FlowDims(N=4, L=2, H=32, nb=1, K=5, B=OF.half_box(4))
+    torch.manual_seed(123)
+    model = build_ref_model(NF, dims)
+    out = dict(seed=123, N=dims.N, L=dims.L, H=dims.H, nb=dims.nb, K=dims.K)
+    for k, v in model.state_dict().items():
+        out["sd/" + k] = v.numpy()
+    np.savez_compressed(os.path.join(HERE, "init.npz"), **out)
+    print("init: ok")
+
+
 def pcg_case():
     seeds = np.arange(42, 42 + 64)
     st = np.zeros((64, 4), np.uint64)
@@ -272,6 +286,7 @@ def main():
     energy_case(MC, SimulationBox)
     mh_trace_case(NF, MC, SimulationBox)
     pcg_case()
+    init_case(NF)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,129 @@
+"""GPU parity of the HIP coupling-flow passes against the oracle and the
+reference goldens.  Tolerance (north star): log_prob within 1e-5 relative.
+The reference itself is float32; its own float32-vs-float64 log_prob error
+reaches ~1e-5 relative on outliers, so the bound is checked as
+|gpu - ref32| <= 1e-5*|ref32| + 1e-4 (absolute floor for values near 0)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from flowstate.models import A1, build_flow, flow_from_state_dict, half_box
+from oracle import flow as OF
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+RTOL, ATOL = 1e-5, 1e-4
+
+
+def close(a, b, rtol=RTOL, atol=ATOL):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    fin = np.isfinite(b)
+    assert np.array_equal(np.isfinite(a), fin) and np.array_equal(a[~fin], b[~fin])
+    err = np.abs(a[fin] - b[fin])
+    bound = rtol * np.abs(b[fin]) + atol
+    bad = err > bound
+    assert not bad.any(), f"{bad.sum()} / {bad.size} out of tolerance; worst rel {np.max(err / (np.abs(b[fin]) + 1e-30))}"
+
+
+def golden_model(name):
+    f = np.load(os.path.join(G, f"flow_{name}.npz"))
+    dims = OF.FlowDims(N=int(f["N"]), L=int(f["L"]), H=int(f["H"]), nb=int(f["nb"]), K=int(f["K"]), B=float(f["B"]))
+    sd = OF.random_state_dict(dims, seed=int(f["seed"]))
+    m = flow_from_state_dict(sd, dims.N, dims.L, dims.H, dims.nb, dims.K, bound=dims.B)
+    return f, dims, sd, m
+
+
+@pytest.mark.parametrize("name", ["tiny", "n16", "n64"])
+def test_log_prob_matches_reference_golden(name):
+    f, dims, sd, m = golden_model(name)
+    lp = m.log_prob(torch.from_numpy(f["x"]).cuda()).cpu().numpy()
+    close(lp, f["log_prob"])
+    z = m.inverse(torch.from_numpy(f["x"]).cuda()).cpu().numpy()
+    np.testing.assert_allclose(z, f["z_layers"][-1], rtol=0, atol=2e-4 * dims.B)
+
+
+@pytest.mark.parametrize("name", ["tiny", "n16", "n64"])
+def test_sample_direction_matches_reference_golden(name):
+    f, dims, sd, m = golden_model(name)
+    x, ld = m.forward_and_log_det(torch.from_numpy(f["z_base"]).cuda())
+    # the sampling direction's root solve is ill-conditioned: abs tolerance in box units
+    np.testing.assert_allclose(x.cpu().numpy(), f["x_sample"], rtol=0, atol=5e-4 * dims.B)
+    close(ld.cpu().numpy(), f["logdet_sample"], rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("N", [16, 64])
+def test_a1_log_prob_matches_oracle(N):
+    """Algorithm-1 hyper-parameters (L=15, H=256, 32 blocks, K=32) at N=16 and N=64."""
+    dims = OF.FlowDims(N=N, B=half_box(N), **A1)
+    sd = OF.random_state_dict(dims, seed=7)
+    m = flow_from_state_dict(sd, N, bound=dims.B, **A1)
+    g = torch.Generator().manual_seed(3)
+    x = (torch.rand((96, dims.D), generator=g) * 2 - 1) * dims.B
+    want = OF.log_prob(sd, x.clone(), dims).numpy()
+    got = m.log_prob(x.cuda()).cpu().numpy()
+    close(got, want)
+
+
+def test_a1_forward_inverse_roundtrip_full_batch():
+    """Size-independent property at the benchmark shape: inverse(forward(z)) == z and
+    log-dets cancel (FlowTest.checkForwardInverse, flows/flow_test.py:40-47)."""
+    N = 64
+    m = build_flow(N, device="cuda", **A1).eval()
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(0)
+        for p in m.parameters():
+            if p.dim() == 2 and p.shape[0] == N * 97:
+                p.copy_(torch.randn(p.shape, generator=g) * 0.01)
+    B = half_box(N)
+    z = ((torch.rand((4096, 2 * N), device="cuda") * 2 - 1) * B).contiguous()
+    x, ld_f = m.forward_and_log_det(z)
+    z2, ld_i = m.inverse_and_log_det(x)
+    assert torch.isfinite(x).all() and torch.isfinite(ld_f).all()
+    err = (z2 - z).abs().max().item()
+    assert err < 5e-3 * B, err
+    assert (ld_f + ld_i).abs().max().item() < 5e-2
+
+
+def test_per_layer_api_matches_stack():
+    f, dims, sd, m = golden_model("n16")
+    x = torch.from_numpy(f["x"]).cuda()
+    z, ld = x, torch.zeros(x.shape[0], device="cuda")
+    for i in range(dims.L - 1, -1, -1):
+        z, l = m.flows[i].inverse(z)
+        ld = ld + l
+    z2, ld2 = m.inverse_and_log_det(x)
+    torch.testing.assert_close(z, z2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ld, ld2, rtol=1e-5, atol=1e-4)
+
+
+def test_outside_bound_is_identity_and_minus_inf():
+    f, dims, sd, m = golden_model("n16")
+    x = torch.from_numpy(f["x"][:4]).cuda()
+    lp = m.log_prob(x).cpu().numpy()
+    assert np.isneginf(lp[2]) and np.isfinite(lp[[0, 1, 3]]).all()
+
+
+def test_ragged_batches():
+    f, dims, sd, m = golden_model("tiny")
+    x = torch.from_numpy(f["x"]).cuda()
+    full = m.log_prob(x).cpu().numpy()
+    for n in (1, 3, 63, 64):
+        part = m.log_prob(x[:n]).cpu().numpy()
+        np.testing.assert_array_equal(part, full[:n])
+    assert m.log_prob(x[:0]).numel() == 0
+
+
+def test_pack_tracks_weight_updates():
+    f, dims, sd, m = golden_model("tiny")
+    x = torch.from_numpy(f["x"]).cuda()
+    a = m.log_prob(x)
+    with torch.no_grad():
+        m.flows[0].prqct.transform_net.final_layer.weight.mul_(2.0)
+    b = m.log_prob(x)
+    assert not torch.equal(a, b)
+    sd2 = {k: v.clone() for k, v in sd.items()}
+    sd2["flows.0.prqct.transform_net.final_layer.weight"] *= 2.0
+    close(b.cpu().numpy(), OF.log_prob(sd2, torch.from_numpy(f["x"]), dims).numpy())

@@ -1,0 +1,128 @@
+"""End-to-end parity of the NF-proposed MH step on the GPU.
+
+1. Reference traces (tests/golden/mh_trace.npz, produced by the reference's
+   own MonteCarlo.nf_big_move) replayed through the drop-in per-chain
+   MonteCarlo: identical accept masks, final states and PCG64 states.
+2. The fused batched step (fs_nf_mh_step, proposals generated on the device)
+   re-checked by the oracle on the proposals it actually made: energies within
+   1e-12, log_prob within 1e-5 relative, accept masks identical given the same
+   PCG64 streams (borderline flips from the float32 log_prob are counted and
+   must be rare).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from flowstate.MCMC import BatchedMonteCarlo, MonteCarlo, Physics, SimulationBox
+from flowstate.models import A1, flow_from_state_dict, half_box
+from oracle import flow as OF
+from oracle import physics as OP
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("N", [16, 64])
+def test_reference_traces_replay(N):
+    f = np.load(os.path.join(G, "mh_trace.npz"))
+    dims = OF.FlowDims(N=N, L=2, H=32, nb=1, K=8, B=OF.half_box(N))
+    sd = OF.random_state_dict(dims, seed=int(f[f"N{N}_flow_seed"]))
+    model = flow_from_state_dict(sd, N, 2, 32, 1, 8, bound=dims.B)
+    L = float(np.sqrt(N / 0.03))
+    for c in range(int(f[f"N{N}_chains"])):
+        k = f"N{N}_c{c}"
+        mc = MonteCarlo(particles=f[k + "_init"], sim_box=SimulationBox(L, L), temperature=1.0, num_particles=N,
+                        num_wells=2, V0_list=[-10.0, -10.5], r0=1.2, k=15, seed=int(f[k + "_seed"]))
+        mc.set_nf_model(model)
+        acc = [mc.nf_big_move(cfg) for cfg in f[k + "_props"]]
+        np.testing.assert_array_equal(np.array(acc), f[k + "_accept"])
+        np.testing.assert_array_equal(np.asarray(mc.particles, np.float64), np.asarray(f[k + "_final"], np.float64))
+        Eref = f[k + "_E"][-1]
+        E = mc.energy_calculator.total_energy
+        assert (np.isinf(Eref) and np.isinf(E)) or abs(E - Eref) <= 1e-12 * max(1.0, abs(Eref))
+        st = mc._b.pcg[0].cpu().numpy().view(np.uint64)
+        np.testing.assert_array_equal(st[:2], f[k + "_pcg_state"][:2])
+        assert mc.attempts_displacement == len(acc) and mc.accepted_displacement == sum(acc)
+
+
+def _fused_vs_oracle(N, dims_kw, C, steps, seed_w=11):
+    dims = OF.FlowDims(N=N, B=half_box(N), **dims_kw)
+    sd = OF.random_state_dict(dims, seed=seed_w)
+    model = flow_from_state_dict(sd, N, bound=dims.B, **dims_kw)
+    L = float(np.sqrt(N / 0.03))
+    phys = Physics(L, L)
+    rng = np.random.default_rng(5)
+    init = np.mod(OP.fcc_lattice(N)[None] + rng.normal(0, 0.05, (C, N, 2)), L)
+    seeds = np.arange(42, 42 + C, dtype=np.uint64)
+    bmc = BatchedMonteCarlo(model, init, phys, seeds)
+    # oracle mirror of the chain state
+    E_o = OP.total_energy_batch(init, OP.make_phys(N))[0]
+    x0 = torch.from_numpy((init - L / 2).astype(np.float32).reshape(C, -1))
+    nll_o = -OF.log_prob(sd, x0, dims).numpy().astype(np.float64)
+    np.testing.assert_allclose(bmc.E_old.cpu().numpy(), E_o, rtol=1e-12)
+    np.testing.assert_allclose(bmc.nll_old.cpu().numpy(), nll_o, rtol=1e-5, atol=1e-4)
+    pcg_o = OP.pcg64_seed_many(seeds)
+    state_o = init.copy()
+    flips = 0
+    total_acc = 0
+    for s in range(steps):
+        bmc.step()
+        ws = bmc._ws
+        D = 2 * N
+        nbytes = C * D * 4
+        cfg = ws.view(torch.uint8)[:nbytes].view(torch.float32).reshape(C, N, 2).cpu().numpy()
+        cen = ws.view(torch.uint8)[(nbytes + 255) // 256 * 256:][:nbytes].view(torch.float32).reshape(C, D).cpu()
+        np.testing.assert_array_equal(cen.numpy(), (cfg.astype(np.float64) - L / 2).astype(np.float32).reshape(C, D))
+        assert np.all(cfg >= 0) and np.all(cfg <= L + 1e-3)
+        E_new = OP.total_energy_batch(cfg, OP.make_phys(N))[0]
+        lq = OF.log_prob(sd, cen.clone(), dims).numpy()
+        acc_o, _ = OP.mh_accept(E_o, E_new, nll_o, -lq.astype(np.float64), pcg_o)
+        acc = bmc.accept.cpu().numpy()
+        diff = acc != acc_o
+        flips += int(diff.sum())
+        total_acc += int(acc.sum())
+        # follow the GPU's decision so the two mirrors stay in lockstep (a flip is counted, not propagated)
+        pcg_o = bmc.pcg.cpu().numpy().view(np.uint64).copy()
+        a = acc.astype(bool)
+        state_o[a] = cfg[a]
+        E_o = np.where(a, E_new, E_o)
+        nll_o = np.where(a, -lq.astype(np.float64), nll_o)
+        np.testing.assert_allclose(bmc.E_old.cpu().numpy(), E_o, rtol=1e-12)
+        np.testing.assert_array_equal(bmc.state.cpu().numpy(), state_o)
+    bmc.check_errors()
+    assert int(bmc.n_accept.item()) == total_acc
+    return flips, total_acc, C * steps
+
+
+def test_fused_step_matches_oracle_small():
+    flips, acc, n = _fused_vs_oracle(16, dict(L=3, H=64, nb=2, K=8), C=512, steps=4)
+    assert flips <= max(1, n // 2000), (flips, n)
+
+
+def test_fused_step_matches_oracle_a1_n64():
+    """Algorithm-1 hyper-parameters at the benchmark N (C kept small for the CPU oracle)."""
+    flips, acc, n = _fused_vs_oracle(64, A1, C=128, steps=2)
+    assert flips <= 1, (flips, n)
+
+
+def test_batched_step_seed_sharding_independent_of_batch():
+    """Chain c's trajectory depends only on (seed_c, proposal stream row c): running the
+    first half of the chains alone reproduces them exactly (the multi-GPU contract)."""
+    N = 16
+    dims_kw = dict(L=2, H=64, nb=1, K=8)
+    dims = OF.FlowDims(N=N, B=half_box(N), **dims_kw)
+    sd = OF.random_state_dict(dims, seed=2)
+    model = flow_from_state_dict(sd, N, bound=dims.B, **dims_kw)
+    L = float(np.sqrt(N / 0.03))
+    init = np.repeat(OP.fcc_lattice(N)[None], 256, axis=0)
+    full = BatchedMonteCarlo(model, init, Physics(L, L), np.arange(42, 42 + 256, dtype=np.uint64))
+    lo = BatchedMonteCarlo(model, init[:128], Physics(L, L), np.arange(42, 42 + 128, dtype=np.uint64))
+    hi = BatchedMonteCarlo(model, init[128:], Physics(L, L), np.arange(42 + 128, 42 + 256, dtype=np.uint64),
+                           chain_offset=128)
+    for m in (full, lo, hi):
+        m.step(3)
+    np.testing.assert_array_equal(full.state[:128].cpu().numpy(), lo.state.cpu().numpy())
+    np.testing.assert_array_equal(full.state[128:].cpu().numpy(), hi.state.cpu().numpy())
+    assert full.accepted.sum().item() > 0

@@ -1,0 +1,79 @@
+"""CPU-only checks of the product's host side: the C-ABI library loads and
+exports every symbol of include/flowstate.h, layouts agree with the module
+tree, state_dict compatibility with the reference key set.  No GPU compute."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from flowstate import _lib
+from flowstate.models import build_flow, half_box
+from oracle import flow as OF
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(REPO, "include", "flowstate.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(fs_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), f"{s} declared in include/flowstate.h but not exported"
+    assert set(syms) == set(_lib.EXPORTED), "ctypes signature table out of sync with the header"
+    assert L.fs_version() >= 10000
+
+
+@pytest.mark.parametrize("N,L,H,nb,K", [(4, 2, 32, 1, 5), (16, 3, 64, 2, 8), (64, 2, 256, 3, 32), (64, 1, 128, 2, 15)])
+def test_raw_layout_matches_module_tree(N, L, H, nb, K):
+    m = build_flow(N, L, H, nb, K)
+    n_mod = sum(t.numel() for f in m.flows for t in f.raw_param_tensors())
+    assert _lib.load().fs_flow_raw_floats(m.dims()) == n_mod
+    assert _lib.load().fs_flow_packed_bytes(m.dims()) > 0
+
+
+def test_unsupported_dims_fail_loudly():
+    m = build_flow(16, 1, 96, 1, 8)
+    assert _lib.load().fs_flow_raw_floats(m.dims()) == -1
+    assert b"unsupported" in _lib.load().fs_last_error()
+
+
+def test_state_dict_keys_match_reference():
+    dims = OF.FlowDims(N=16, L=3, H=64, nb=2, K=8, B=OF.half_box(16))
+    sd_ref_format = OF.random_state_dict(dims, seed=0)  # reference key set, pinned by goldens
+    m = build_flow(16, 3, 64, 2, 8)
+    ours = m.state_dict()
+    assert set(ours) == set(sd_ref_format)
+    for k in ours:
+        assert ours[k].shape == sd_ref_format[k].shape and ours[k].dtype == sd_ref_format[k].dtype, k
+    m.load_state_dict(sd_ref_format, strict=True)
+
+
+def test_init_matches_reference_rng_order(golden_dir):
+    f = np.load(os.path.join(golden_dir, "init.npz"))
+    torch.manual_seed(int(f["seed"]))
+    m = build_flow(int(f["N"]), int(f["L"]), int(f["H"]), int(f["nb"]), int(f["K"]))
+    sd = m.state_dict()
+    for k in f.files:
+        if k.startswith("sd/"):
+            np.testing.assert_array_equal(sd[k[3:]].numpy(), f[k])
+
+
+def test_product_has_no_oracle_dependency():
+    pkg = os.path.join(REPO, "flow-state_amd")
+    for root, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith((".py", ".hip", ".cpp", ".h")):
+                src = open(os.path.join(root, fn)).read()
+                assert "import oracle" not in src and "from oracle" not in src, fn
+
+
+def test_half_box():
+    assert half_box(64) == pytest.approx(np.sqrt(64 / 0.03) / 2)

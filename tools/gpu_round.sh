@@ -1,0 +1,26 @@
+#!/bin/bash
+# One gpurun call: each GPU step under its own time limit; continue past plain
+# test failures (rc 1) but stop at anything that looks like a fault/abort/timeout.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+for step in "$@"; do
+  case "$step" in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    bench) run bench 600 python bench.py ;;
+    bench_short) run bench_short 400 python bench.py --steps 3 --warmup 1 --cpu-budget 10 ;;
+    prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
