@@ -74,7 +74,7 @@ int fs_flow_log_prob(const fs_flow_dims *d, const void *packed, const float *x, 
                      float *z_out, int32_t *err, void *stream) {
     int rc = check_dims(d);
     if (rc) return rc;
-    REQUIRE(packed && x && log_q && B >= 0, "fs_flow_log_prob: invalid arguments");
+    REQUIRE(B == 0 || (packed && x && log_q && B > 0), "fs_flow_log_prob: invalid arguments");
     return hip_rc(fs_flow_pass_impl(d, packed, 0, x, B, z_out, log_q, 1, nullptr, nullptr, 0, 0, 0, 0.0, err,
                                     (hipStream_t)stream),
                   "fs_flow_log_prob");
@@ -84,7 +84,7 @@ int fs_flow_inverse(const fs_flow_dims *d, const void *packed, const float *x, i
                     float *log_det, int32_t *err, void *stream) {
     int rc = check_dims(d);
     if (rc) return rc;
-    REQUIRE(packed && x && (z_out || log_det) && B >= 0, "fs_flow_inverse: invalid arguments");
+    REQUIRE(B == 0 || (packed && x && (z_out || log_det) && B > 0), "fs_flow_inverse: invalid arguments");
     return hip_rc(fs_flow_pass_impl(d, packed, 0, x, B, z_out, log_det, 0, nullptr, nullptr, 0, 0, 0, 0.0, err,
                                     (hipStream_t)stream),
                   "fs_flow_inverse");
@@ -94,7 +94,7 @@ int fs_flow_forward(const fs_flow_dims *d, const void *packed, const float *z, i
                     float *log_det, int32_t *err, void *stream) {
     int rc = check_dims(d);
     if (rc) return rc;
-    REQUIRE(packed && z && (x_out || log_det) && B >= 0, "fs_flow_forward: invalid arguments");
+    REQUIRE(B == 0 || (packed && z && (x_out || log_det) && B > 0), "fs_flow_forward: invalid arguments");
     return hip_rc(fs_flow_pass_impl(d, packed, 1, z, B, x_out, log_det, 0, nullptr, nullptr, 0, 0, 0, 0.0, err,
                                     (hipStream_t)stream),
                   "fs_flow_forward");

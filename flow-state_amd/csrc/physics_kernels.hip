@@ -28,7 +28,10 @@ __device__ __forceinline__ double dist_f32(float ax, float ay, float bx, float b
     const double w1 = (double)d1 - Ly * rint((double)d1 / Ly);
     const float t0 = (float)w0, t1 = (float)w1;
     const float s = __fadd_rn(__fmul_rn(t0, t0), __fmul_rn(t1, t1));  // OpenBLAS sdot
-    return (double)__fsqrt_rn(s);
+    // correctly rounded float32 sqrt (np.sqrt on float32): the double sqrt of a float
+    // rounded once more to float is exact-rounded (53 >= 2*24+2 bits); the device
+    // f32 sqrt instruction is only faithful
+    return (double)(float)__dsqrt_rn((double)s);
 }
 
 __device__ __forceinline__ double dist_f64(double ax, double ay, double bx, double by, double Lx, double Ly) {
