@@ -64,10 +64,6 @@ struct FlowArgs {
     float base_lp;        // fl32(-D * log(fl32(2B)))      (Uniform.py:70)
 };
 
-__device__ __forceinline__ int swz(int row, int col) {
-    return (((col >> 2) ^ (row & 15)) << 2) | (col & 3);
-}
-
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -77,48 +73,65 @@ __device__ __forceinline__ void wave_lds_sync() {
 // ---------------------------------------------------------------------------
 // GEMM: acc[rt][ct] (32x32 tiles, rows 32*rt.., cols 32*(tile0+ct)..) =
 //       X[64 x 8*kg] . Bpacked[tiles tile0..tile0+CT-1]
+// Operands of k-group g live in ring slot g % PD; the loads of group g+PD are
+// issued right after the MFMAs of group g (sched_barrier keeps hipcc from
+// sinking them next to their use), so PD-1 groups of MFMAs (>= 1024 cycles)
+// cover the L2 latency of every weight fragment at one wave per SIMD.
 // ---------------------------------------------------------------------------
-template <int CT>
-__device__ __forceinline__ void gemm64(const float *__restrict__ X, int xw,
-                                       const f32x4 *__restrict__ Bp, int kg, int tile0,
-                                       f32x16 (&acc)[2][CT]) {
+template <int XS, int CT, int PD>
+__device__ __forceinline__ void gemm64(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
+                                       int tile0, f32x16 (&acc)[2][CT]) {
+    // W: buffer descriptor of the layer's packed parameters; sec: byte offset of
+    // this GEMM's fragment section (wave-uniform).  32-bit offsets only: no 64-bit
+    // pointer per ring slot to keep live.
     const int lane = threadIdx.x & 63;
-    const int h = lane >> 5, r = lane & 31, sw = r & 15;
+    const int h = lane >> 5, r = lane & 31;
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[rt][ct][i] = 0.f;
-    const float *xa0 = X + r * xw;
-    const float *xa1 = X + (32 + r) * xw;
-    const f32x4 *bp = Bp + (size_t)tile0 * kg * 64 + lane;
-    f32x4 a0 = *(const f32x4 *)(xa0 + ((h ^ sw) << 2));
-    f32x4 a1 = *(const f32x4 *)(xa1 + ((h ^ sw) << 2));
-    f32x4 b[CT];
+    const float *xa0 = X + r * XS + 4 * h;
+    const float *xa1 = xa0 + 32 * XS;
+    const int voff = (tile0 * kg * 64 + lane) * 16;
+    auto ldb = [&](int ct, int g) {
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(W, voff, sec + (ct * kg + g) * 1024, 0));
+    };
+    f32x4 ra0[PD], ra1[PD], rb[PD][CT];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) b[ct] = bp[(size_t)ct * kg * 64];
-    for (int g = 0; g < kg; ++g) {
-        // prefetch next k-group while the MFMAs of this one run
-        const int gn = (g + 1 < kg) ? g + 1 : g;
-        const int sn = ((2 * gn + h) ^ sw) << 2;
-        f32x4 na0 = *(const f32x4 *)(xa0 + sn);
-        f32x4 na1 = *(const f32x4 *)(xa1 + sn);
-        f32x4 nb[CT];
+    for (int s = 0; s < PD; ++s) {
+        if (s < kg) {
+            ra0[s] = *(const f32x4 *)(xa0 + 8 * s);
+            ra1[s] = *(const f32x4 *)(xa1 + 8 * s);
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) nb[ct] = bp[((size_t)ct * kg + gn) * 64];
+            for (int ct = 0; ct < CT; ++ct) rb[s][ct] = ldb(ct, s);
+        }
+    }
+    for (int g0 = 0; g0 < kg; g0 += PD) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int s = 0; s < PD; ++s) {
+            const int g = g0 + s;
+            if (g < kg) {
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                acc[0][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[j], b[ct][j], acc[0][ct], 0, 0, 0);
-                acc[1][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[j], b[ct][j], acc[1][ct], 0, 0, 0);
+                for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                    for (int ct = 0; ct < CT; ++ct) {
+                        acc[0][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra0[s][j], rb[s][ct][j], acc[0][ct], 0, 0, 0);
+                        acc[1][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra1[s][j], rb[s][ct][j], acc[1][ct], 0, 0, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const int gn = g + PD;
+                if (gn < kg) {
+                    ra0[s] = *(const f32x4 *)(xa0 + 8 * gn);
+                    ra1[s] = *(const f32x4 *)(xa1 + 8 * gn);
+#pragma unroll
+                    for (int ct = 0; ct < CT; ++ct) rb[s][ct] = ldb(ct, gn);
+                }
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
-        a0 = na0;
-        a1 = na1;
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) b[ct] = nb[ct];
     }
 }
 
@@ -245,8 +258,8 @@ __device__ __forceinline__ void stage_tile(float *STG, const f32x16 &t0, const f
 // of the wave: three single-tile GEMMs (widths, heights, derivatives), each
 // staged through the wave's LDS transpose buffer right away so that only one
 // 32x64 accumulator pair is live at a time.
-template <int K, bool INV>
-__device__ __forceinline__ float cond_spline(const float *__restrict__ X, int xw, const f32x4 *__restrict__ Wf,
+template <int XS, int K, bool INV>
+__device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec,
                                              int kg, const float *__restrict__ bf, float *STG, const float *TL,
                                              int tstride, float *CO, int cs, int p, int j, const FlowArgs &a,
                                              bool &nan_any) {
@@ -255,7 +268,7 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, int xw
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
         f32x16 acc[2][1];
-        gemm64<1>(X, xw, Wf, kg, 3 * j + t, acc);
+        gemm64<XS, 1, 4>(X, W, sec, kg, 3 * j + t, acc);
         stage_tile(STG, acc[0][0], acc[1][0], bf[32 * t + r]);
         wave_lds_sync();
         if (t < 2) {
@@ -325,6 +338,7 @@ template <int H, int K, int MODE>
 __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
     constexpr int NT = H / 32;
     constexpr int CTW = (NT + kWaves - 1) / kWaves;
+    constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;  // == lds_layout().xs
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int N = a.N, D = 2 * N;
     const LdsLayout LL = lds_layout(N, H);
@@ -336,7 +350,7 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
     float *STG = (float *)(smem + LL.stg) + wid * kRows * 33;
     float *TL = (float *)(smem + LL.tail);
     float *LDP = (float *)(smem + LL.ld);
-    const int xw = LL.xw, cs = LL.cstride, ts = LL.tstride;
+    const int cs = LL.cstride, ts = LL.tstride;
     const int64_t row0 = (int64_t)blockIdx.x * kRows;
     const bool row_valid = row0 + lane < a.nrows;
 
@@ -377,6 +391,8 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
         const int layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
         const float *P = a.packed + (int64_t)layer * PL.stride;
         const float *V = P + PL.vec;
+        const __amdgpu_buffer_rsrc_t W =
+            __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
         if (MODE != MODE_DENSITY) {
             off = (off + N) % D;  // Coupling.inverse rolls first (coupling.py:113-114)
             ld += uncond_spline<K, true>(P + PL.unc, CO, cs, N, D, off, a, nan_any);
@@ -386,15 +402,15 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
         for (int f = wid; f < N; f += kWaves) {
             const float v = CO[lane * cs + (2 * f + off) % D];
             const float sv = a.scale_pf * v;
-            X[lane * xw + swz(lane, f)] = cosf(sv);
-            X[lane * xw + swz(lane, N + f)] = sinf(sv);
+            X[lane * XS + f] = cosf(sv);
+            X[lane * XS + N + f] = sinf(sv);
         }
-        for (int c = D + wid; c < 8 * PL.kg_in; c += kWaves) X[lane * xw + swz(lane, c)] = 0.f;
+        for (int c = D + wid; c < 8 * PL.kg_in; c += kWaves) X[lane * XS + c] = 0.f;
         __syncthreads();
 
         f32x16 hr[2][CTW], acc[2][CTW];
         if (act) {  // initial_layer
-            gemm64<CTW>(X, xw, (const f32x4 *)(P + PL.win), PL.kg_in, tile0, acc);
+            gemm64<XS, CTW, 3>(X, W, (int)(PL.win * 4), PL.kg_in, tile0, acc);
 #pragma unroll
             for (int ct = 0; ct < CTW; ++ct) {
                 const float bb = V[32 * (tile0 + ct) + r];
@@ -406,8 +422,8 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
         }
         for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
             const float *VB = V + PL.v_blocks + (int64_t)6 * H * jb;
-            const f32x4 *W0 = (const f32x4 *)(P + PL.blocks + jb * PL.block_stride);
-            const f32x4 *W1 = W0 + PL.block_stride / 8;
+            const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4);
+            const int w1 = w0 + (int)(PL.block_stride * 2);
             __syncthreads();
             if (act) {
 #pragma unroll
@@ -419,12 +435,12 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
 #pragma unroll
                         for (int i = 0; i < 16; ++i) {
                             const int R = acc_row(rt, i, h);
-                            X[R * xw + swz(R, col)] = fmaxf(hr[rt][ct][i] * al + be, 0.f);
+                            X[R * XS + col] = fmaxf(hr[rt][ct][i] * al + be, 0.f);
                         }
                 }
             }
             __syncthreads();
-            if (act) gemm64<CTW>(X, xw, W0, PL.kg_h, tile0, acc);
+            if (act) gemm64<XS, CTW, 3>(X, W, w0, PL.kg_h, tile0, acc);
             __syncthreads();
             if (act) {
 #pragma unroll
@@ -436,13 +452,13 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
 #pragma unroll
                         for (int i = 0; i < 16; ++i) {
                             const int R = acc_row(rt, i, h);
-                            X[R * xw + swz(R, col)] = fmaxf((acc[rt][ct][i] + b0) * al + be, 0.f);
+                            X[R * XS + col] = fmaxf((acc[rt][ct][i] + b0) * al + be, 0.f);
                         }
                 }
             }
             __syncthreads();
             if (act) {
-                gemm64<CTW>(X, xw, W1, PL.kg_h, tile0, acc);
+                gemm64<XS, CTW, 3>(X, W, w1, PL.kg_h, tile0, acc);
 #pragma unroll
                 for (int ct = 0; ct < CTW; ++ct) {
                     const float b1 = VB[5 * H + 32 * (tile0 + ct) + r];
@@ -463,7 +479,7 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         const int R = acc_row(rt, i, h);
-                        X[R * xw + swz(R, col)] = hr[rt][ct][i];
+                        X[R * XS + col] = hr[rt][ct][i];
                     }
             }
         }
@@ -471,7 +487,7 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
         // tail block: d_K of every transform feature -> TL[row][feature]
         for (int q = wid; q < PL.ntt; q += kWaves) {
             f32x16 t[2][1];
-            gemm64<1>(X, xw, (const f32x4 *)(P + PL.wt), PL.kg_h, q, t);
+            gemm64<XS, 1, 4>(X, W, (int)(PL.wt * 4), PL.kg_h, q, t);
             const float bt = V[PL.v_bt + 32 * q + r];
 #pragma unroll
             for (int rt = 0; rt < 2; ++rt)
@@ -482,7 +498,7 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
         // final layer + conditional spline, feature by feature
         for (int j = wid; j < N; j += kWaves) {
             const int p = (2 * j + 1 + off) % D;
-            ld += cond_spline<K, MODE != MODE_DENSITY>(X, xw, (const f32x4 *)(P + PL.wf), PL.kg_h,
+            ld += cond_spline<XS, K, MODE != MODE_DENSITY>(X, W, (int)(PL.wf * 4), PL.kg_h,
                                                         V + PL.v_bf + 96 * j, STG, TL, ts, CO, cs, p, j, a,
                                                         nan_any);
         }
@@ -675,6 +691,11 @@ bool fs_flow_supported(const fs_flow_dims *d, char *why, size_t n) {
     if (d->N < 1 || d->N > kMaxN || d->L < 1 || d->nb < 0 || d->K < 1 || d->K > kMaxK || !(d->tail_bound > 0)) {
         snprintf(why, n, "invalid dims N=%d L=%d nb=%d K=%d B=%g (N<=%d, K<=%d)", d->N, d->L, d->nb, d->K,
                  d->tail_bound, kMaxN, kMaxK);
+        return false;
+    }
+    if (2 * d->N > flow_xw(d->H)) {
+        snprintf(why, n, "2N=%d input features exceed the activation tile width %d (H=%d)", 2 * d->N,
+                 flow_xw(d->H), d->H);
         return false;
     }
     if (lds_layout(d->N, d->H).total > 163840) {

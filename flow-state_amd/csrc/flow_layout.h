@@ -89,24 +89,26 @@ FS_HD PackLayout pack_layout(int N, int H, int nb, int K) {
     return p;
 }
 
-// LDS bytes of the flow-pass kernel.
-FS_HD int flow_xw(int N, int H) {  // X row width in floats: holds H hidden or 2N inputs, 16-slot swizzle groups
-    int w = H > 2 * N ? H : 2 * N;
-    return (int)rup(w, 64);
-}
+// X (activation tile) row width in floats: max(H, 2*kMaxN) so that it holds the
+// H hidden units and the 2N <= 128 periodic input features.  Rows are padded by 4 floats (one 16-byte
+// slot): ds_read_b128 A fragments (16 rows x one slot per lane group) and the
+// epilogue's ds_write_b32 (32 consecutive columns of one row) are conflict-free,
+// and every address is base + immediate offset.
+FS_HD int flow_xw(int H) { return H < 2 * kMaxN ? 2 * kMaxN : H; }
 
 struct LdsLayout {
     int x, coord, stg, tail, ld, total;  // byte offsets
-    int xw, cstride, tstride;
+    int xw, xs, cstride, tstride;
 };
 
 FS_HD LdsLayout lds_layout(int N, int H) {
     LdsLayout l;
-    l.xw = flow_xw(N, H);
+    l.xw = flow_xw(H);
+    l.xs = l.xw + 4;
     l.cstride = 2 * N + 1;                 // odd stride: lane-per-row reads are conflict-free
     l.tstride = ((N + 31) / 32) * 32 + 1;
     l.x = 0;
-    l.coord = l.x + kRows * l.xw * 4;
+    l.coord = l.x + kRows * l.xs * 4;
     l.stg = (int)rup(l.coord + kRows * l.cstride * 4, 16);
     l.tail = l.stg + kWaves * kRows * 33 * 4;
     l.ld = (int)rup(l.tail + kRows * l.tstride * 4, 16);
