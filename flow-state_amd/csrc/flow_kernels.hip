@@ -78,32 +78,32 @@ __device__ __forceinline__ void wave_lds_sync() {
 // sinking them next to their use), so PD-1 groups of MFMAs (>= 1024 cycles)
 // cover the L2 latency of every weight fragment at one wave per SIMD.
 // ---------------------------------------------------------------------------
-template <int XS, int CT, int PD>
+template <int XS, int RT, int CT, int PD>
 __device__ __forceinline__ void gemm64(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
-                                       int tile0, f32x16 (&acc)[2][CT]) {
+                                       int rt0, int ct0, f32x16 (&acc)[RT][CT]) {
+    // acc[rt][ct] = X[rows 32*(rt0+rt)..+31][0 : 8*kg] . B[tile ct0+ct]
     // W: buffer descriptor of the layer's packed parameters; sec: byte offset of
     // this GEMM's fragment section (wave-uniform).  32-bit offsets only: no 64-bit
     // pointer per ring slot to keep live.
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, r = lane & 31;
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[rt][ct][i] = 0.f;
-    const float *xa0 = X + r * XS + 4 * h;
-    const float *xa1 = xa0 + 32 * XS;
-    const int voff = (tile0 * kg * 64 + lane) * 16;
+    const float *xa = X + (32 * rt0 + r) * XS + 4 * h;
+    const int voff = (ct0 * kg * 64 + lane) * 16;
     auto ldb = [&](int ct, int g) {
         return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(W, voff, sec + (ct * kg + g) * 1024, 0));
     };
-    f32x4 ra0[PD], ra1[PD], rb[PD][CT];
+    f32x4 ra[PD][RT], rb[PD][CT];
 #pragma unroll
     for (int s = 0; s < PD; ++s) {
         if (s < kg) {
-            ra0[s] = *(const f32x4 *)(xa0 + 8 * s);
-            ra1[s] = *(const f32x4 *)(xa1 + 8 * s);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) ra[s][rt] = *(const f32x4 *)(xa + rt * 32 * XS + 8 * s);
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) rb[s][ct] = ldb(ct, s);
         }
@@ -114,18 +114,18 @@ __device__ __forceinline__ void gemm64(const float *__restrict__ X, __amdgpu_buf
             const int g = g0 + s;
             if (g < kg) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < 4; ++j)
 #pragma unroll
-                    for (int ct = 0; ct < CT; ++ct) {
-                        acc[0][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra0[s][j], rb[s][ct][j], acc[0][ct], 0, 0, 0);
-                        acc[1][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra1[s][j], rb[s][ct][j], acc[1][ct], 0, 0, 0);
-                    }
-                }
+                    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt)
+                            acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[s][rt][j], rb[s][ct][j], acc[rt][ct],
+                                                                              0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
                 const int gn = g + PD;
                 if (gn < kg) {
-                    ra0[s] = *(const f32x4 *)(xa0 + 8 * gn);
-                    ra1[s] = *(const f32x4 *)(xa1 + 8 * gn);
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt) ra[s][rt] = *(const f32x4 *)(xa + rt * 32 * XS + 8 * gn);
 #pragma unroll
                     for (int ct = 0; ct < CT; ++ct) rb[s][ct] = ldb(ct, gn);
                 }
@@ -243,21 +243,42 @@ __device__ __forceinline__ float uncond_spline(const float *__restrict__ U, floa
     return ld;
 }
 
-// Stage one 32-column accumulator tile (64 rows) + column bias into the
-// wave's [64][33] LDS buffer so that lane r can read chain r's row.
-__device__ __forceinline__ void stage_tile(float *STG, const f32x16 &t0, const f32x16 &t1, float bias) {
+// Stage columns [16*half, 16*half+16) of a 32-column accumulator tile (64 rows,
+// + column bias) into the wave's [64][17] LDS buffer: lane r then reads chain
+// r's 16 values (odd stride: conflict-free lane-per-row reads).
+__device__ __forceinline__ void stage_half(float *STG, const f32x16 &t0, const f32x16 &t1, float bias, int half) {
     const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+    if ((r >> 4) == half) {
+        const int c = r & 15;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        STG[acc_row(0, i, h) * 33 + r] = t0[i] + bias;
-        STG[acc_row(1, i, h) * 33 + r] = t1[i] + bias;
+        for (int i = 0; i < 16; ++i) {
+            STG[acc_row(0, i, h) * 17 + c] = t0[i] + bias;
+            STG[acc_row(1, i, h) * 17 + c] = t1[i] + bias;
+        }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void load_logits(float *STG, const f32x16 &t0, const f32x16 &t1, float bias,
+                                            float inv_scale_div, float (&u)[K]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        if (16 * half < K) {
+            stage_half(STG, t0, t1, bias, half);
+            wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (16 * half + k < K) u[16 * half + k] = STG[lane * 17 + k] / inv_scale_div;
+            wave_lds_sync();
+        }
     }
 }
 
 // Final layer + conditional spline of transform feature j for the 64 chains
-// of the wave: three single-tile GEMMs (widths, heights, derivatives), each
-// staged through the wave's LDS transpose buffer right away so that only one
-// 32x64 accumulator pair is live at a time.
+// of the wave (lane = chain): three single-tile GEMMs (widths, heights,
+// derivatives d_0..d_{K-1}; d_K from the tail block TL), each transposed
+// through LDS right away so only one 64x32 accumulator pair is live.
 template <int XS, int K, bool INV>
 __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec,
                                              int kg, const float *__restrict__ bf, float *STG, const float *TL,
@@ -266,21 +287,15 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
     const int lane = threadIdx.x & 63, r = lane & 31;
     float cw[K + 1], ch[K + 1];
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
+    for (int t = 0; t < 2; ++t) {
         f32x16 acc[2][1];
-        gemm64<XS, 1, 4>(X, W, sec, kg, 3 * j + t, acc);
-        stage_tile(STG, acc[0][0], acc[1][0], bf[32 * t + r]);
-        wave_lds_sync();
-        if (t < 2) {
-            float u[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) u[k] = STG[lane * 33 + k] / a.sqrtH;
-            if (t == 0)
-                knots_from_logits<K>(u, cw, kMinW, a.twoB, a.negB, a.B);
-            else
-                knots_from_logits<K>(u, ch, kMinH, a.twoB, a.negB, a.B);
-            wave_lds_sync();
-        }
+        gemm64<XS, 2, 1, 4>(X, W, sec, kg, 0, 3 * j + t, acc);
+        float u[K];
+        load_logits<K>(STG, acc[0][0], acc[1][0], bf[32 * t + r], a.sqrtH, u);
+        if (t == 0)
+            knots_from_logits<K>(u, cw, kMinW, a.twoB, a.negB, a.B);
+        else
+            knots_from_logits<K>(u, ch, kMinH, a.twoB, a.negB, a.B);
     }
     const float x = CO[lane * cs + p];
     const bool inside = (x >= a.negB) && (x <= a.B);
@@ -299,14 +314,28 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
             ch1 = ch[k + 1];
         }
     }
-    const float ud0 = STG[lane * 33 + bin];
-    const float ud1 = (bin + 1 < K) ? STG[lane * 33 + bin + 1] : TL[lane * tstride + j];
+    float ud0 = 0.f, ud1 = TL[lane * tstride + j];  // d_K unless bin + 1 < K
+    {
+        f32x16 acc[2][1];
+        gemm64<XS, 2, 1, 4>(X, W, sec, kg, 0, 3 * j + 2, acc);
+        const float bias = bf[64 + r];
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            if (16 * half < K) {
+                stage_half(STG, acc[0][0], acc[1][0], bias, half);
+                wave_lds_sync();
+                const int b0 = bin - 16 * half, b1 = bin + 1 - 16 * half;
+                if (b0 >= 0 && b0 < 16) ud0 = STG[lane * 17 + b0];
+                if (b1 >= 0 && b1 < 16 && bin + 1 < K) ud1 = STG[lane * 17 + b1];
+                wave_lds_sync();
+            }
+        }
+    }
     const float d0 = kMinD + softplus_t(ud0);
     const float d1 = kMinD + softplus_t(ud1);
     float y, l;
     bool nd;
     rqs_eval<INV>(x, icw, cw1 - icw, ich, ch1 - ich, d0, d1, y, l, nd);
-    wave_lds_sync();  // STG reads done before the next feature restages
     if (inside) {
         CO[lane * cs + p] = y;
         nan_any |= nd;
@@ -335,9 +364,12 @@ __device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
 // The pass kernel (K = spline bins, compile time).
 // ---------------------------------------------------------------------------
 template <int H, int K, int MODE>
-__global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
+__global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
+    // ResNet GEMM work split: NT column tiles x 2 row tiles over the 8 waves
     constexpr int NT = H / 32;
-    constexpr int CTW = (NT + kWaves - 1) / kWaves;
+    constexpr int RT = NT >= kWaves ? 2 : 1;          // row tiles per wave
+    constexpr int CT = NT >= kWaves ? NT / kWaves : 1;  // column tiles per wave
+    constexpr int NU = (2 / RT) * (NT / CT);          // active waves
     constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;  // == lds_layout().xs
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int N = a.N, D = 2 * N;
@@ -347,7 +379,7 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
     const int h = lane >> 5, r = lane & 31;
     float *X = (float *)(smem + LL.x);
     float *CO = (float *)(smem + LL.coord);
-    float *STG = (float *)(smem + LL.stg) + wid * kRows * 33;
+    float *STG = (float *)(smem + LL.stg) + wid * kRows * 17;
     float *TL = (float *)(smem + LL.tail);
     float *LDP = (float *)(smem + LL.ld);
     const int cs = LL.cstride, ts = LL.tstride;
@@ -383,8 +415,9 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
     float ld = 0.f;
     bool nan_any = false;
     int off = 0;
-    const int tile0 = wid * CTW;
-    const bool act = tile0 < NT;
+    const bool act = wid < NU;
+    const int rt0 = (RT == 2) ? 0 : (wid & 1);
+    const int ct0 = (RT == 2) ? wid * CT : (wid >> 1) * CT;
     __syncthreads();
 
     for (int s = 0; s < a.L; ++s) {
@@ -408,14 +441,14 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
         for (int c = D + wid; c < 8 * PL.kg_in; c += kWaves) X[lane * XS + c] = 0.f;
         __syncthreads();
 
-        f32x16 hr[2][CTW], acc[2][CTW];
+        f32x16 hr[RT][CT], acc[RT][CT];
         if (act) {  // initial_layer
-            gemm64<XS, CTW, 3>(X, W, (int)(PL.win * 4), PL.kg_in, tile0, acc);
+            gemm64<XS, RT, CT, 3>(X, W, (int)(PL.win * 4), PL.kg_in, rt0, ct0, acc);
 #pragma unroll
-            for (int ct = 0; ct < CTW; ++ct) {
-                const float bb = V[32 * (tile0 + ct) + r];
+            for (int ct = 0; ct < CT; ++ct) {
+                const float bb = V[32 * (ct0 + ct) + r];
 #pragma unroll
-                for (int rt = 0; rt < 2; ++rt)
+                for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                     for (int i = 0; i < 16; ++i) hr[rt][ct][i] = acc[rt][ct][i] + bb;
             }
@@ -427,43 +460,43 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
             __syncthreads();
             if (act) {
 #pragma unroll
-                for (int ct = 0; ct < CTW; ++ct) {
-                    const int col = 32 * (tile0 + ct) + r;
+                for (int ct = 0; ct < CT; ++ct) {
+                    const int col = 32 * (ct0 + ct) + r;
                     const float al = VB[col], be = VB[H + col];
 #pragma unroll
-                    for (int rt = 0; rt < 2; ++rt)
+                    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                         for (int i = 0; i < 16; ++i) {
-                            const int R = acc_row(rt, i, h);
+                            const int R = acc_row(rt0 + rt, i, h);
                             X[R * XS + col] = fmaxf(hr[rt][ct][i] * al + be, 0.f);
                         }
                 }
             }
             __syncthreads();
-            if (act) gemm64<XS, CTW, 3>(X, W, w0, PL.kg_h, tile0, acc);
+            if (act) gemm64<XS, RT, CT, 3>(X, W, w0, PL.kg_h, rt0, ct0, acc);
             __syncthreads();
             if (act) {
 #pragma unroll
-                for (int ct = 0; ct < CTW; ++ct) {
-                    const int col = 32 * (tile0 + ct) + r;
+                for (int ct = 0; ct < CT; ++ct) {
+                    const int col = 32 * (ct0 + ct) + r;
                     const float b0 = VB[2 * H + col], al = VB[3 * H + col], be = VB[4 * H + col];
 #pragma unroll
-                    for (int rt = 0; rt < 2; ++rt)
+                    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                         for (int i = 0; i < 16; ++i) {
-                            const int R = acc_row(rt, i, h);
+                            const int R = acc_row(rt0 + rt, i, h);
                             X[R * XS + col] = fmaxf((acc[rt][ct][i] + b0) * al + be, 0.f);
                         }
                 }
             }
             __syncthreads();
             if (act) {
-                gemm64<XS, CTW, 3>(X, W, w1, PL.kg_h, tile0, acc);
+                gemm64<XS, RT, CT, 3>(X, W, w1, PL.kg_h, rt0, ct0, acc);
 #pragma unroll
-                for (int ct = 0; ct < CTW; ++ct) {
-                    const float b1 = VB[5 * H + 32 * (tile0 + ct) + r];
+                for (int ct = 0; ct < CT; ++ct) {
+                    const float b1 = VB[5 * H + 32 * (ct0 + ct) + r];
 #pragma unroll
-                    for (int rt = 0; rt < 2; ++rt)
+                    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                         for (int i = 0; i < 16; ++i) hr[rt][ct][i] = hr[rt][ct][i] + (acc[rt][ct][i] + b1);
                 }
@@ -472,13 +505,13 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
         __syncthreads();
         if (act) {  // X <- h for the final layer
 #pragma unroll
-            for (int ct = 0; ct < CTW; ++ct) {
-                const int col = 32 * (tile0 + ct) + r;
+            for (int ct = 0; ct < CT; ++ct) {
+                const int col = 32 * (ct0 + ct) + r;
 #pragma unroll
-                for (int rt = 0; rt < 2; ++rt)
+                for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
-                        const int R = acc_row(rt, i, h);
+                        const int R = acc_row(rt0 + rt, i, h);
                         X[R * XS + col] = hr[rt][ct][i];
                     }
             }
@@ -487,7 +520,7 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
         // tail block: d_K of every transform feature -> TL[row][feature]
         for (int q = wid; q < PL.ntt; q += kWaves) {
             f32x16 t[2][1];
-            gemm64<XS, 1, 4>(X, W, (int)(PL.wt * 4), PL.kg_h, q, t);
+            gemm64<XS, 2, 1, 4>(X, W, (int)(PL.wt * 4), PL.kg_h, 0, q, t);
             const float bt = V[PL.v_bt + 32 * q + r];
 #pragma unroll
             for (int rt = 0; rt < 2; ++rt)
@@ -514,7 +547,9 @@ __global__ void __launch_bounds__(kThreads, 1) flow_pass_kernel(FlowArgs a) {
     if (nan_any && row_valid && a.err) atomicOr(a.err, 1);
     __syncthreads();
     if (wid == 0) {
-        const float tot = ((LDP[lane] + LDP[kRows + lane]) + LDP[2 * kRows + lane]) + LDP[3 * kRows + lane];
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) tot += LDP[w * kRows + lane];
         float outv = tot;
         if (MODE == MODE_DENSITY && a.add_base) {
             bool inb = true;

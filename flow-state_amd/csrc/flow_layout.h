@@ -15,7 +15,7 @@
 namespace fs {
 
 constexpr int kRows = 64;     // chains per workgroup (= lanes of a wave: lane-per-chain spline)
-constexpr int kWaves = 4;     // waves per workgroup
+constexpr int kWaves = 8;     // waves per workgroup (2 per SIMD: one wave's VALU hides under the other's MFMAs)
 constexpr int kThreads = kRows * kWaves;
 constexpr int kMaxN = 64;     // particles (energy kernel: lane-per-particle, nbr mask in one u64)
 constexpr int kMaxK = 32;     // spline bins (one 32-column MFMA tile per parameter group)
@@ -110,7 +110,7 @@ FS_HD LdsLayout lds_layout(int N, int H) {
     l.x = 0;
     l.coord = l.x + kRows * l.xs * 4;
     l.stg = (int)rup(l.coord + kRows * l.cstride * 4, 16);
-    l.tail = l.stg + kWaves * kRows * 33 * 4;
+    l.tail = l.stg + kWaves * kRows * 17 * 4;  // per-wave [64][17] half-tile transpose buffer
     l.ld = (int)rup(l.tail + kRows * l.tstride * 4, 16);
     l.total = l.ld + kWaves * kRows * 4 + 16;
     return l;
