@@ -16,7 +16,6 @@ Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -31,6 +30,7 @@ for _p in (REPO, os.path.join(REPO, "flow-state_amd")):
 
 from flowstate import _lib  # noqa: E402
 from flowstate.MCMC import BatchedMonteCarlo, Physics, initialise_fcc  # noqa: E402
+from flowstate import parallel  # noqa: E402
 from flowstate.models import A1, build_flow, half_box  # noqa: E402
 
 PEAK_F32_TFLOPS = 157.3  # MI355X dense FP32 (MFMA = vector rate), MI355X_MICROARCH.md
@@ -186,12 +186,11 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     N, C = args.particles, args.chains
-    c0 = rank * C
+    c0, seeds = parallel.shard(C, rank)
     model = synthetic_model(N, dev)
     init, L = synthetic_states(N, C, c0)
     phys = Physics(L, L, temperature=1.0, num_wells=2, V0_list=(-10.0, -10.5), r0=1.2, k=15)
-    bmc = BatchedMonteCarlo(model, init, phys, np.arange(42 + c0, 42 + c0 + C, dtype=np.uint64), device=dev,
-                            chain_offset=c0)
+    bmc = BatchedMonteCarlo(model, init, phys, seeds, device=dev, chain_offset=c0)
     stepper = Stepper(bmc)
     for _ in range(args.warmup):
         stepper.step(timed=False)
@@ -206,9 +205,7 @@ def main():
     # final reduction: density histogram + well occupancy of the current states
     hist = bmc.histogram2d(100)
     wells = bmc.well_counts().sum(dim=0)
-    if dist:
-        dist.all_reduce(hist)
-        dist.all_reduce(wells)
+    parallel.all_reduce_stats(hist, wells)
     torch.cuda.synchronize()
     stepper.harvest()
     if dist:
@@ -245,6 +242,8 @@ def main():
                    "particles": N, "chains_per_gpu": C, "flow": "A1: L=15 H=256 blocks=32 K=32",
                    "parallelism": f"dp{world} (chains sharded, RCCL all-reduce of final histogram)"},
         "acceptance_rate": n_acc.item() / total_steps,
+        "final_stats": {"hist_total": int(hist.sum().item()), "all_in_A": int(wells[0].item()),
+                        "all_in_B": int(wells[1].item()), "chains": int(wells[2].item())},
         "kernel_ms": {"flow_propose": t_prop, "flow_log_prob": t_lp, "energy": t_en, "mh_accept": t_acc},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_F32_TFLOPS, "traffic": None,
