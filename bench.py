@@ -118,6 +118,19 @@ class Stepper:
         self.events = []
 
 
+def _pmc_traffic():
+    """HBM bytes per flow-pass launch from the committed rocprofv3 PMC passes
+    (FETCH_SIZE x2 per the gfx950 calibration + WRITE_SIZE, tools/pmc_traffic.py);
+    None if no profile of the current build has been recorded."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t.get("flow_pass_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(N, budget_s=15.0):
     """The oracle's restatement of the reference CPU path, per chain, on the host
     cores: proposals generated in a batch (as main_algorithm_1.py:340-343 does)
@@ -172,18 +185,24 @@ def main():
     ap.add_argument("--particles", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    local = local % max(1, ndev)  # rehearsal with more ranks than GPUs (gloo) shares devices
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     N, C = args.particles, args.chains
     c0, seeds = parallel.shard(C, rank)
@@ -246,7 +265,7 @@ def main():
                         "all_in_B": int(wells[1].item()), "chains": int(wells[2].item())},
         "kernel_ms": {"flow_propose": t_prop, "flow_log_prob": t_lp, "energy": t_en, "mh_accept": t_acc},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_F32_TFLOPS, "traffic": None,
+                     "frac": achieved / PEAK_F32_TFLOPS, "traffic": _pmc_traffic(),
                      "kernel": "flow_pass_kernel<256,32,*> (propose + log_prob)",
                      "algorithmic_flop_per_launch": fpp * C},
     }

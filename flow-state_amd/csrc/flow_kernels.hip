@@ -78,13 +78,37 @@ __device__ __forceinline__ void wave_lds_sync() {
 // sinking them next to their use), so PD-1 groups of MFMAs (>= 1024 cycles)
 // cover the L2 latency of every weight fragment at one wave per SIMD.
 // ---------------------------------------------------------------------------
+// B-operand ring: weight fragments of k-groups 0..PD-1 can be issued BEFORE the
+// barrier that precedes a GEMM (they do not depend on the activation tile),
+// so their L2 latency overlaps the epilogue of the previous GEMM.
+template <int CT, int PD>
+struct BRing {
+    f32x4 rb[PD][CT];
+};
+
+__device__ __forceinline__ f32x4 ldb_frag(__amdgpu_buffer_rsrc_t W, int voff, int soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(W, voff, soff, 0));
+}
+
+template <int CT, int PD>
+__device__ __forceinline__ void b_prologue(BRing<CT, PD> &br, __amdgpu_buffer_rsrc_t W, int sec, int kg, int ct0) {
+    const int voff = (ct0 * kg * 64 + (int)(threadIdx.x & 63)) * 16;
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+        if (s < kg)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) br.rb[s][ct] = ldb_frag(W, voff, sec + (ct * kg + s) * 1024);
+}
+
+// acc[rt][ct] = X[rows 32*(rt0+rt)..+31][0 : 8*kg] . B[tile ct0+ct]
+// W: buffer descriptor of the layer's packed parameters; sec: byte offset of
+// this GEMM's fragment section (wave-uniform).  32-bit offsets only: no 64-bit
+// pointer per ring slot to keep live.  Operands of k-group g live in ring slot
+// g % PD; the loads of group g+PD are issued right after the MFMAs of group g
+// (sched_barrier keeps hipcc from sinking them next to their use).
 template <int XS, int RT, int CT, int PD>
-__device__ __forceinline__ void gemm64(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
-                                       int rt0, int ct0, f32x16 (&acc)[RT][CT]) {
-    // acc[rt][ct] = X[rows 32*(rt0+rt)..+31][0 : 8*kg] . B[tile ct0+ct]
-    // W: buffer descriptor of the layer's packed parameters; sec: byte offset of
-    // this GEMM's fragment section (wave-uniform).  32-bit offsets only: no 64-bit
-    // pointer per ring slot to keep live.
+__device__ __forceinline__ void gemm_run(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
+                                         int rt0, int ct0, BRing<CT, PD> &br, f32x16 (&acc)[RT][CT]) {
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, r = lane & 31;
 #pragma unroll
@@ -95,19 +119,12 @@ __device__ __forceinline__ void gemm64(const float *__restrict__ X, __amdgpu_buf
             for (int i = 0; i < 16; ++i) acc[rt][ct][i] = 0.f;
     const float *xa = X + (32 * rt0 + r) * XS + 4 * h;
     const int voff = (ct0 * kg * 64 + lane) * 16;
-    auto ldb = [&](int ct, int g) {
-        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(W, voff, sec + (ct * kg + g) * 1024, 0));
-    };
-    f32x4 ra[PD][RT], rb[PD][CT];
+    f32x4 ra[PD][RT];
 #pragma unroll
-    for (int s = 0; s < PD; ++s) {
-        if (s < kg) {
+    for (int s = 0; s < PD; ++s)
+        if (s < kg)
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) ra[s][rt] = *(const f32x4 *)(xa + rt * 32 * XS + 8 * s);
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) rb[s][ct] = ldb(ct, s);
-        }
-    }
     for (int g0 = 0; g0 < kg; g0 += PD) {
 #pragma unroll
         for (int s = 0; s < PD; ++s) {
@@ -119,20 +136,28 @@ __device__ __forceinline__ void gemm64(const float *__restrict__ X, __amdgpu_buf
                     for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
                         for (int rt = 0; rt < RT; ++rt)
-                            acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[s][rt][j], rb[s][ct][j], acc[rt][ct],
-                                                                              0, 0, 0);
+                            acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[s][rt][j], br.rb[s][ct][j],
+                                                                              acc[rt][ct], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
                 const int gn = g + PD;
                 if (gn < kg) {
 #pragma unroll
                     for (int rt = 0; rt < RT; ++rt) ra[s][rt] = *(const f32x4 *)(xa + rt * 32 * XS + 8 * gn);
 #pragma unroll
-                    for (int ct = 0; ct < CT; ++ct) rb[s][ct] = ldb(ct, gn);
+                    for (int ct = 0; ct < CT; ++ct) br.rb[s][ct] = ldb_frag(W, voff, sec + (ct * kg + gn) * 1024);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
     }
+}
+
+template <int XS, int RT, int CT, int PD>
+__device__ __forceinline__ void gemm64(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
+                                       int rt0, int ct0, f32x16 (&acc)[RT][CT]) {
+    BRing<CT, PD> br;
+    b_prologue<CT, PD>(br, W, sec, kg, ct0);
+    gemm_run<XS, RT, CT, PD>(X, W, sec, kg, rt0, ct0, br, acc);
 }
 
 // accumulator element i of tile rt -> row
@@ -453,53 +478,61 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
                     for (int i = 0; i < 16; ++i) hr[rt][ct][i] = acc[rt][ct][i] + bb;
             }
         }
+        BRing<CT, 3> br;
+        if (act && a.nb > 0) b_prologue<CT, 3>(br, W, (int)(PL.blocks * 4), PL.kg_h, ct0);
         for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
             const float *VB = V + PL.v_blocks + (int64_t)6 * H * jb;
             const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4);
             const int w1 = w0 + (int)(PL.block_stride * 2);
+            // this block's per-column epilogue vectors, loaded ahead of the barriers
+            float ev[6][CT];
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) ev[q][ct] = VB[q * H + 32 * (ct0 + ct) + r];
             __syncthreads();
             if (act) {
 #pragma unroll
                 for (int ct = 0; ct < CT; ++ct) {
                     const int col = 32 * (ct0 + ct) + r;
-                    const float al = VB[col], be = VB[H + col];
 #pragma unroll
                     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                         for (int i = 0; i < 16; ++i) {
                             const int R = acc_row(rt0 + rt, i, h);
-                            X[R * XS + col] = fmaxf(hr[rt][ct][i] * al + be, 0.f);
+                            X[R * XS + col] = fmaxf(hr[rt][ct][i] * ev[0][ct] + ev[1][ct], 0.f);
                         }
                 }
             }
             __syncthreads();
-            if (act) gemm64<XS, RT, CT, 3>(X, W, w0, PL.kg_h, rt0, ct0, acc);
+            if (act) {
+                gemm_run<XS, RT, CT, 3>(X, W, w0, PL.kg_h, rt0, ct0, br, acc);
+                b_prologue<CT, 3>(br, W, w1, PL.kg_h, ct0);  // next GEMM's first weight groups
+            }
             __syncthreads();
             if (act) {
 #pragma unroll
                 for (int ct = 0; ct < CT; ++ct) {
                     const int col = 32 * (ct0 + ct) + r;
-                    const float b0 = VB[2 * H + col], al = VB[3 * H + col], be = VB[4 * H + col];
 #pragma unroll
                     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                         for (int i = 0; i < 16; ++i) {
                             const int R = acc_row(rt0 + rt, i, h);
-                            X[R * XS + col] = fmaxf((acc[rt][ct][i] + b0) * al + be, 0.f);
+                            X[R * XS + col] = fmaxf((acc[rt][ct][i] + ev[2][ct]) * ev[3][ct] + ev[4][ct], 0.f);
                         }
                 }
             }
             __syncthreads();
             if (act) {
-                gemm64<XS, RT, CT, 3>(X, W, w1, PL.kg_h, rt0, ct0, acc);
+                gemm_run<XS, RT, CT, 3>(X, W, w1, PL.kg_h, rt0, ct0, br, acc);
+                if (jb + 1 < a.nb) b_prologue<CT, 3>(br, W, w1 + (int)(PL.block_stride * 2), PL.kg_h, ct0);
 #pragma unroll
-                for (int ct = 0; ct < CT; ++ct) {
-                    const float b1 = VB[5 * H + 32 * (ct0 + ct) + r];
+                for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
                     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                        for (int i = 0; i < 16; ++i) hr[rt][ct][i] = hr[rt][ct][i] + (acc[rt][ct][i] + b1);
-                }
+                        for (int i = 0; i < 16; ++i) hr[rt][ct][i] = hr[rt][ct][i] + (acc[rt][ct][i] + ev[5][ct]);
             }
         }
         __syncthreads();
