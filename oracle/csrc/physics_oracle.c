@@ -316,3 +316,162 @@ void oracle_mh_accept(long C, const double *E_old, const double *E_new, const do
         if (u_out) u_out[c] = u;
     }
 }
+
+/* ------------------------------------------------------------------ */
+/* Local moves: MonteCarlo.particle_displacement (monte_carlo.py:146-189),  */
+/* metropolis_acceptance_particle_move (:191-223), adjust_displacement     */
+/* (:375-403), EnergyCalculator.calculate_particle_energy_virial           */
+/* (energy_calculator.py:48-108).  RNG state per chain: u64[6] =           */
+/* {state_hi, state_lo, inc_hi, inc_lo, has_uint32, uinteger} (numpy       */
+/* PCG64 keeps a 32-bit half buffered for next_uint32).                    */
+/* ------------------------------------------------------------------ */
+static uint64_t pcg_next64(uint64_t s[6])
+{
+    const u128 mult = ((u128)0x2360ED051FC65DA4ull << 64) | 0x4385DF649FCCF645ull;
+    u128 st = ((u128)s[0] << 64) | s[1];
+    u128 inc = ((u128)s[2] << 64) | s[3];
+    st = st * mult + inc;
+    s[0] = (uint64_t)(st >> 64);
+    s[1] = (uint64_t)st;
+    uint64_t x = s[0] ^ s[1];
+    unsigned rot = (unsigned)(s[0] >> 58);
+    return (x >> rot) | (x << ((64 - rot) & 63));
+}
+
+static double pcg_double(uint64_t s[6]) { return (double)(pcg_next64(s) >> 11) * (1.0 / 9007199254740992.0); }
+
+static uint32_t pcg_next32(uint64_t s[6])  /* pcg64_next32 */
+{
+    if (s[4]) {
+        s[4] = 0;
+        return (uint32_t)s[5];
+    }
+    uint64_t v = pcg_next64(s);
+    s[4] = 1;
+    s[5] = v >> 32;
+    return (uint32_t)(v & 0xffffffffu);
+}
+
+/* Generator.integers(n) for 1 <= n <= 2^32: random_bounded_uint64_fill ->
+ * buffered_bounded_lemire_uint32 (numpy/random/src/distributions) */
+static int64_t pcg_integers(uint64_t s[6], uint64_t n)
+{
+    uint32_t rng = (uint32_t)(n - 1);
+    if (rng == 0) return 0;
+    if (rng == 0xFFFFFFFFu) return pcg_next32(s);
+    uint32_t rng_excl = rng + 1;
+    uint64_t m = (uint64_t)pcg_next32(s) * rng_excl;
+    uint32_t leftover = (uint32_t)m;
+    if (leftover < rng_excl) {
+        uint32_t threshold = (UINT32_MAX - rng) % rng_excl;
+        while (leftover < threshold) {
+            m = (uint64_t)pcg_next32(s) * rng_excl;
+            leftover = (uint32_t)m;
+        }
+    }
+    return (int64_t)(m >> 32);
+}
+
+int64_t oracle_pcg64_integers(uint64_t s[6], uint64_t n) { return pcg_integers(s, n); }
+double oracle_pcg64_double6(uint64_t s[6]) { return pcg_double(s); }
+
+/* numpy floor remainder (npy_divmod): fmod, sign-adjusted toward the divisor */
+static double np_remainder(double a, double b)
+{
+    double mod = fmod(a, b);
+    if (mod != 0.0) {
+        if ((b < 0) != (mod < 0)) mod += b;
+    } else {
+        mod = copysign(0.0, b);
+    }
+    return mod;
+}
+
+/* calculate_particle_energy_virial for particle p; positions as doubles holding
+ * the reference dtype's values.  Returns 1 on the hard core (E = W = inf). */
+static int particle_energy(const double *xy, int f32, int N, int p, const oracle_phys *ph, double *E, double *W)
+{
+    double e_row[4096], w_row[4096];
+    double sr6c = pow(1.0 / ph->r_cut, 6.0);
+    double e_cut = 4.0 * (sr6c * sr6c - sr6c);
+    int n = 0, hit = 0;
+    for (int j = 0; j < N; j++) {
+        if (j == p) continue;
+        double r = f32 ? min_image_dist_f32((float)xy[2 * p], (float)xy[2 * p + 1], (float)xy[2 * j],
+                                            (float)xy[2 * j + 1], ph->Lx, ph->Ly)
+                       : min_image_dist_f64(xy[2 * p], xy[2 * p + 1], xy[2 * j], xy[2 * j + 1], ph->Lx, ph->Ly);
+        if (r < ph->r_core) hit = 1;
+        lj_pair(r, ph->r_cut, e_cut, &e_row[n], &w_row[n]);
+        n++;
+    }
+    if (hit) {
+        *E = INFINITY;
+        *W = INFINITY;
+        return 1;
+    }
+    double e = pairwise_sum(e_row, n), w = pairwise_sum(w_row, n);
+    if (ph->num_wells > 0) e += dw_particle(xy[2 * p], xy[2 * p + 1], ph);
+    *E = e;
+    *W = w;
+    return 0;
+}
+
+/* One chain, n_moves local moves.  xy: (N,2) as doubles (float32 values when
+ * f32); E/W: running totals; counters: attempts/accepted; every adjust_every
+ * moves (0 = never) adjust_displacement with prev_* bookkeeping.
+ * accept_log (nullable): per-move 0/1. */
+void oracle_local_moves(double *xy, int f32, int N, const oracle_phys *ph, double beta, uint64_t s[6],
+                        double *max_disp, double target_acc, double *E, double *W, int64_t *attempts,
+                        int64_t *accepted, int64_t *prev_att, int64_t *prev_acc, int n_moves, int adjust_every,
+                        int adjust_phase, int8_t *accept_log)
+{
+    for (int t = 0; t < n_moves; t++) {
+        *attempts += 1;
+        int p = (int)pcg_integers(s, (uint64_t)N);
+        double eno, viro, enn, virn;
+        particle_energy(xy, f32, N, p, ph, &eno, &viro);
+        double u0 = pcg_double(s), u1 = pcg_double(s);
+        double d0 = (u0 - 0.5) * *max_disp, d1 = (u1 - 0.5) * *max_disp;
+        double ox = xy[2 * p], oy = xy[2 * p + 1];
+        double nx, ny;
+        if (f32) {
+            float fx = (float)(ox + d0), fy = (float)(oy + d1);            /* f32 row += f64 array */
+            nx = (double)(float)np_remainder((double)fx, ph->Lx);         /* f32 % f64 -> f64 -> f32 */
+            ny = (double)(float)np_remainder((double)fy, ph->Ly);
+        } else {
+            nx = np_remainder(ox + d0, ph->Lx);
+            ny = np_remainder(oy + d1, ph->Ly);
+        }
+        xy[2 * p] = nx;
+        xy[2 * p + 1] = ny;
+        particle_energy(xy, f32, N, p, ph, &enn, &virn);
+        double dE = enn - eno, dW = virn - viro;
+        int acc;
+        if (enn <= eno) acc = 1;
+        else if (isinf(enn)) acc = 0;
+        else acc = pcg_double(s) < exp(-beta * (enn - eno));
+        if (acc) {
+            *accepted += 1;
+            *E += dE;
+            *W += dW;
+        } else {
+            xy[2 * p] = ox;
+            xy[2 * p + 1] = oy;
+        }
+        if (accept_log) accept_log[t] = (int8_t)acc;
+        if (adjust_every > 0 && (t + 1 + adjust_phase) % adjust_every == 0) {
+            if (*attempts > *prev_att) {
+                int64_t da = *attempts - *prev_att, dc = *accepted - *prev_acc;
+                double frac = da > 0 ? (double)dc / (double)da : 0.0;
+                double factor = frac / target_acc;
+                double nm = *max_disp * factor;
+                double ratio = nm / *max_disp;
+                if (ratio > 1.5) nm = *max_disp * 1.5;
+                else if (ratio < 0.5) nm = *max_disp * 0.5;
+                *max_disp = nm;
+                *prev_att = *attempts;
+                *prev_acc = *accepted;
+            }
+        }
+    }
+}

@@ -72,6 +72,16 @@ def lib():
         L.oracle_mh_accept.argtypes = [
             ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_double, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_local_moves.restype = None
+        L.oracle_local_moves.argtypes = [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(Phys), ctypes.c_double,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+            ctypes.c_int, ctypes.c_void_p]
+        L.oracle_pcg64_double6.restype = ctypes.c_double
+        L.oracle_pcg64_double6.argtypes = [ctypes.c_void_p]
+        L.oracle_pcg64_integers.restype = ctypes.c_int64
+        L.oracle_pcg64_integers.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         L.oracle_pairwise_sum.restype = ctypes.c_double
         L.oracle_pairwise_sum.argtypes = [ctypes.c_void_p, ctypes.c_long]
         _lib = L
@@ -147,6 +157,73 @@ def mh_accept(E_old, E_new, nll_old, nll_new, pcg, beta=1.0, correct_sign=False)
     lib().oracle_mh_accept(C, _ptr(E_old), _ptr(E_new), _ptr(nll_old), _ptr(nll_new), beta,
                            _ptr(pcg), int(bool(correct_sign)), _ptr(acc), _ptr(u))
     return acc, u
+
+
+class LocalChain:
+    """One chain's local-move state, as MonteCarlo holds it (monte_carlo.py:60-95):
+    particles (float64, or float32 after an accepted big move), the running
+    total energy / virial, max_displacement, the attempt/accept counters and
+    their adjust_displacement snapshots, and the numpy PCG64 state including the
+    buffered 32-bit half (u64[6])."""
+
+    def __init__(self, particles, seed, phys, E=None, W=None, max_disp=0.65, target=0.5, beta=1.0):
+        self.xy = np.array(particles, np.float64)
+        self.f32 = np.asarray(particles).dtype == np.float32
+        self.phys, self.beta, self.target = phys, beta, target
+        self.pcg = np.zeros(6, np.uint64)
+        self.pcg[:4] = pcg64_seed(seed)
+        if E is None:
+            E, W, _ = total_energy(np.asarray(particles), phys)
+        self.E = np.array([E], np.float64)
+        self.W = np.array([W], np.float64)
+        self.max_disp = np.array([max_disp], np.float64)
+        self.cnt = np.zeros(4, np.int64)   # attempts, accepted, prev_attempts, prev_accepted
+
+    @property
+    def particles(self):
+        return self.xy.astype(np.float32) if self.f32 else self.xy.copy()
+
+    def local_moves(self, n, adjust_every=0, phase=0):
+        """n particle_displacement calls (monte_carlo.py:146-189), with
+        adjust_displacement (:375-403) after every adjust_every-th; returns the
+        per-move accept flags."""
+        log = np.zeros(n, np.int8)
+        c = self.cnt
+        lib().oracle_local_moves(_ptr(self.xy), int(self.f32), self.xy.shape[0], ctypes.byref(self.phys),
+                                 self.beta, _ptr(self.pcg), _ptr(self.max_disp), self.target, _ptr(self.E),
+                                 _ptr(self.W), _ptr(c[0:]), _ptr(c[1:]), _ptr(c[2:]), _ptr(c[3:]), n,
+                                 adjust_every, phase, _ptr(log))
+        return log
+
+    def big_move(self, cfg, nll_old, nll_new, correct_sign=False):
+        """nf_big_move (monte_carlo.py:235-301) given both NLLs: the attempt counts
+        as a displacement attempt (:240); on reject the total energy is recomputed
+        from the current particles (:299-301), replacing the running sum."""
+        self.cnt[0] += 1
+        cfg = np.asarray(cfg, np.float32)
+        En, Wn, _ = total_energy(cfg, self.phys)
+        pcg4 = self.pcg[None, :4].copy()   # random() never touches the 32-bit buffer
+        acc, _ = mh_accept(self.E, np.array([En]), np.array([nll_old]), np.array([nll_new]), pcg4,
+                           self.beta, correct_sign)
+        self.pcg[:4] = pcg4[0]
+        if acc[0]:
+            self.xy = cfg.astype(np.float64)
+            self.f32 = True
+            self.cnt[1] += 1
+            self.E[0], self.W[0] = En, Wn
+        else:
+            self.E[0], self.W[0], _ = total_energy(self.particles, self.phys)
+        return bool(acc[0])
+
+
+def pcg64_integers(state6, n):
+    """Generator.integers(n) (buffered 32-bit Lemire) on a u64[6] state."""
+    return int(lib().oracle_pcg64_integers(_ptr(state6), int(n)))
+
+
+def pcg64_random6(state6):
+    """Generator.random() on a u64[6] state."""
+    return float(lib().oracle_pcg64_double6(_ptr(state6)))
 
 
 def pairwise_sum(a):

@@ -262,6 +262,73 @@ def init_case(NF):
     print("init: ok")
 
 
+def local_case(NF, MC):
+    """Reference local-move traces (monte_carlo.py:146-223, 375-403): float64
+    state, then one accepted big move (state -> float32), then float32 local
+    moves; adjust_displacement every 50 moves (with the big move counted in the
+    displacement counters, monte_carlo.py:240)."""
+    from oracle import flow as OF
+    out = {}
+    for N, chains, moves in ((3, 2, 200), (16, 3, 300), (64, 2, 200)):
+        dims = OF.FlowDims(N=N, L=1, H=32, nb=1, K=5, B=OF.half_box(N))
+        sd = OF.random_state_dict(dims, seed=77)
+        model = build_ref_model(NF, dims)
+        model.load_state_dict(sd, strict=True)
+        model.eval()
+        for c in range(chains):
+            with contextlib.redirect_stdout(io.StringIO()):
+                if N > 12:
+                    particles, box = MC.initialise_fcc(num_particles=N, rho=0.03, aspect_ratio=1.0)
+                else:
+                    particles, box = MC.initialise_low_left(num_particles=N, rho=0.03, aspect_ratio=1.0,
+                                                            visualise=False, checking=False)
+                mc = MC.MonteCarlo(particles=particles, sim_box=box, temperature=1.0, num_particles=N,
+                                   num_wells=2, V0_list=[-10.0, -10.5], r0=1.2, k=15,
+                                   initial_max_displacement=0.65, target_acceptance=0.5, timing=False,
+                                   checking=False, logger=None, seed=42 + c, device=torch.device("cpu"))
+                mc.set_nf_model(model)
+            key = f"N{N}_c{c}"
+            out[key + "_init"] = np.asarray(particles, np.float64)
+            acc, E, W, mdisp = [], [], [], []
+            big = []
+            for phase in range(2):
+                for t in range(moves):
+                    a0 = mc.accepted_displacement
+                    with contextlib.redirect_stdout(io.StringIO()):
+                        mc.particle_displacement()
+                        if (t + 1) % 50 == 0:
+                            mc.adjust_displacement()
+                    acc.append(mc.accepted_displacement - a0)
+                    E.append(mc.energy_calculator.total_energy)
+                    W.append(mc.energy_calculator.total_virial)
+                    mdisp.append(mc.max_displacement)
+                if phase == 0:
+                    # a big move to (nearly) the current state as float32: the state becomes float32
+                    cfg = np.asarray(mc.particles, np.float32)
+                    with contextlib.redirect_stdout(io.StringIO()):
+                        big.append(bool(mc.nf_big_move(cfg)))
+                    out[key + "_bigcfg"] = cfg
+            st = mc.rng.bit_generator.state
+            out[key + "_accept"] = np.array(acc, np.int8)
+            out[key + "_E"] = np.array(E)
+            out[key + "_W"] = np.array(W)
+            out[key + "_maxdisp"] = np.array(mdisp)
+            out[key + "_big"] = np.array(big)
+            out[key + "_final"] = np.asarray(mc.particles)
+            out[key + "_final_dtype32"] = np.int8(np.asarray(mc.particles).dtype == np.float32)
+            out[key + "_attempts"] = np.int64(mc.attempts_displacement)
+            out[key + "_accepted"] = np.int64(mc.accepted_displacement)
+            s_ = st["state"]
+            out[key + "_pcg"] = np.array([s_["state"] >> 64, s_["state"] & (2**64 - 1), s_["inc"] >> 64,
+                                          s_["inc"] & (2**64 - 1), st["has_uint32"], st["uinteger"]], np.uint64)
+            out[key + "_seed"] = np.int64(42 + c)
+            print(f"local {key}: accepted {sum(acc)}/{2 * moves}, big {big}, maxdisp {mc.max_displacement:.4f}")
+        out[f"N{N}_chains"] = np.int64(chains)
+        out[f"N{N}_moves"] = np.int64(moves)
+        out[f"N{N}_flow_seed"] = np.int64(77)
+    np.savez_compressed(os.path.join(HERE, "local_trace.npz"), **out)
+
+
 def pcg_case():
     seeds = np.arange(42, 42 + 64)
     st = np.zeros((64, 4), np.uint64)
@@ -287,6 +354,7 @@ def main():
     mh_trace_case(NF, MC, SimulationBox)
     pcg_case()
     init_case(NF)
+    local_case(NF, MC)
 
 
 if __name__ == "__main__":
