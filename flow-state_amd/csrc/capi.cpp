@@ -148,7 +148,8 @@ int64_t fs_nf_mh_step_ws_bytes(const fs_flow_dims *d, int64_t C) {
     if (check_dims(d) != FS_OK || C < 0) return -1;
     const int64_t D = 2 * d->N;
     // config f32 [C][D] | centered f32 [C][D] | log_q f32 [C] | E_new f64 [C] | W_new f64 [C]
-    return fs::rup(C * D * 4, 256) * 2 + fs::rup(C * 4, 256) + fs::rup(C * 8, 256) * 2;
+    // | (FS_MH_HYBRID) centered_old f32 [C][D] | log_q_old f32 [C] | E_cur f64 [C] | W_cur f64 [C]
+    return (fs::rup(C * D * 4, 256) * 2 + fs::rup(C * 4, 256) + fs::rup(C * 8, 256) * 2) * 2;
 }
 
 int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C, uint64_t seed,
@@ -170,8 +171,18 @@ int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, i
     double *E_new = (double *)w;
     w += fs::rup(C * 8, 256);
     double *W_new = (double *)w;
+    w += fs::rup(C * 8, 256);
+    float *centered_old = (float *)w;
+    w += fs::rup(C * D * 4, 256);
+    float *log_q_old = (float *)w;
+    w += fs::rup(C * 4, 256);
+    double *E_cur = (double *)w;
+    w += fs::rup(C * 8, 256);
+    double *W_cur = (double *)w;
     hipStream_t st = (hipStream_t)stream;
     const double half_width = p->Lx / 2.0;  // MonteCarlo.half_width (monte_carlo.py:66)
+    const bool hybrid = (flags & FS_MH_HYBRID) != 0;
+    REQUIRE(!hybrid || state, "fs_nf_mh_step: FS_MH_HYBRID needs the state");
     hipError_t e = fs_flow_pass_impl(d, packed, 2, nullptr, C, nullptr, nullptr, 0, config, centered, seed, step,
                                      chain_offset, half_width, err, st);
     if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/propose");
@@ -179,9 +190,46 @@ int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, i
     if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/log_prob");
     e = fs_energy_impl(p, config, 1, C, d->N, E_new, W_new, nullptr, nullptr, st);
     if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/energy");
+    if (hybrid) {  // the state moved since nll_old / E_old were exact: re-derive both
+        e = fs_center_impl(state, C * D, half_width, centered_old, st);
+        if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/center");
+        e = fs_flow_pass_impl(d, packed, 0, centered_old, C, nullptr, log_q_old, 1, nullptr, nullptr, 0, 0, 0, 0.0,
+                              err, st);
+        if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/log_prob_old");
+        e = fs_energy_impl(p, state, 0, C, d->N, E_cur, W_cur, nullptr, nullptr, st, state_is_f32);
+        if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/energy_old");
+    }
     e = fs_mh_accept_impl(p, C, d->N, E_old, W_old, nll_old, E_new, W_new, log_q, pcg, state, state_is_f32,
-                          state ? config : nullptr, accept, attempts, accepted, n_accept, flags, st);
+                          state ? config : nullptr, accept, attempts, accepted, n_accept, flags, st,
+                          hybrid ? log_q_old : nullptr, hybrid ? E_cur : nullptr, hybrid ? W_cur : nullptr);
     return hip_rc(e, "fs_nf_mh_step/accept");
+}
+
+int fs_local_moves(const fs_phys *p, int64_t C, int32_t N, double *state, const uint8_t *state_is_f32, double *E,
+                   double *W, uint64_t *pcg, uint64_t *pcg_buf, double *max_disp, int64_t *attempts,
+                   int64_t *accepted, int64_t *prev_counts, int64_t n_moves, int64_t step0, int32_t adjust_every,
+                   double target_acceptance, int32_t sample_every, double *samples_xy, double *samples_ew,
+                   uint8_t *accept_log, unsigned long long *n_accept, void *stream) {
+    REQUIRE(p && state && E && pcg && pcg_buf && max_disp && attempts && accepted && C >= 0 && n_moves >= 0 &&
+                step0 >= 0,
+            "fs_local_moves: invalid arguments");
+    REQUIRE(N >= 1 && N <= fs::kMaxN, "fs_local_moves: N=%d outside [1, %d]", N, fs::kMaxN);
+    REQUIRE(adjust_every <= 0 || (prev_counts && target_acceptance > 0.0),
+            "fs_local_moves: adjust_every needs prev_counts and target_acceptance > 0");
+    REQUIRE(sample_every <= 0 || samples_xy || samples_ew, "fs_local_moves: sample_every needs a sample buffer");
+    return hip_rc(fs_local_moves_impl(p, C, N, state, state_is_f32, E, W, pcg, pcg_buf, max_disp, attempts, accepted,
+                                      prev_counts, n_moves, step0, adjust_every, target_acceptance, sample_every,
+                                      samples_xy, samples_ew, accept_log, n_accept, (hipStream_t)stream),
+                  "fs_local_moves");
+}
+
+int fs_adjust_displacement(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,
+                           int64_t *prev_counts, double target_acceptance, void *stream) {
+    REQUIRE(max_disp && attempts && accepted && prev_counts && C >= 0 && target_acceptance > 0.0,
+            "fs_adjust_displacement: invalid arguments");
+    return hip_rc(fs_adjust_displacement_impl(C, max_disp, attempts, accepted, prev_counts, target_acceptance,
+                                              (hipStream_t)stream),
+                  "fs_adjust_displacement");
 }
 
 int fs_hist2d(const double *pos, int64_t C, int32_t N, double shift, const double *edges, int32_t nbins,

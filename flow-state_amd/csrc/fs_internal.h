@@ -19,11 +19,22 @@ hipError_t fs_flow_pass_impl(const fs_flow_dims *d, const void *packed, int mode
                              int32_t *err, hipStream_t st);
 
 hipError_t fs_energy_impl(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int N, double *E,
-                          double *W, uint8_t *overlap, uint64_t *nbr, hipStream_t st);
+                          double *W, uint8_t *overlap, uint64_t *nbr, hipStream_t st,
+                          const uint8_t *chain_is_f32 = nullptr);
 hipError_t fs_mh_accept_impl(const fs_phys *p, int64_t C, int N, double *E_old, double *W_old, double *nll_old,
                              const double *E_new, const double *W_new, const float *log_q_new, uint64_t *pcg,
                              double *state, uint8_t *state_is_f32, const float *config, uint8_t *accept,
                              int64_t *attempts, int64_t *accepted, unsigned long long *n_accept, int flags,
-                             hipStream_t st);
+                             hipStream_t st, const float *log_q_old = nullptr, const double *E_cur = nullptr,
+                             const double *W_cur = nullptr);
+hipError_t fs_adjust_displacement_impl(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,
+                                       int64_t *prev, double target, hipStream_t st);
+hipError_t fs_center_impl(const double *state, int64_t n, double hw, float *out, hipStream_t st);
+hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state, const uint8_t *is_f32,
+                               double *E, double *W, uint64_t *pcg, uint64_t *pcg_buf, double *max_disp,
+                               int64_t *attempts, int64_t *accepted, int64_t *prev, int64_t n_moves, int64_t step0,
+                               int adjust_every, double target, int sample_every, double *samples_xy,
+                               double *samples_ew, uint8_t *accept_log, unsigned long long *n_accept,
+                               hipStream_t st);
 
 void fs_set_error(const char *fmt, ...);

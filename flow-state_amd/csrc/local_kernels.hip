@@ -1,0 +1,286 @@
+// Batched local Metropolis moves on MI355X: MonteCarlo.particle_displacement
+// (monte_carlo.py:146-189) + metropolis_acceptance_particle_move (:191-223),
+// adjust_displacement (:375-403) and the sample() snapshots (:416-444) that the
+// Algorithm-1 driver interleaves with them (main_algorithm_1.py:203-210, 245-252,
+// 384-390).
+//
+// Layout: a group of LPC lanes owns one chain (LPC = 64/32/16/8 for N <= 64/32/16/8);
+// lane j holds particle j's coordinates in registers for the whole launch, so a
+// launch of n moves touches HBM only to load and store the state.  Every lane of a
+// group runs the chain's PCG64 redundantly (group-uniform values, no broadcast).
+// Per move each lane evaluates its two pair terms (particle p before / after the
+// displacement against particle j); the per-particle sums use numpy's pairwise
+// order over the np.delete-compacted index (loops_utils.h): 8 partial sums with
+// 8-lane shuffles for the tree, then the tail — so E, W and the accept decisions
+// track the reference to the ulp.  The double-well terms are spread over lanes
+// 0..3 (before/after x well 0/1).  Chains are independent: no grid-level sync,
+// each group exits after its n moves.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "fs_internal.h"
+#include "physics_device.h"
+
+#pragma clang fp contract(off)
+
+namespace fs {
+
+struct LocalArgs {
+    fs_phys p;
+    int64_t C;
+    int N;
+    double *state;
+    const uint8_t *is_f32;
+    double *E, *W;
+    uint64_t *pcg, *pcg_buf;
+    double *max_disp;
+    int64_t *attempts, *accepted, *prev;
+    int64_t n_moves, step0;
+    int adjust_every;
+    double target;
+    int sample_every;
+    int64_t n_samp;
+    double *samples_xy, *samples_ew;
+    uint8_t *accept_log;
+    unsigned long long *n_accept;
+};
+
+constexpr int kLocalWaves = 4;
+
+// adjust_displacement (monte_carlo.py:375-403) on one chain's registers
+__device__ __forceinline__ void adjust_md(double &md, int64_t att, int64_t acc, int64_t &prev_att, int64_t &prev_acc,
+                                          double target) {
+    if (att > prev_att) {
+        const int64_t da = att - prev_att, dc = acc - prev_acc;
+        const double frac = da > 0 ? (double)dc / (double)da : 0.0;  // Python int / int
+        const double factor = frac / target;
+        double nm = md * factor;
+        const double ratio = nm / md;
+        if (ratio > 1.5) nm = md * 1.5;
+        else if (ratio < 0.5) nm = md * 0.5;
+        md = nm;
+        prev_att = att;
+        prev_acc = acc;
+    }
+}
+
+__global__ void adjust_kernel(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,
+                              int64_t *prev, double target) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double md = max_disp[c];
+    int64_t pa = prev[2 * c], pc = prev[2 * c + 1];
+    adjust_md(md, attempts[c], accepted[c], pa, pc, target);
+    max_disp[c] = md;
+    prev[2 * c] = pa;
+    prev[2 * c + 1] = pc;
+}
+
+template <int LPC>
+__global__ void __launch_bounds__(64 * kLocalWaves) local_moves_kernel(LocalArgs a) {
+    constexpr int G = 64 / LPC;  // chains per wave
+    __shared__ double lds[kLocalWaves][4][64];
+    __shared__ double res[kLocalWaves][G][4];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = lane / LPC, gl = lane % LPC, gb = g * LPC;
+    const int64_t c = ((int64_t)blockIdx.x * kLocalWaves + wid) * G + g;
+    if (c >= a.C) return;  // whole groups leave; only group-internal shuffles below
+    const int N = a.N;
+    const fs_phys &P = a.p;
+    const bool f32 = a.is_f32 && a.is_f32[c];
+    const bool own = gl < N;
+    double xj = 0.0, yj = 0.0;
+    if (own) {
+        xj = a.state[(c * N + gl) * 2];
+        yj = a.state[(c * N + gl) * 2 + 1];
+    }
+    Pcg64 rng;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rng.s[i] = a.pcg[4 * c + i];
+    rng.has = (uint32_t)a.pcg_buf[2 * c];
+    rng.buf = (uint32_t)a.pcg_buf[2 * c + 1];
+    double E = a.E[c], W = a.W ? a.W[c] : 0.0, md = a.max_disp[c];
+    int64_t att = a.attempts[c], acc_n = a.accepted[c];
+    int64_t prev_att = a.prev ? a.prev[2 * c] : 0, prev_acc = a.prev ? a.prev[2 * c + 1] : 0;
+    const double sr6c = pow6(1.0 / P.r_cut);
+    const double e_cut = 4.0 * (sr6c * sr6c - sr6c);
+    const int n = N - 1;
+    const uint64_t gmask = (LPC == 64) ? ~0ull : (((1ull << LPC) - 1ull) << gb);
+    int64_t samp = 0;
+    unsigned long long n_acc_local = 0;
+
+    for (int64_t t = 0; t < a.n_moves; ++t) {
+        const int64_t step = a.step0 + t + 1;
+        att += 1;
+        const int p = (int)pcg64_integers(rng, (uint32_t)N);
+        const double ox = __shfl(xj, p, LPC), oy = __shfl(yj, p, LPC);
+        const double d0 = (pcg64_double(rng) - 0.5) * md;
+        const double d1 = (pcg64_double(rng) - 0.5) * md;
+        double nx, ny;
+        if (f32) {  // float32 row += float64 array, then float32 % np.float64 stored back
+            nx = (double)(float)np_remainder((double)(float)(ox + d0), P.Lx);
+            ny = (double)(float)np_remainder((double)(float)(oy + d1), P.Ly);
+        } else {
+            nx = np_remainder(ox + d0, P.Lx);
+            ny = np_remainder(oy + d1, P.Ly);
+        }
+        // pair terms of particle p against particle j (np.delete order: index j - (j > p))
+        const bool act = own && gl != p;
+        double eo = 0.0, wo = 0.0, en = 0.0, wn = 0.0;
+        bool ho = false, hn = false;
+        if (act) {
+            const double ro = f32 ? dist_f32((float)ox, (float)oy, (float)xj, (float)yj, P.Lx, P.Ly)
+                                  : dist_f64(ox, oy, xj, yj, P.Lx, P.Ly);
+            const double rn = f32 ? dist_f32((float)nx, (float)ny, (float)xj, (float)yj, P.Lx, P.Ly)
+                                  : dist_f64(nx, ny, xj, yj, P.Lx, P.Ly);
+            ho = ro < P.r_core;
+            hn = rn < P.r_core;
+            lj_pair(ro, P.r_cut, e_cut, eo, wo);
+            lj_pair(rn, P.r_cut, e_cut, en, wn);
+            const int tt = gb + gl - (gl > p ? 1 : 0);
+            lds[wid][0][tt] = eo;
+            lds[wid][1][tt] = wo;
+            lds[wid][2][tt] = en;
+            lds[wid][3][tt] = wn;
+        }
+        const bool hit_old = (__ballot(ho) & gmask) != 0;
+        const bool hit_new = (__ballot(hn) & gmask) != 0;
+        // double-well terms: lane 0/1 = old position well 0/1, lane 2/3 = new position
+        double dw = 0.0;
+        if (gl < 4 && (gl & 1) < P.num_wells)
+            dw = dw_term(gl < 2 ? ox : nx, gl < 2 ? oy : ny, gl & 1, P.Lx, P.Ly, P.V0[gl & 1], P.r0, P.k);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // numpy pairwise sums of the four compacted rows
+        if (n < 8) {
+            if (gl < 4) {
+                double r = 0.0;
+                for (int k = 0; k < n; ++k) r += lds[wid][gl][gb + k];
+                res[wid][g][gl] = r;
+            }
+        } else {
+            const int nfull = n - (n % 8);
+            for (int ak = gl; ak < 32; ak += LPC) {  // LPC >= 16 here (N > 8)
+                const int arr = ak >> 3, k = ak & 7;
+                double r = lds[wid][arr][gb + k];
+                for (int b = 8; b < nfull; b += 8) r += lds[wid][arr][gb + b + k];
+                r += __shfl_xor(r, 1, LPC);
+                r += __shfl_xor(r, 2, LPC);
+                r += __shfl_xor(r, 4, LPC);
+                if (k == 0) {
+                    for (int i = nfull; i < n; ++i) r += lds[wid][arr][gb + i];
+                    res[wid][g][arr] = r;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // V = 0; V += term(well 0); V += term(well 1)   (potential.py:96-112)
+        const double dw0o = __shfl(dw, 0, LPC), dw1o = __shfl(dw, 1, LPC);
+        const double dw0n = __shfl(dw, 2, LPC), dw1n = __shfl(dw, 3, LPC);
+        double eno = res[wid][g][0], viro = res[wid][g][1];
+        double enn = res[wid][g][2], virn = res[wid][g][3];
+        if (P.num_wells > 0) {
+            double vo = 0.0 + dw0o, vn = 0.0 + dw0n;
+            if (P.num_wells > 1) {
+                vo += dw1o;
+                vn += dw1n;
+            }
+            eno += vo;
+            enn += vn;
+        }
+        if (hit_old) eno = viro = INFINITY;  // energy_calculator.py:69-73
+        if (hit_new) enn = virn = INFINITY;
+        bool accept;
+        if (enn <= eno) accept = true;
+        else if (isinf(enn)) accept = false;
+        else accept = pcg64_double(rng) < exp(-P.beta * (enn - eno));
+        if (accept) {
+            acc_n += 1;
+            E += enn - eno;
+            W += virn - viro;
+            n_acc_local += 1;
+            if (gl == p) {
+                xj = nx;
+                yj = ny;
+            }
+        }
+        if (a.accept_log && gl == 0) a.accept_log[c * a.n_moves + t] = accept ? 1 : 0;
+        if (a.adjust_every > 0 && step % a.adjust_every == 0) adjust_md(md, att, acc_n, prev_att, prev_acc, a.target);
+        if (a.sample_every > 0 && step % a.sample_every == 0 && samp < a.n_samp) {
+            if (a.samples_xy && own) {
+                double *q = a.samples_xy + ((c * a.n_samp + samp) * N + gl) * 2;
+                q[0] = xj;
+                q[1] = yj;
+            }
+            if (a.samples_ew && gl == 0) {
+                a.samples_ew[(c * a.n_samp + samp) * 2] = E;
+                a.samples_ew[(c * a.n_samp + samp) * 2 + 1] = W;
+            }
+            ++samp;
+        }
+    }
+    if (own) {
+        a.state[(c * N + gl) * 2] = xj;
+        a.state[(c * N + gl) * 2 + 1] = yj;
+    }
+    if (gl == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a.pcg[4 * c + i] = rng.s[i];
+        a.pcg_buf[2 * c] = rng.has;
+        a.pcg_buf[2 * c + 1] = rng.buf;
+        a.E[c] = E;
+        if (a.W) a.W[c] = W;
+        a.max_disp[c] = md;
+        a.attempts[c] = att;
+        a.accepted[c] = acc_n;
+        if (a.prev) {
+            a.prev[2 * c] = prev_att;
+            a.prev[2 * c + 1] = prev_acc;
+        }
+        if (a.n_accept && n_acc_local) atomicAdd(a.n_accept, n_acc_local);
+    }
+}
+
+}  // namespace fs
+
+using namespace fs;
+
+int64_t fs_local_samples_per_chain(int64_t step0, int64_t n_moves, int32_t sample_every) {
+    if (sample_every <= 0 || n_moves <= 0) return 0;
+    return (step0 + n_moves) / sample_every - step0 / sample_every;
+}
+
+hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state, const uint8_t *is_f32,
+                               double *E, double *W, uint64_t *pcg, uint64_t *pcg_buf, double *max_disp,
+                               int64_t *attempts, int64_t *accepted, int64_t *prev, int64_t n_moves, int64_t step0,
+                               int adjust_every, double target, int sample_every, double *samples_xy,
+                               double *samples_ew, uint8_t *accept_log, unsigned long long *n_accept,
+                               hipStream_t st) {
+    if (C <= 0 || n_moves <= 0) return hipSuccess;
+    LocalArgs a{*p,       C,         N,        state,      is_f32,     E,          W,
+                pcg,      pcg_buf,   max_disp, attempts,   accepted,   prev,       n_moves,
+                step0,    adjust_every, target, sample_every, fs_local_samples_per_chain(step0, n_moves, sample_every),
+                samples_xy, samples_ew, accept_log, n_accept};
+    const int lpc = N > 32 ? 64 : N > 16 ? 32 : N > 8 ? 16 : 8;
+    const int64_t chains_per_block = (int64_t)kLocalWaves * (64 / lpc);
+    const dim3 grid((unsigned)((C + chains_per_block - 1) / chains_per_block)), block(64 * kLocalWaves);
+    switch (lpc) {
+    case 64: hipLaunchKernelGGL(local_moves_kernel<64>, grid, block, 0, st, a); break;
+    case 32: hipLaunchKernelGGL(local_moves_kernel<32>, grid, block, 0, st, a); break;
+    case 16: hipLaunchKernelGGL(local_moves_kernel<16>, grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL(local_moves_kernel<8>, grid, block, 0, st, a); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t fs_adjust_displacement_impl(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,
+                                       int64_t *prev, double target, hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    hipLaunchKernelGGL(adjust_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, C, max_disp, attempts,
+                       accepted, prev, target);
+    return hipGetLastError();
+}

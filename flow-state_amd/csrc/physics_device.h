@@ -1,0 +1,155 @@
+// Device helpers shared by the physics kernels (energy, local moves, MH accept):
+// numpy-order minimum-image distances, the shifted LJ pair term and the numpy
+// PCG64 stream.  Evaluation order follows the reference line by line (cited per
+// helper) so that results track numpy to the ulp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace fs {
+
+// minimum-image distance (simulation_box.py:31-56) with numpy's promotion rules
+__device__ __forceinline__ double dist_f32(float ax, float ay, float bx, float by, double Lx, double Ly) {
+    const float d0 = __fsub_rn(ax, bx), d1 = __fsub_rn(ay, by);
+    const double w0 = (double)d0 - Lx * rint((double)d0 / Lx);
+    const double w1 = (double)d1 - Ly * rint((double)d1 / Ly);
+    const float t0 = (float)w0, t1 = (float)w1;
+    const float s = __fadd_rn(__fmul_rn(t0, t0), __fmul_rn(t1, t1));  // OpenBLAS sdot
+    // correctly rounded float32 sqrt (np.sqrt on float32): the double sqrt of a float
+    // rounded once more to float is exact-rounded (53 >= 2*24+2 bits); the device
+    // f32 sqrt instruction is only faithful
+    return (double)(float)__dsqrt_rn((double)s);
+}
+
+__device__ __forceinline__ double dist_f64(double ax, double ay, double bx, double by, double Lx, double Ly) {
+    const double d0 = ax - bx, d1 = ay - by;
+    const double t0 = d0 - Lx * rint(d0 / Lx);
+    const double t1 = d1 - Ly * rint(d1 / Ly);
+    return __dsqrt_rn(fma(t1, t1, __dmul_rn(t0, t0)));  // OpenBLAS ddot (FMA kernel)
+}
+
+// x^6 rounded once from a double-double product (tracks the correctly rounded pow)
+__device__ __forceinline__ double pow6(double x) {
+    const double x2 = x * x, x2e = fma(x, x, -x2);
+    const double x3 = x2 * x, x3e = fma(x2, x, -x3) + x2e * x;
+    const double x6 = x3 * x3, x6e = fma(x3, x3, -x6) + 2.0 * x3 * x3e;
+    return x6 + x6e;
+}
+
+__device__ __forceinline__ void lj_pair(double r, double r_cut, double e_cut, double &e, double &w) {
+    if (r <= r_cut) {  // potential.py:11 inclusive
+        const double sr6 = pow6(1.0 / r);
+        const double sr12 = sr6 * sr6;
+        e = 4.0 * (sr12 - sr6) - e_cut;
+        w = 48.0 * (sr12 - 0.5 * sr6);
+    } else {
+        e = 0.0;
+        w = 0.0;
+    }
+}
+
+// ---------------------------------------------------------------- PCG64
+struct u128 {
+    uint64_t hi, lo;
+};
+
+__device__ __forceinline__ u128 mul_add(u128 a, u128 m, u128 inc) {
+    u128 r;
+    r.lo = a.lo * m.lo;
+    r.hi = __umul64hi(a.lo, m.lo) + a.lo * m.hi + a.hi * m.lo;
+    const uint64_t lo = r.lo + inc.lo;
+    r.hi += inc.hi + (lo < r.lo ? 1 : 0);
+    r.lo = lo;
+    return r;
+}
+
+__device__ __forceinline__ double pcg64_next_double(uint64_t *s) {
+    const u128 M = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull};
+    u128 st = {s[0], s[1]}, inc = {s[2], s[3]};
+    st = mul_add(st, M, inc);
+    s[0] = st.hi;
+    s[1] = st.lo;
+    const uint64_t x = st.hi ^ st.lo;
+    const unsigned rot = (unsigned)(st.hi >> 58);
+    const uint64_t out = (x >> rot) | (x << ((64 - rot) & 63));
+    return (double)(out >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// numpy PCG64 with the 32-bit half buffer (numpy/random/src/pcg64/pcg64.h
+// pcg64_next32: has_uint32 / uinteger), as Generator.integers consumes it
+struct Pcg64 {
+    uint64_t s[4];
+    uint32_t has, buf;
+};
+
+__device__ __forceinline__ uint64_t pcg64_next64(uint64_t *s) {
+    const u128 M = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull};
+    u128 st = {s[0], s[1]}, inc = {s[2], s[3]};
+    st = mul_add(st, M, inc);
+    s[0] = st.hi;
+    s[1] = st.lo;
+    const uint64_t x = st.hi ^ st.lo;
+    const unsigned rot = (unsigned)(st.hi >> 58);
+    return (x >> rot) | (x << ((64 - rot) & 63));
+}
+
+__device__ __forceinline__ double pcg64_double(Pcg64 &g) {
+    return (double)(pcg64_next64(g.s) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+__device__ __forceinline__ uint32_t pcg64_next32(Pcg64 &g) {
+    if (g.has) {
+        g.has = 0;
+        return g.buf;
+    }
+    const uint64_t v = pcg64_next64(g.s);
+    g.has = 1;
+    g.buf = (uint32_t)(v >> 32);
+    return (uint32_t)v;
+}
+
+// Generator.integers(n), 1 <= n <= 2^32 (random_bounded_uint64_fill ->
+// buffered_bounded_lemire_uint32); n == 1 draws nothing
+__device__ __forceinline__ uint32_t pcg64_integers(Pcg64 &g, uint32_t n) {
+    const uint32_t rng = n - 1u;
+    if (rng == 0u) return 0u;
+    const uint32_t excl = rng + 1u;
+    uint64_t m = (uint64_t)pcg64_next32(g) * excl;
+    uint32_t left = (uint32_t)m;
+    if (left < excl) {
+        const uint32_t thr = (0xFFFFFFFFu - rng) % excl;
+        while (left < thr) {
+            m = (uint64_t)pcg64_next32(g) * excl;
+            left = (uint32_t)m;
+        }
+    }
+    return (uint32_t)(m >> 32);
+}
+
+// one well's term V0_i * (1 - transition) of double_well_potential (potential.py:98-112)
+__device__ __forceinline__ double dw_term(double x, double y, int well, double Lx, double Ly, double V0, double r0,
+                                          double k) {
+    const double cx = (well == 0) ? Lx / 4.0 : 3.0 * Lx / 4.0, cy = Ly / 2.0;
+    double dx = x - cx, dy = y - cy;
+    dx -= Lx * rint(dx / Lx);
+    dy -= Ly * rint(dy / Ly);
+    const double r = sqrt(dx * dx + dy * dy);
+    const double tr = 0.5 * (1.0 + tanh(k * (r - r0)));
+    return V0 * (1.0 - tr);
+}
+
+// numpy floor remainder (npy_divmod) for SimulationBox.apply_pbc (simulation_box.py:19-29)
+__device__ __forceinline__ double np_remainder(double a, double b) {
+    double mod = fmod(a, b);
+    if (mod != 0.0) {
+        if ((b < 0) != (mod < 0)) mod += b;
+    } else {
+        mod = copysign(0.0, b);
+    }
+    return mod;
+}
+
+}  // namespace fs

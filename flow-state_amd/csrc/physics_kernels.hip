@@ -15,52 +15,13 @@
 
 #include "flow_layout.h"
 #include "fs_internal.h"
+#include "physics_device.h"
 
 #pragma clang fp contract(off)
 
 namespace fs {
 
 // ---------------------------------------------------------------- energy
-// minimum-image distance (simulation_box.py:31-56) with numpy's promotion rules
-__device__ __forceinline__ double dist_f32(float ax, float ay, float bx, float by, double Lx, double Ly) {
-    const float d0 = __fsub_rn(ax, bx), d1 = __fsub_rn(ay, by);
-    const double w0 = (double)d0 - Lx * rint((double)d0 / Lx);
-    const double w1 = (double)d1 - Ly * rint((double)d1 / Ly);
-    const float t0 = (float)w0, t1 = (float)w1;
-    const float s = __fadd_rn(__fmul_rn(t0, t0), __fmul_rn(t1, t1));  // OpenBLAS sdot
-    // correctly rounded float32 sqrt (np.sqrt on float32): the double sqrt of a float
-    // rounded once more to float is exact-rounded (53 >= 2*24+2 bits); the device
-    // f32 sqrt instruction is only faithful
-    return (double)(float)__dsqrt_rn((double)s);
-}
-
-__device__ __forceinline__ double dist_f64(double ax, double ay, double bx, double by, double Lx, double Ly) {
-    const double d0 = ax - bx, d1 = ay - by;
-    const double t0 = d0 - Lx * rint(d0 / Lx);
-    const double t1 = d1 - Ly * rint(d1 / Ly);
-    return __dsqrt_rn(fma(t1, t1, __dmul_rn(t0, t0)));  // OpenBLAS ddot (FMA kernel)
-}
-
-// x^6 rounded once from a double-double product (tracks the correctly rounded pow)
-__device__ __forceinline__ double pow6(double x) {
-    const double x2 = x * x, x2e = fma(x, x, -x2);
-    const double x3 = x2 * x, x3e = fma(x2, x, -x3) + x2e * x;
-    const double x6 = x3 * x3, x6e = fma(x3, x3, -x6) + 2.0 * x3 * x3e;
-    return x6 + x6e;
-}
-
-__device__ __forceinline__ void lj_pair(double r, double r_cut, double e_cut, double &e, double &w) {
-    if (r <= r_cut) {  // potential.py:11 inclusive
-        const double sr6 = pow6(1.0 / r);
-        const double sr12 = sr6 * sr6;
-        e = 4.0 * (sr12 - sr6) - e_cut;
-        w = 48.0 * (sr12 - 0.5 * sr6);
-    } else {
-        e = 0.0;
-        w = 0.0;
-    }
-}
-
 // numpy pairwise sum of n <= 128 values held in LDS (serial, one lane)
 __device__ double pairwise_lds(const double *a, int n) {
     if (n < 8) {
@@ -81,11 +42,15 @@ __device__ double pairwise_lds(const double *a, int n) {
 template <bool F32>
 __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, const void *__restrict__ pos, int64_t C, int N,
                                                      double *__restrict__ E, double *__restrict__ W,
-                                                     uint8_t *__restrict__ ov, uint64_t *__restrict__ nbr) {
+                                                     uint8_t *__restrict__ ov, uint64_t *__restrict__ nbr,
+                                                     const uint8_t *__restrict__ is_f32) {
     __shared__ double sx[4][64], sy[4][64], se[4][64], sw[4][64], sv[4][64];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t c = (int64_t)blockIdx.x * 4 + wid;
     if (c >= C) return;  // whole wave leaves; no block-level barrier below
+    // float64 storage holding a chain whose reference state is float32 (after an accepted
+    // big move, monte_carlo.py:296): the float32 distance path on the exact float values
+    const bool as_f32 = F32 || (is_f32 && is_f32[c]);
     if (lane < N) {
         if (F32) {
             const float *q = (const float *)pos + c * 2 * N;
@@ -109,7 +74,7 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, const void *__re
     uint64_t mask = 0;
     auto pair = [&](int t, double &e, double &w) {
         const int j = i + 1 + t;
-        const double r = F32 ? dist_f32((float)xi, (float)yi, (float)sx[wid][j], (float)sy[wid][j], p.Lx, p.Ly)
+        const double r = as_f32 ? dist_f32((float)xi, (float)yi, (float)sx[wid][j], (float)sy[wid][j], p.Lx, p.Ly)
                              : dist_f64(xi, yi, sx[wid][j], sy[wid][j], p.Lx, p.Ly);
         hit |= r < p.r_core;
         if (r <= p.r_cut) mask |= (uint64_t)1 << j;
@@ -187,32 +152,6 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, const void *__re
 }
 
 // ---------------------------------------------------------------- PCG64
-struct u128 {
-    uint64_t hi, lo;
-};
-
-__device__ __forceinline__ u128 mul_add(u128 a, u128 m, u128 inc) {
-    u128 r;
-    r.lo = a.lo * m.lo;
-    r.hi = __umul64hi(a.lo, m.lo) + a.lo * m.hi + a.hi * m.lo;
-    const uint64_t lo = r.lo + inc.lo;
-    r.hi += inc.hi + (lo < r.lo ? 1 : 0);
-    r.lo = lo;
-    return r;
-}
-
-__device__ __forceinline__ double pcg64_next_double(uint64_t *s) {
-    const u128 M = {0x2360ED051FC65DA4ull, 0x4385DF649FCCF645ull};
-    u128 st = {s[0], s[1]}, inc = {s[2], s[3]};
-    st = mul_add(st, M, inc);
-    s[0] = st.hi;
-    s[1] = st.lo;
-    const uint64_t x = st.hi ^ st.lo;
-    const unsigned rot = (unsigned)(st.hi >> 58);
-    const uint64_t out = (x >> rot) | (x << ((64 - rot) & 63));
-    return (double)(out >> 11) * (1.0 / 9007199254740992.0);
-}
-
 __device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t &hc) {
     v ^= hc;
     hc *= 0x931e8875u;
@@ -284,7 +223,9 @@ __global__ void __launch_bounds__(256) mh_accept_kernel(fs_phys p, int64_t C, in
                                                         const float *log_q_new, uint64_t *pcg, double *state,
                                                         uint8_t *state_is_f32, const float *config,
                                                         uint8_t *accept, int64_t *attempts, int64_t *accepted,
-                                                        unsigned long long *n_accept, int flags) {
+                                                        unsigned long long *n_accept, int flags,
+                                                        const float *log_q_old, const double *E_cur,
+                                                        const double *W_cur) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const bool valid = c < C;
@@ -293,7 +234,9 @@ __global__ void __launch_bounds__(256) mh_accept_kernel(fs_phys p, int64_t C, in
         const double en = E_new[c];
         const double nll_new = -(double)log_q_new[c];  // - log_prob(new).item()
         const double dE = en - E_old[c];
-        const double dN = nll_new - nll_old[c];
+        // hybrid: old NLL of the current (locally moved) state, monte_carlo.py:251-261
+        const double no = log_q_old ? -(double)log_q_old[c] : nll_old[c];
+        const double dN = nll_new - no;
         const double ratio_log = (flags & FS_MH_CORRECT_SIGN) ? (-p.beta * dE + dN) : (-p.beta * dE - dN);
         const double ratio = exp(ratio_log);
         if (ratio >= 1.0) {
@@ -310,6 +253,12 @@ __global__ void __launch_bounds__(256) mh_accept_kernel(fs_phys p, int64_t C, in
             nll_old[c] = nll_new;
             if (accepted) accepted[c] += 1;
             if (state_is_f32) state_is_f32[c] = 1;
+        } else {
+            if (log_q_old) nll_old[c] = no;
+            if (E_cur) {  // reject recomputes the total energy (monte_carlo.py:299-301)
+                E_old[c] = E_cur[c];
+                if (W_old && W_cur) W_old[c] = W_cur[c];
+            }
         }
     }
     uint64_t m = __ballot(acc);
@@ -324,6 +273,13 @@ __global__ void __launch_bounds__(256) mh_accept_kernel(fs_phys p, int64_t C, in
             for (int t = lane; t < D; t += 64) state[cc * D + t] = (double)config[cc * D + t];
         }
     }
+}
+
+// (float32)(particles - half_width): the NF coordinates of the current state
+// (monte_carlo.py:251-257)
+__global__ void center_kernel(const double *__restrict__ state, int64_t n, double hw, float *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) out[t] = (float)(state[t] - hw);
 }
 
 // ---------------------------------------------------------------- reductions
@@ -379,13 +335,14 @@ __global__ void well_stats_kernel(fs_phys p, const double *__restrict__ pos, int
 using namespace fs;
 
 hipError_t fs_energy_impl(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int N, double *E,
-                          double *W, uint8_t *overlap, uint64_t *nbr, hipStream_t st) {
+                          double *W, uint8_t *overlap, uint64_t *nbr, hipStream_t st, const uint8_t *chain_is_f32) {
     if (C <= 0) return hipSuccess;
     const dim3 grid((unsigned)((C + 3) / 4));
     if (pos_is_f32)
-        hipLaunchKernelGGL(energy_kernel<true>, grid, dim3(256), 0, st, *p, pos, C, N, E, W, overlap, nbr);
+        hipLaunchKernelGGL(energy_kernel<true>, grid, dim3(256), 0, st, *p, pos, C, N, E, W, overlap, nbr, nullptr);
     else
-        hipLaunchKernelGGL(energy_kernel<false>, grid, dim3(256), 0, st, *p, pos, C, N, E, W, overlap, nbr);
+        hipLaunchKernelGGL(energy_kernel<false>, grid, dim3(256), 0, st, *p, pos, C, N, E, W, overlap, nbr,
+                           chain_is_f32);
     return hipGetLastError();
 }
 
@@ -393,11 +350,11 @@ hipError_t fs_mh_accept_impl(const fs_phys *p, int64_t C, int N, double *E_old, 
                              const double *E_new, const double *W_new, const float *log_q_new, uint64_t *pcg,
                              double *state, uint8_t *state_is_f32, const float *config, uint8_t *accept,
                              int64_t *attempts, int64_t *accepted, unsigned long long *n_accept, int flags,
-                             hipStream_t st) {
+                             hipStream_t st, const float *log_q_old, const double *E_cur, const double *W_cur) {
     if (C <= 0) return hipSuccess;
     hipLaunchKernelGGL(mh_accept_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, *p, C, N, E_old,
                        W_old, nll_old, E_new, W_new, log_q_new, pcg, state, state_is_f32, config, accept,
-                       attempts, accepted, n_accept, flags);
+                       attempts, accepted, n_accept, flags, log_q_old, E_cur, W_cur);
     return hipGetLastError();
 }
 
@@ -427,5 +384,11 @@ hipError_t fs_well_stats_impl(const fs_phys *p, const double *pos, int64_t C, in
     if (C <= 0) return hipSuccess;
     hipLaunchKernelGGL(well_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, *p, pos, C, N,
                        (long long *)counts);
+    return hipGetLastError();
+}
+
+hipError_t fs_center_impl(const double *state, int64_t n, double hw, float *out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(center_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, state, n, hw, out);
     return hipGetLastError();
 }

@@ -11,11 +11,22 @@ chains live on the device:
   E_old, W_old (C,) float64       cached total energy / virial (energy_calculator.py:46)
   nll_old      (C,) float64       cached -log q(state) (float32 value, exact on replay)
   pcg          (C, 4) u64         numpy PCG64 state, seeded like default_rng(seed_c)
-  attempts, accepted (C,) int64   monte_carlo.py:80-81 counters
+  pcg_buf      (C, 2) u64         its buffered 32-bit half (has_uint32, uinteger)
+  attempts, accepted (C,) int64   monte_carlo.py:80-81 counters (shared by local
+                                   and big moves, as in the reference)
+  max_disp     (C,) float64       max_displacement
+  prev_counts  (C, 2) int64       previous_{attempts,accepted}_displacement
 
+``local_moves(n)`` = fs_local_moves: n particle_displacement calls per chain
+(with adjust_displacement / sample() on the driver's step schedule).
 ``step()`` = fs_nf_mh_step: proposal sampling pass (base draws in-kernel) ->
 density pass on the proposals -> energies -> accept/update.  ``nf_big_move``
 takes externally supplied proposals (the reference's pre-generated configs).
+After local moves the next big move re-derives the old NLL from the current
+state and recomputes the energy on reject, as nf_big_move does on every call
+(monte_carlo.py:243-261, 299-301); without local moves in between the cached
+values are exactly those numbers.  The flow model is optional until the first
+big move (the reference equilibrates before set_nf_model).
 """
 import numpy as np
 import torch
@@ -41,18 +52,19 @@ class Physics:
 
 class BatchedMonteCarlo:
     def __init__(self, model, particles, physics, seeds, device=None, proposal_seed=1234,
-                 correct_sign=False, state_is_f32=None, chain_offset=0):
-        self.model = model
+                 correct_sign=False, state_is_f32=None, chain_offset=0, initial_max_displacement=0.5,
+                 target_acceptance=0.5):
+        self.model = None
         self.phys = physics
-        dev = torch.device(device) if device is not None else next(model.parameters()).device
+        if device is None:
+            device = next(model.parameters()).device if model is not None else "cuda"
+        dev = torch.device(device)
         _lib.require_device(torch.empty(0, device=dev))
         self.device = dev
         p = torch.as_tensor(np.asarray(particles) if not torch.is_tensor(particles) else particles)
         if p.dim() == 2:
             p = p[None]
         self.C, self.N = int(p.shape[0]), int(p.shape[1])
-        if 2 * self.N != model.flows[0].num_input_channels:
-            raise ValueError("particles do not match the flow dimension")
         if state_is_f32 is None:
             state_is_f32 = p.dtype == torch.float32
         self.state = p.to(device=dev, dtype=torch.float64).contiguous()
@@ -73,16 +85,33 @@ class BatchedMonteCarlo:
         self.n_accept = torch.zeros(1, dtype=torch.int64, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.accept = torch.zeros(self.C, dtype=torch.uint8, device=dev)
-        self.E_old, self.W_old, self.nll_old = self._initial_energy_and_nll()
+        self.pcg_buf = torch.zeros((self.C, 2), dtype=torch.int64, device=dev)
+        self.max_disp = torch.full((self.C,), float(initial_max_displacement), dtype=torch.float64, device=dev)
+        self.prev_counts = torch.zeros((self.C, 2), dtype=torch.int64, device=dev)
+        self.target_acceptance = float(target_acceptance)
+        self.E_old, self.W_old = self._energy_of_state()
+        self.nll_old = torch.zeros(self.C, dtype=torch.float64, device=dev)
+        self._moved = False  # local moves since E_old / nll_old were exact
         self._ws = None
+        if model is not None:
+            self.set_model(model)
+
+    def set_model(self, model):
+        """MonteCarlo.set_nf_model (monte_carlo.py:229-233)."""
+        if 2 * self.N != model.flows[0].num_input_channels:
+            raise ValueError("particles do not match the flow dimension")
+        self.model = model
+        self._ws = None
+        self.nll_old = -(model.log_prob(self._centered_f32(self.state)).to(torch.float64))
 
     # ------------------------------------------------------------------
     def _centered_f32(self, pos, is_f32_mask=None):
         """fl32(pos - half_width) as nf_big_move feeds the flow (monte_carlo.py:251-258)."""
         return (pos - self.phys.half_width).to(torch.float32).reshape(pos.shape[0], -1).contiguous()
 
-    def _initial_energy_and_nll(self):
-        # energies in the reference dtype of each chain's state
+    def _energy_of_state(self):
+        """Total energy / virial in the reference dtype of each chain's state
+        (EnergyCalculator.__init__, energy_calculator.py:46)."""
         E = torch.empty(self.C, dtype=torch.float64, device=self.device)
         W = torch.empty_like(E)
         f32 = self.state_is_f32.bool()
@@ -91,8 +120,11 @@ class BatchedMonteCarlo:
             if idx.numel():
                 e, w, _ = total_energy(self.state[idx].to(dt), self.phys.c)
                 E[idx], W[idx] = e, w
-        lq = self.model.log_prob(self._centered_f32(self.state))
-        return E, W, -(lq.to(torch.float64))
+        return E, W
+
+    def _need_model(self):
+        if self.model is None:
+            raise RuntimeError("no flow model: set_model() / set_nf_model() first")
 
     def _workspace(self):
         if self._ws is None:
@@ -104,6 +136,7 @@ class BatchedMonteCarlo:
     # ------------------------------------------------------------------
     def step(self, n=1):
         """n fused NF-MH steps for all chains (stream-ordered, no host sync)."""
+        self._need_model()
         L = _lib.load()
         packed = self.model.packed()
         dims = self.model.dims()
@@ -115,9 +148,44 @@ class BatchedMonteCarlo:
                                        _lib.ptr(self.nll_old), _lib.ptr(self.pcg), _lib.ptr(self.state),
                                        _lib.ptr(self.state_is_f32), _lib.ptr(self.accept),
                                        _lib.ptr(self.attempts), _lib.ptr(self.accepted), _lib.ptr(self.n_accept),
-                                       _lib.ptr(self.err), self.flags, _lib.ptr(ws), st), "fs_nf_mh_step")
+                                       _lib.ptr(self.err), self.flags | (_lib.FS_MH_HYBRID if self._moved else 0),
+                                       _lib.ptr(ws), st), "fs_nf_mh_step")
             self.step_count += 1
+            self._moved = False
         return self.accept
+
+    def local_moves(self, n, adjust_every=0, sample_every=0, step0=0, log_accepts=False):
+        """n MonteCarlo.particle_displacement calls per chain (monte_carlo.py:146-223),
+        numbered step0+1 .. step0+n like the driver's loop counter
+        (main_algorithm_1.py:204-210): adjust_displacement after each step divisible
+        by adjust_every, a sample() snapshot after each step divisible by
+        sample_every.  Returns (samples_xy (C,S,N,2) f64, samples_ew (C,S,2) f64,
+        accept_log (C,n) u8) — the unused ones None."""
+        L = _lib.load()
+        n, step0 = int(n), int(step0)
+        S = L.fs_local_samples_per_chain(step0, n, int(sample_every))
+        sxy = sew = log = None
+        if S > 0:
+            sxy = torch.empty((self.C, S, self.N, 2), dtype=torch.float64, device=self.device)
+            sew = torch.empty((self.C, S, 2), dtype=torch.float64, device=self.device)
+        if log_accepts:
+            log = torch.empty((self.C, n), dtype=torch.uint8, device=self.device)
+        _lib.check(L.fs_local_moves(self.phys.c, self.C, self.N, _lib.ptr(self.state), _lib.ptr(self.state_is_f32),
+                                    _lib.ptr(self.E_old), _lib.ptr(self.W_old), _lib.ptr(self.pcg),
+                                    _lib.ptr(self.pcg_buf), _lib.ptr(self.max_disp), _lib.ptr(self.attempts),
+                                    _lib.ptr(self.accepted), _lib.ptr(self.prev_counts), n, step0, int(adjust_every),
+                                    self.target_acceptance, int(sample_every), _lib.ptr(sxy), _lib.ptr(sew),
+                                    _lib.ptr(log), None, _lib.stream_ptr()), "fs_local_moves")
+        if n > 0:
+            self._moved = True
+        return sxy, sew, log
+
+    def adjust_displacement(self):
+        """MonteCarlo.adjust_displacement (monte_carlo.py:375-403) for every chain."""
+        _lib.check(_lib.load().fs_adjust_displacement(self.C, _lib.ptr(self.max_disp), _lib.ptr(self.attempts),
+                                                      _lib.ptr(self.accepted), _lib.ptr(self.prev_counts),
+                                                      self.target_acceptance, _lib.stream_ptr()),
+                   "fs_adjust_displacement")
 
     def check_errors(self):
         if int(self.err.item()) & 1:
@@ -129,6 +197,11 @@ class BatchedMonteCarlo:
         if cfg.dtype != torch.float32:
             raise ValueError("proposals are float32 (main_algorithm_1.py:340-343)")
         cfg = cfg.reshape(self.C, self.N, 2).contiguous()
+        self._need_model()
+        stale = self._moved
+        if stale:  # old NLL of the current state (monte_carlo.py:251-261); energy for a reject (:299-301)
+            self.nll_old = -(self.model.log_prob(self._centered_f32(self.state)).to(torch.float64))
+            E_cur, W_cur = self._energy_of_state()
         E_new, W_new, _ = total_energy(cfg, self.phys.c)
         lq = self.model.log_prob(self._centered_f32(cfg.to(torch.float64)))
         L = _lib.load()
@@ -138,6 +211,11 @@ class BatchedMonteCarlo:
                                   _lib.ptr(cfg), _lib.ptr(self.accept), _lib.ptr(self.attempts),
                                   _lib.ptr(self.accepted), _lib.ptr(self.n_accept), self.flags,
                                   _lib.stream_ptr()), "fs_mh_accept")
+        if stale:
+            rej = self.accept == 0
+            self.E_old = torch.where(rej, E_cur, self.E_old)
+            self.W_old = torch.where(rej, W_cur, self.W_old)
+            self._moved = False
         return self.accept
 
     # ------------------------------------------------------------------

@@ -2,10 +2,12 @@
 
 Keeps the reference constructor and the attributes/methods the Algorithm-1
 driver touches around ``nf_big_move`` (main_algorithm_1.py:168-186, 372-422).
-Each instance is a 1-chain ``BatchedMonteCarlo``; ``nf_big_move(config)``
-returns a bool exactly like monte_carlo.py:235-303 (reference acceptance sign,
-same PCG64 stream as ``np.random.default_rng(seed)``).  Local moves
-(``particle_displacement``) are the next row of SURVEY §8(f) and raise here.
+Each instance is a 1-chain ``BatchedMonteCarlo`` created with the chain (its
+device state exists before set_nf_model, as the reference equilibrates first).
+``particle_displacement`` / ``adjust_displacement`` / ``nf_big_move`` follow
+monte_carlo.py:146-223, 375-403 and 235-303 on the same numpy PCG64 stream as
+``np.random.default_rng(seed)`` — bit-exact trajectories.  One call = one kernel
+launch, so drivers with many chains should use ``BatchedMonteCarlo.local_moves``.
 """
 import numpy as np
 import torch
@@ -37,7 +39,6 @@ class MonteCarlo:
         self.beta = 1.0 / temperature
         self.num_particles = num_particles
         self.num_wells, self.V0_list, self.r0, self.k = num_wells, V0_list, r0, k
-        self.max_displacement = initial_max_displacement
         self.target_acceptance = target_acceptance
         self.timing, self.checking, self.logger = timing, checking, logger
         if seed is None:
@@ -47,35 +48,48 @@ class MonteCarlo:
         self._particles0 = np.asarray(particles)
         self.physics = Physics(sim_box.box_size_x, sim_box.box_size_y, temperature, num_wells, V0_list, r0, k)
         self.nf_model = None
-        self._b = None
+        self._b = BatchedMonteCarlo(None, self._particles0[None], self.physics, [self.seed], device=self.device,
+                                    state_is_f32=self._particles0.dtype == np.float32,
+                                    initial_max_displacement=initial_max_displacement,
+                                    target_acceptance=target_acceptance)
         self.energy_calculator = _EnergyView(self)
         self.local_samples = []
         self.testing_samples = []
 
     @property
     def attempts_displacement(self):
-        return int(self._b.attempts.item()) if self._b is not None else 0
+        return int(self._b.attempts.item())
 
     @property
     def accepted_displacement(self):
-        return int(self._b.accepted.item()) if self._b is not None else 0
+        return int(self._b.accepted.item())
+
+    @property
+    def max_displacement(self):
+        return float(self._b.max_disp.item())
+
+    @property
+    def rng_state(self):
+        """numpy bit_generator.state-style dict of the chain's PCG64 stream."""
+        s = self._b.pcg[0].cpu().numpy().view(np.uint64)
+        b = self._b.pcg_buf[0].cpu().numpy().view(np.uint64)
+        return {"bit_generator": "PCG64",
+                "state": {"state": (int(s[0]) << 64) | int(s[1]), "inc": (int(s[2]) << 64) | int(s[3])},
+                "has_uint32": int(b[0]), "uinteger": int(b[1])}
 
     @property
     def particles(self):
-        if self._b is None:
-            return self._particles0
         s = self._b.state[0].cpu().numpy()
         return s.astype(np.float32) if int(self._b.state_is_f32[0].item()) else s
 
     def set_nf_model(self, nf_model):
         """monte_carlo.py:229-233; the chain's device state is created here."""
         self.nf_model = nf_model
-        self._b = BatchedMonteCarlo(nf_model, self._particles0[None], self.physics, [self.seed], device=self.device,
-                                    state_is_f32=self._particles0.dtype == np.float32)
+        self._b.set_model(nf_model)
 
     def nf_big_move(self, config):
         """monte_carlo.py:235-303: returns True if the NF proposal was accepted."""
-        if self._b is None:
+        if self.nf_model is None:
             raise RuntimeError("set_nf_model() first")
         cfg = np.asarray(config, dtype=np.float32).reshape(1, self.num_particles, 2)
         acc = self._b.nf_big_move(torch.from_numpy(cfg))
@@ -91,7 +105,9 @@ class MonteCarlo:
                 self.sim_box.box_size_y, self.particles.copy())
 
     def particle_displacement(self):
-        raise NotImplementedError("local moves (monte_carlo.py:146-189) are the next hot-path row (SURVEY §8(f))")
+        """monte_carlo.py:146-189: one local Metropolis move of a random particle."""
+        self._b.local_moves(1)
 
     def adjust_displacement(self):
-        raise NotImplementedError("local moves (monte_carlo.py:375-403) are the next hot-path row (SURVEY §8(f))")
+        """monte_carlo.py:375-403."""
+        self._b.adjust_displacement()

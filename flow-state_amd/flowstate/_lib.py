@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libflowstate.so")
 _lib = None
 
 FS_MH_CORRECT_SIGN = 1
+FS_MH_HYBRID = 2
 
 
 class FlowDims(ctypes.Structure):
@@ -53,6 +54,10 @@ _SIGS = {
     "fs_nf_mh_step_ws_bytes": (_I64, [_D, _I64]),
     "fs_nf_mh_step": (ctypes.c_int, [_D, _P, _PH, _I64, ctypes.c_uint64, ctypes.c_uint64, _I64] + [_P] * 11
                       + [ctypes.c_int, _P, _P]),
+    "fs_local_moves": (ctypes.c_int, [_PH, _I64, ctypes.c_int32] + [_P] * 10
+                       + [_I64, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_int32] + [_P] * 5),
+    "fs_local_samples_per_chain": (_I64, [_I64, _I64, ctypes.c_int32]),
+    "fs_adjust_displacement": (ctypes.c_int, [_I64, _P, _P, _P, _P, ctypes.c_double, _P]),
     "fs_hist2d": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_double, _P, ctypes.c_int32, _P, _P]),
     "fs_well_stats": (ctypes.c_int, [_PH, _P, _I64, ctypes.c_int32, _P, _P]),
 }

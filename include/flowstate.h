@@ -145,6 +145,12 @@ int fs_pcg64_random(uint64_t *state, int64_t C, double *out, void *stream);
  * (monte_carlo.py:240).  accept [C] u8 out; n_accept (nullable) += accepts
  * (wave ballot + popcount, one atomic per wave). */
 #define FS_MH_CORRECT_SIGN 1
+/* flags bit1 (fs_nf_mh_step): the state moved (local moves) since E_old / nll_old
+ * were exact.  The step then does what nf_big_move does on every call: old NLL
+ * from a density pass of the current state (monte_carlo.py:251-261; the ratio
+ * still uses the running E_old, :243), and on reject the total energy recomputed
+ * from the current state (:299-301). */
+#define FS_MH_HYBRID 2
 int fs_mh_accept(const fs_phys *p, int64_t C, int32_t N, double *E_old, double *W_old,
                  double *nll_old, const double *E_new, const double *W_new, const float *log_q_new,
                  uint64_t *pcg, double *state, uint8_t *state_is_f32, const float *config,
@@ -157,13 +163,50 @@ int fs_mh_accept(const fs_phys *p, int64_t C, int32_t N, double *E_old, double *
  * chain's trajectory does not depend on how chains are sharded over GPUs.
  * ws: caller workspace of fs_nf_mh_step_ws_bytes() bytes (256-byte aligned):
  * config f32 [C][2N] | centered f32 [C][2N] | log_q f32 [C] | E_new f64 [C] |
- * W_new f64 [C], each section padded to 256 bytes. */
+ * W_new f64 [C] | centered_old f32 [C][2N] | log_q_old f32 [C] | E_cur f64 [C] |
+ * W_cur f64 [C] (the last four used with FS_MH_HYBRID), each section padded to
+ * 256 bytes. */
 int64_t fs_nf_mh_step_ws_bytes(const fs_flow_dims *d, int64_t C);
 int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C,
                   uint64_t seed, uint64_t step, int64_t chain_offset, double *E_old, double *W_old, double *nll_old,
                   uint64_t *pcg, double *state, uint8_t *state_is_f32, uint8_t *accept,
                   int64_t *attempts, int64_t *accepted, unsigned long long *n_accept,
                   int32_t *err, int flags, void *ws, void *stream);
+
+/* ------------------------------------------------------------------ */
+/* Local moves (MCMC/monte_carlo.py)                                   */
+/* ------------------------------------------------------------------ */
+
+/* n_moves x MonteCarlo.particle_displacement per chain (monte_carlo.py:146-189)
+ * with metropolis_acceptance_particle_move (:191-223), batched over C chains.
+ * The moves are numbered step0+1 .. step0+n_moves (the driver's step counter,
+ * main_algorithm_1.py:204-210); after a move whose number s satisfies
+ *   s % adjust_every == 0   adjust_displacement (:375-403) runs (0: never),
+ *   s % sample_every == 0   a sample() snapshot (:416-444) is written (0: never).
+ * state [C][N][2] float64 (float32 values where state_is_f32[c], nullable = all
+ * float64); E, W [C] running total energy / virial (update_total_energy_virial);
+ * pcg [C][4] as fs_pcg64_seed, pcg_buf [C][2] = {has_uint32, uinteger}, the
+ * 32-bit half numpy buffers for Generator.integers (start at {0,0});
+ * max_disp [C]; attempts / accepted [C] = attempts_ / accepted_displacement
+ * (shared with fs_mh_accept, monte_carlo.py:240, 296); prev_counts [C][2] =
+ * previous_{attempts,accepted}_displacement (needed when adjust_every > 0).
+ * samples_xy [C][S][N][2], samples_ew [C][S][2] = {total_energy, total_virial},
+ * S = fs_local_samples_per_chain(step0, n_moves, sample_every), either nullable.
+ * accept_log [C][n_moves] (nullable), n_accept (nullable) += accepted moves. */
+int fs_local_moves(const fs_phys *p, int64_t C, int32_t N, double *state, const uint8_t *state_is_f32,
+                   double *E, double *W, uint64_t *pcg, uint64_t *pcg_buf, double *max_disp,
+                   int64_t *attempts, int64_t *accepted, int64_t *prev_counts, int64_t n_moves,
+                   int64_t step0, int32_t adjust_every, double target_acceptance, int32_t sample_every,
+                   double *samples_xy, double *samples_ew, uint8_t *accept_log,
+                   unsigned long long *n_accept, void *stream);
+
+/* MonteCarlo.adjust_displacement (monte_carlo.py:375-403) for C chains, arrays
+ * as in fs_local_moves. */
+int fs_adjust_displacement(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,
+                           int64_t *prev_counts, double target_acceptance, void *stream);
+
+/* Number of sample() snapshots moves step0+1 .. step0+n_moves produce. */
+int64_t fs_local_samples_per_chain(int64_t step0, int64_t n_moves, int32_t sample_every);
 
 /* ------------------------------------------------------------------ */
 /* Analysis reductions (hybrid_NF_MCMC/utils.py)                       */

@@ -19,6 +19,9 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
     bench) run bench 600 python bench.py ;;
+    tests_local) run pytest_local 600 python -m pytest tests/test_gpu_local.py -q -rf -x ;;
+    bench_local) run bench_local 400 python tools/bench_local.py ;;
+    prof_local) run rocprof_local 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_local -o run --output-format csv -- python tools/bench_local.py --steps 3 --no-cpu-baseline ;;
     bench_short) run bench_short 400 python bench.py --steps 3 --warmup 1 --cpu-budget 10 ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     counters) run counters 120 rocprofv3 -L ;;
