@@ -216,7 +216,8 @@ int fs_local_moves(const fs_phys *p, int64_t C, int32_t N, double *state, const 
     REQUIRE(N >= 1 && N <= fs::kMaxN, "fs_local_moves: N=%d outside [1, %d]", N, fs::kMaxN);
     REQUIRE(adjust_every <= 0 || (prev_counts && target_acceptance > 0.0),
             "fs_local_moves: adjust_every needs prev_counts and target_acceptance > 0");
-    REQUIRE(sample_every <= 0 || samples_xy || samples_ew, "fs_local_moves: sample_every needs a sample buffer");
+    REQUIRE(fs_local_samples_per_chain(step0, n_moves, sample_every) == 0 || samples_xy || samples_ew,
+            "fs_local_moves: sample_every needs a sample buffer");
     return hip_rc(fs_local_moves_impl(p, C, N, state, state_is_f32, E, W, pcg, pcg_buf, max_disp, attempts, accepted,
                                       prev_counts, n_moves, step0, adjust_every, target_acceptance, sample_every,
                                       samples_xy, samples_ew, accept_log, n_accept, (hipStream_t)stream),

@@ -601,7 +601,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
         const float v = CO[rr * cs + (i + off) % D];
         if (a.out) a.out[gr * D + i] = v;
         if (MODE == MODE_PROPOSE) {
-            const float cfg = __fadd_rn(v, a.B);  // a_ + HALF_BOX in float32 (main_algorithm_1.py:343)
+            const float cfg = v + a.B;  // a_ + HALF_BOX in float32 (main_algorithm_1.py:343)
             if (a.config) a.config[gr * D + i] = cfg;
             if (a.centered) a.centered[gr * D + i] = (float)((double)cfg - a.half_width);
         }

@@ -13,11 +13,15 @@ namespace fs {
 
 // minimum-image distance (simulation_box.py:31-56) with numpy's promotion rules
 __device__ __forceinline__ double dist_f32(float ax, float ay, float bx, float by, double Lx, double Ly) {
-    const float d0 = __fsub_rn(ax, bx), d1 = __fsub_rn(ay, by);
+    // plain operators under fp contract(off): HIP's __f*_rn helpers are defined in a
+    // header outside this pragma and carry the `contract` flag, which lets the backend
+    // fuse t0*t0 + t1*t1 into an FMA (a different float32 rounding than sdot's)
+    const float d0 = ax - bx, d1 = ay - by;
     const double w0 = (double)d0 - Lx * rint((double)d0 / Lx);
     const double w1 = (double)d1 - Ly * rint((double)d1 / Ly);
     const float t0 = (float)w0, t1 = (float)w1;
-    const float s = __fadd_rn(__fmul_rn(t0, t0), __fmul_rn(t1, t1));  // OpenBLAS sdot
+    const float s0 = t0 * t0, s1 = t1 * t1;
+    const float s = s0 + s1;  // OpenBLAS sdot
     // correctly rounded float32 sqrt (np.sqrt on float32): the double sqrt of a float
     // rounded once more to float is exact-rounded (53 >= 2*24+2 bits); the device
     // f32 sqrt instruction is only faithful
@@ -28,7 +32,8 @@ __device__ __forceinline__ double dist_f64(double ax, double ay, double bx, doub
     const double d0 = ax - bx, d1 = ay - by;
     const double t0 = d0 - Lx * rint(d0 / Lx);
     const double t1 = d1 - Ly * rint(d1 / Ly);
-    return __dsqrt_rn(fma(t1, t1, __dmul_rn(t0, t0)));  // OpenBLAS ddot (FMA kernel)
+    const double s0 = t0 * t0;
+    return __dsqrt_rn(fma(t1, t1, s0));  // OpenBLAS ddot (FMA kernel)
 }
 
 // x^6 rounded once from a double-double product (tracks the correctly rounded pow)

@@ -263,18 +263,25 @@ def init_case(NF):
 
 
 def local_case(NF, MC):
-    """Reference local-move traces (monte_carlo.py:146-223, 375-403): float64
-    state, then one accepted big move (state -> float32), then float32 local
-    moves; adjust_displacement every 50 moves (with the big move counted in the
-    displacement counters, monte_carlo.py:240)."""
+    """Reference local-move traces (monte_carlo.py:146-223, 375-403) in three phases
+    of local moves with adjust_displacement every 50 moves, separated by two
+    nf_big_move calls (which count in the displacement counters, monte_carlo.py:240):
+      A) a proposal with a hard-core overlap: E = inf, ratio 0, one draw, rejected
+         (the running energy is replaced by a recomputed total, :299-301);
+      B) a jittered copy of the current state chosen (with the pinned oracle) so
+         that log ratio > 0.02: accepted without a draw, state -> float32.
+    Both decisions are far from the ratio = 1 boundary, so a float32 log_prob that
+    is not bit-identical to torch's cannot change the random stream."""
     from oracle import flow as OF
+    from oracle import physics as OP
     out = {}
-    for N, chains, moves in ((3, 2, 200), (16, 3, 300), (64, 2, 200)):
+    for N, chains, moves in ((3, 2, 200), (16, 3, 200), (64, 2, 150)):
         dims = OF.FlowDims(N=N, L=1, H=32, nb=1, K=5, B=OF.half_box(N))
         sd = OF.random_state_dict(dims, seed=77)
         model = build_ref_model(NF, dims)
         model.load_state_dict(sd, strict=True)
         model.eval()
+        phys = OP.make_phys(N)
         for c in range(chains):
             with contextlib.redirect_stdout(io.StringIO()):
                 if N > 12:
@@ -287,11 +294,11 @@ def local_case(NF, MC):
                                    initial_max_displacement=0.65, target_acceptance=0.5, timing=False,
                                    checking=False, logger=None, seed=42 + c, device=torch.device("cpu"))
                 mc.set_nf_model(model)
+            hw = box.box_size_x / 2
             key = f"N{N}_c{c}"
             out[key + "_init"] = np.asarray(particles, np.float64)
-            acc, E, W, mdisp = [], [], [], []
-            big = []
-            for phase in range(2):
+            acc, E, W, mdisp, big = [], [], [], [], []
+            for phase in range(3):
                 for t in range(moves):
                     a0 = mc.accepted_displacement
                     with contextlib.redirect_stdout(io.StringIO()):
@@ -302,12 +309,32 @@ def local_case(NF, MC):
                     E.append(mc.energy_calculator.total_energy)
                     W.append(mc.energy_calculator.total_virial)
                     mdisp.append(mc.max_displacement)
-                if phase == 0:
-                    # a big move to (nearly) the current state as float32: the state becomes float32
-                    cfg = np.asarray(mc.particles, np.float32)
-                    with contextlib.redirect_stdout(io.StringIO()):
-                        big.append(bool(mc.nf_big_move(cfg)))
-                    out[key + "_bigcfg"] = cfg
+                if phase == 2:
+                    break
+                cur = np.asarray(mc.particles, np.float64)
+                if phase == 0:  # A: particle 1 on top of particle 0
+                    cfg = cur.astype(np.float32)
+                    cfg[1] = cfg[0] + np.float32(0.1)
+                else:           # B: decisive accept
+                    def nll(x):
+                        t = torch.tensor((np.asarray(x, np.float64) - hw).reshape(1, -1), dtype=torch.float)
+                        return -OF.log_prob(sd, t, dims).item()
+                    E_old, nll_old = mc.energy_calculator.total_energy, nll(cur)
+                    cfg = None
+                    for sigma in (0.02, 0.01, 0.005, 0.002, 0.001):
+                        for s in range(400):
+                            cand = np.mod(cur + np.random.default_rng(s).normal(0, sigma, cur.shape),
+                                          box.box_size_x).astype(np.float32)
+                            lr = -(OP.total_energy(cand, phys)[0] - E_old) - (nll(cand) - nll_old)
+                            if lr > 0.02:
+                                cfg = cand
+                                break
+                        if cfg is not None:
+                            break
+                    assert cfg is not None, key
+                with contextlib.redirect_stdout(io.StringIO()):
+                    big.append(bool(mc.nf_big_move(cfg)))
+                out[key + f"_bigcfg{phase}"] = cfg
             st = mc.rng.bit_generator.state
             out[key + "_accept"] = np.array(acc, np.int8)
             out[key + "_E"] = np.array(E)
@@ -322,7 +349,7 @@ def local_case(NF, MC):
             out[key + "_pcg"] = np.array([s_["state"] >> 64, s_["state"] & (2**64 - 1), s_["inc"] >> 64,
                                           s_["inc"] & (2**64 - 1), st["has_uint32"], st["uinteger"]], np.uint64)
             out[key + "_seed"] = np.int64(42 + c)
-            print(f"local {key}: accepted {sum(acc)}/{2 * moves}, big {big}, maxdisp {mc.max_displacement:.4f}")
+            print(f"local {key}: accepted {sum(acc)}/{3 * moves}, big {big}, maxdisp {mc.max_displacement:.4f}")
         out[f"N{N}_chains"] = np.int64(chains)
         out[f"N{N}_moves"] = np.int64(moves)
         out[f"N{N}_flow_seed"] = np.int64(77)
@@ -342,10 +369,13 @@ def pcg_case():
     print("pcg64: ok")
 
 
-def main():
+def main(only=None):
     NF, MC, SimulationBox = import_reference()
     from oracle import flow as OF
     torch.set_num_threads(1)
+    if only == "local":
+        local_case(NF, MC)
+        return
     flow_case(NF, "tiny", OF.FlowDims(N=4, L=2, H=32, nb=1, K=5, B=OF.half_box(4)), 1, 64, True)
     flow_case(NF, "n16", OF.FlowDims(N=16, L=3, H=64, nb=2, K=8, B=OF.half_box(16)), 2, 48, False)
     flow_case(NF, "n64", OF.FlowDims(N=64, L=2, H=128, nb=2, K=32, B=OF.half_box(64)), 3, 16, False)
@@ -358,4 +388,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

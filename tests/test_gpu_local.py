@@ -6,6 +6,7 @@ FS_MH_HYBRID big move that follows local moves).
    MonteCarlo and through one batched launch: identical per-move accept flags,
    max_displacement sequence, float64 -> float32 switch, final particles, counters
    and the full PCG64 state (including the buffered 32-bit half); E/W within 1e-12.
+   Both big moves are decisive (an overlap reject, a log-ratio > 0.02 accept).
 2. Random batches at N = 1, 5, 16, 33, 64 with mixed float32/float64 chains against
    the C oracle (bit-exact accept logs, states, max_displacement, RNG state).
 3. Sample snapshots (sample(), monte_carlo.py:416-444) at the driver's schedule.
@@ -55,7 +56,7 @@ def test_reference_local_traces_dropin(N):
                     target_acceptance=0.5, seed=int(f[k + "_seed"]))
     mc.set_nf_model(model)
     acc, E, md = [], [], []
-    for phase in range(2):
+    for phase in range(3):
         for t in range(moves):
             a0 = mc.accepted_displacement
             mc.particle_displacement()
@@ -64,8 +65,8 @@ def test_reference_local_traces_dropin(N):
             acc.append(mc.accepted_displacement - a0)
             E.append(mc.energy_calculator.total_energy)
             md.append(mc.max_displacement)
-        if phase == 0:
-            assert mc.nf_big_move(f[k + "_bigcfg"]) == bool(f[k + "_big"][0])
+        if phase < 2:
+            assert mc.nf_big_move(f[k + f"_bigcfg{phase}"]) == bool(f[k + "_big"][phase])
     np.testing.assert_array_equal(np.array(acc, np.int8), f[k + "_accept"])
     assert all(_close(a, b) for a, b in zip(E, f[k + "_E"]))
     np.testing.assert_array_equal(np.array(md), f[k + "_maxdisp"])
@@ -90,14 +91,15 @@ def test_reference_local_traces_batched(N):
     seeds = np.array([int(f[k + "_seed"]) for k in keys], np.uint64)
     b = BatchedMonteCarlo(None, init, Physics(L, L), seeds, initial_max_displacement=0.65)
     logs, ews = [], []
-    for phase in range(2):
+    for phase in range(3):
         _, sew, log = b.local_moves(moves, adjust_every=50, sample_every=1, log_accepts=True)
         logs.append(log.cpu().numpy())
         ews.append(sew.cpu().numpy())
         if phase == 0:
             b.set_model(model)
-            acc = b.nf_big_move(torch.from_numpy(np.stack([f[k + "_bigcfg"] for k in keys])))
-            np.testing.assert_array_equal(acc.cpu().numpy().astype(bool), [bool(f[k + "_big"][0]) for k in keys])
+        if phase < 2:
+            acc = b.nf_big_move(torch.from_numpy(np.stack([f[k + f"_bigcfg{phase}"] for k in keys])))
+            np.testing.assert_array_equal(acc.cpu().numpy().astype(bool), [bool(f[k + "_big"][phase]) for k in keys])
     log = np.concatenate(logs, axis=1)
     ew = np.concatenate(ews, axis=1)
     for c, k in enumerate(keys):

@@ -39,16 +39,16 @@ def test_local_trace_matches_reference(N):
         ch = OP.LocalChain(f[k + "_init"], int(f[k + "_seed"]), phys)
         acc = []
         E, W, md = [], [], []
-        for phase in range(2):
+        for phase in range(3):
             for t in range(moves):
                 acc.append(ch.local_moves(1, adjust_every=50, phase=t)[0])
                 E.append(ch.E[0])
                 W.append(ch.W[0])
                 md.append(ch.max_disp[0])
-            if phase == 0:
-                cfg = f[k + "_bigcfg"]
+            if phase < 2:
+                cfg = f[k + f"_bigcfg{phase}"]
                 big = ch.big_move(cfg, _nll(sd, dims, ch.particles, hw), _nll(sd, dims, cfg, hw))
-                assert big == bool(f[k + "_big"][0])
+                assert big == bool(f[k + "_big"][phase])
         np.testing.assert_array_equal(np.array(acc, np.int8), f[k + "_accept"])
         for a, b in zip(E, f[k + "_E"]):
             assert _close(a, b)
