@@ -21,6 +21,8 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     tests_local) run pytest_local 600 python -m pytest tests/test_gpu_local.py -q -rf -x ;;
     bench_local) run bench_local 400 python tools/bench_local.py ;;
+    pmc_local) run pmc_local 400 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/pmc_local -o run --output-format csv -- python tools/bench_local.py --steps 2 --no-cpu-baseline ;;
+    pmc_local_wait) run pmc_local_wait 400 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_local_wait -o run --output-format csv -- python tools/bench_local.py --steps 2 --no-cpu-baseline ;;
     prof_local) run rocprof_local 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_local -o run --output-format csv -- python tools/bench_local.py --steps 3 --no-cpu-baseline ;;
     bench_short) run bench_short 400 python bench.py --steps 3 --warmup 1 --cpu-budget 10 ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
