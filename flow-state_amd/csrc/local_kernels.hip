@@ -77,8 +77,33 @@ __global__ void adjust_kernel(int64_t C, double *max_disp, const int64_t *attemp
     prev[2 * c + 1] = pc;
 }
 
+// group broadcast of lane `src` (group-relative); a whole-wave group uses v_readlane
+// with a wave-uniform index, smaller groups a ds_bpermute shuffle
 template <int LPC>
-__global__ void __launch_bounds__(64 * kLocalWaves) local_moves_kernel(LocalArgs a) {
+__device__ __forceinline__ double bcast(double v, int src) {
+    if constexpr (LPC == 64) {
+        const uint64_t u = __double_as_longlong(v);
+        const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, src);
+        const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
+        return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+    } else {
+        return __shfl(v, src, LPC);
+    }
+}
+
+template <int LPC>
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    if constexpr (LPC == 64) {  // one chain per wave: keep the chain's scalars in SGPRs
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+        return ((uint64_t)hi << 32) | lo;
+    } else {
+        return v;
+    }
+}
+
+template <int LPC>
+__global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 1) local_moves_kernel(LocalArgs a) {
     constexpr int G = 64 / LPC;  // chains per wave
     __shared__ double lds[kLocalWaves][4][64];
     __shared__ double res[kLocalWaves][G][4];
@@ -97,16 +122,22 @@ __global__ void __launch_bounds__(64 * kLocalWaves) local_moves_kernel(LocalArgs
     }
     Pcg64 rng;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) rng.s[i] = a.pcg[4 * c + i];
-    rng.has = (uint32_t)a.pcg_buf[2 * c];
-    rng.buf = (uint32_t)a.pcg_buf[2 * c + 1];
+    for (int i = 0; i < 4; ++i) rng.s[i] = uniform_u64<LPC>(a.pcg[4 * c + i]);
+    rng.has = (uint32_t)uniform_u64<LPC>(a.pcg_buf[2 * c]);
+    rng.buf = (uint32_t)uniform_u64<LPC>(a.pcg_buf[2 * c + 1]);
     double E = a.E[c], W = a.W ? a.W[c] : 0.0, md = a.max_disp[c];
     int64_t att = a.attempts[c], acc_n = a.accepted[c];
     int64_t prev_att = a.prev ? a.prev[2 * c] : 0, prev_acc = a.prev ? a.prev[2 * c + 1] : 0;
     const double sr6c = pow6(1.0 / P.r_cut);
     const double e_cut = 4.0 * (sr6c * sr6c - sr6c);
+    const double iLx = 1.0 / P.Lx, iLy = 1.0 / P.Ly;
     const int n = N - 1;
+    const int nfull = n - (n % 8);
     const uint64_t gmask = (LPC == 64) ? ~0ull : (((1ull << LPC) - 1ull) << gb);
+    // double-well role of this lane: 0/1 = old position well 0/1, 2/3 = new position
+    const int dw_well = gl & 1;
+    const bool dw_lane = gl < 4 && dw_well < P.num_wells;
+    const double dw_V0 = P.V0[dw_well];
     int64_t samp = 0;
     unsigned long long n_acc_local = 0;
 
@@ -114,7 +145,7 @@ __global__ void __launch_bounds__(64 * kLocalWaves) local_moves_kernel(LocalArgs
         const int64_t step = a.step0 + t + 1;
         att += 1;
         const int p = (int)pcg64_integers(rng, (uint32_t)N);
-        const double ox = __shfl(xj, p, LPC), oy = __shfl(yj, p, LPC);
+        const double ox = bcast<LPC>(xj, p), oy = bcast<LPC>(yj, p);
         const double d0 = (pcg64_double(rng) - 0.5) * md;
         const double d1 = (pcg64_double(rng) - 0.5) * md;
         double nx, ny;
@@ -130,10 +161,15 @@ __global__ void __launch_bounds__(64 * kLocalWaves) local_moves_kernel(LocalArgs
         double eo = 0.0, wo = 0.0, en = 0.0, wn = 0.0;
         bool ho = false, hn = false;
         if (act) {
-            const double ro = f32 ? dist_f32((float)ox, (float)oy, (float)xj, (float)yj, P.Lx, P.Ly)
-                                  : dist_f64(ox, oy, xj, yj, P.Lx, P.Ly);
-            const double rn = f32 ? dist_f32((float)nx, (float)ny, (float)xj, (float)yj, P.Lx, P.Ly)
-                                  : dist_f64(nx, ny, xj, yj, P.Lx, P.Ly);
+            double ro, rn;
+            if (f32) {
+                const float fx = (float)xj, fy = (float)yj;
+                ro = dist_f32((float)ox, (float)oy, fx, fy, P.Lx, P.Ly, iLx, iLy);
+                rn = dist_f32((float)nx, (float)ny, fx, fy, P.Lx, P.Ly, iLx, iLy);
+            } else {
+                ro = dist_f64(ox, oy, xj, yj, P.Lx, P.Ly, iLx, iLy);
+                rn = dist_f64(nx, ny, xj, yj, P.Lx, P.Ly, iLx, iLy);
+            }
             ho = ro < P.r_core;
             hn = rn < P.r_core;
             lj_pair(ro, P.r_cut, e_cut, eo, wo);
@@ -146,22 +182,36 @@ __global__ void __launch_bounds__(64 * kLocalWaves) local_moves_kernel(LocalArgs
         }
         const bool hit_old = (__ballot(ho) & gmask) != 0;
         const bool hit_new = (__ballot(hn) & gmask) != 0;
-        // double-well terms: lane 0/1 = old position well 0/1, lane 2/3 = new position
         double dw = 0.0;
-        if (gl < 4 && (gl & 1) < P.num_wells)
-            dw = dw_term(gl < 2 ? ox : nx, gl < 2 ? oy : ny, gl & 1, P.Lx, P.Ly, P.V0[gl & 1], P.r0, P.k);
+        if (dw_lane)
+            dw = dw_term(gl < 2 ? ox : nx, gl < 2 ? oy : ny, dw_well, P.Lx, P.Ly, dw_V0, P.r0, P.k, iLx, iLy);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // numpy pairwise sums of the four compacted rows
+        // numpy pairwise sums of the four compacted rows: eno, viro, enn, virn
+        double sums[4];
         if (n < 8) {
-            if (gl < 4) {
-                double r = 0.0;
+            double r = 0.0;
+            if (gl < 4)
                 for (int k = 0; k < n; ++k) r += lds[wid][gl][gb + k];
-                res[wid][g][gl] = r;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sums[q] = bcast<LPC>(r, q);
+        } else if constexpr (LPC == 64) {
+            // lanes 8*arr + k: partial sum k of array arr, tree by xor-shuffles, tail on lane 8*arr
+            double r = 0.0;
+            if (gl < 32) {
+                const int arr = gl >> 3, k = gl & 7;
+                r = lds[wid][arr][k];
+                for (int b = 8; b < nfull; b += 8) r += lds[wid][arr][b + k];
             }
+            r += __shfl_xor(r, 1, 64);
+            r += __shfl_xor(r, 2, 64);
+            r += __shfl_xor(r, 4, 64);
+            if (gl < 32 && (gl & 7) == 0)
+                for (int i = nfull; i < n; ++i) r += lds[wid][gl >> 3][i];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sums[q] = bcast<LPC>(r, 8 * q);
         } else {
-            const int nfull = n - (n % 8);
             for (int ak = gl; ak < 32; ak += LPC) {  // LPC >= 16 here (N > 8)
                 const int arr = ak >> 3, k = ak & 7;
                 double r = lds[wid][arr][gb + k];
@@ -174,20 +224,18 @@ __global__ void __launch_bounds__(64 * kLocalWaves) local_moves_kernel(LocalArgs
                     res[wid][g][arr] = r;
                 }
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sums[q] = res[wid][g][q];
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // V = 0; V += term(well 0); V += term(well 1)   (potential.py:96-112)
-        const double dw0o = __shfl(dw, 0, LPC), dw1o = __shfl(dw, 1, LPC);
-        const double dw0n = __shfl(dw, 2, LPC), dw1n = __shfl(dw, 3, LPC);
-        double eno = res[wid][g][0], viro = res[wid][g][1];
-        double enn = res[wid][g][2], virn = res[wid][g][3];
-        if (P.num_wells > 0) {
-            double vo = 0.0 + dw0o, vn = 0.0 + dw0n;
+        double eno = sums[0], viro = sums[1], enn = sums[2], virn = sums[3];
+        if (P.num_wells > 0) {  // V = 0; V += term(well 0); V += term(well 1)  (potential.py:96-112)
+            double vo = 0.0 + bcast<LPC>(dw, 0), vn = 0.0 + bcast<LPC>(dw, 2);
             if (P.num_wells > 1) {
-                vo += dw1o;
-                vn += dw1n;
+                vo += bcast<LPC>(dw, 1);
+                vn += bcast<LPC>(dw, 3);
             }
             eno += vo;
             enn += vn;

@@ -11,14 +11,26 @@
 
 namespace fs {
 
+// np.round(d / L) (round half to even) without the division: q = d * (1/L) is within
+// a few ulps of the correctly rounded quotient, so rint(q) can only differ when q is
+// within that distance of a half-integer; those (rare) lanes take the exact division.
+// |d| <= 2L on every call site, so 1e-12 is many ulps of q.
+__device__ __forceinline__ double rint_div(double d, double L, double invL) {
+    const double q = d * invL;
+    const double k = rint(q);
+    if (__builtin_expect(fabs(fabs(q - k) - 0.5) < 1e-12, 0)) return rint(d / L);
+    return k;
+}
+
 // minimum-image distance (simulation_box.py:31-56) with numpy's promotion rules
-__device__ __forceinline__ double dist_f32(float ax, float ay, float bx, float by, double Lx, double Ly) {
+__device__ __forceinline__ double dist_f32(float ax, float ay, float bx, float by, double Lx, double Ly,
+                                           double iLx, double iLy) {
     // plain operators under fp contract(off): HIP's __f*_rn helpers are defined in a
     // header outside this pragma and carry the `contract` flag, which lets the backend
     // fuse t0*t0 + t1*t1 into an FMA (a different float32 rounding than sdot's)
     const float d0 = ax - bx, d1 = ay - by;
-    const double w0 = (double)d0 - Lx * rint((double)d0 / Lx);
-    const double w1 = (double)d1 - Ly * rint((double)d1 / Ly);
+    const double w0 = (double)d0 - Lx * rint_div((double)d0, Lx, iLx);
+    const double w1 = (double)d1 - Ly * rint_div((double)d1, Ly, iLy);
     const float t0 = (float)w0, t1 = (float)w1;
     const float s0 = t0 * t0, s1 = t1 * t1;
     const float s = s0 + s1;  // OpenBLAS sdot
@@ -28,10 +40,11 @@ __device__ __forceinline__ double dist_f32(float ax, float ay, float bx, float b
     return (double)(float)__dsqrt_rn((double)s);
 }
 
-__device__ __forceinline__ double dist_f64(double ax, double ay, double bx, double by, double Lx, double Ly) {
+__device__ __forceinline__ double dist_f64(double ax, double ay, double bx, double by, double Lx, double Ly,
+                                           double iLx, double iLy) {
     const double d0 = ax - bx, d1 = ay - by;
-    const double t0 = d0 - Lx * rint(d0 / Lx);
-    const double t1 = d1 - Ly * rint(d1 / Ly);
+    const double t0 = d0 - Lx * rint_div(d0, Lx, iLx);
+    const double t1 = d1 - Ly * rint_div(d1, Ly, iLy);
     const double s0 = t0 * t0;
     return __dsqrt_rn(fma(t1, t1, s0));  // OpenBLAS ddot (FMA kernel)
 }
@@ -136,11 +149,11 @@ __device__ __forceinline__ uint32_t pcg64_integers(Pcg64 &g, uint32_t n) {
 
 // one well's term V0_i * (1 - transition) of double_well_potential (potential.py:98-112)
 __device__ __forceinline__ double dw_term(double x, double y, int well, double Lx, double Ly, double V0, double r0,
-                                          double k) {
+                                          double k, double iLx, double iLy) {
     const double cx = (well == 0) ? Lx / 4.0 : 3.0 * Lx / 4.0, cy = Ly / 2.0;
     double dx = x - cx, dy = y - cy;
-    dx -= Lx * rint(dx / Lx);
-    dy -= Ly * rint(dy / Ly);
+    dx -= Lx * rint_div(dx, Lx, iLx);
+    dy -= Ly * rint_div(dy, Ly, iLy);
     const double r = sqrt(dx * dx + dy * dy);
     const double tr = 0.5 * (1.0 + tanh(k * (r - r0)));
     return V0 * (1.0 - tr);
@@ -148,6 +161,10 @@ __device__ __forceinline__ double dw_term(double x, double y, int well, double L
 
 // numpy floor remainder (npy_divmod) for SimulationBox.apply_pbc (simulation_box.py:19-29)
 __device__ __forceinline__ double np_remainder(double a, double b) {
+    // fast paths (b > 0): fmod is exact, so these equal the general branch bit for bit
+    if (a > 0.0 && a < b) return a;
+    if (a < 0.0 && a > -b) return a + b;
+    if (a >= b && a < 2.0 * b) return a - b;  // Sterbenz: exact
     double mod = fmod(a, b);
     if (mod != 0.0) {
         if ((b < 0) != (mod < 0)) mod += b;

@@ -67,6 +67,7 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, const void *__re
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const double sr6c = pow6(1.0 / p.r_cut);
     const double e_cut = 4.0 * (sr6c * sr6c - sr6c);
+    const double iLx = 1.0 / p.Lx, iLy = 1.0 / p.Ly;
     const int i = lane;
     const int n = (i < N - 1) ? N - 1 - i : 0;
     const double xi = sx[wid][i < N ? i : 0], yi = sy[wid][i < N ? i : 0];
@@ -74,8 +75,9 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, const void *__re
     uint64_t mask = 0;
     auto pair = [&](int t, double &e, double &w) {
         const int j = i + 1 + t;
-        const double r = as_f32 ? dist_f32((float)xi, (float)yi, (float)sx[wid][j], (float)sy[wid][j], p.Lx, p.Ly)
-                             : dist_f64(xi, yi, sx[wid][j], sy[wid][j], p.Lx, p.Ly);
+        const double r = as_f32 ? dist_f32((float)xi, (float)yi, (float)sx[wid][j], (float)sy[wid][j], p.Lx, p.Ly,
+                                           iLx, iLy)
+                                : dist_f64(xi, yi, sx[wid][j], sy[wid][j], p.Lx, p.Ly, iLx, iLy);
         hit |= r < p.r_core;
         if (r <= p.r_cut) mask |= (uint64_t)1 << j;
         lj_pair(r, p.r_cut, e_cut, e, w);
@@ -119,8 +121,8 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, const void *__re
         for (int k = 0; k < p.num_wells && k < 2; ++k) {
             const double cx = (k == 0) ? p.Lx / 4.0 : 3.0 * p.Lx / 4.0;
             double dx = xi - cx, dy = yi - cy;
-            dx -= p.Lx * rint(dx / p.Lx);
-            dy -= p.Ly * rint(dy / p.Ly);
+            dx -= p.Lx * rint_div(dx, p.Lx, iLx);
+            dy -= p.Ly * rint_div(dy, p.Ly, iLy);
             const double r = sqrt(dx * dx + dy * dy);
             const double tr = 0.5 * (1.0 + tanh(p.k * (r - p.r0)));
             v += p.V0[k] * (1.0 - tr);
