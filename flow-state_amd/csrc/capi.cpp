@@ -244,4 +244,25 @@ int fs_well_stats(const fs_phys *p, const double *pos, int64_t C, int32_t N, int
     return hip_rc(fs_well_stats_impl(p, pos, C, N, counts, (hipStream_t)stream), "fs_well_stats");
 }
 
+int fs_classify_wells(const void *pos, int pos_is_f32, int64_t M, int32_t N, double half_box, double r0,
+                      uint8_t *cls, uint8_t *state, double *avg_x, void *stream) {
+    REQUIRE(pos && M >= 0 && N >= 1 && half_box > 0.0, "fs_classify_wells: invalid arguments");
+    return hip_rc(fs_classify_wells_impl(pos, pos_is_f32, M, N, half_box, r0, cls, state, avg_x, (hipStream_t)stream),
+                  "fs_classify_wells");
+}
+
+int fs_pair_hist(const void *pos, int pos_is_f32, int64_t M, int32_t N, double bound, const double *edges,
+                 int32_t nbins, int32_t *counts, void *stream) {
+    REQUIRE(pos && edges && counts && M >= 0 && N >= 1 && bound > 0.0, "fs_pair_hist: invalid arguments");
+    REQUIRE(N <= 256 && nbins >= 1 && nbins <= 128, "fs_pair_hist: N <= 256 and 1 <= nbins <= 128 (got %d, %d)", N,
+            nbins);
+    return hip_rc(fs_pair_hist_impl(pos, pos_is_f32, M, N, bound, edges, nbins, counts, (hipStream_t)stream),
+                  "fs_pair_hist");
+}
+
+int fs_rdf_mean(const int32_t *counts, int64_t M, int32_t nbins, const double *denom, double *g_r, void *stream) {
+    REQUIRE(counts && denom && g_r && M >= 1 && nbins >= 1, "fs_rdf_mean: invalid arguments");
+    return hip_rc(fs_rdf_mean_impl(counts, M, nbins, denom, g_r, (hipStream_t)stream), "fs_rdf_mean");
+}
+
 }  // extern "C"

@@ -29,6 +29,11 @@ hipError_t fs_mh_accept_impl(const fs_phys *p, int64_t C, int N, double *E_old, 
                              const double *W_cur = nullptr);
 hipError_t fs_adjust_displacement_impl(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,
                                        int64_t *prev, double target, hipStream_t st);
+hipError_t fs_classify_wells_impl(const void *pos, int f32, int64_t M, int N, double half_box, double r0,
+                                  uint8_t *cls, uint8_t *state, double *avg_x, hipStream_t st);
+hipError_t fs_pair_hist_impl(const void *pos, int f32, int64_t M, int N, double bound, const double *edges, int nb,
+                             int32_t *counts, hipStream_t st);
+hipError_t fs_rdf_mean_impl(const int32_t *counts, int64_t M, int nb, const double *denom, double *g, hipStream_t st);
 hipError_t fs_center_impl(const double *state, int64_t n, double hw, float *out, hipStream_t st);
 hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state, const uint8_t *is_f32,
                                double *E, double *W, uint64_t *pcg, uint64_t *pcg_buf, double *max_disp,

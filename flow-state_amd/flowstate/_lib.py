@@ -58,6 +58,11 @@ _SIGS = {
                        + [_I64, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_int32] + [_P] * 5),
     "fs_local_samples_per_chain": (_I64, [_I64, _I64, ctypes.c_int32]),
     "fs_adjust_displacement": (ctypes.c_int, [_I64, _P, _P, _P, _P, ctypes.c_double, _P]),
+    "fs_classify_wells": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                                          _P, _P, _P, _P]),
+    "fs_pair_hist": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, _P, ctypes.c_int32,
+                                    _P, _P]),
+    "fs_rdf_mean": (ctypes.c_int, [_P, _I64, ctypes.c_int32, _P, _P, _P]),
     "fs_hist2d": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_double, _P, ctypes.c_int32, _P, _P]),
     "fs_well_stats": (ctypes.c_int, [_PH, _P, _I64, ctypes.c_int32, _P, _P]),
 }

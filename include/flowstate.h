@@ -225,6 +225,28 @@ int fs_hist2d(const double *pos, int64_t C, int32_t N, double shift, const doubl
 int fs_well_stats(const fs_phys *p, const double *pos, int64_t C, int32_t N, int64_t *counts,
                   void *stream);
 
+/* classify_particles (utils.py:104-141) + the per-configuration part of
+ * calculate_well_statistics (utils.py:61-101) for M configurations
+ * pos [M][N][2] (float32 if pos_is_f32, else float64; numpy's promotion of the
+ * Python-float centres / radius into that dtype is reproduced):
+ *   cls [M][N]  0 = 'A' (left well), 1 = 'B', 2 = 'Outside'      (nullable)
+ *   state [M]   1 = all in A, 2 = all in B, 0 = neither           (nullable)
+ *   avg_x [M]   np.mean(config[:, 0]) in the array dtype          (nullable) */
+int fs_classify_wells(const void *pos, int pos_is_f32, int64_t M, int32_t N, double half_box, double r0,
+                      uint8_t *cls, uint8_t *state, double *avg_x, void *stream);
+
+/* Pair-distance histogram of calculate_pair_correlation (utils.py:546-556) per
+ * configuration: minimum image with box 2*bound in the array dtype, all ordered
+ * pairs, zero distances dropped, np.histogram over edges [nbins+1] (f64, right
+ * edge inclusive).  counts [M][nbins] int32 (overwritten). */
+int fs_pair_hist(const void *pos, int pos_is_f32, int64_t M, int32_t N, double bound, const double *edges,
+                 int32_t nbins, int32_t *counts, void *stream);
+
+/* g(r) = mean over the M configurations of counts[m][k] / denom[k]
+ * (utils.py:558-566: per-configuration float64 ratio, pandas mean = numpy
+ * pairwise sum / M).  g_r [nbins] f64. */
+int fs_rdf_mean(const int32_t *counts, int64_t M, int32_t nbins, const double *denom, double *g_r, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

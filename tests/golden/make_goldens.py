@@ -356,6 +356,62 @@ def local_case(NF, MC):
     np.savez_compressed(os.path.join(HERE, "local_trace.npz"), **out)
 
 
+def analysis_case():
+    """classify_particles / calculate_well_statistics / calculate_pair_correlation of
+    hybrid_NF_MCMC/utils.py (loaded by path: the name `utils` is taken by MCMC/utils.py)
+    on float64 and float32 configuration sets, including all-in-A / all-in-B
+    configurations, particles across the periodic edges and on the well radius."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("hyb_utils", os.path.join(LINK, "hybrid_NF_MCMC", "utils.py"))
+    U = importlib.util.module_from_spec(spec)
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        spec.loader.exec_module(U)
+    out = {}
+    N, M = 16, 240
+    hb = ((N / 0.03) ** (1 / 2)) / 2  # HALF_BOX, main_algorithm_1.py:50
+    L = 2 * hb
+    rng = np.random.default_rng(123)
+    cfg = rng.random((M, N, 2)) * L
+    for m in range(0, M, 3):  # all in well A
+        cfg[m, :, 0] = L / 4 + rng.normal(0, 0.35, N)
+        cfg[m, :, 1] = L / 2 + rng.normal(0, 0.35, N)
+    for m in range(1, M, 5):  # all in well B
+        cfg[m, :, 0] = 3 * L / 4 + rng.normal(0, 0.35, N)
+        cfg[m, :, 1] = L / 2 + rng.normal(0, 0.35, N)
+    cfg[2, :, 0] = rng.choice([1e-9, L - 1e-9, 0.0], N)  # across the periodic edge
+    rad = 1.2 * 1.1
+    ang = rng.random(N) * 2 * np.pi
+    cfg[4, :, 0] = L / 4 + rad * np.cos(ang)  # on the well radius (both dtypes)
+    cfg[4, :, 1] = L / 2 + rad * np.sin(ang)
+    for name, arr in (("f64", cfg), ("f32", cfg.astype(np.float32))):
+        cls = U.classify_particles(arr, hb, 1.2)
+        ax, pa, pb, dF, runs = U.calculate_well_statistics(arr, 3, hb, 1.2)
+        out[f"{name}_cfg"] = arr
+        out[f"{name}_cls"] = cls.astype("U7")
+        out[f"{name}_avg_x"] = np.array(ax)
+        out[f"{name}_avg_x_dtype32"] = np.int8(np.asarray(ax).dtype == np.float32)
+        out[f"{name}_p_a"] = np.array(pa)
+        out[f"{name}_p_b"] = np.array(pb)
+        out[f"{name}_dF"] = np.array(dF, np.float64)
+        out[f"{name}_runs"] = np.array(runs)
+    out["half_box"] = np.float64(hb)
+    # pair correlation of centred float32 samples (as main_algorithm_1.py:354 passes a_ - HALF_BOX)
+    samp = (rng.random((150, N, 2)) * L).astype(np.float32)
+    samp[0, 1] = samp[0, 0]  # a coincident pair (distance 0 is dropped)
+    cen = samp - hb
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        r, g = U.calculate_pair_correlation(cen, N, hb, dr=hb / 50)
+        r2, g2 = U.calculate_pair_correlation(cen.astype(np.float64)[:40], N, hb, dr=hb / 30)
+    out["rdf_samples"] = cen
+    out["rdf_r"] = r
+    out["rdf_g"] = np.asarray(g, np.float64)
+    out["rdf64_r"] = r2
+    out["rdf64_g"] = np.asarray(g2, np.float64)
+    np.savez_compressed(os.path.join(HERE, "analysis.npz"), **out)
+    print("analysis: ok", np.bincount([{"A": 0, "B": 1, "Outside": 2}[c] for c in out["f64_cls"].ravel()]))
+
+
 def pcg_case():
     seeds = np.arange(42, 42 + 64)
     st = np.zeros((64, 4), np.uint64)
@@ -376,6 +432,9 @@ def main(only=None):
     if only == "local":
         local_case(NF, MC)
         return
+    if only == "analysis":
+        analysis_case()
+        return
     flow_case(NF, "tiny", OF.FlowDims(N=4, L=2, H=32, nb=1, K=5, B=OF.half_box(4)), 1, 64, True)
     flow_case(NF, "n16", OF.FlowDims(N=16, L=3, H=64, nb=2, K=8, B=OF.half_box(16)), 2, 48, False)
     flow_case(NF, "n64", OF.FlowDims(N=64, L=2, H=128, nb=2, K=32, B=OF.half_box(64)), 3, 16, False)
@@ -385,6 +444,7 @@ def main(only=None):
     pcg_case()
     init_case(NF)
     local_case(NF, MC)
+    analysis_case()
 
 
 if __name__ == "__main__":
