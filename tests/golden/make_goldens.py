@@ -297,7 +297,7 @@ def local_case(NF, MC):
             hw = box.box_size_x / 2
             key = f"N{N}_c{c}"
             out[key + "_init"] = np.asarray(particles, np.float64)
-            acc, E, W, mdisp, big = [], [], [], [], []
+            acc, E, W, mdisp, big, samp = [], [], [], [], [], []
             for phase in range(3):
                 for t in range(moves):
                     a0 = mc.accepted_displacement
@@ -305,6 +305,9 @@ def local_case(NF, MC):
                         mc.particle_displacement()
                         if (t + 1) % 50 == 0:
                             mc.adjust_displacement()
+                        if (t + 1) % 75 == 0:  # sample() tuples (monte_carlo.py:416-444)
+                            s_ = mc.sample(t + 1)
+                            samp.append([float(v) for v in s_[:6]])
                     acc.append(mc.accepted_displacement - a0)
                     E.append(mc.energy_calculator.total_energy)
                     W.append(mc.energy_calculator.total_virial)
@@ -340,6 +343,7 @@ def local_case(NF, MC):
             out[key + "_E"] = np.array(E)
             out[key + "_W"] = np.array(W)
             out[key + "_maxdisp"] = np.array(mdisp)
+            out[key + "_samples"] = np.array(samp)
             out[key + "_big"] = np.array(big)
             out[key + "_final"] = np.asarray(mc.particles)
             out[key + "_final_dtype32"] = np.int8(np.asarray(mc.particles).dtype == np.float32)

@@ -19,6 +19,7 @@ import numpy as np
 import pytest
 import torch
 
+from flowstate import io
 from flowstate.MCMC import BatchedMonteCarlo, MonteCarlo, Physics, SimulationBox
 from flowstate.models import flow_from_state_dict
 from oracle import flow as OF
@@ -90,11 +91,16 @@ def test_reference_local_traces_batched(N):
     init = np.stack([f[k + "_init"] for k in keys])
     seeds = np.array([int(f[k + "_seed"]) for k in keys], np.uint64)
     b = BatchedMonteCarlo(None, init, Physics(L, L), seeds, initial_max_displacement=0.65)
-    logs, ews = [], []
+    logs, ews, tuples = [], [], [[] for _ in keys]
     for phase in range(3):
-        _, sew, log = b.local_moves(moves, adjust_every=50, sample_every=1, log_accepts=True)
+        sxy, sew, log = b.local_moves(moves, adjust_every=50, sample_every=1, log_accepts=True)
         logs.append(log.cpu().numpy())
         ews.append(sew.cpu().numpy())
+        # the driver's sample() every 75 steps, from the per-step snapshots
+        for c in range(C):
+            for tup in io.sample_tuples(b, sxy, sew, c, 0, 1, moves):
+                if tup[0] % 75 == 0:
+                    tuples[c].append(tup)
         if phase == 0:
             b.set_model(model)
         if phase < 2:
@@ -112,6 +118,32 @@ def test_reference_local_traces_batched(N):
         assert b.attempts[c].item() == f[k + "_attempts"] and b.accepted[c].item() == f[k + "_accepted"]
         np.testing.assert_array_equal(_u64(b.pcg[c]), f[k + "_pcg"][:4])
         np.testing.assert_array_equal(_u64(b.pcg_buf[c]), f[k + "_pcg"][4:])
+        ref = f[k + "_samples"]
+        assert len(tuples[c]) == len(ref)
+        for tup, r in zip(tuples[c], ref):
+            assert tup[0] == r[0] and tup[2] == r[2] and tup[4] == r[4] and tup[5] == r[5]
+            assert _close(tup[1], r[1]) and _close(tup[3], r[3])
+
+
+def test_writers_round_trip(tmp_path):
+    """sampled_data.csv / configs .npy in the driver's format (main_algorithm_1.py:499-547)."""
+    import ast
+    import csv
+
+    N, C = 16, 4
+    L, init, _ = _random_batch(N, C, seed=2, spread=0.2)
+    b = BatchedMonteCarlo(None, init, Physics(L, L), np.arange(C, dtype=np.uint64), initial_max_displacement=0.65)
+    sxy, sew, _ = b.local_moves(600, sample_every=150)
+    tup = io.sample_tuples(b, sxy, sew, 1, 0, 150, 600)
+    io.write_run_dir(str(tmp_path / "run_002"), tup, [t[6] for t in tup[:2]])
+    rows = list(csv.reader(open(tmp_path / "run_002" / "sampled_data.csv")))
+    assert rows[0][0] == "cycle_number" and len(rows) == 5
+    for row, t in zip(rows[1:], tup):
+        assert int(row[0]) == t[0] and float(row[1]) == t[1] and float(row[3]) == t[3]
+        np.testing.assert_array_equal(np.array(ast.literal_eval(row[6])), t[6].ravel())
+    cf = np.load(tmp_path / "run_002" / "mc_run_configs.npy")
+    assert cf.shape == (4, N, 2)
+    np.testing.assert_array_equal(cf[-1], b.state[1].cpu().numpy())
 
 
 def _random_batch(N, C, seed, spread):
