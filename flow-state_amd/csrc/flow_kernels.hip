@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "flow_layout.h"
 #include "fs_internal.h"
@@ -38,6 +39,10 @@ constexpr float kMinH = 1e-3f;
 constexpr float kMinD = 1e-3f;
 
 enum { MODE_DENSITY = 0, MODE_SAMPLE = 1, MODE_PROPOSE = 2 };
+
+#ifndef FS_RPD
+#define FS_RPD 3  // weight-fragment ring depth of the ResNet GEMMs
+#endif
 
 // (H, K) instantiations: A1 of main_algorithm_1.py:59-67 (H=256, K=32), A2 of
 // main_algorithm_2.py:43-51 (H=128, K=15), and the small test/golden shapes.
@@ -63,6 +68,45 @@ struct FlowArgs {
     float sqrtH;          // fl32(sqrt(H))                 (coupling.py:340-342)
     float base_lp;        // fl32(-D * log(fl32(2B)))      (Uniform.py:70)
 };
+
+// Phase timers for tools/flow_phases.py (built only into libflowstate_prof.so,
+// -DFS_PROF): per wave, s_memtime deltas accumulated per phase of the pass.
+enum { PH_INPUT, PH_PF, PH_INIT_GEMM, PH_EPI, PH_RES_GEMM, PH_BARRIER, PH_TAIL_GEMM, PH_FINAL_GEMM, PH_SPLINE,
+       PH_UNCOND, PH_COUNT };
+#ifdef FS_PROF
+__device__ unsigned long long g_prof[16];
+struct Prof {
+    uint64_t t, acc[PH_COUNT];
+    __device__ Prof() : t(__builtin_amdgcn_s_memtime()) {
+        for (int i = 0; i < PH_COUNT; ++i) acc[i] = 0;
+    }
+    __device__ __forceinline__ void mark(int ph) {
+        const uint64_t n = __builtin_amdgcn_s_memtime();
+        acc[ph] += n - t;
+        t = n;
+    }
+    __device__ void flush() {
+        if ((threadIdx.x & 63) == 0)
+            for (int i = 0; i < PH_COUNT; ++i) atomicAdd(&g_prof[i], (unsigned long long)acc[i]);
+    }
+};
+#else
+struct Prof {
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush() {}
+};
+#endif
+
+// Barrier of the 4 waves of a row group: LDS arrival counter (monotonic; phase
+// counts this wave's arrivals x 4), workgroup-scope release / acquire.
+__device__ __forceinline__ void group_barrier(int *ctr, int &phase) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    phase += 4;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < phase)
+        __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -186,8 +230,8 @@ __device__ __forceinline__ void knots_from_logits(const float (&u)[K], float (&k
     float e[K];
     float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        e[k] = expf(u[k] - m);
+    for (int k = 0; k < K; ++k) {  // exp via v_exp_f32 (2^x): a few ulp, far inside the 1e-5 parity bound
+        e[k] = __builtin_amdgcn_exp2f((u[k] - m) * 1.4426950408889634f);
         s += e[k];
     }
     const float inv = 1.f / s;
@@ -283,9 +327,11 @@ __device__ __forceinline__ void stage_half(float *STG, const f32x16 &t0, const f
     }
 }
 
+// widths / heights logits of one feature, already divided by sqrt(H) (folded into
+// the packed final-layer columns and biases)
 template <int K>
 __device__ __forceinline__ void load_logits(float *STG, const f32x16 &t0, const f32x16 &t1, float bias,
-                                            float inv_scale_div, float (&u)[K]) {
+                                            float (&u)[K]) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -294,7 +340,7 @@ __device__ __forceinline__ void load_logits(float *STG, const f32x16 &t0, const 
             wave_lds_sync();
 #pragma unroll
             for (int k = 0; k < 16; ++k)
-                if (16 * half + k < K) u[16 * half + k] = STG[lane * 17 + k] / inv_scale_div;
+                if (16 * half + k < K) u[16 * half + k] = STG[lane * 17 + k];
             wave_lds_sync();
         }
     }
@@ -308,19 +354,21 @@ template <int XS, int K, bool INV>
 __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec,
                                              int kg, const float *__restrict__ bf, float *STG, const float *TL,
                                              int tstride, float *CO, int cs, int p, int j, const FlowArgs &a,
-                                             bool &nan_any) {
+                                             bool &nan_any, Prof &pf, int *tail_ctr, int tail_target) {
     const int lane = threadIdx.x & 63, r = lane & 31;
     float cw[K + 1], ch[K + 1];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         f32x16 acc[2][1];
         gemm64<XS, 2, 1, 4>(X, W, sec, kg, 0, 3 * j + t, acc);
+        pf.mark(PH_FINAL_GEMM);
         float u[K];
-        load_logits<K>(STG, acc[0][0], acc[1][0], bf[32 * t + r], a.sqrtH, u);
+        load_logits<K>(STG, acc[0][0], acc[1][0], bf[32 * t + r], u);
         if (t == 0)
             knots_from_logits<K>(u, cw, kMinW, a.twoB, a.negB, a.B);
         else
             knots_from_logits<K>(u, ch, kMinH, a.twoB, a.negB, a.B);
+        pf.mark(PH_SPLINE);
     }
     const float x = CO[lane * cs + p];
     const bool inside = (x >= a.negB) && (x <= a.B);
@@ -339,10 +387,15 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
             ch1 = ch[k + 1];
         }
     }
+    while (__hip_atomic_load(tail_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < tail_target)
+        __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     float ud0 = 0.f, ud1 = TL[lane * tstride + j];  // d_K unless bin + 1 < K
     {
         f32x16 acc[2][1];
+        pf.mark(PH_SPLINE);
         gemm64<XS, 2, 1, 4>(X, W, sec, kg, 0, 3 * j + 2, acc);
+        pf.mark(PH_FINAL_GEMM);
         const float bias = bf[64 + r];
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
@@ -361,6 +414,7 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
     float y, l;
     bool nd;
     rqs_eval<INV>(x, icw, cw1 - icw, ich, ch1 - ich, d0, d1, y, l, nd);
+    pf.mark(PH_SPLINE);
     if (inside) {
         CO[lane * cs + p] = y;
         nan_any |= nd;
@@ -392,9 +446,8 @@ template <int H, int K, int MODE>
 __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
     // ResNet GEMM work split: NT column tiles x 2 row tiles over the 8 waves
     constexpr int NT = H / 32;
-    constexpr int RT = NT >= kWaves ? 2 : 1;          // row tiles per wave
-    constexpr int CT = NT >= kWaves ? NT / kWaves : 1;  // column tiles per wave
-    constexpr int NU = (2 / RT) * (NT / CT);          // active waves
+    constexpr int CTg = NT >= 4 ? NT / 4 : 1;          // ResNet: column tiles per wave of a row group
+    constexpr int NUg = NT / CTg;                      // ResNet: active waves per row group
     constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;  // == lds_layout().xs
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int N = a.N, D = 2 * N;
@@ -440,10 +493,18 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
     float ld = 0.f;
     bool nan_any = false;
     int off = 0;
-    const bool act = wid < NU;
-    const int rt0 = (RT == 2) ? 0 : (wid & 1);
-    const int ct0 = (RT == 2) ? wid * CT : (wid >> 1) * CT;
+    const int grp = wid >> 2, gw = wid & 3;
+    const bool gact = gw < NUg;
+    const int gct0 = gw * CTg;
+    int *gbar = (int *)(smem + LL.ld + kWaves * kRows * 4);  // one arrival counter per row group
+    int gphase = 0, tail_target = 0;
+    if (tid < 4) gbar[tid] = 0;
+#ifdef FS_PRIO_HI
+    if (wid >= 4) __builtin_amdgcn_s_setprio(1);  // second-dispatched half wins VALU arbitration
+#endif
+    Prof pf;
     __syncthreads();
+    pf.mark(PH_INPUT);
 
     for (int s = 0; s < a.L; ++s) {
         const int layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
@@ -454,7 +515,9 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
         if (MODE != MODE_DENSITY) {
             off = (off + N) % D;  // Coupling.inverse rolls first (coupling.py:113-114)
             ld += uncond_spline<K, true>(P + PL.unc, CO, cs, N, D, off, a, nan_any);
+            pf.mark(PH_UNCOND);
             __syncthreads();
+            pf.mark(PH_BARRIER);
         }
         // periodic features [cos(s x_id) | sin(s x_id)] (nn.py:120-137) -> X
         for (int f = wid; f < N; f += kWaves) {
@@ -464,116 +527,142 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
             X[lane * XS + N + f] = sinf(sv);
         }
         for (int c = D + wid; c < 8 * PL.kg_in; c += kWaves) X[lane * XS + c] = 0.f;
+        pf.mark(PH_PF);
         __syncthreads();
+        pf.mark(PH_BARRIER);
 
-        f32x16 hr[RT][CT], acc[RT][CT];
-        if (act) {  // initial_layer
-            gemm64<XS, RT, CT, 3>(X, W, (int)(PL.win * 4), PL.kg_in, rt0, ct0, acc);
+        // ResidualNet on two independent row groups: waves 0-3 carry rows 0-31,
+        // waves 4-7 rows 32-63, each group splitting the H/32 column tiles; the
+        // groups synchronise only internally (LDS-counter barriers), so one group's
+        // epilogue / barrier bubbles run under the other group's MFMAs.
+        f32x16 hr[1][CTg], acc[1][CTg];
+        if (gact) {  // initial_layer
+            gemm64<XS, 1, CTg, FS_RPD>(X, W, (int)(PL.win * 4), PL.kg_in, grp, gct0, acc);
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                const float bb = V[32 * (ct0 + ct) + r];
+            for (int ct = 0; ct < CTg; ++ct) {
+                const float bb = V[32 * (gct0 + ct) + r];
 #pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) hr[rt][ct][i] = acc[rt][ct][i] + bb;
+                for (int i = 0; i < 16; ++i) hr[0][ct][i] = acc[0][ct][i] + bb;
             }
         }
-        BRing<CT, 3> br;
-        if (act && a.nb > 0) b_prologue<CT, 3>(br, W, (int)(PL.blocks * 4), PL.kg_h, ct0);
-        for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
+        pf.mark(PH_INIT_GEMM);
+        // per-column epilogue vectors {a0,c0,b0,a1,c1,b1} of a block: loaded one block
+        // ahead and always BEFORE the next GEMM's weight prologue, so the epilogue's
+        // vmcnt wait never covers the prologue's (L2 / MALL latency) loads
+        float ev[6][CTg];
+        auto load_ev = [&](int jb, float (&e)[6][CTg]) {
             const float *VB = V + PL.v_blocks + (int64_t)6 * H * jb;
-            const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4);
-            const int w1 = w0 + (int)(PL.block_stride * 2);
-            // this block's per-column epilogue vectors, loaded ahead of the barriers
-            float ev[6][CT];
 #pragma unroll
             for (int q = 0; q < 6; ++q)
 #pragma unroll
-                for (int ct = 0; ct < CT; ++ct) ev[q][ct] = VB[q * H + 32 * (ct0 + ct) + r];
-            __syncthreads();
-            if (act) {
+                for (int ct = 0; ct < CTg; ++ct) e[q][ct] = VB[q * H + 32 * (gct0 + ct) + r];
+        };
+        if (a.nb > 0) load_ev(0, ev);
+        BRing<CTg, FS_RPD> br;
+        if (gact && a.nb > 0) b_prologue<CTg, FS_RPD>(br, W, (int)(PL.blocks * 4), PL.kg_h, gct0);
+        for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
+            const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4);
+            const int w1 = w0 + (int)(PL.block_stride * 2);
+            pf.mark(PH_EPI);
+            group_barrier(gbar + grp, gphase);
+            pf.mark(PH_BARRIER);
+            if (gact) {
 #pragma unroll
-                for (int ct = 0; ct < CT; ++ct) {
-                    const int col = 32 * (ct0 + ct) + r;
+                for (int ct = 0; ct < CTg; ++ct) {
+                    const int col = 32 * (gct0 + ct) + r;
 #pragma unroll
-                    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            const int R = acc_row(rt0 + rt, i, h);
-                            X[R * XS + col] = fmaxf(hr[rt][ct][i] * ev[0][ct] + ev[1][ct], 0.f);
-                        }
+                    for (int i = 0; i < 16; ++i)
+                        X[acc_row(grp, i, h) * XS + col] = fmaxf(hr[0][ct][i] * ev[0][ct] + ev[1][ct], 0.f);
                 }
             }
-            __syncthreads();
-            if (act) {
-                gemm_run<XS, RT, CT, 3>(X, W, w0, PL.kg_h, rt0, ct0, br, acc);
-                b_prologue<CT, 3>(br, W, w1, PL.kg_h, ct0);  // next GEMM's first weight groups
+            pf.mark(PH_EPI);
+            group_barrier(gbar + grp, gphase);
+            pf.mark(PH_BARRIER);
+            if (gact) {
+                gemm_run<XS, 1, CTg, FS_RPD>(X, W, w0, PL.kg_h, grp, gct0, br, acc);
+                b_prologue<CTg, FS_RPD>(br, W, w1, PL.kg_h, gct0);  // next GEMM's first weight groups
             }
-            __syncthreads();
-            if (act) {
+            pf.mark(PH_RES_GEMM);
+            group_barrier(gbar + grp, gphase);
+            pf.mark(PH_BARRIER);
+            if (gact) {
 #pragma unroll
-                for (int ct = 0; ct < CT; ++ct) {
-                    const int col = 32 * (ct0 + ct) + r;
+                for (int ct = 0; ct < CTg; ++ct) {
+                    const int col = 32 * (gct0 + ct) + r;
 #pragma unroll
-                    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            const int R = acc_row(rt0 + rt, i, h);
-                            X[R * XS + col] = fmaxf((acc[rt][ct][i] + ev[2][ct]) * ev[3][ct] + ev[4][ct], 0.f);
-                        }
+                    for (int i = 0; i < 16; ++i)
+                        X[acc_row(grp, i, h) * XS + col] =
+                            fmaxf((acc[0][ct][i] + ev[2][ct]) * ev[3][ct] + ev[4][ct], 0.f);
                 }
             }
-            __syncthreads();
-            if (act) {
-                gemm_run<XS, RT, CT, 3>(X, W, w1, PL.kg_h, rt0, ct0, br, acc);
-                if (jb + 1 < a.nb) b_prologue<CT, 3>(br, W, w1 + (int)(PL.block_stride * 2), PL.kg_h, ct0);
+            pf.mark(PH_EPI);
+            group_barrier(gbar + grp, gphase);
+            pf.mark(PH_BARRIER);
+            float evn[6][CTg];
+            if (jb + 1 < a.nb) load_ev(jb + 1, evn);
+            if (gact) {
+                gemm_run<XS, 1, CTg, FS_RPD>(X, W, w1, PL.kg_h, grp, gct0, br, acc);
+                if (jb + 1 < a.nb) b_prologue<CTg, FS_RPD>(br, W, w1 + (int)(PL.block_stride * 2), PL.kg_h, gct0);
 #pragma unroll
-                for (int ct = 0; ct < CT; ++ct)
+                for (int ct = 0; ct < CTg; ++ct)
 #pragma unroll
-                    for (int rt = 0; rt < RT; ++rt)
+                    for (int i = 0; i < 16; ++i) hr[0][ct][i] = hr[0][ct][i] + (acc[0][ct][i] + ev[5][ct]);
+            }
+            if (jb + 1 < a.nb)
 #pragma unroll
-                        for (int i = 0; i < 16; ++i) hr[rt][ct][i] = hr[rt][ct][i] + (acc[rt][ct][i] + ev[5][ct]);
+                for (int q = 0; q < 6; ++q)
+#pragma unroll
+                    for (int ct = 0; ct < CTg; ++ct) ev[q][ct] = evn[q][ct];
+            pf.mark(PH_RES_GEMM);
+        }
+        group_barrier(gbar + grp, gphase);
+        pf.mark(PH_BARRIER);
+        if (gact) {  // X <- h for the final layer
+#pragma unroll
+            for (int ct = 0; ct < CTg; ++ct) {
+                const int col = 32 * (gct0 + ct) + r;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) X[acc_row(grp, i, h) * XS + col] = hr[0][ct][i];
             }
         }
+        pf.mark(PH_EPI);
         __syncthreads();
-        if (act) {  // X <- h for the final layer
+        pf.mark(PH_BARRIER);
+        // tail block (d_K of every transform feature -> TL) on waves 4-7, one
+        // 32-row half tile each; waves 0-3 start their features at once, which puts
+        // the two waves of every SIMD about half a GEMM apart for the final phase
+        // (one's spline VALU runs under the other's MFMAs).  TL readers wait on
+        // the tail counter (cond_spline).
+        tail_target += 4;
+        if (wid >= 4) {
+            for (int piece = wid - 4; piece < 2 * PL.ntt; piece += 4) {
+                const int q = piece >> 1, rt = piece & 1;
+                f32x16 t[1][1];
+                gemm64<XS, 1, 1, 4>(X, W, (int)(PL.wt * 4), PL.kg_h, rt, q, t);
+                const float bt = V[PL.v_bt + 32 * q + r];
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                const int col = 32 * (ct0 + ct) + r;
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int R = acc_row(rt0 + rt, i, h);
-                        X[R * XS + col] = hr[rt][ct][i];
-                    }
+                for (int i = 0; i < 16; ++i) TL[acc_row(rt, i, h) * ts + 32 * q + r] = t[0][0][i] + bt;
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            if (lane == 0) __hip_atomic_fetch_add(gbar + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        __syncthreads();
-        // tail block: d_K of every transform feature -> TL[row][feature]
-        for (int q = wid; q < PL.ntt; q += kWaves) {
-            f32x16 t[2][1];
-            gemm64<XS, 2, 1, 4>(X, W, (int)(PL.wt * 4), PL.kg_h, 0, q, t);
-            const float bt = V[PL.v_bt + 32 * q + r];
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) TL[acc_row(rt, i, h) * ts + 32 * q + r] = t[rt][0][i] + bt;
-        }
-        __syncthreads();
+        pf.mark(PH_TAIL_GEMM);
         // final layer + conditional spline, feature by feature
         for (int j = wid; j < N; j += kWaves) {
             const int p = (2 * j + 1 + off) % D;
             ld += cond_spline<XS, K, MODE != MODE_DENSITY>(X, W, (int)(PL.wf * 4), PL.kg_h,
                                                         V + PL.v_bf + 96 * j, STG, TL, ts, CO, cs, p, j, a,
-                                                        nan_any);
+                                                        nan_any, pf, gbar + 2, tail_target);
         }
         if (MODE == MODE_DENSITY) {
             ld += uncond_spline<K, false>(P + PL.unc, CO, cs, N, D, off, a, nan_any);
             off = (off + N) % D;  // Coupling.forward rolls last (coupling.py:100-101)
+            pf.mark(PH_UNCOND);
         }
         __syncthreads();
+        pf.mark(PH_BARRIER);
     }
+    pf.flush();
 
     // ---- outputs
     LDP[wid * kRows + lane] = ld;
@@ -614,7 +703,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
 // kind 0: plain linear W[nout][kin];  kind 1: final layer main (feature tiles);
 // kind 2: final layer tail (d_K per feature)
 __global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restrict__ src, int kin, int kg,
-                                   int ntiles, int nout, int kind, int K) {
+                                   int ntiles, int nout, int kind, int K, float inv_div) {
     const int64_t total = (int64_t)ntiles * kg * 256;
     const int P = 3 * K + 1;
     for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
@@ -627,17 +716,19 @@ __global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restr
         const int k = 8 * g + 4 * (lane >> 5) + j;
         const int c = lane & 31;
         int64_t row = -1;
+        float div = 1.f;
         if (kind == 0) {
             const int col = 32 * tile + c;
             row = col < nout ? col : -1;
         } else if (kind == 1) {
             const int feat = tile / 3, t = tile % 3;
             if (c < K) row = (int64_t)feat * P + t * K + c;
+            if (t < 2) div = inv_div;  // widths / heights: / sqrt(H) folded in (coupling.py:340-342)
         } else {
             const int feat = 32 * tile + c;
             if (feat < nout) row = (int64_t)feat * P + 3 * K;
         }
-        dst[idx] = (row >= 0 && k < kin) ? src[row * kin + k] : 0.f;
+        dst[idx] = (row >= 0 && k < kin) ? src[row * kin + k] / div : 0.f;
     }
 }
 
@@ -678,7 +769,8 @@ __global__ void pack_vec_kernel(float *__restrict__ dst, const float *__restrict
     }
     for (int i = tid; i < N * 96; i += nthr) {
         const int feat = i / 96, t = (i % 96) / 32, c = i % 32;
-        V[PL.v_bf + i] = (c < K) ? src[R.bf + (int64_t)feat * P + t * K + c] : 0.f;
+        const float div = t < 2 ? (float)sqrt((double)H) : 1.f;  // / sqrt(H) of widths, heights folded in
+        V[PL.v_bf + i] = (c < K) ? src[R.bf + (int64_t)feat * P + t * K + c] / div : 0.f;
     }
     for (int i = tid; i < PL.ntt * 32; i += nthr) V[PL.v_bt + i] = (i < N) ? src[R.bf + (int64_t)i * P + 3 * K] : 0.f;
     // unconditional knots (PiecewiseRationalQuadraticCDF, coupling.py:227-259): batch independent
@@ -719,7 +811,6 @@ __global__ void pack_vec_kernel(float *__restrict__ dst, const float *__restrict
 // ---------------------------------------------------------------------------
 template <int H, int K, int MODE>
 static hipError_t launch_pass_t(const FlowArgs &a, int N, hipStream_t st) {
-    const LdsLayout LL = lds_layout(N, H);
     auto kfn = flow_pass_kernel<H, K, MODE>;
     static bool attr_set = false;  // per instantiation
     if (!attr_set) {
@@ -728,7 +819,7 @@ static hipError_t launch_pass_t(const FlowArgs &a, int N, hipStream_t st) {
         attr_set = true;
     }
     const int64_t blocks = (a.nrows + kRows - 1) / kRows;
-    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kThreads), LL.total, st, a);
+    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kThreads), lds_layout(N, H).total, st, a);
     return hipGetLastError();
 }
 
@@ -744,6 +835,17 @@ static hipError_t launch_pass_mode(const FlowArgs &a, int N, int H, int K, hipSt
 }  // namespace fs
 
 using namespace fs;
+
+#ifdef FS_PROF
+extern "C" int fs_prof_read(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
 
 bool fs_flow_supported(const fs_flow_dims *d, char *why, size_t n) {
     if (!d) return false;
@@ -795,7 +897,7 @@ hipError_t fs_flow_pack_impl(const fs_flow_dims *d, const float *raw, float *pac
             int blocks = (int)((tot + 255) / 256);
             if (blocks > 4096) blocks = 4096;
             hipLaunchKernelGGL(pack_linear_kernel, dim3(blocks), dim3(256), 0, st, o, w, kin, kg, ntiles, nout,
-                               kind, K);
+                               kind, K, (float)sqrt((double)H));
         };
         lin(dst + PL.win, src + R.win, 2 * N, PL.kg_in, H / 32, H, 0);
         for (int jb = 0; jb < nb; ++jb) {

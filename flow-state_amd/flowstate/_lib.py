@@ -9,7 +9,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libflowstate.so")
+# FLOWSTATE_LIB: an alternative build of the same library (A/B kernel measurements)
+LIB_PATH = os.environ.get("FLOWSTATE_LIB") or os.path.join(_HERE, "lib", "libflowstate.so")
 _lib = None
 
 FS_MH_CORRECT_SIGN = 1
