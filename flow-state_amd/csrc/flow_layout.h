@@ -116,26 +116,4 @@ FS_HD LdsLayout lds_layout(int N, int H) {
     return l;
 }
 
-// v5 pass kernel: 32 chains per workgroup, 4 waves (one per SIMD), two resident
-// workgroups per CU whose barriers are independent, so one workgroup's epilogues,
-// barriers and spline VALU run under the other's MFMAs.
-constexpr int kRows32 = 32;
-constexpr int kWaves32 = 4;
-constexpr int kThreads32 = 64 * kWaves32;
-
-FS_HD LdsLayout lds_layout32(int N, int H) {
-    LdsLayout l;
-    l.xw = flow_xw(H);
-    l.xs = l.xw + 4;
-    l.cstride = 2 * N + 1;
-    l.tstride = ((N + 31) / 32) * 32 + 1;
-    l.x = 0;
-    l.coord = l.x + kRows32 * l.xs * 4;
-    l.stg = (int)rup(l.coord + kRows32 * l.cstride * 4, 16);
-    l.tail = l.stg + kWaves32 * 64 * 17 * 4;  // per-wave [2 features x 32 rows][17] transpose buffer
-    l.ld = (int)rup(l.tail + kRows32 * l.tstride * 4, 16);
-    l.total = l.ld + kWaves32 * 64 * 4 + 16;
-    return l;
-}
-
 }  // namespace fs

@@ -32,3 +32,72 @@ class UniformParticle(nn.Module):
         out = torch.full((z.size(0),), self.log_prob_constant(), device=z.device, dtype=z.dtype)
         out[~in_bounds] = -float("inf")
         return out
+
+
+class SimpleLJ(nn.Module):
+    """Pairwise LJ energy of flow samples for reverse_kld (reference:
+    NF/normflows/Energy/SimpleLJ.py:5-41): minimum image in a box of 2*bound, an
+    extra particle at the origin, linear core below r = 0.82, no cutoff.  The
+    reference allocates its zero row on 'cuda' unconditionally; here it follows x."""
+
+    def __init__(self, dim, n_particles, temperature, bound):
+        super().__init__()
+        self._dim = dim
+        self._n_particles = n_particles
+        self._n_dimensions = dim // n_particles
+        self.temperature = temperature
+        self.bound = bound
+
+    def _energy(self, x):
+        x = x.contiguous()
+        xp = x.clone().reshape(-1, self._n_particles, self._n_dimensions)
+        d_norm = xp - 2 * self.bound * torch.round(xp / (self.bound * 2))
+        zeros = torch.zeros((d_norm.shape[0], 1, d_norm.shape[2]), device=x.device, dtype=d_norm.dtype)
+        d_norm = torch.cat((zeros, d_norm), dim=1)
+        e = d_norm.unsqueeze(2)
+        dist = torch.norm(e - e.transpose(1, 2), dim=-1)
+        n = d_norm.size(1)
+        iu = torch.triu_indices(n, n, offset=1, device=x.device)
+        r = dist[:, iu[0], iu[1]]
+        bk = 0.82
+        en = torch.where(r <= bk, -80 * (r - bk) + 30, 4 * (pow(1 / r, 12) - pow(1 / r, 6)))
+        return en.sum(dim=1) / self.temperature
+
+
+class DoubleWellLJ(SimpleLJ):
+    """SimpleLJ + the two-well external potential (reference: Energy/SimpleLJ.py:44-130),
+    wells at (-bound/2, 0) and (bound/2, 0) in the centred frame."""
+
+    def __init__(self, dim, n_particles, temperature, bound, V0_list=None, r0=1.0, k=10.0):
+        super().__init__(dim, n_particles, temperature, bound)
+        if V0_list is None:
+            V0_list = [-4.0, -4.0]
+        self.V0_list = torch.tensor(V0_list, dtype=torch.float32)
+        self.r0 = r0
+        self.k = k
+        self.centers = torch.tensor([[-bound / 2, 0.0], [bound / 2, 0.0]], dtype=torch.float32)
+
+    def double_well_potential(self, positions):
+        batch, n_particles, _ = positions.shape
+        L = 2 * self.bound
+        V = torch.zeros(batch, device=positions.device)
+        centers = self.centers.to(positions.device)
+        V0 = self.V0_list.to(positions.device)
+        for p in range(n_particles):
+            x = positions[:, p, 0]
+            y = positions[:, p, 1]
+            Vp = torch.zeros(batch, device=positions.device)
+            for i, c in enumerate(centers):
+                dx = x - c[0]
+                dy = y - c[1]
+                dx = dx - L * torch.round(dx / L)
+                dy = dy - L * torch.round(dy / L)
+                r = torch.sqrt(dx ** 2 + dy ** 2)
+                transition = 0.5 * (1 + torch.tanh(self.k * (r - self.r0)))
+                Vp = Vp + V0[i] * (1 - transition)
+            V = V + Vp
+        return V
+
+    def _energy(self, x):
+        lj = super()._energy(x)
+        return lj + self.double_well_potential(x.view(x.shape[0], self._n_particles, self._n_dimensions))

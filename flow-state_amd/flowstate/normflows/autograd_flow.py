@@ -1,0 +1,163 @@
+"""Differentiable (PyTorch autograd) coupling-layer math for training (SURVEY §8(f)
+row 4: Algorithm 2's forward_kld / reverse_kld, hybrid_NF_MCMC/main_algorithm_2.py:314-331).
+
+Training needs gradients and train-mode BatchNorm (batch statistics + running
+statistics updates), which the fused inference kernels (eval mode, forward only)
+do not provide.  This module evaluates the same layers with torch ops on the
+layers' own nn.Modules (nn.Linear / nn.BatchNorm1d, so train/eval semantics and
+running-statistics updates are torch's), on the device the parameters live on
+(PyTorch-ROCm on MI355X: hipBLASLt GEMMs + elementwise kernels).  After an
+optimizer step the inference kernels pick the new parameters up through the
+packed-image cache (tensor version counters).
+
+Reference math (paths relative to the reference root):
+  Coupling.forward / inverse          NF/normflows/flows/neural_spline/coupling.py:71-134
+  _piecewise_cdf (/ sqrt(H) scaling)   coupling.py:335-368
+  PiecewiseRationalQuadraticCDF       coupling.py:176-265 (K+1 derivatives, shared over the batch)
+  unconstrained RQS, circular branch  NF/normflows/utils/splines.py:16-88
+  rational_quadratic_spline           splines.py:91-222
+  ResidualNet / ResidualBlock         NF/normflows/nets/resnet.py:7-104 (dropout p = 0)
+  PeriodicFeaturesElementwise         NF/normflows/utils/nn.py:120-137
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+MIN_BIN_WIDTH = 1e-3  # splines.py:6-8
+MIN_BIN_HEIGHT = 1e-3
+MIN_DERIVATIVE = 1e-3
+
+
+def _knots(unnorm, min_size, lo, hi):
+    """softmax -> min-size affine -> cumsum -> [lo, hi] with pinned ends (splines.py:117-127)."""
+    K = unnorm.shape[-1]
+    s = F.softmax(unnorm, dim=-1)
+    s = min_size + (1 - min_size * K) * s
+    c = torch.cumsum(s, dim=-1)
+    c = F.pad(c, pad=(1, 0), mode="constant", value=0.0)
+    c = (hi - lo) * c + lo
+    c = torch.cat([torch.full_like(c[..., :1], lo), c[..., 1:-1], torch.full_like(c[..., :1], hi)], dim=-1)
+    return c, c[..., 1:] - c[..., :-1]
+
+
+def rational_quadratic_spline(x, uw, uh, ud, inverse, left, right, bottom, top):
+    """splines.py:91-222 (inputs already inside [left, right])."""
+    cw, w = _knots(uw, MIN_BIN_WIDTH, left, right)
+    d = MIN_DERIVATIVE + F.softplus(ud)
+    ch, h = _knots(uh, MIN_BIN_HEIGHT, bottom, top)
+    knots = (ch if inverse else cw).detach().clone()
+    knots[..., -1] += 1e-6  # searchsorted eps (splines.py:11-13)
+    b = (torch.sum(x[..., None] >= knots, dim=-1) - 1)[..., None]
+    icw = cw.gather(-1, b)[..., 0]
+    ibw = w.gather(-1, b)[..., 0]
+    ich = ch.gather(-1, b)[..., 0]
+    delta = h / w
+    idl = delta.gather(-1, b)[..., 0]
+    id0 = d.gather(-1, b)[..., 0]
+    id1 = d[..., 1:].gather(-1, b)[..., 0]
+    ih = h.gather(-1, b)[..., 0]
+    if inverse:
+        s = id0 + id1 - 2 * idl
+        a = (x - ich) * s + ih * (idl - id0)
+        bb = ih * id0 - (x - ich) * s
+        c = -idl * (x - ich)
+        disc = torch.abs(bb.pow(2) - 4 * a * c)
+        if torch.isnan(disc).any():
+            raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
+        root = (2 * c) / (-bb - torch.sqrt(disc))
+        out = root * ibw + icw
+        tomt = root * (1 - root)
+        den = idl + (id0 + id1 - 2 * idl) * tomt
+        dnum = idl.pow(2) * (id1 * root.pow(2) + 2 * idl * tomt + id0 * (1 - root).pow(2))
+        return out, -(torch.log(dnum) - 2 * torch.log(den))
+    theta = (x - icw) / ibw
+    tomt = theta * (1 - theta)
+    num = ih * (idl * theta.pow(2) + id0 * tomt)
+    den = idl + (id0 + id1 - 2 * idl) * tomt
+    out = ich + num / den
+    dnum = idl.pow(2) * (id1 * theta.pow(2) + 2 * idl * tomt + id0 * (1 - theta).pow(2))
+    return out, torch.log(dnum) - 2 * torch.log(den)
+
+
+def circular_rqs(x, uw, uh, ud, B, inverse):
+    """unconstrained_rational_quadratic_spline, circular tails (splines.py:16-88): identity
+    outside [-B, B]; the derivative pad writes index K+1, which is never read."""
+    inside = (x >= -B) & (x <= B)
+    out = x.clone()
+    lad = torch.zeros_like(x)
+    if inside.any():
+        o, l = rational_quadratic_spline(x[inside], uw[inside, :], uh[inside, :], ud[inside, :], inverse,
+                                         -B, B, -B, B)
+        out = out.masked_scatter(inside, o)
+        lad = lad.masked_scatter(inside, l)
+    return out, lad
+
+
+def conditioner(net, ident, B):
+    """ResidualNet.forward with PeriodicFeaturesElementwise (fork: cos/sin of all identity
+    features, nn.py:120-137); BatchNorm modules in their current train/eval mode."""
+    scale = np.pi / B
+    t = torch.cat([torch.cos(scale * ident), torch.sin(scale * ident)], dim=-1)
+    t = net.initial_layer(t)
+    for blk in net.blocks:
+        u = blk.batch_norm_layers[0](t)
+        u = F.relu(u)
+        u = blk.linear_layers[0](u)
+        u = blk.batch_norm_layers[1](u)
+        u = F.relu(u)
+        u = blk.linear_layers[1](u)
+        t = t + u
+    return net.final_layer(t)
+
+
+def _cond_spline(layer, trans, params, inverse):
+    K = layer.num_bins
+    b, d = trans.shape
+    params = params.reshape(b, d, -1)
+    sq = np.sqrt(layer.num_hidden_channels)
+    uw = params[..., :K] / sq
+    uh = params[..., K:2 * K] / sq
+    ud = params[..., 2 * K:]
+    out, lad = circular_rqs(trans, uw, uh, ud, layer.tail_bound, inverse)
+    return out, lad.sum(dim=1)
+
+
+def _uncond_spline(layer, ident, inverse):
+    u = layer.prqct.unconditional_transform
+    n = ident.shape[0]
+    uw = u.unnormalized_widths[None].expand(n, *u.unnormalized_widths.shape)
+    uh = u.unnormalized_heights[None].expand(n, *u.unnormalized_heights.shape)
+    ud = u.unnormalized_derivatives[None].expand(n, *u.unnormalized_derivatives.shape)
+    out, lad = circular_rqs(ident, uw, uh, ud, layer.tail_bound, inverse)
+    return out, lad.sum(dim=1)
+
+
+def coupling_density(layer, x):
+    """Coupling.forward (coupling.py:71-102) = the layer's inverse (density direction)."""
+    p = layer.prqct
+    ident = x[:, p.identity_features]
+    trans = x[:, p.transform_features]
+    params = conditioner(p.transform_net, ident, layer.tail_bound)
+    trans, lad = _cond_spline(layer, trans, params, inverse=False)
+    ident, lad_u = _uncond_spline(layer, ident, inverse=False)
+    lad = lad + lad_u
+    out = torch.empty_like(x)
+    out = out.index_copy(1, p.identity_features, ident).index_copy(1, p.transform_features, trans)
+    split = layer.num_input_channels // 2
+    return torch.cat([out[:, split:], out[:, :split]], dim=1), lad
+
+
+def coupling_sample(layer, z):
+    """Coupling.inverse (coupling.py:104-134) = the layer's forward (sampling direction)."""
+    p = layer.prqct
+    split = layer.num_input_channels // 2
+    z = torch.cat([z[:, split:], z[:, :split]], dim=1)
+    ident = z[:, p.identity_features]
+    trans = z[:, p.transform_features]
+    ident, lad = _uncond_spline(layer, ident, inverse=True)
+    params = conditioner(p.transform_net, ident, layer.tail_bound)
+    trans, lad_s = _cond_spline(layer, trans, params, inverse=True)
+    lad = lad + lad_s
+    out = torch.empty_like(z)
+    out = out.index_copy(1, p.identity_features, ident).index_copy(1, p.transform_features, trans)
+    return out, lad

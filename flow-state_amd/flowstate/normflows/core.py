@@ -9,8 +9,9 @@ libflowstate launch over the whole coupling stack (fs_flow_*), reading a packed
 copy of the parameters that is rebuilt on the device whenever a parameter or
 BatchNorm buffer changes (eval-mode BatchNorm is folded at pack time).
 
-Training (forward_kld / reverse_kld with autograd) is not part of the
-inference hot path this build covers; those methods raise.
+Training (forward_kld / reverse_kld, Algorithm 2) runs the same layers through
+PyTorch autograd (autograd_flow.py) with train-mode BatchNorm, as the reference
+does; the inference kernels then see the updated parameters.
 """
 import torch
 import torch.nn as nn
@@ -172,10 +173,44 @@ class NormalizingFlow(nn.Module):
         return self.forward(z.to(dev))
 
     def forward_kld(self, x):
-        raise NotImplementedError("training (core.py:88-103) is outside the inference hot path (SURVEY §8(f))")
+        """core.py:88-103 (fork: no base term): -mean of the summed density-direction
+        log-dets, differentiable, BatchNorm in the module's current mode."""
+        from . import autograd_flow as AF
+
+        log_q = torch.zeros(len(x), device=x.device)
+        z = x
+        for i in range(len(self.flows) - 1, -1, -1):
+            z, log_det = AF.coupling_density(self.flows[i], z)
+            log_q += log_det
+        return -torch.mean(log_q)
 
     def reverse_kld(self, num_samples=1, beta=1.0, score_fn=True):
-        raise NotImplementedError("training (core.py:105-142) is outside the inference hot path (SURVEY §8(f))")
+        """core.py:105-142 (fork): base draws -> sampling direction -> mean(target
+        energy) + mean(log q); returns (loss, samples)."""
+        z = self.q0(num_samples).to(next(self.parameters()).device)
+        return self._reverse_kld_from(z, score_fn)
+
+    def _reverse_kld_from(self, z, score_fn=True):
+        from . import autograd_flow as AF
+
+        log_q = torch.zeros(len(z), device=z.device)
+        for flow in self.flows:
+            z, log_det = AF.coupling_sample(flow, z)
+            log_q -= log_det
+        if not score_fn:
+            z_ = z
+            log_q = torch.zeros(len(z_), device=z_.device)
+            req = [p.requires_grad for p in self.parameters()]
+            for p in self.parameters():
+                p.requires_grad_(False)
+            for i in range(len(self.flows) - 1, -1, -1):
+                z_, log_det = AF.coupling_density(self.flows[i], z_)
+                log_q += log_det
+            log_q += self.q0.log_prob(z_)
+            for p, r in zip(self.parameters(), req):
+                p.requires_grad_(r)
+        energy = self.p._energy(z)
+        return torch.mean(energy) + torch.mean(log_q), z
 
     def save(self, path):
         torch.save(self.state_dict(), path)

@@ -416,6 +416,75 @@ def analysis_case():
     print("analysis: ok", np.bincount([{"A": 0, "B": 1, "Outside": 2}[c] for c in out["f64_cls"].ravel()]))
 
 
+def train_case(NF):
+    """Algorithm-2 training pieces (main_algorithm_2.py:314-331) on a small flow in
+    train mode: forward_kld / reverse_kld losses, their parameter gradients, the
+    BatchNorm running statistics they update, and one Adam step of
+    loss = ALPHA*forward_kld + (1-ALPHA)*reverse_kld with ALPHA = 1.  reverse_kld's
+    base draw is supplied (q0 patched) so a GPU run can replay it; SimpleLJ._energy's
+    hard-coded device='cuda' zero row is routed to the CPU by a local torch.zeros
+    wrapper."""
+    from oracle import flow as OF
+    dims = OF.FlowDims(N=4, L=2, H=32, nb=2, K=5, B=OF.half_box(4))
+    sd = OF.random_state_dict(dims, seed=5, final_std=0.05)
+    g = torch.Generator().manual_seed(11)
+    x = (torch.rand((64, dims.D), generator=g) * 2 - 1) * dims.B * 0.9
+    z0 = (torch.rand((64, dims.D), generator=g) * 2 - 1) * dims.B
+    real_zeros = torch.zeros
+
+    def zeros_cpu(*a, **k):
+        if k.get("device") == "cuda":
+            k["device"] = "cpu"
+        return real_zeros(*a, **k)
+
+    def fresh():
+        model = build_ref_model(NF, dims)
+        model.load_state_dict(sd, strict=True)
+        model.p = NF.Energy.DoubleWellLJ(dims.D, dims.N, 1.0, dims.B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+        model.q0.forward = lambda n: z0[:n].clone()
+        model.train()
+        return model
+
+    out = {"x": x.numpy(), "z0": z0.numpy()}
+    names = [n for n, _ in fresh().named_parameters()]
+    torch.zeros = zeros_cpu
+    try:
+        m = fresh()
+        lf = m.forward_kld(x)
+        gf = torch.autograd.grad(lf, list(m.parameters()), allow_unused=True)
+        out["fkld"] = lf.detach().numpy()
+        for n, gr in zip(names, gf):
+            out["gf/" + n] = (gr if gr is not None else torch.zeros(0)).numpy()
+        for k, v in m.state_dict().items():
+            if "running" in k:
+                out["bn_after_f/" + k] = v.numpy()
+        m = fresh()
+        lr_, zr = m.reverse_kld(64)
+        gr_ = torch.autograd.grad(lr_, list(m.parameters()), allow_unused=True)
+        out["rkld"] = lr_.detach().numpy()
+        out["rkld_z"] = zr.detach().numpy()
+        out["energy"] = m.p._energy(zr.detach()).numpy()
+        for n, gr in zip(names, gr_):
+            out["gr/" + n] = (gr if gr is not None else torch.zeros(0)).numpy()
+        m = fresh()
+        opt = torch.optim.Adam(m.parameters(), lr=0.000543510751759681, weight_decay=9.5857178422352e-05)
+        opt.zero_grad()
+        energy_loss, _ = m.reverse_kld(64)
+        sample_loss = m.forward_kld(x)
+        loss = 1.0 * sample_loss + (1 - 1.0) * energy_loss
+        out["step_loss"] = loss.detach().numpy()
+        if ~(torch.isnan(loss) | torch.isinf(loss)):
+            loss.backward()
+            opt.step()
+        for k, v in m.state_dict().items():
+            out["after_step/" + k] = v.numpy()
+    finally:
+        torch.zeros = real_zeros
+    out["names"] = np.array(names)
+    np.savez_compressed(os.path.join(HERE, "train.npz"), **out)
+    print("train: ok", float(out["fkld"]), float(out["rkld"]), float(out["step_loss"]))
+
+
 def pcg_case():
     seeds = np.arange(42, 42 + 64)
     st = np.zeros((64, 4), np.uint64)
@@ -439,6 +508,9 @@ def main(only=None):
     if only == "analysis":
         analysis_case()
         return
+    if only == "train":
+        train_case(NF)
+        return
     flow_case(NF, "tiny", OF.FlowDims(N=4, L=2, H=32, nb=1, K=5, B=OF.half_box(4)), 1, 64, True)
     flow_case(NF, "n16", OF.FlowDims(N=16, L=3, H=64, nb=2, K=8, B=OF.half_box(16)), 2, 48, False)
     flow_case(NF, "n64", OF.FlowDims(N=64, L=2, H=128, nb=2, K=32, B=OF.half_box(64)), 3, 16, False)
@@ -449,6 +521,7 @@ def main(only=None):
     init_case(NF)
     local_case(NF, MC)
     analysis_case()
+    train_case(NF)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,78 @@
+"""Algorithm-2 training path (forward_kld / reverse_kld / one Adam step in train
+mode, main_algorithm_2.py:314-331) against the reference's own values
+(tests/golden/train.npz).  The training path is PyTorch autograd over the layers'
+modules (flowstate/normflows/autograd_flow.py), so it runs on CPU tensors too;
+tests/test_gpu_train.py repeats it on the MI355X."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def build(device):
+    from flowstate.models import build_flow
+    from flowstate.normflows.Energy import DoubleWellLJ
+    from oracle import flow as OF
+
+    f = np.load(os.path.join(G, "train.npz"))
+    dims = OF.FlowDims(N=4, L=2, H=32, nb=2, K=5, B=OF.half_box(4))
+    sd = OF.random_state_dict(dims, seed=5, final_std=0.05)
+    m = build_flow(4, L=2, H=32, nb=2, K=5, bound=dims.B, device="cpu")
+    m.load_state_dict(sd, strict=True)
+    m.p = DoubleWellLJ(dims.D, dims.N, 1.0, dims.B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+    m = m.to(device)
+    z0 = torch.from_numpy(f["z0"]).to(device)
+    m.q0.forward = lambda n: z0[:n].clone()
+    m.train()
+    return m, f
+
+
+def check_training(device, rtol_loss, rtol_grad, atol_grad):
+    torch.manual_seed(0)
+    m, f = build(device)
+    names = [str(n) for n in f["names"]]
+    assert names == [n for n, _ in m.named_parameters()]
+    x = torch.from_numpy(f["x"]).to(device)
+    lf = m.forward_kld(x)
+    np.testing.assert_allclose(lf.item(), float(f["fkld"]), rtol=rtol_loss)
+    gf = torch.autograd.grad(lf, list(m.parameters()), allow_unused=True)
+    for n, g in zip(names, gf):
+        ref = f["gf/" + n]
+        if ref.size == 0:
+            assert g is None or not g.abs().max().item()
+            continue
+        np.testing.assert_allclose(g.cpu().numpy(), ref, rtol=rtol_grad, atol=atol_grad, err_msg=n)
+    for k, v in m.state_dict().items():
+        if "running" in k:
+            np.testing.assert_allclose(v.cpu().numpy(), f["bn_after_f/" + k], rtol=1e-5, atol=1e-6, err_msg=k)
+    m, _ = build(device)
+    lr_, zr = m.reverse_kld(64)
+    np.testing.assert_allclose(lr_.item(), float(f["rkld"]), rtol=rtol_loss)
+    np.testing.assert_allclose(zr.detach().cpu().numpy(), f["rkld_z"], rtol=1e-5, atol=5e-4 * 1.0)
+    gr = torch.autograd.grad(lr_, list(m.parameters()), allow_unused=True)
+    for n, g in zip(names, gr):
+        ref = f["gr/" + n]
+        if ref.size == 0:
+            continue
+        scale = max(1.0, float(np.abs(ref).max()))
+        np.testing.assert_allclose(g.cpu().numpy(), ref, rtol=rtol_grad, atol=atol_grad * scale, err_msg=n)
+    m, _ = build(device)
+    opt = torch.optim.Adam(m.parameters(), lr=0.000543510751759681, weight_decay=9.5857178422352e-05)
+    opt.zero_grad()
+    energy_loss, _ = m.reverse_kld(64)
+    sample_loss = m.forward_kld(x)
+    loss = 1.0 * sample_loss + (1 - 1.0) * energy_loss
+    np.testing.assert_allclose(loss.item(), float(f["step_loss"]), rtol=rtol_loss)
+    assert bool(~(torch.isnan(loss) | torch.isinf(loss)))
+    loss.backward()
+    opt.step()
+    for k, v in m.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), f["after_step/" + k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_training_step_matches_reference_cpu():
+    torch.set_num_threads(4)
+    check_training("cpu", rtol_loss=1e-6, rtol_grad=1e-4, atol_grad=1e-6)
