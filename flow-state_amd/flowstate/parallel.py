@@ -41,6 +41,69 @@ def all_reduce_stats(hist, well_totals, group=None):
     return hist, well_totals
 
 
+def allreduce_gradients(model, group=None, bucket_bytes=64 << 20):
+    """Average the gradients of `model` over the group (Algorithm 2 data-parallel
+    training): gradients are flattened into buckets of at most
+    bucket_bytes (A2 N=64: 42.9 MB of parameters -> one bucket; xGMI ring
+    all-reduce is per-link bound, so fewer, larger calls) and all-reduced over
+    RCCL.  No-op without an initialised process group."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    world = dist.get_world_size(group)
+    grads = [p.grad for p in model.parameters() if p.grad is not None]
+    buckets, cur, size = [], [], 0
+    for g in grads:
+        nbytes = g.numel() * g.element_size()
+        if cur and size + nbytes > bucket_bytes:
+            buckets.append(cur)
+            cur, size = [], 0
+        cur.append(g)
+        size += nbytes
+    if cur:
+        buckets.append(cur)
+    for bucket in buckets:
+        flat = torch.cat([t.reshape(-1) for t in bucket])
+        dist.all_reduce(flat, group=group)
+        flat /= world
+        off = 0
+        for t in bucket:
+            t.copy_(flat[off:off + t.numel()].view_as(t))
+            off += t.numel()
+
+
+def broadcast_state(model, src=0, group=None):
+    """Rank `src`'s parameters and buffers (BatchNorm running statistics) to every rank."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    with torch.no_grad():
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, src=src, group=group)
+
+
+def all_gather_configs(local, group=None):
+    """Concatenate every rank's new training configurations (M_r, N, 2) in rank order
+    (main_algorithm_2.py:393-420, per-cycle sample collection)."""
+    import torch.distributed as dist
+
+    local = torch.as_tensor(local)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return local
+    world = dist.get_world_size(group)
+    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    m = int(max(int(v.item()) for v in ns))
+    pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    outs = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad, group=group)
+    return torch.cat([o[: int(k.item())] for o, k in zip(outs, ns)], 0)
+
+
 def free_energy(well_totals):
     """ΔF = ln(p_B / p_A) of calculate_well_statistics (utils.py:92-96), 0 if either is empty."""
     a, b, n = (int(v) for v in torch.as_tensor(well_totals).tolist())

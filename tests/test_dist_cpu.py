@@ -75,3 +75,43 @@ def test_shard_offsets():
 def test_free_energy():
     assert parallel.free_energy([10, 20, 100]) == pytest.approx(np.log(2.0))
     assert parallel.free_energy([0, 5, 10]) == 0.0
+
+
+def _train_worker(rank, world, port, out_path):
+    """Algorithm-2 data-parallel pieces on gloo: all-gather of per-rank training configs,
+    bucketed gradient averaging, state broadcast."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from flowstate.models import build_flow
+
+    torch.manual_seed(100 + rank)  # ranks start from different weights: broadcast must fix that
+    m = build_flow(4, L=2, H=32, nb=1, K=5, bound=5.0, device="cpu")
+    parallel.broadcast_state(m)
+    local = torch.full((3 + rank, 4, 2), float(rank))
+    allc = parallel.all_gather_configs(local)
+    x = torch.rand((16, 8), generator=torch.Generator().manual_seed(7 + rank)) * 8 - 4
+    m.train()
+    m.forward_kld(x).backward()
+    own = [p.grad.clone() for p in m.parameters() if p.grad is not None]
+    parallel.allreduce_gradients(m, bucket_bytes=4096)  # many small buckets
+    got = [p.grad.clone() for p in m.parameters() if p.grad is not None]
+    gathered = [None] * world
+    dist.all_gather_object(gathered, ([g.numpy() for g in own], [g.numpy() for g in got],
+                                      [p.detach().numpy() for p in m.parameters()], allc.numpy()))
+    if rank == 0:
+        np.save(out_path, np.array(gathered, dtype=object), allow_pickle=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_training_collectives(tmp_path):
+    out = str(tmp_path / "train.npy")
+    mp.spawn(_train_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    (own0, got0, p0, c0), (own1, got1, p1, c1) = np.load(out, allow_pickle=True)
+    for a, b in zip(p0, p1):
+        np.testing.assert_array_equal(a, b)  # broadcast made the replicas identical
+    for o0, o1, g0, g1 in zip(own0, own1, got0, got1):
+        np.testing.assert_allclose(g0, (o0 + o1) / 2, rtol=1e-6, atol=1e-7)
+        np.testing.assert_array_equal(g0, g1)
+    assert c0.shape == (7, 4, 2) and (c0[:3] == 0).all() and (c0[3:] == 1).all()
+    np.testing.assert_array_equal(c0, c1)
