@@ -78,25 +78,24 @@ class DoubleWellLJ(SimpleLJ):
         self.centers = torch.tensor([[-bound / 2, 0.0], [bound / 2, 0.0]], dtype=torch.float32)
 
     def double_well_potential(self, positions):
-        batch, n_particles, _ = positions.shape
+        """Energy/SimpleLJ.py:63-115, vectorised over particles (the reference loops over
+        them in Python; the per-particle terms are identical, the particle sum is a
+        tensor reduction)."""
         L = 2 * self.bound
-        V = torch.zeros(batch, device=positions.device)
         centers = self.centers.to(positions.device)
         V0 = self.V0_list.to(positions.device)
-        for p in range(n_particles):
-            x = positions[:, p, 0]
-            y = positions[:, p, 1]
-            Vp = torch.zeros(batch, device=positions.device)
-            for i, c in enumerate(centers):
-                dx = x - c[0]
-                dy = y - c[1]
-                dx = dx - L * torch.round(dx / L)
-                dy = dy - L * torch.round(dy / L)
-                r = torch.sqrt(dx ** 2 + dy ** 2)
-                transition = 0.5 * (1 + torch.tanh(self.k * (r - self.r0)))
-                Vp = Vp + V0[i] * (1 - transition)
-            V = V + Vp
-        return V
+        x = positions[:, :, 0]
+        y = positions[:, :, 1]
+        Vp = torch.zeros_like(x)
+        for i in range(centers.shape[0]):
+            dx = x - centers[i, 0]
+            dy = y - centers[i, 1]
+            dx = dx - L * torch.round(dx / L)
+            dy = dy - L * torch.round(dy / L)
+            r = torch.sqrt(dx ** 2 + dy ** 2)
+            transition = 0.5 * (1 + torch.tanh(self.k * (r - self.r0)))
+            Vp = Vp + V0[i] * (1 - transition)
+        return Vp.sum(dim=1)
 
     def _energy(self, x):
         lj = super()._energy(x)

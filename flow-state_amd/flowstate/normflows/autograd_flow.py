@@ -62,8 +62,7 @@ def rational_quadratic_spline(x, uw, uh, ud, inverse, left, right, bottom, top):
         bb = ih * id0 - (x - ich) * s
         c = -idl * (x - ich)
         disc = torch.abs(bb.pow(2) - 4 * a * c)
-        if torch.isnan(disc).any():
-            raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
+        _nan_flags.append(torch.isnan(disc).any())  # splines.py:176-183, raised after the pass
         root = (2 * c) / (-bb - torch.sqrt(disc))
         out = root * ibw + icw
         tomt = root * (1 - root)
@@ -79,18 +78,28 @@ def rational_quadratic_spline(x, uw, uh, ud, inverse, left, right, bottom, top):
     return out, torch.log(dnum) - 2 * torch.log(den)
 
 
+_nan_flags = []
+
+
+def check_nan_flags():
+    """Raise the reference's discriminant error if any inverse spline of the pass hit
+    a NaN (one device->host read per pass instead of one per layer)."""
+    flags = list(_nan_flags)
+    _nan_flags.clear()
+    if flags and bool(torch.stack(flags).any()):
+        raise ValueError("Discriminant computation resulted in NaN.")
+
+
 def circular_rqs(x, uw, uh, ud, B, inverse):
     """unconstrained_rational_quadratic_spline, circular tails (splines.py:16-88): identity
-    outside [-B, B]; the derivative pad writes index K+1, which is never read."""
+    outside [-B, B]; the derivative pad writes index K+1, which is never read.  Evaluated
+    on every element with the outside ones parked at 0 (so their unused branch stays
+    finite and contributes exact zeros to the gradient) and selected with where: no
+    data-dependent shapes, no host synchronisation."""
     inside = (x >= -B) & (x <= B)
-    out = x.clone()
-    lad = torch.zeros_like(x)
-    if inside.any():
-        o, l = rational_quadratic_spline(x[inside], uw[inside, :], uh[inside, :], ud[inside, :], inverse,
-                                         -B, B, -B, B)
-        out = out.masked_scatter(inside, o)
-        lad = lad.masked_scatter(inside, l)
-    return out, lad
+    xin = torch.where(inside, x, torch.zeros_like(x))
+    o, l = rational_quadratic_spline(xin, uw, uh, ud, inverse, -B, B, -B, B)
+    return torch.where(inside, o, x), torch.where(inside, l, torch.zeros_like(l))
 
 
 def conditioner(net, ident, B):

@@ -182,6 +182,7 @@ class NormalizingFlow(nn.Module):
         for i in range(len(self.flows) - 1, -1, -1):
             z, log_det = AF.coupling_density(self.flows[i], z)
             log_q += log_det
+        AF.check_nan_flags()
         return -torch.mean(log_q)
 
     def reverse_kld(self, num_samples=1, beta=1.0, score_fn=True):
@@ -209,6 +210,7 @@ class NormalizingFlow(nn.Module):
             log_q += self.q0.log_prob(z_)
             for p, r in zip(self.parameters(), req):
                 p.requires_grad_(r)
+        AF.check_nan_flags()
         energy = self.p._energy(z)
         return torch.mean(energy) + torch.mean(log_q), z
 

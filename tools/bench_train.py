@@ -1,0 +1,81 @@
+"""Algorithm-2 training throughput (main_algorithm_2.py:314-331):
+one optimizer step = reverse_kld(BATCH) + forward_kld(batch) in train mode,
+loss = ALPHA*forward + (1-ALPHA)*reverse (ALPHA = 1), backward, Adam; A2 flow
+(L=23, H=128, 2 blocks, 15 bins), N=64, batch 256, synthetic training configs
+(FCC + jitter, centred).  Also times the eval-mode proposal generation of the
+refeeding phase (model.sample through the HIP kernel).  Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (REPO, os.path.join(REPO, "flow-state_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+from flowstate.MCMC import initialise_fcc  # noqa: E402
+from flowstate.models import A2, build_flow, half_box  # noqa: E402
+from flowstate.normflows.Energy import DoubleWellLJ  # noqa: E402
+
+
+def main(steps=20, warmup=3, batch=256, N=64):
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    B = half_box(N)
+    m = build_flow(N, bound=B, device="cpu", **A2)
+    m.p = DoubleWellLJ(2 * N, N, 1.0, B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+    m = m.to(dev)
+    m.q0.device = dev
+    base, box = initialise_fcc(num_particles=N, rho=0.03, aspect_ratio=1.0)
+    rng = np.random.default_rng(3)
+    data = np.mod(base[None] + rng.normal(0, 0.3, (batch * (steps + warmup), N, 2)), 2 * B) - B
+    data = torch.from_numpy(data.astype(np.float32).reshape(-1, 2 * N)).to(dev)
+    opt = torch.optim.Adam(m.parameters(), lr=0.000543510751759681, weight_decay=9.5857178422352e-05)
+    m.train()
+
+    def step(i):
+        opt.zero_grad()
+        energy_loss, _ = m.reverse_kld(batch)
+        sample_loss = m.forward_kld(data[i * batch:(i + 1) * batch])
+        loss = 1.0 * sample_loss + 0.0 * energy_loss
+        ok = bool(~(torch.isnan(loss) | torch.isinf(loss)))
+        if ok:
+            loss.backward()
+            opt.step()
+        return loss.item(), ok
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    losses, skipped = [], 0
+    for i in range(warmup, warmup + steps):
+        l, ok = step(i)
+        losses.append(l)
+        skipped += not ok
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    m.eval()
+    with torch.no_grad():
+        m.sample(8192)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(5):
+            m.sample(65536)
+        torch.cuda.synchronize()
+        ts = (time.perf_counter() - t1) / 5
+    print(json.dumps({
+        "metric": "Algorithm-2 NF training steps/s (reverse_kld + forward_kld + Adam, A2 flow, N=64, batch 256)",
+        "value": steps / dt, "unit": "steps/s", "ms_per_step": dt / steps * 1e3, "n_gpus": 1,
+        "steps": steps, "warmup": warmup, "dtype": "f32", "data": "synthetic (FCC + jitter configs)",
+        "skipped_nan_steps": skipped, "last_loss": losses[-1],
+        "sampling_65536_ms": ts * 1e3, "samples_per_s": 65536 / ts,
+        "config": {"workload": "A2: L=23 H=128 blocks=2 K=15, N=64, batch 256"}}))
+
+
+if __name__ == "__main__":
+    main()
