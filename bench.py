@@ -223,8 +223,10 @@ def main():
         stepper.step(timed=True)
     # final reduction: density histogram + well occupancy of the current states
     hist = bmc.histogram2d(100)
-    wells = bmc.well_counts().sum(dim=0)
+    per_chain = bmc.well_counts()
+    wells = per_chain.sum(dim=0)
     parallel.all_reduce_stats(hist, wells)
+    table = parallel.gather_chain_counters(torch.cat([per_chain, bmc.accepted[:, None], bmc.attempts[:, None]], 1))
     torch.cuda.synchronize()
     stepper.harvest()
     if dist:
@@ -259,10 +261,12 @@ def main():
         "data": "synthetic (FCC+jitter states, random-init A1 flow with perturbed final layers)",
         "config": {"workload": f"Algorithm-1 NF-proposed MH step, N={N}, {C} chains per GPU",
                    "particles": N, "chains_per_gpu": C, "flow": "A1: L=15 H=256 blocks=32 K=32",
-                   "parallelism": f"dp{world} (chains sharded, RCCL all-reduce of final histogram)"},
+                   "parallelism": f"dp{world} (chains sharded; RCCL all-reduce of the final histogram, all-gather of per-chain counters)"},
         "acceptance_rate": n_acc.item() / total_steps,
         "final_stats": {"hist_total": int(hist.sum().item()), "all_in_A": int(wells[0].item()),
-                        "all_in_B": int(wells[1].item()), "chains": int(wells[2].item())},
+                        "all_in_B": int(wells[1].item()), "chains": int(wells[2].item()),
+                        "gathered_chain_rows": int(table.shape[0]),
+                        "deltaF_mean_sem": parallel.free_energy_stats(table)[:2]},
         "kernel_ms": {"flow_propose": t_prop, "flow_log_prob": t_lp, "energy": t_en, "mh_accept": t_acc},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_F32_TFLOPS, "traffic": _pmc_traffic(),

@@ -104,6 +104,32 @@ def all_gather_configs(local, group=None):
     return torch.cat([o[: int(k.item())] for o, k in zip(outs, ns)], 0)
 
 
+def gather_chain_counters(counters, group=None):
+    """All-gather per-chain order-parameter counters (C, k) int64 — count_A, count_B, n,
+    accepts, attempts (utils.py:739-747) — in rank order, so every rank
+    (the driver reads rank 0) holds the (world*C, k) table."""
+    import torch.distributed as dist
+
+    counters = torch.as_tensor(counters)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return counters
+    outs = [torch.empty_like(counters) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(outs, counters.contiguous(), group=group)
+    return torch.cat(outs, 0)
+
+
+def free_energy_stats(counters):
+    """Per-chain ΔF = ln(p_B / p_A) (0 unless both wells were visited, utils.py:92-96) and
+    its mean / standard error / std over chains as plot_avg_free_energy reports them
+    (utils.py:738-747: nanmean, nanstd / sqrt(runs))."""
+    c = np.asarray(torch.as_tensor(counters).cpu().numpy(), dtype=np.float64)
+    a, b, n = c[:, 0], c[:, 1], c[:, 2]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        pa, pb = a / n, b / n
+        dF = np.where((pa > 0) & (pb > 0), np.log(pb / pa), 0.0)
+    return float(np.nanmean(dF)), float(np.nanstd(dF) / np.sqrt(len(dF))), float(np.nanstd(dF))
+
+
 def free_energy(well_totals):
     """ΔF = ln(p_B / p_A) of calculate_well_statistics (utils.py:92-96), 0 if either is empty."""
     a, b, n = (int(v) for v in torch.as_tensor(well_totals).tolist())

@@ -72,6 +72,29 @@ def test_shard_offsets():
     assert c0 == 3 * 65536 and s[0] == 42 + 3 * 65536 and len(s) == 65536
 
 
+def _gather_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = torch.arange(12, dtype=torch.int64).reshape(4, 3) + 100 * rank
+    g = parallel.gather_chain_counters(c)
+    if rank == 0:
+        np.save(out_path, g.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_chain_counters(tmp_path):
+    out = str(tmp_path / "g.npy")
+    mp.spawn(_gather_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    g = np.load(out)
+    want = np.concatenate([np.arange(12).reshape(4, 3) + 100 * r for r in range(2)])
+    np.testing.assert_array_equal(g, want)
+    m, sem, sd = parallel.free_energy_stats(np.array([[10, 20, 100], [0, 5, 10], [5, 5, 10]]))
+    dF = np.array([np.log(2.0), 0.0, 0.0])
+    assert m == pytest.approx(dF.mean()) and sd == pytest.approx(dF.std())
+    assert sem == pytest.approx(dF.std() / np.sqrt(3))
+
+
 def test_free_energy():
     assert parallel.free_energy([10, 20, 100]) == pytest.approx(np.log(2.0))
     assert parallel.free_energy([0, 5, 10]) == 0.0

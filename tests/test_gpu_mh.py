@@ -107,6 +107,12 @@ def test_fused_step_matches_oracle_a1_n64():
     assert flips <= 1, (flips, n)
 
 
+def test_fused_step_matches_oracle_a1_n16():
+    """BASELINE config 2 (Algorithm 1, N=16) at the A1 flow hyper-parameters."""
+    flips, acc, n = _fused_vs_oracle(16, A1, C=256, steps=2)
+    assert flips <= 1, (flips, n)
+
+
 def test_batched_step_seed_sharding_independent_of_batch():
     """Chain c's trajectory depends only on (seed_c, proposal stream row c): running the
     first half of the chains alone reproduces them exactly (the multi-GPU contract)."""
