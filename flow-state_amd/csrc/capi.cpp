@@ -244,6 +244,26 @@ int fs_well_stats(const fs_phys *p, const double *pos, int64_t C, int32_t N, int
     return hip_rc(fs_well_stats_impl(p, pos, C, N, counts, (hipStream_t)stream), "fs_well_stats");
 }
 
+int fs_rqs_forward(int64_t M, int32_t K, int32_t inverse, const float *x, const float *uw, const float *uh,
+                   const float *ud, double tail_bound, float *out, float *lad, int32_t *nan_flag, void *stream) {
+    REQUIRE(M >= 0 && x && uw && uh && ud && out && lad && tail_bound > 0, "fs_rqs_forward: invalid arguments");
+    REQUIRE(K == 5 || K == 8 || K == 15 || K == 32, "fs_rqs_forward: K=%d not instantiated (5, 8, 15, 32)", K);
+    return hip_rc(fs_rqs_forward_impl(M, K, inverse, x, uw, uh, ud, (float)tail_bound, out, lad, nan_flag,
+                                      (hipStream_t)stream),
+                  "fs_rqs_forward");
+}
+
+int fs_rqs_backward(int64_t M, int32_t K, int32_t inverse, const float *x, const float *uw, const float *uh,
+                    const float *ud, double tail_bound, const float *g_out, const float *g_lad, float *gx,
+                    float *guw, float *guh, float *gud, void *stream) {
+    REQUIRE(M >= 0 && x && uw && uh && ud && gx && guw && guh && gud && tail_bound > 0,
+            "fs_rqs_backward: invalid arguments");
+    REQUIRE(K == 5 || K == 8 || K == 15 || K == 32, "fs_rqs_backward: K=%d not instantiated (5, 8, 15, 32)", K);
+    return hip_rc(fs_rqs_backward_impl(M, K, inverse, x, uw, uh, ud, (float)tail_bound, g_out, g_lad, gx, guw, guh,
+                                       gud, (hipStream_t)stream),
+                  "fs_rqs_backward");
+}
+
 int fs_classify_wells(const void *pos, int pos_is_f32, int64_t M, int32_t N, double half_box, double r0,
                       uint8_t *cls, uint8_t *state, double *avg_x, void *stream) {
     REQUIRE(pos && M >= 0 && N >= 1 && half_box > 0.0, "fs_classify_wells: invalid arguments");

@@ -34,6 +34,11 @@ hipError_t fs_classify_wells_impl(const void *pos, int f32, int64_t M, int N, do
 hipError_t fs_pair_hist_impl(const void *pos, int f32, int64_t M, int N, double bound, const double *edges, int nb,
                              int32_t *counts, hipStream_t st);
 hipError_t fs_rdf_mean_impl(const int32_t *counts, int64_t M, int nb, const double *denom, double *g, hipStream_t st);
+hipError_t fs_rqs_forward_impl(int64_t M, int K, int inverse, const float *x, const float *uw, const float *uh,
+                               const float *ud, float B, float *out, float *lad, int32_t *nan_flag, hipStream_t st);
+hipError_t fs_rqs_backward_impl(int64_t M, int K, int inverse, const float *x, const float *uw, const float *uh,
+                                const float *ud, float B, const float *g_out, const float *g_lad, float *gx,
+                                float *guw, float *guh, float *gud, hipStream_t st);
 hipError_t fs_center_impl(const double *state, int64_t n, double hw, float *out, hipStream_t st);
 hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state, const uint8_t *is_f32,
                                double *E, double *W, uint64_t *pcg, uint64_t *pcg_buf, double *max_disp,

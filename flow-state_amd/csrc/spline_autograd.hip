@@ -1,0 +1,320 @@
+// Fused circular rational-quadratic spline with its backward, for the training path
+// (Algorithm 2).  One thread per spline element (sample x
+// feature); the knots are rebuilt from the unnormalised parameters in registers in
+// both passes, so the backward stores nothing but the inputs.
+//
+// Forward: unconstrained_rational_quadratic_spline, circular-tail branch
+// (NF/normflows/utils/splines.py:16-88) + rational_quadratic_spline (:91-222): identity
+// and log-det 0 outside [-B, B]; inside: softmax -> min-width affine -> cumsum
+// (double accumulation, as torch CPU) -> [-B, B] with pinned ends; derivatives
+// 1e-3 + softplus; searchsorted with the eps on the last knot; the rational-quadratic
+// map (forward) or its quadratic-root inverse, and the log|det|.
+// Backward: reverse-mode by hand.  Forward direction: through theta = (x - cw_b)/w_b.
+// Inverse direction: the root theta* solves F(theta) = y, so its adjoint reaches y and
+// the knot values through -F_q / F_theta (implicit function theorem).  Knot adjoints go
+// back through the pinned cumsum (suffix sums), the min-width affine and softmax;
+// derivative adjoints through softplus (threshold 20, as torch).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "fs_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace fs {
+
+constexpr float kMin = 1e-3f;  // DEFAULT_MIN_BIN_WIDTH / HEIGHT / DERIVATIVE (splines.py:6-8)
+
+template <int K>
+struct Knots {
+    float c[K + 1];  // cumulative knots, pinned ends
+    float p[K];      // softmax probabilities
+};
+
+template <int K>
+__device__ __forceinline__ void build_knots(const float *u, float B, Knots<K> &kn) {
+    float m = u[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) m = fmaxf(m, u[k]);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        kn.p[k] = expf(u[k] - m);
+        s += kn.p[k];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) kn.p[k] = kn.p[k] / s;
+    const float c1 = 1.f - kMin * (float)K;
+    double cs = 0.0;
+    kn.c[0] = -B;
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) {
+        cs += (double)(kMin + c1 * kn.p[k]);
+        kn.c[k + 1] = (2.f * B) * (float)cs + (-B);
+    }
+    kn.c[K] = B;
+}
+
+__device__ __forceinline__ float softplus(float v) { return v > 20.f ? v : log1pf(expf(v)); }
+__device__ __forceinline__ float softplus_grad(float v) {
+    if (v > 20.f) return 1.f;
+    const float z = expf(v);
+    return z / (z + 1.f);
+}
+
+// values of the bin that contains x (searchsorted over `knots`, eps on the last one)
+template <int K>
+__device__ __forceinline__ int find_bin(float x, const float *knots) {
+    int b = -1;
+#pragma unroll
+    for (int k = 0; k <= K; ++k) {
+        const float kv = (k == K) ? knots[K] + 1e-6f : knots[k];
+        b += (x >= kv) ? 1 : 0;
+    }
+    return b < 0 ? 0 : (b > K - 1 ? K - 1 : b);
+}
+
+template <int K, bool INV>
+__global__ void rqs_forward_kernel(int64_t M, const float *__restrict__ x, const float *__restrict__ uw,
+                                   const float *__restrict__ uh, const float *__restrict__ ud, float B,
+                                   float *__restrict__ out, float *__restrict__ lad, int32_t *__restrict__ nan_flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const float xv = x[i];
+    if (!(xv >= -B && xv <= B)) {
+        out[i] = xv;
+        lad[i] = 0.f;
+        return;
+    }
+    Knots<K> W, Hh;
+    build_knots<K>(uw + i * K, B, W);
+    build_knots<K>(uh + i * K, B, Hh);
+    const int b = find_bin<K>(xv, INV ? Hh.c : W.c);
+    const float *dd = ud + i * (K + 1);
+    const float d0 = kMin + softplus(dd[b]), d1 = kMin + softplus(dd[b + 1]);
+    const float icw = W.c[b], ibw = W.c[b + 1] - W.c[b];
+    const float ich = Hh.c[b], ih = Hh.c[b + 1] - Hh.c[b];
+    const float s = ih / ibw;
+    float th;
+    if (INV) {
+        const float sdd = d0 + d1 - 2.f * s;
+        const float a = (xv - ich) * sdd + ih * (s - d0);
+        const float bb = ih * d0 - (xv - ich) * sdd;
+        const float c = -s * (xv - ich);
+        const float disc = fabsf(bb * bb - 4.f * a * c);
+        if (disc != disc && nan_flag) atomicOr(nan_flag, 1);
+        th = (2.f * c) / (-bb - sqrtf(disc));
+    } else {
+        th = (xv - icw) / ibw;
+    }
+    const float t = th * (1.f - th);
+    const float den = s + (d0 + d1 - 2.f * s) * t;
+    const float A = d1 * th * th + 2.f * s * t + d0 * (1.f - th) * (1.f - th);
+    const float l = logf(s * s * A) - 2.f * logf(den);
+    if (INV) {
+        out[i] = th * ibw + icw;
+        lad[i] = -l;
+    } else {
+        out[i] = ich + ih * (s * th * th + d0 * t) / den;
+        lad[i] = l;
+    }
+}
+
+// knot adjoints (g_c over c[0..K]) -> unnormalised-parameter adjoints
+template <int K>
+__device__ __forceinline__ void knots_backward(const Knots<K> &kn, const float *gc, float B, float *gu) {
+    const float c1 = 1.f - kMin * (float)K;
+    // c[k] = 2B * C[k] - B (k = 1..K-1), C[k] = sum_{j<k} w_j; c[0], c[K] pinned
+    float gw[K];
+    float suffix = 0.f;
+#pragma unroll
+    for (int j = K - 1; j >= 0; --j) {
+        gw[j] = suffix;                                  // sum over k = j+1 .. K-1 of g_C[k]
+        if (j >= 1) suffix += (2.f * B) * gc[j];         // add k = j for the next (smaller) j
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < K; ++j) dot += kn.p[j] * (c1 * gw[j]);
+#pragma unroll
+    for (int j = 0; j < K; ++j) gu[j] = kn.p[j] * (c1 * gw[j] - dot);
+}
+
+template <int K, bool INV>
+__global__ void rqs_backward_kernel(int64_t M, const float *__restrict__ x, const float *__restrict__ uw,
+                                    const float *__restrict__ uh, const float *__restrict__ ud, float B,
+                                    const float *__restrict__ g_out, const float *__restrict__ g_lad,
+                                    float *__restrict__ gx, float *__restrict__ guw, float *__restrict__ guh,
+                                    float *__restrict__ gud) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const float xv = x[i];
+    const float go = g_out ? g_out[i] : 0.f, gl = g_lad ? g_lad[i] : 0.f;
+    if (!(xv >= -B && xv <= B)) {
+        gx[i] = go;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            guw[i * K + k] = 0.f;
+            guh[i * K + k] = 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k <= K; ++k) gud[i * (K + 1) + k] = 0.f;
+        return;
+    }
+    Knots<K> W, Hh;
+    build_knots<K>(uw + i * K, B, W);
+    build_knots<K>(uh + i * K, B, Hh);
+    const int b = find_bin<K>(xv, INV ? Hh.c : W.c);
+    const float *dd = ud + i * (K + 1);
+    const float e0 = dd[b], e1 = dd[b + 1];
+    const float d0 = kMin + softplus(e0), d1 = kMin + softplus(e1);
+    const float icw = W.c[b], ibw = W.c[b + 1] - W.c[b];
+    const float ich = Hh.c[b], ih = Hh.c[b + 1] - Hh.c[b];
+    const float s = ih / ibw;
+    float th;
+    if (INV) {
+        const float sdd = d0 + d1 - 2.f * s;
+        const float a = (xv - ich) * sdd + ih * (s - d0);
+        const float bb = ih * d0 - (xv - ich) * sdd;
+        const float c = -s * (xv - ich);
+        const float disc = fabsf(bb * bb - 4.f * a * c);
+        th = (2.f * c) / (-bb - sqrtf(disc));
+    } else {
+        th = (xv - icw) / ibw;
+    }
+    const float t = th * (1.f - th);
+    const float omt = 1.f - th;
+    const float Nn = s * th * th + d0 * t;
+    const float den = s + (d0 + d1 - 2.f * s) * t;
+    const float A = d1 * th * th + 2.f * s * t + d0 * omt * omt;
+    const float dnum = s * s * A;
+    float g_th = 0.f, g_s = 0.f, g_t = 0.f, g_d0 = 0.f, g_d1 = 0.f;
+    float g_icw = 0.f, g_ibw = 0.f, g_ich = 0.f, g_ih = 0.f, g_x = 0.f;
+    // log-det part: l = log(dnum) - 2 log(den); forward lad = l, inverse lad = -l
+    const float gll = INV ? -gl : gl;
+    {
+        const float g_dnum = gll / dnum;
+        const float g_den = -2.f * gll / den;
+        const float g_A = g_dnum * s * s;
+        g_s += g_dnum * 2.f * s * A + g_A * 2.f * t;
+        g_d1 += g_A * th * th;
+        g_d0 += g_A * omt * omt;
+        g_th += g_A * (2.f * d1 * th - 2.f * d0 * omt);
+        g_t += g_A * 2.f * s;
+        g_s += g_den * (1.f - 2.f * t);
+        g_d0 += g_den * t;
+        g_d1 += g_den * t;
+        g_t += g_den * (d0 + d1 - 2.f * s);
+    }
+    if (INV) {
+        // out = theta * w_b + cw_b
+        g_th += go * ibw;
+        g_icw += go;
+        g_ibw += go * th;
+        g_th += g_t * (1.f - 2.f * th);
+        // theta* solves F(theta) = y, F = ch_b + h_b * N / den
+        const float N_th = 2.f * s * th + d0 * (1.f - 2.f * th);
+        const float den_th = (d0 + d1 - 2.f * s) * (1.f - 2.f * th);
+        const float F_th = ih * (N_th * den - Nn * den_th) / (den * den);
+        const float F_s = ih * (th * th * den - Nn * (1.f - 2.f * t)) / (den * den);
+        const float F_d0 = ih * (t * den - Nn * t) / (den * den);
+        const float F_d1 = -ih * Nn * t / (den * den);
+        const float wgt = g_th / F_th;
+        g_x += wgt;
+        g_ich -= wgt;
+        g_ih -= wgt * Nn / den;
+        g_s -= wgt * F_s;
+        g_d0 -= wgt * F_d0;
+        g_d1 -= wgt * F_d1;
+    } else {
+        // out = ch_b + h_b * N / den
+        const float g_num = go / den;
+        const float g_den = -go * (ih * Nn) / (den * den);
+        g_ich += go;
+        g_ih += g_num * Nn;
+        const float g_N = g_num * ih;
+        g_s += g_N * th * th;
+        g_th += g_N * 2.f * s * th;
+        g_d0 += g_N * t;
+        g_t += g_N * d0;
+        g_s += g_den * (1.f - 2.f * t);
+        g_d0 += g_den * t;
+        g_d1 += g_den * t;
+        g_t += g_den * (d0 + d1 - 2.f * s);
+        g_th += g_t * (1.f - 2.f * th);
+        // theta = (x - cw_b) / w_b
+        g_x += g_th / ibw;
+        g_icw -= g_th / ibw;
+        g_ibw -= g_th * th / ibw;
+    }
+    // s = h_b / w_b
+    g_ih += g_s / ibw;
+    g_ibw -= g_s * s / ibw;
+    gx[i] = g_x;
+    float gcw[K + 1], gch[K + 1];
+#pragma unroll
+    for (int k = 0; k <= K; ++k) {
+        gcw[k] = (k == b) ? (g_icw - g_ibw) : ((k == b + 1) ? g_ibw : 0.f);
+        gch[k] = (k == b) ? (g_ich - g_ih) : ((k == b + 1) ? g_ih : 0.f);
+    }
+    float gu[K];
+    knots_backward<K>(W, gcw, B, gu);
+#pragma unroll
+    for (int k = 0; k < K; ++k) guw[i * K + k] = gu[k];
+    knots_backward<K>(Hh, gch, B, gu);
+#pragma unroll
+    for (int k = 0; k < K; ++k) guh[i * K + k] = gu[k];
+#pragma unroll
+    for (int k = 0; k <= K; ++k) {
+        float g = 0.f;
+        if (k == b) g = g_d0 * softplus_grad(e0);
+        if (k == b + 1) g = g_d1 * softplus_grad(e1);
+        gud[i * (K + 1) + k] = g;
+    }
+}
+
+}  // namespace fs
+
+using namespace fs;
+
+#define FS_RQS_K(X) X(5) X(8) X(15) X(32)
+
+hipError_t fs_rqs_forward_impl(int64_t M, int K, int inverse, const float *x, const float *uw, const float *uh,
+                               const float *ud, float B, float *out, float *lad, int32_t *nan_flag,
+                               hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((M + 255) / 256)), block(256);
+#define FS_F(KK)                                                                                          \
+    if (K == KK) {                                                                                        \
+        if (inverse)                                                                                      \
+            hipLaunchKernelGGL((rqs_forward_kernel<KK, true>), grid, block, 0, st, M, x, uw, uh, ud, B, out, \
+                               lad, nan_flag);                                                            \
+        else                                                                                              \
+            hipLaunchKernelGGL((rqs_forward_kernel<KK, false>), grid, block, 0, st, M, x, uw, uh, ud, B, out, \
+                               lad, nan_flag);                                                            \
+        return hipGetLastError();                                                                         \
+    }
+    FS_RQS_K(FS_F)
+#undef FS_F
+    return hipErrorInvalidValue;
+}
+
+hipError_t fs_rqs_backward_impl(int64_t M, int K, int inverse, const float *x, const float *uw, const float *uh,
+                                const float *ud, float B, const float *g_out, const float *g_lad, float *gx,
+                                float *guw, float *guh, float *gud, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((M + 255) / 256)), block(256);
+#define FS_B(KK)                                                                                              \
+    if (K == KK) {                                                                                            \
+        if (inverse)                                                                                          \
+            hipLaunchKernelGGL((rqs_backward_kernel<KK, true>), grid, block, 0, st, M, x, uw, uh, ud, B, g_out, \
+                               g_lad, gx, guw, guh, gud);                                                     \
+        else                                                                                                  \
+            hipLaunchKernelGGL((rqs_backward_kernel<KK, false>), grid, block, 0, st, M, x, uw, uh, ud, B, g_out, \
+                               g_lad, gx, guw, guh, gud);                                                     \
+        return hipGetLastError();                                                                             \
+    }
+    FS_RQS_K(FS_B)
+#undef FS_B
+    return hipErrorInvalidValue;
+}

@@ -59,6 +59,10 @@ _SIGS = {
                        + [_I64, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_int32] + [_P] * 5),
     "fs_local_samples_per_chain": (_I64, [_I64, _I64, ctypes.c_int32]),
     "fs_adjust_displacement": (ctypes.c_int, [_I64, _P, _P, _P, _P, ctypes.c_double, _P]),
+    "fs_rqs_forward": (ctypes.c_int, [_I64, ctypes.c_int32, ctypes.c_int32] + [_P] * 4 + [ctypes.c_double]
+                       + [_P] * 4),
+    "fs_rqs_backward": (ctypes.c_int, [_I64, ctypes.c_int32, ctypes.c_int32] + [_P] * 4 + [ctypes.c_double]
+                        + [_P] * 7),
     "fs_classify_wells": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
                                           _P, _P, _P, _P]),
     "fs_pair_hist": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, _P, ctypes.c_int32,

@@ -90,7 +90,63 @@ def check_nan_flags():
         raise ValueError("Discriminant computation resulted in NaN.")
 
 
+_HIP_K = (5, 8, 15, 32)
+
+
+class _CircularRQS(torch.autograd.Function):
+    """The circular RQS of M elements as one HIP kernel each way (csrc/spline_autograd.hip:
+    fs_rqs_forward / fs_rqs_backward) instead of ~100 small torch kernels."""
+
+    @staticmethod
+    def forward(ctx, x, uw, uh, ud, B, inverse):
+        from .. import _lib
+
+        x, uw, uh, ud = (t.detach().contiguous().float() for t in (x, uw, uh, ud))
+        M, K = x.numel(), uw.shape[-1]
+        out = torch.empty_like(x)
+        lad = torch.empty_like(x)
+        flag = torch.zeros(1, dtype=torch.int32, device=x.device)
+        L = _lib.load()
+        _lib.check(L.fs_rqs_forward(M, K, int(inverse), _lib.ptr(x), _lib.ptr(uw), _lib.ptr(uh), _lib.ptr(ud),
+                                    float(B), _lib.ptr(out), _lib.ptr(lad), _lib.ptr(flag), _lib.stream_ptr()),
+                   "fs_rqs_forward")
+        _nan_flags.append(flag[0] != 0)
+        ctx.save_for_backward(x, uw, uh, ud)
+        ctx.B, ctx.inverse = float(B), int(inverse)
+        return out, lad
+
+    @staticmethod
+    def backward(ctx, g_out, g_lad):
+        from .. import _lib
+
+        x, uw, uh, ud = ctx.saved_tensors
+        M, K = x.numel(), uw.shape[-1]
+        go = g_out.contiguous().float() if g_out is not None else None
+        gl = g_lad.contiguous().float() if g_lad is not None else None
+        gx = torch.empty_like(x)
+        guw = torch.empty_like(uw)
+        guh = torch.empty_like(uh)
+        gud = torch.empty_like(ud)
+        L = _lib.load()
+        _lib.check(L.fs_rqs_backward(M, K, ctx.inverse, _lib.ptr(x), _lib.ptr(uw), _lib.ptr(uh), _lib.ptr(ud),
+                                     ctx.B, _lib.ptr(go), _lib.ptr(gl), _lib.ptr(gx), _lib.ptr(guw),
+                                     _lib.ptr(guh), _lib.ptr(gud), _lib.stream_ptr()), "fs_rqs_backward")
+        return gx, guw, guh, gud, None, None
+
+
 def circular_rqs(x, uw, uh, ud, B, inverse):
+    """Dispatch: the fused HIP spline for device tensors (K instantiated), the torch
+    restatement below otherwise (CPU tensors in tests and host-side use)."""
+    if x.is_cuda and uw.shape[-1] in _HIP_K:
+        shp = x.shape
+        K = uw.shape[-1]
+        out, lad = _CircularRQS.apply(x.reshape(-1), uw.reshape(-1, K), uh.reshape(-1, K), ud.reshape(-1, K + 1),
+                                      B, inverse)
+        return out.reshape(shp), lad.reshape(shp)
+    return circular_rqs_torch(x, uw, uh, ud, B, inverse)
+
+
+def circular_rqs_torch(x, uw, uh, ud, B, inverse):
     """unconstrained_rational_quadratic_spline, circular tails (splines.py:16-88): identity
     outside [-B, B]; the derivative pad writes index K+1, which is never read.  Evaluated
     on every element with the outside ones parked at 0 (so their unused branch stays

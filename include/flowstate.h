@@ -174,6 +174,24 @@ int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, i
                   int32_t *err, int flags, void *ws, void *stream);
 
 /* ------------------------------------------------------------------ */
+/* Training (Algorithm 2): the circular RQS element-wise, with backward */
+/* ------------------------------------------------------------------ */
+
+/* unconstrained_rational_quadratic_spline, circular tails (NF/normflows/utils/
+ * splines.py:16-222) for M independent elements: x [M], unnormalised widths /
+ * heights uw, uh [M][K], derivatives ud [M][K+1] (row-major, contiguous).
+ * inverse = 0: forward map, 1: inverse map.  out, lad [M]; nan_flag (nullable)
+ * |= 1 when an inverse discriminant is NaN (splines.py:176-183).  K in {5, 8, 15, 32}. */
+int fs_rqs_forward(int64_t M, int32_t K, int32_t inverse, const float *x, const float *uw, const float *uh,
+                   const float *ud, double tail_bound, float *out, float *lad, int32_t *nan_flag, void *stream);
+
+/* Gradients of sum(g_out * out + g_lad * lad) with respect to x, uw, uh, ud (g_out /
+ * g_lad nullable = zero), recomputing the forward from the same inputs. */
+int fs_rqs_backward(int64_t M, int32_t K, int32_t inverse, const float *x, const float *uw, const float *uh,
+                    const float *ud, double tail_bound, const float *g_out, const float *g_lad, float *gx,
+                    float *guw, float *guh, float *gud, void *stream);
+
+/* ------------------------------------------------------------------ */
 /* Local moves (MCMC/monte_carlo.py)                                   */
 /* ------------------------------------------------------------------ */
 
