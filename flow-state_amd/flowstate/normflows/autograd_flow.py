@@ -86,7 +86,7 @@ def check_nan_flags():
     a NaN (one device->host read per pass instead of one per layer)."""
     flags = list(_nan_flags)
     _nan_flags.clear()
-    if flags and bool(torch.stack(flags).any()):
+    if flags and bool(torch.stack([f.reshape(()).to(flags[0].device) for f in flags]).any()):
         raise ValueError("Discriminant computation resulted in NaN.")
 
 
