@@ -230,19 +230,18 @@ __device__ __forceinline__ void knots_from_logits(const float (&u)[K], float (&k
     float e[K];
     float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {  // exp via v_exp_f32 (2^x): a few ulp, far inside the 1e-5 parity bound
-        e[k] = __builtin_amdgcn_exp2f((u[k] - m) * 1.4426950408889634f);
+    for (int k = 0; k < K; ++k) {  // logits carry log2(e) (folded at pack time): one v_exp_f32 each
+        e[k] = __builtin_amdgcn_exp2f(u[k] - m);
         s += e[k];
     }
-    const float inv = 1.f / s;
     const float c1 = (float)(1.0 - 1e-3 * (double)K);
+    const float c1inv = c1 / s;
     double cs = 0.0;
     kn[0] = negB;
 #pragma unroll
-    for (int k = 0; k < K - 1; ++k) {
-        const float w = minb + c1 * (e[k] * inv);
-        cs += (double)w;
-        kn[k + 1] = twoB * (float)cs + negB;
+    for (int k = 0; k < K - 1; ++k) {  // fused affines: a rounding or two from torch's op-by-op, << 1e-5
+        cs += (double)__builtin_fmaf(e[k], c1inv, minb);
+        kn[k + 1] = __builtin_fmaf(twoB, (float)cs, negB);
     }
     kn[K] = B;
 }
@@ -327,8 +326,8 @@ __device__ __forceinline__ void stage_half(float *STG, const f32x16 &t0, const f
     }
 }
 
-// widths / heights logits of one feature, already divided by sqrt(H) (folded into
-// the packed final-layer columns and biases)
+// widths / heights logits of one feature, already scaled by log2(e) / sqrt(H) (folded
+// into the packed final-layer columns and biases)
 template <int K>
 __device__ __forceinline__ void load_logits(float *STG, const f32x16 &t0, const f32x16 &t1, float bias,
                                             float (&u)[K]) {
@@ -703,7 +702,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
 // kind 0: plain linear W[nout][kin];  kind 1: final layer main (feature tiles);
 // kind 2: final layer tail (d_K per feature)
 __global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restrict__ src, int kin, int kg,
-                                   int ntiles, int nout, int kind, int K, float inv_div) {
+                                   int ntiles, int nout, int kind, int K, float wh_scale) {
     const int64_t total = (int64_t)ntiles * kg * 256;
     const int P = 3 * K + 1;
     for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
@@ -716,19 +715,19 @@ __global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restr
         const int k = 8 * g + 4 * (lane >> 5) + j;
         const int c = lane & 31;
         int64_t row = -1;
-        float div = 1.f;
+        float sc = 1.f;
         if (kind == 0) {
             const int col = 32 * tile + c;
             row = col < nout ? col : -1;
         } else if (kind == 1) {
             const int feat = tile / 3, t = tile % 3;
             if (c < K) row = (int64_t)feat * P + t * K + c;
-            if (t < 2) div = inv_div;  // widths / heights: / sqrt(H) folded in (coupling.py:340-342)
+            if (t < 2) sc = wh_scale;  // widths / heights: / sqrt(H) (coupling.py:340-342) and * log2(e) folded in
         } else {
             const int feat = 32 * tile + c;
             if (feat < nout) row = (int64_t)feat * P + 3 * K;
         }
-        dst[idx] = (row >= 0 && k < kin) ? src[row * kin + k] / div : 0.f;
+        dst[idx] = (row >= 0 && k < kin) ? (sc == 1.f ? src[row * kin + k] : src[row * kin + k] * sc) : 0.f;
     }
 }
 
@@ -769,8 +768,10 @@ __global__ void pack_vec_kernel(float *__restrict__ dst, const float *__restrict
     }
     for (int i = tid; i < N * 96; i += nthr) {
         const int feat = i / 96, t = (i % 96) / 32, c = i % 32;
-        const float div = t < 2 ? (float)sqrt((double)H) : 1.f;  // / sqrt(H) of widths, heights folded in
-        V[PL.v_bf + i] = (c < K) ? src[R.bf + (int64_t)feat * P + t * K + c] / div : 0.f;
+        // widths, heights: / sqrt(H) and * log2(e) folded in (the kernel's softmax uses exp2)
+        const float sc = t < 2 ? (float)(1.4426950408889634 / sqrt((double)H)) : 1.f;
+        V[PL.v_bf + i] = (c < K) ? (t < 2 ? src[R.bf + (int64_t)feat * P + t * K + c] * sc
+                                         : src[R.bf + (int64_t)feat * P + t * K + c]) : 0.f;
     }
     for (int i = tid; i < PL.ntt * 32; i += nthr) V[PL.v_bt + i] = (i < N) ? src[R.bf + (int64_t)i * P + 3 * K] : 0.f;
     // unconditional knots (PiecewiseRationalQuadraticCDF, coupling.py:227-259): batch independent
@@ -897,7 +898,7 @@ hipError_t fs_flow_pack_impl(const fs_flow_dims *d, const float *raw, float *pac
             int blocks = (int)((tot + 255) / 256);
             if (blocks > 4096) blocks = 4096;
             hipLaunchKernelGGL(pack_linear_kernel, dim3(blocks), dim3(256), 0, st, o, w, kin, kg, ntiles, nout,
-                               kind, K, (float)sqrt((double)H));
+                               kind, K, (float)(1.4426950408889634 / sqrt((double)H)));
         };
         lin(dst + PL.win, src + R.win, 2 * N, PL.kg_in, H / 32, H, 0);
         for (int jb = 0; jb < nb; ++jb) {
