@@ -77,3 +77,30 @@ def test_product_has_no_oracle_dependency():
 
 def test_half_box():
     assert half_box(64) == pytest.approx(np.sqrt(64 / 0.03) / 2)
+
+
+def test_abi_rejects_invalid_arguments_before_touching_the_device():
+    """Argument checks of the C ABI run on the host: bad shapes / nulls return FS_EINVAL
+    (-1) or FS_EUNSUPPORTED (-2) with a message, and never launch."""
+    import ctypes
+
+    from flowstate import _lib
+
+    L = _lib.load()
+    ph = _lib.Phys()
+    one = ctypes.c_void_p(1)  # never dereferenced: validation fails first
+    rc = L.fs_local_moves(ph, 4, 65, one, None, one, None, one, one, one, one, one, None, 10, 0, 0, 0.5, 0, None,
+                          None, None, None, None)
+    assert rc == -1 and b"N=65" in L.fs_last_error()
+    rc = L.fs_local_moves(ph, 4, 16, one, None, one, None, one, one, one, one, one, None, 10, 0, 50, 0.5, 0, None,
+                          None, None, None, None)
+    assert rc == -1 and b"adjust_every" in L.fs_last_error()
+    rc = L.fs_rqs_forward(8, 7, 0, one, one, one, one, 3.0, one, one, None, None)
+    assert rc == -1 and b"K=7" in L.fs_last_error()
+    rc = L.fs_pair_hist(one, 1, 4, 300, 5.0, one, 10, one, None)
+    assert rc == -1
+    d = _lib.FlowDims(N=16, L=2, H=96, nb=1, K=8, reserved=0, tail_bound=5.0)
+    assert L.fs_flow_packed_bytes(d) == -1 and b"H=96" in L.fs_last_error()
+    rc = L.fs_nf_mh_step(_lib.FlowDims(N=16, L=2, H=64, nb=1, K=8, reserved=0, tail_bound=5.0), one, ph, 4, 0, 0, 0,
+                         None, None, None, None, None, None, None, None, None, None, None, 0, one, None)
+    assert rc == -1
