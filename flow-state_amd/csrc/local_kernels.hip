@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "fs_internal.h"
 #include "physics_device.h"
@@ -102,23 +104,39 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
     }
 }
 
-template <int LPC>
-__global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 1) local_moves_kernel(LocalArgs a) {
-    constexpr int G = 64 / LPC;  // chains per wave
-    __shared__ double lds[kLocalWaves][4][64];
+// select element q (group-uniform, runtime) of a small register array
+template <int PPL>
+__device__ __forceinline__ double pick(const double (&v)[PPL], int q) {
+    double r = v[0];
+#pragma unroll
+    for (int i = 1; i < PPL; ++i)
+        if (q == i) r = v[i];
+    return r;
+}
+
+// LPC lanes per chain, PPL particles per lane (particle j = gl + LPC * q): LPC*PPL >= N.
+// Several chains per wave amortise the per-move work that does not scale with N
+// (the PCG64 stream, broadcasts, the reduction tree, the double well, the accept).
+template <int LPC, int PPL>
+__global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_moves_kernel(LocalArgs a) {
+    constexpr int G = 64 / LPC;          // chains per wave
+    constexpr int SLOTS = LPC * PPL;     // LDS slots per chain and array
+    __shared__ double lds[kLocalWaves][4][G * SLOTS];
     __shared__ double res[kLocalWaves][G][4];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int g = lane / LPC, gl = lane % LPC, gb = g * LPC;
+    const int g = lane / LPC, gl = lane % LPC;
+    const int sb = g * SLOTS;            // this chain's slot base
     const int64_t c = ((int64_t)blockIdx.x * kLocalWaves + wid) * G + g;
     if (c >= a.C) return;  // whole groups leave; only group-internal shuffles below
     const int N = a.N;
     const fs_phys &P = a.p;
     const bool f32 = a.is_f32 && a.is_f32[c];
-    const bool own = gl < N;
-    double xj = 0.0, yj = 0.0;
-    if (own) {
-        xj = a.state[(c * N + gl) * 2];
-        yj = a.state[(c * N + gl) * 2 + 1];
+    double xj[PPL], yj[PPL];
+#pragma unroll
+    for (int q = 0; q < PPL; ++q) {
+        const int j = gl + LPC * q;
+        xj[q] = j < N ? a.state[(c * N + j) * 2] : 0.0;
+        yj[q] = j < N ? a.state[(c * N + j) * 2 + 1] : 0.0;
     }
     Pcg64 rng;
 #pragma unroll
@@ -133,7 +151,7 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 1) local_mov
     const double iLx = 1.0 / P.Lx, iLy = 1.0 / P.Ly;
     const int n = N - 1;
     const int nfull = n - (n % 8);
-    const uint64_t gmask = (LPC == 64) ? ~0ull : (((1ull << LPC) - 1ull) << gb);
+    const uint64_t gmask = (LPC == 64) ? ~0ull : (((1ull << LPC) - 1ull) << (g * LPC));
     // double-well role of this lane: 0/1 = old position well 0/1, 2/3 = new position
     const int dw_well = gl & 1;
     const bool dw_lane = gl < 4 && dw_well < P.num_wells;
@@ -145,7 +163,8 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 1) local_mov
         const int64_t step = a.step0 + t + 1;
         att += 1;
         const int p = (int)pcg64_integers(rng, (uint32_t)N);
-        const double ox = bcast<LPC>(xj, p), oy = bcast<LPC>(yj, p);
+        const int pq = p / LPC, pl = p % LPC;
+        const double ox = bcast<LPC>(pick<PPL>(xj, pq), pl), oy = bcast<LPC>(pick<PPL>(yj, pq), pl);
         const double d0 = (pcg64_double(rng) - 0.5) * md;
         const double d1 = (pcg64_double(rng) - 0.5) * md;
         double nx, ny;
@@ -156,29 +175,32 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 1) local_mov
             nx = np_remainder(ox + d0, P.Lx);
             ny = np_remainder(oy + d1, P.Ly);
         }
-        // pair terms of particle p against particle j (np.delete order: index j - (j > p))
-        const bool act = own && gl != p;
-        double eo = 0.0, wo = 0.0, en = 0.0, wn = 0.0;
+        // pair terms of particle p against this lane's particles (np.delete order: j - (j > p))
         bool ho = false, hn = false;
-        if (act) {
-            double ro, rn;
-            if (f32) {
-                const float fx = (float)xj, fy = (float)yj;
-                ro = dist_f32((float)ox, (float)oy, fx, fy, P.Lx, P.Ly, iLx, iLy);
-                rn = dist_f32((float)nx, (float)ny, fx, fy, P.Lx, P.Ly, iLx, iLy);
-            } else {
-                ro = dist_f64(ox, oy, xj, yj, P.Lx, P.Ly, iLx, iLy);
-                rn = dist_f64(nx, ny, xj, yj, P.Lx, P.Ly, iLx, iLy);
+#pragma unroll
+        for (int q = 0; q < PPL; ++q) {
+            const int j = gl + LPC * q;
+            if (j < N && j != p) {
+                double ro, rn;
+                if (f32) {
+                    const float fx = (float)xj[q], fy = (float)yj[q];
+                    ro = dist_f32((float)ox, (float)oy, fx, fy, P.Lx, P.Ly, iLx, iLy);
+                    rn = dist_f32((float)nx, (float)ny, fx, fy, P.Lx, P.Ly, iLx, iLy);
+                } else {
+                    ro = dist_f64(ox, oy, xj[q], yj[q], P.Lx, P.Ly, iLx, iLy);
+                    rn = dist_f64(nx, ny, xj[q], yj[q], P.Lx, P.Ly, iLx, iLy);
+                }
+                ho |= ro < P.r_core;
+                hn |= rn < P.r_core;
+                double eo, wo, en, wn;
+                lj_pair(ro, P.r_cut, e_cut, eo, wo);
+                lj_pair(rn, P.r_cut, e_cut, en, wn);
+                const int tt = sb + j - (j > p ? 1 : 0);
+                lds[wid][0][tt] = eo;
+                lds[wid][1][tt] = wo;
+                lds[wid][2][tt] = en;
+                lds[wid][3][tt] = wn;
             }
-            ho = ro < P.r_core;
-            hn = rn < P.r_core;
-            lj_pair(ro, P.r_cut, e_cut, eo, wo);
-            lj_pair(rn, P.r_cut, e_cut, en, wn);
-            const int tt = gb + gl - (gl > p ? 1 : 0);
-            lds[wid][0][tt] = eo;
-            lds[wid][1][tt] = wo;
-            lds[wid][2][tt] = en;
-            lds[wid][3][tt] = wn;
         }
         const bool hit_old = (__ballot(ho) & gmask) != 0;
         const bool hit_new = (__ballot(hn) & gmask) != 0;
@@ -193,7 +215,7 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 1) local_mov
         if (n < 8) {
             double r = 0.0;
             if (gl < 4)
-                for (int k = 0; k < n; ++k) r += lds[wid][gl][gb + k];
+                for (int k = 0; k < n; ++k) r += lds[wid][gl][sb + k];
 #pragma unroll
             for (int q = 0; q < 4; ++q) sums[q] = bcast<LPC>(r, q);
         } else if constexpr (LPC == 64) {
@@ -212,15 +234,15 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 1) local_mov
 #pragma unroll
             for (int q = 0; q < 4; ++q) sums[q] = bcast<LPC>(r, 8 * q);
         } else {
-            for (int ak = gl; ak < 32; ak += LPC) {  // LPC >= 16 here (N > 8)
+            for (int ak = gl; ak < 32; ak += LPC) {  // LPC >= 8
                 const int arr = ak >> 3, k = ak & 7;
-                double r = lds[wid][arr][gb + k];
-                for (int b = 8; b < nfull; b += 8) r += lds[wid][arr][gb + b + k];
+                double r = lds[wid][arr][sb + k];
+                for (int b = 8; b < nfull; b += 8) r += lds[wid][arr][sb + b + k];
                 r += __shfl_xor(r, 1, LPC);
                 r += __shfl_xor(r, 2, LPC);
                 r += __shfl_xor(r, 4, LPC);
                 if (k == 0) {
-                    for (int i = nfull; i < n; ++i) r += lds[wid][arr][gb + i];
+                    for (int i = nfull; i < n; ++i) r += lds[wid][arr][sb + i];
                     res[wid][g][arr] = r;
                 }
             }
@@ -251,18 +273,28 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 1) local_mov
             E += enn - eno;
             W += virn - viro;
             n_acc_local += 1;
-            if (gl == p) {
-                xj = nx;
-                yj = ny;
+            if (gl == pl) {
+#pragma unroll
+                for (int q = 0; q < PPL; ++q)
+                    if (q == pq) {
+                        xj[q] = nx;
+                        yj[q] = ny;
+                    }
             }
         }
         if (a.accept_log && gl == 0) a.accept_log[c * a.n_moves + t] = accept ? 1 : 0;
         if (a.adjust_every > 0 && step % a.adjust_every == 0) adjust_md(md, att, acc_n, prev_att, prev_acc, a.target);
         if (a.sample_every > 0 && step % a.sample_every == 0 && samp < a.n_samp) {
-            if (a.samples_xy && own) {
-                double *q = a.samples_xy + ((c * a.n_samp + samp) * N + gl) * 2;
-                q[0] = xj;
-                q[1] = yj;
+            if (a.samples_xy) {
+#pragma unroll
+                for (int q = 0; q < PPL; ++q) {
+                    const int j = gl + LPC * q;
+                    if (j < N) {
+                        double *o = a.samples_xy + ((c * a.n_samp + samp) * N + j) * 2;
+                        o[0] = xj[q];
+                        o[1] = yj[q];
+                    }
+                }
             }
             if (a.samples_ew && gl == 0) {
                 a.samples_ew[(c * a.n_samp + samp) * 2] = E;
@@ -271,9 +303,13 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 1) local_mov
             ++samp;
         }
     }
-    if (own) {
-        a.state[(c * N + gl) * 2] = xj;
-        a.state[(c * N + gl) * 2 + 1] = yj;
+#pragma unroll
+    for (int q = 0; q < PPL; ++q) {
+        const int j = gl + LPC * q;
+        if (j < N) {
+            a.state[(c * N + j) * 2] = xj[q];
+            a.state[(c * N + j) * 2 + 1] = yj[q];
+        }
     }
     if (gl == 0) {
 #pragma unroll
@@ -313,16 +349,28 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
                 pcg,      pcg_buf,   max_disp, attempts,   accepted,   prev,       n_moves,
                 step0,    adjust_every, target, sample_every, fs_local_samples_per_chain(step0, n_moves, sample_every),
                 samples_xy, samples_ew, accept_log, n_accept};
-    const int lpc = N > 32 ? 64 : N > 16 ? 32 : N > 8 ? 16 : 8;
+    // lanes per chain x particles per lane (FS_LOCAL_LAYOUT=LPCxPPL overrides, for A/B runs)
+    // measured at 65536 chains x 1000 moves: 8 lanes per chain is fastest at every N
+    // (N=64: 1.90 G moves/s with 8x8 vs 1.11 G with 64x1; N=32: 2.68 G; N=16: 3.50 G)
+    int lpc = 8;
+    int ppl = N > 32 ? 8 : N > 16 ? 4 : N > 8 ? 2 : 1;
+    if (const char *e = getenv("FS_LOCAL_LAYOUT")) {
+        int l = 0, q = 0;
+        if (sscanf(e, "%dx%d", &l, &q) == 2 && l * q >= N) {
+            lpc = l;
+            ppl = q;
+        }
+    }
     const int64_t chains_per_block = (int64_t)kLocalWaves * (64 / lpc);
     const dim3 grid((unsigned)((C + chains_per_block - 1) / chains_per_block)), block(64 * kLocalWaves);
-    switch (lpc) {
-    case 64: hipLaunchKernelGGL(local_moves_kernel<64>, grid, block, 0, st, a); break;
-    case 32: hipLaunchKernelGGL(local_moves_kernel<32>, grid, block, 0, st, a); break;
-    case 16: hipLaunchKernelGGL(local_moves_kernel<16>, grid, block, 0, st, a); break;
-    default: hipLaunchKernelGGL(local_moves_kernel<8>, grid, block, 0, st, a); break;
+#define FS_LCASE(L, Q)                                                                \
+    if (lpc == L && ppl == Q) {                                                       \
+        hipLaunchKernelGGL((local_moves_kernel<L, Q>), grid, block, 0, st, a);        \
+        return hipGetLastError();                                                     \
     }
-    return hipGetLastError();
+    FS_LCASE(8, 1) FS_LCASE(8, 2) FS_LCASE(8, 4) FS_LCASE(8, 8) FS_LCASE(64, 1) FS_LCASE(16, 4)
+#undef FS_LCASE
+    return hipErrorInvalidValue;
 }
 
 hipError_t fs_adjust_displacement_impl(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,
