@@ -77,13 +77,21 @@ class DoubleWellLJ(SimpleLJ):
         self.k = k
         self.centers = torch.tensor([[-bound / 2, 0.0], [bound / 2, 0.0]], dtype=torch.float32)
 
+    def _on(self, device):
+        """centers / V0_list on `device`, copied once (no host->device copy per call, so
+        the energy can sit inside a captured HIP graph)."""
+        cache = self.__dict__.setdefault("_dev_cache", {})
+        key = str(device)
+        if key not in cache:
+            cache[key] = (self.centers.to(device), self.V0_list.to(device))
+        return cache[key]
+
     def double_well_potential(self, positions):
         """Energy/SimpleLJ.py:63-115, vectorised over particles (the reference loops over
         them in Python; the per-particle terms are identical, the particle sum is a
         tensor reduction)."""
         L = 2 * self.bound
-        centers = self.centers.to(positions.device)
-        V0 = self.V0_list.to(positions.device)
+        centers, V0 = self._on(positions.device)
         x = positions[:, :, 0]
         y = positions[:, :, 1]
         Vp = torch.zeros_like(x)

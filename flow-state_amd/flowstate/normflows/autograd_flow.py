@@ -79,11 +79,23 @@ def rational_quadratic_spline(x, uw, uh, ud, inverse, left, right, bottom, top):
 
 
 _nan_flags = []
+_defer_nan = False  # set while a training step is captured in a graph (train.py)
+
+
+def reduce_nan_flags(device):
+    """All pending NaN flags as one device bool (graph-capturable, no host read)."""
+    flags = [f.reshape(()).to(device) for f in _nan_flags]
+    _nan_flags.clear()
+    if not flags:
+        return torch.zeros((), dtype=torch.bool, device=device)
+    return torch.stack(flags).any()
 
 
 def check_nan_flags():
     """Raise the reference's discriminant error if any inverse spline of the pass hit
     a NaN (one device->host read per pass instead of one per layer)."""
+    if _defer_nan:
+        return
     flags = list(_nan_flags)
     _nan_flags.clear()
     if flags and bool(torch.stack([f.reshape(()).to(flags[0].device) for f in flags]).any()):

@@ -1,0 +1,103 @@
+"""Algorithm-2 training step captured in a HIP graph (hybrid_NF_MCMC/main_algorithm_2.py:314-331).
+
+One step of the reference loop is
+
+    optimizer.zero_grad()
+    energy_loss, z = model.reverse_kld(BATCH_SIZE)
+    sample_loss = model.forward_kld(batch)
+    loss = ALPHA * sample_loss + (1 - ALPHA) * energy_loss
+    if ~(torch.isnan(loss) | torch.isinf(loss)):
+        loss.backward(); optimizer.step()
+
+With eager PyTorch that is ~7 k small kernel launches per step at A2 / batch 256, so the
+step is launch-bound.  `GraphedTrainStep` records the whole step once with
+torch.cuda.graph (fused spline kernels and HIP GEMMs included) and replays it:
+
+  * the batch is copied into a static input buffer before each replay;
+  * the base draws of reverse_kld come from the default generator inside the graph
+    (fresh draws every replay, as the reference's q0 sampling);
+  * Adam runs with capturable=True; the reference's "skip the step when the loss is
+    NaN / inf" is a device-side select: parameters and optimizer state are snapshotted
+    before the update and restored where the loss was not finite;
+  * the spline's NaN-discriminant flags are reduced inside the graph and checked after
+    the replay (the reference raises ValueError; here it is raised after the step).
+"""
+import torch
+
+from . import autograd_flow as AF
+
+
+class GraphedTrainStep:
+    def __init__(self, model, batch_size, lr, weight_decay=0.0, alpha=1.0, warmup=3, example=None):
+        dev = next(model.parameters()).device
+        if dev.type != "cuda":
+            raise ValueError("GraphedTrainStep needs the model on the GPU")
+        self.model = model
+        self.batch_size = int(batch_size)
+        self.alpha = float(alpha)
+        D = model.flows[0].num_input_channels
+        self.x = torch.zeros((self.batch_size, D), device=dev) if example is None else example.clone().to(dev)
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.opt = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay, capturable=True)
+        model.train()
+        # warm up on a side stream (allocator, hipBLASLt heuristics, Adam state), then put
+        # the parameters, BatchNorm buffers and optimizer state back: capturing must not
+        # change the model
+        saved = [t.detach().clone() for t in list(model.parameters()) + list(model.buffers())]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._eager_step(self.x)
+        torch.cuda.current_stream().wait_stream(s)
+        with torch.no_grad():
+            for t, v in zip(list(model.parameters()) + list(model.buffers()), saved):
+                t.copy_(v)
+            for p in self.params:
+                for v in self.opt.state[p].values():
+                    if torch.is_tensor(v):
+                        v.zero_()
+        # snapshots of everything the optimizer step mutates
+        self._state_tensors = []
+        for p in self.params:
+            st = self.opt.state[p]
+            self._state_tensors += [p] + [v for v in st.values() if torch.is_tensor(v)]
+        self._backup = [t.detach().clone() for t in self._state_tensors]
+        self.graph = torch.cuda.CUDAGraph()
+        self.opt.zero_grad(set_to_none=False)
+        AF._defer_nan = True
+        try:
+            with torch.cuda.graph(self.graph):
+                self.opt.zero_grad(set_to_none=False)
+                energy_loss, _ = model.reverse_kld(self.batch_size)
+                sample_loss = model.forward_kld(self.x)
+                self.loss = self.alpha * sample_loss + (1 - self.alpha) * energy_loss
+                self.loss.backward()
+                self.finite = ~(torch.isnan(self.loss) | torch.isinf(self.loss))
+                for b, t in zip(self._backup, self._state_tensors):
+                    b.copy_(t.detach())
+                self.opt.step()
+                with torch.no_grad():
+                    for b, t in zip(self._backup, self._state_tensors):
+                        t.copy_(torch.where(self.finite, t, b))
+                self.nan_flag = AF.reduce_nan_flags(dev)
+        finally:
+            AF._defer_nan = False
+
+    def _eager_step(self, x):
+        self.opt.zero_grad(set_to_none=False)
+        energy_loss, _ = self.model.reverse_kld(self.batch_size)
+        sample_loss = self.model.forward_kld(x)
+        loss = self.alpha * sample_loss + (1 - self.alpha) * energy_loss
+        if bool(~(torch.isnan(loss) | torch.isinf(loss))):
+            loss.backward()
+            self.opt.step()
+        return loss
+
+    def step(self, batch):
+        """One training step on `batch` (B, D); returns the loss tensor (device scalar)."""
+        self.x.copy_(batch)
+        self.graph.replay()
+        if bool(self.nan_flag):
+            raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
+        return self.loss
