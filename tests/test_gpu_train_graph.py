@@ -31,6 +31,7 @@ def test_graphed_step_matches_eager(alpha):
     x = torch.from_numpy(f["x"]).cuda()
     opt = torch.optim.Adam(m1.parameters(), lr=lr, weight_decay=wd)
     g = GraphedTrainStep(m2, 64, lr, wd, alpha=alpha, example=x)
+    p0 = {k: v.clone() for k, v in m1.state_dict().items()}
     for sd1, sd2 in zip(m1.state_dict().values(), m2.state_dict().values()):
         assert torch.equal(sd1, sd2)  # capture left the model untouched
     for i in range(4):
@@ -38,10 +39,16 @@ def test_graphed_step_matches_eager(alpha):
         l1 = _eager(m1, opt, xb, alpha)
         l2 = g.step(xb)
         np.testing.assert_allclose(l2.item(), l1.item(), rtol=1e-4)
+    # Adam normalises each coordinate, so a near-zero gradient turns float32 noise between
+    # the capturable and the default implementation into an lr-sized difference on that
+    # coordinate: compare the updates per tensor in norm
     for (k, v1), v2 in zip(m1.state_dict().items(), m2.state_dict().values()):
-        # Adam normalises each coordinate: near-zero gradients turn float32 noise between the
-        # capturable and the default implementation into ~lr-sized update differences
-        np.testing.assert_allclose(v2.cpu().numpy(), v1.cpu().numpy(), rtol=1e-4, atol=2e-5, err_msg=k)
+        if not v1.is_floating_point():
+            assert torch.equal(v1, v2), k
+            continue
+        moved = (v1 - p0[k]).norm().item()
+        diff = (v2 - v1).norm().item()
+        assert diff <= 2e-2 * moved + 1e-6, (k, diff, moved)
 
 
 def test_graphed_step_skips_non_finite_loss():
