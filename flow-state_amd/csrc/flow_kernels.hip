@@ -150,17 +150,20 @@ __device__ __forceinline__ void b_prologue(BRing<CT, PD> &br, __amdgpu_buffer_rs
 // pointer per ring slot to keep live.  Operands of k-group g live in ring slot
 // g % PD; the loads of group g+PD are issued right after the MFMAs of group g
 // (sched_barrier keeps hipcc from sinking them next to their use).
-template <int XS, int RT, int CT, int PD>
+// ACC = true accumulates onto the incoming acc (the residual add of a ResidualBlock
+// done by the matrix cores instead of 16 VALU adds per tile).
+template <int XS, int RT, int CT, int PD, bool ACC = false>
 __device__ __forceinline__ void gemm_run(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
                                          int rt0, int ct0, BRing<CT, PD> &br, f32x16 (&acc)[RT][CT]) {
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, r = lane & 31;
+    if (!ACC)
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+        for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
+            for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) acc[rt][ct][i] = 0.f;
+                for (int i = 0; i < 16; ++i) acc[rt][ct][i] = 0.f;
     const float *xa = X + (32 * rt0 + r) * XS + 4 * h;
     const int voff = (ct0 * kg * 64 + lane) * 16;
     f32x4 ra[PD][RT];
@@ -535,24 +538,20 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
         // groups synchronise only internally (LDS-counter barriers), so one group's
         // epilogue / barrier bubbles run under the other group's MFMAs.
         f32x16 hr[1][CTg], acc[1][CTg];
-        if (gact) {  // initial_layer
-            gemm64<XS, 1, CTg, FS_RPD>(X, W, (int)(PL.win * 4), PL.kg_in, grp, gct0, acc);
-#pragma unroll
-            for (int ct = 0; ct < CTg; ++ct) {
-                const float bb = V[32 * (gct0 + ct) + r];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) hr[0][ct][i] = acc[0][ct][i] + bb;
-            }
-        }
+        // hr = the residual stream WITHOUT its biases: b_in and every block's b1 are
+        // deferred (pack_vec_kernel folds a0 * their running sum into each block's c0 and
+        // their total into s_h), b0 is folded into c1, and the residual add is the
+        // accumulator input of the second GEMM.  The epilogues are 1 FMA + 1 max.
+        if (gact) gemm64<XS, 1, CTg, FS_RPD>(X, W, (int)(PL.win * 4), PL.kg_in, grp, gct0, hr);  // initial_layer
         pf.mark(PH_INIT_GEMM);
-        // per-column epilogue vectors {a0,c0,b0,a1,c1,b1} of a block: loaded one block
+        // per-column epilogue vectors {a0,c0',a1,c1'} of a block: loaded one block
         // ahead and always BEFORE the next GEMM's weight prologue, so the epilogue's
         // vmcnt wait never covers the prologue's (L2 / MALL latency) loads
-        float ev[6][CTg];
-        auto load_ev = [&](int jb, float (&e)[6][CTg]) {
-            const float *VB = V + PL.v_blocks + (int64_t)6 * H * jb;
+        float ev[4][CTg];
+        auto load_ev = [&](int jb, float (&e)[4][CTg]) {
+            const float *VB = V + PL.v_blocks + (int64_t)4 * H * jb;
 #pragma unroll
-            for (int q = 0; q < 6; ++q)
+            for (int q = 0; q < 4; ++q)
 #pragma unroll
                 for (int ct = 0; ct < CTg; ++ct) e[q][ct] = VB[q * H + 32 * (gct0 + ct) + r];
         };
@@ -571,7 +570,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
                     const int col = 32 * (gct0 + ct) + r;
 #pragma unroll
                     for (int i = 0; i < 16; ++i)
-                        X[acc_row(grp, i, h) * XS + col] = fmaxf(hr[0][ct][i] * ev[0][ct] + ev[1][ct], 0.f);
+                        X[acc_row(grp, i, h) * XS + col] = fmaxf(fmaf(hr[0][ct][i], ev[0][ct], ev[1][ct]), 0.f);
                 }
             }
             pf.mark(PH_EPI);
@@ -590,38 +589,34 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
                     const int col = 32 * (gct0 + ct) + r;
 #pragma unroll
                     for (int i = 0; i < 16; ++i)
-                        X[acc_row(grp, i, h) * XS + col] =
-                            fmaxf((acc[0][ct][i] + ev[2][ct]) * ev[3][ct] + ev[4][ct], 0.f);
+                        X[acc_row(grp, i, h) * XS + col] = fmaxf(fmaf(acc[0][ct][i], ev[2][ct], ev[3][ct]), 0.f);
                 }
             }
             pf.mark(PH_EPI);
             group_barrier(gbar + grp, gphase);
             pf.mark(PH_BARRIER);
-            float evn[6][CTg];
+            float evn[4][CTg];
             if (jb + 1 < a.nb) load_ev(jb + 1, evn);
             if (gact) {
-                gemm_run<XS, 1, CTg, FS_RPD>(X, W, w1, PL.kg_h, grp, gct0, br, acc);
+                gemm_run<XS, 1, CTg, FS_RPD, true>(X, W, w1, PL.kg_h, grp, gct0, br, hr);  // h += Lin1(t)
                 if (jb + 1 < a.nb) b_prologue<CTg, FS_RPD>(br, W, w1 + (int)(PL.block_stride * 2), PL.kg_h, gct0);
-#pragma unroll
-                for (int ct = 0; ct < CTg; ++ct)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) hr[0][ct][i] = hr[0][ct][i] + (acc[0][ct][i] + ev[5][ct]);
             }
             if (jb + 1 < a.nb)
 #pragma unroll
-                for (int q = 0; q < 6; ++q)
+                for (int q = 0; q < 4; ++q)
 #pragma unroll
                     for (int ct = 0; ct < CTg; ++ct) ev[q][ct] = evn[q][ct];
             pf.mark(PH_RES_GEMM);
         }
         group_barrier(gbar + grp, gphase);
         pf.mark(PH_BARRIER);
-        if (gact) {  // X <- h for the final layer
+        if (gact) {  // X <- h (+ the deferred biases) for the final layer
 #pragma unroll
             for (int ct = 0; ct < CTg; ++ct) {
                 const int col = 32 * (gct0 + ct) + r;
+                const float sh = V[col];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) X[acc_row(grp, i, h) * XS + col] = hr[0][ct][i];
+                for (int i = 0; i < 16; ++i) X[acc_row(grp, i, h) * XS + col] = hr[0][ct][i] + sh;
             }
         }
         pf.mark(PH_EPI);
@@ -742,29 +737,34 @@ __global__ void pack_vec_kernel(float *__restrict__ dst, const float *__restrict
     const int P = 3 * K + 1;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     const int nthr = gridDim.x * blockDim.x;
-    for (int i = tid; i < H; i += nthr) V[i] = src[R.bin + i];
+    // ResidualBlocks with the biases re-associated (the kernel's residual stream hr
+    // omits b_in and the blocks' b1; S_jb = b_in + sum_{j<jb} b1_j is carried here):
+    //   relu(BN0(h)) = relu(a0*hr + (c0 + a0*S_jb))        -> {a0, c0'}
+    //   relu(BN1(Lin0 + b0)) = relu(a1*acc + (c1 + a1*b0))  -> {a1, c1'}
+    //   final input h = hr + S_nb                           -> s_h = V[0:H)
+    // with eval BN a = w / sqrt(var + eps), c = b - mean * a.
     const float eps = 1e-3f;
-    for (int i = tid; i < nb * H; i += nthr) {
-        const int jb = i / H, c = i % H;
-        const float *B = src + R.blocks + (int64_t)jb * R.block_stride;
-        float *VB = V + PL.v_blocks + (int64_t)6 * H * jb;
-        {
-            const float w = B[c], b = B[H + c], m = B[2 * H + c], v = B[3 * H + c];
-            const float inv = 1.f / sqrtf(v + eps);
-            const float al = inv * w;
-            VB[c] = al;
-            VB[H + c] = b - m * al;
+    for (int c = tid; c < H; c += nthr) {
+        double S = src[R.bin + c];
+        for (int jb = 0; jb < nb; ++jb) {
+            const float *B = src + R.blocks + (int64_t)jb * R.block_stride;
+            float *VB = V + PL.v_blocks + (int64_t)4 * H * jb;
+            {
+                const float w = B[c], b = B[H + c], m = B[2 * H + c], v = B[3 * H + c];
+                const float al = (1.f / sqrtf(v + eps)) * w;
+                VB[c] = al;
+                VB[H + c] = (float)((double)(b - m * al) + (double)al * S);
+            }
+            {
+                const float *B1 = B + RawLayout::bn1(H);
+                const float w = B1[c], b = B1[H + c], m = B1[2 * H + c], v = B1[3 * H + c];
+                const float al = (1.f / sqrtf(v + eps)) * w;
+                VB[2 * H + c] = al;
+                VB[3 * H + c] = (float)((double)(b - m * al) + (double)al * B[RawLayout::b0(H) + c]);
+            }
+            S += B[RawLayout::b1(H) + c];
         }
-        VB[2 * H + c] = B[RawLayout::b0(H) + c];
-        {
-            const float *B1 = B + RawLayout::bn1(H);
-            const float w = B1[c], b = B1[H + c], m = B1[2 * H + c], v = B1[3 * H + c];
-            const float inv = 1.f / sqrtf(v + eps);
-            const float al = inv * w;
-            VB[3 * H + c] = al;
-            VB[4 * H + c] = b - m * al;
-        }
-        VB[5 * H + c] = B[RawLayout::b1(H) + c];
+        V[c] = (float)S;
     }
     for (int i = tid; i < N * 96; i += nthr) {
         const int feat = i / 96, t = (i % 96) / 32, c = i % 32;

@@ -63,7 +63,7 @@ struct PackLayout {
     int64_t block_stride;
     int64_t wf;      // final layer, per feature j: 3 tiles (widths, heights, d_0..d_{K-1})
     int64_t wt;      // tail block: column n = d_K of feature n
-    int64_t vec;     // b_in[H]; nb x {a0,c0,b0,a1,c1,b1}[H]; bf[N][3][32]; bt[ntt*32]
+    int64_t vec;     // s_h[H]; nb x {a0,c0',a1,c1'}[H]; bf[N][3][32]; bt[ntt*32] (see pack_vec_kernel)
     int64_t v_blocks, v_bf, v_bt;
     int64_t unc;     // unconditional knots: [N][3][K+1] = cumwidths, cumheights, derivatives
     int64_t stride;
@@ -82,7 +82,7 @@ FS_HD PackLayout pack_layout(int N, int H, int nb, int K) {
     p.wt = rup(p.wf + (int64_t)N * 3 * p.kg_h * 256, 64);
     p.vec = rup(p.wt + (int64_t)p.ntt * p.kg_h * 256, 64);
     p.v_blocks = H;
-    p.v_bf = p.v_blocks + 6 * (int64_t)H * nb;
+    p.v_bf = p.v_blocks + 4 * (int64_t)H * nb;
     p.v_bt = p.v_bf + (int64_t)N * 96;
     p.unc = rup(p.vec + p.v_bt + p.ntt * 32, 64);
     p.stride = rup(p.unc + (int64_t)N * 3 * (K + 1), 64);
