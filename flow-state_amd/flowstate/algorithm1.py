@@ -1,0 +1,223 @@
+"""The phases of the Algorithm-1 driver (hybrid_NF_MCMC/main_algorithm_1.py) with every
+run ("MC run" = chain) batched on the device.
+
+The reference drives NUM_MC_RUNS MonteCarlo objects one after the other in Python
+loops.  Runs never interact, so each loop below is one device call over all runs;
+the bookkeeping that depends on the reference's run-major loop order (the global
+acceptance history, total_mcmc_steps, the order of the training samples) is
+rebuilt from the per-run device results afterwards:
+
+  equilibrate        main_algorithm_1.py:202-210  (particle_displacement, adjust_displacement, sample)
+  production         main_algorithm_1.py:240-251  (training samples, run-major)
+  testing_phase      main_algorithm_1.py:375-424  (BIG_MOVE_INTERVAL local moves + one nf_big_move per attempt)
+  well_statistics    main_algorithm_1.py:443-455 -> utils.py:61-101 (calculate_well_statistics per run)
+  free_energy_curve  utils.py:738-763 (plot_avg_free_energy's mean / sem / std, no plotting)
+  write_outputs      main_algorithm_1.py:434-440, 499-547 (acceptance CSV, per-run CSV / npy)
+
+Snapshots stay on the device as (runs, samples, N, 2) float64 tensors together with
+the reference dtype each snapshot had (a run's state turns float32 after its first
+accepted big move, monte_carlo.py:289-292); tuples and files are produced only when
+asked for.
+"""
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import analysis, io
+from .MCMC.batched import BatchedMonteCarlo
+
+
+@dataclass
+class Snapshots:
+    """sample() snapshots of one batched local-move call: cycle numbers `steps`,
+    configurations xy (C, S, N, 2) f64, (E, W) (C, S, 2) f64, and the reference dtype
+    of every run's state during the call (C,) bool (True = float32)."""
+    steps: list
+    xy: torch.Tensor
+    ew: torch.Tensor
+    is_f32: torch.Tensor
+
+    def configs(self):
+        return self.xy
+
+    def tuples(self, bmc, run):
+        """The reference's sample() tuples of one run (monte_carlo.py:416-444)."""
+        if not self.steps:
+            return []
+        xy = self.xy[run].cpu().numpy()
+        ew = self.ew[run].cpu().numpy()
+        f32 = bool(self.is_f32[run].item())
+        bx, by = np.float64(bmc.phys.box_x), np.float64(bmc.phys.box_y)
+        return [io.sample_tuple(s, np.float64(ew[k, 0]), np.float64(ew[k, 1]), bmc.N, bx, by, bmc.phys.beta,
+                                xy[k].astype(np.float32) if f32 else xy[k])
+                for k, s in enumerate(self.steps)]
+
+
+def _local(bmc, n, adjust_every, sample_every):
+    is_f32 = bmc.state_is_f32.bool().clone()
+    xy, ew, _ = bmc.local_moves(n, adjust_every=adjust_every, sample_every=sample_every, step0=0)
+    steps = [s for s in range(1, n + 1) if sample_every and s % sample_every == 0]
+    if xy is None:
+        xy = torch.empty((bmc.C, 0, bmc.N, 2), dtype=torch.float64, device=bmc.device)
+        ew = torch.empty((bmc.C, 0, 2), dtype=torch.float64, device=bmc.device)
+    return Snapshots(steps, xy, ew, is_f32)
+
+
+def equilibrate(bmc: BatchedMonteCarlo, steps, adjusting_frequency, sampling_frequency):
+    """main_algorithm_1.py:202-210: `steps` particle_displacement calls per run,
+    adjust_displacement after every step divisible by adjusting_frequency, a sample()
+    after every step divisible by sampling_frequency."""
+    return _local(bmc, int(steps), int(adjusting_frequency), int(sampling_frequency))
+
+
+def production(bmc: BatchedMonteCarlo, steps, sampling_frequency, half_box=None):
+    """main_algorithm_1.py:240-253: local moves with sampling (no adjustment).  Returns
+    (snapshots, global_samples_nf): the training set in the reference's order (run 0's
+    samples first) shifted by -HALF_BOX, float64 on the device, as the reference's
+    np.array(... particle - [HALF_BOX, HALF_BOX] ...) builds it."""
+    snap = _local(bmc, int(steps), 0, int(sampling_frequency))
+    hb = bmc.phys.half_width if half_box is None else float(half_box)
+    samples = snap.xy.reshape(-1, bmc.N, 2) - hb
+    return snap, samples
+
+
+@dataclass
+class TestingResult:
+    """Outputs of the testing phase, per run (C) and attempt (A)."""
+    accepts: torch.Tensor                  # (C, A) u8 nf_big_move decisions
+    snapshots: list                        # A Snapshots (one per attempt)
+    p_acc_history: list = field(default_factory=list)
+    mcmc_steps_history: list = field(default_factory=list)
+    total_mcmc_steps: int = 0
+    big_move_attempts: int = 0
+    big_move_accepts: int = 0
+
+    def testing_configs(self):
+        """(C, A*S, N, 2) f64: every run's mc_run.testing_samples in order."""
+        return torch.cat([s.xy for s in self.snapshots], 1)
+
+    def testing_is_f32(self):
+        """(C,) bool: np.array(mc_run.testing_samples) is float32 only if every
+        snapshot of the run was taken from a float32 state."""
+        m = torch.ones_like(self.snapshots[0].is_f32)
+        for s in self.snapshots:
+            m &= s.is_f32
+        return m
+
+    def local_sample_tuples(self, bmc, run):
+        out = []
+        for s in self.snapshots:
+            out += s.tuples(bmc, run)
+        return out
+
+    def test_moves(self):
+        """Per-run (test_moves_attempted, test_moves_accepted) (main_algorithm_1.py:401-408)."""
+        a = self.accepts.to(torch.int64)
+        return torch.full((a.shape[0],), a.shape[1], dtype=torch.int64, device=a.device), a.sum(1)
+
+
+def acceptance_history(accepts, interval, total_mcmc_steps=0, big_move_attempts=0, big_move_accepts=0):
+    """The global acceptance history of the reference's run-major testing loop
+    (main_algorithm_1.py:381-419) from the (C, A) accept matrix: for run r, attempt a,
+    total_mcmc_steps grows by `interval`, then the cumulative global acceptance is
+    appended.  Returns (p_acc_history, mcmc_steps_history, total_mcmc_steps,
+    big_move_attempts, big_move_accepts) — the appended entries and the new counters."""
+    acc = np.asarray(torch.as_tensor(accepts).cpu().numpy(), dtype=np.int64).reshape(-1)  # run-major
+    n = acc.size
+    cum = big_move_accepts + np.cumsum(acc)
+    att = big_move_attempts + np.arange(1, n + 1)
+    steps = total_mcmc_steps + interval * np.arange(1, n + 1)
+    p = [int(c) / int(t) for c, t in zip(cum, att)]  # Python int / int, as the reference
+    return (p, [int(s) for s in steps], total_mcmc_steps + interval * n, big_move_attempts + n,
+            big_move_accepts + int(acc.sum()))
+
+
+def testing_phase(bmc: BatchedMonteCarlo, test_configs, attempts, interval, sampling_frequency,
+                  total_mcmc_steps=0, big_move_attempts=0, big_move_accepts=0):
+    """main_algorithm_1.py:375-424 for all runs: per attempt, `interval` local moves with
+    sampling, then nf_big_move with test_configs[attempt * C + run] (float32 box
+    coordinates, (>= attempts*C, N, 2), numpy or device)."""
+    C = bmc.C
+    cfg = torch.as_tensor(test_configs)
+    if cfg.dtype != torch.float32:
+        raise ValueError("test configurations are float32 (main_algorithm_1.py:340-343)")
+    if cfg.shape[0] < attempts * C:
+        raise IndexError(f"index {attempts * C - 1} is out of bounds for axis 0 with size {cfg.shape[0]}")
+    cfg = cfg.to(bmc.device)
+    snaps, acc = [], []
+    for a in range(int(attempts)):
+        snaps.append(_local(bmc, int(interval), 0, int(sampling_frequency)))
+        acc.append(bmc.nf_big_move(cfg[a * C:(a + 1) * C]).clone())
+    accepts = torch.stack(acc, 1) if acc else torch.zeros((C, 0), dtype=torch.uint8, device=bmc.device)
+    p, s, tot, att, nacc = acceptance_history(accepts, int(interval), total_mcmc_steps, big_move_attempts,
+                                              big_move_accepts)
+    return TestingResult(accepts, snaps, p, s, tot, att, nacc)
+
+
+def well_statistics(configs, is_f32, half_box, r0=1.2):
+    """calculate_well_statistics(configs[run], 0, half_box, r0) for every run at once
+    (utils.py:61-101).  configs (C, M, N, 2) f64 device tensor, is_f32 (C,) bool (the
+    dtype np.array gives the run's snapshots).  Returns device tensors avg_x (C, M) f64
+    (np.mean of the x column, in the run's dtype, widened), p_a, p_b (C, M) f64 and
+    deltaF (C, M) f64 (log on the device: within 1 ulp of numpy's)."""
+    C, M, N, _ = configs.shape
+    dev = configs.device
+    state = torch.zeros((C, M), dtype=torch.uint8, device=dev)
+    avg_x = torch.zeros((C, M), dtype=torch.float64, device=dev)
+    f32 = torch.as_tensor(is_f32, device=dev).bool()
+    for mask, dt in ((f32, torch.float32), (~f32, torch.float64)):
+        idx = mask.nonzero().flatten()
+        if idx.numel() == 0 or M == 0:
+            continue
+        _, st, ax = analysis.classify_wells(configs[idx].to(dt).reshape(-1, N, 2), half_box, r0)
+        state[idx] = st.reshape(-1, M)
+        avg_x[idx] = ax.reshape(-1, M)
+    i = torch.arange(1, M + 1, dtype=torch.float64, device=dev)
+    p_a = torch.cumsum((state == 1).to(torch.int64), 1).to(torch.float64) / i
+    p_b = torch.cumsum((state == 2).to(torch.int64), 1).to(torch.float64) / i
+    both = (p_a > 0) & (p_b > 0)
+    dF = torch.where(both, torch.log(torch.where(both, p_b / p_a, torch.ones_like(p_a))), torch.zeros_like(p_a))
+    return avg_x, p_a, p_b, dF
+
+
+def free_energy_curve(deltaF):
+    """plot_avg_free_energy's statistics (utils.py:738-763) over runs: mean_deltaF,
+    sem_deltaF (per sample index, numpy arrays), final_mean, final_sem, final_std."""
+    d = np.asarray(torch.as_tensor(deltaF).cpu().numpy(), dtype=np.float64)
+    mean = np.nanmean(d, axis=0)
+    sem = np.nanstd(d, axis=0) / np.sqrt(d.shape[0])
+    final_mean, final_sem = float(mean[-1]), float(sem[-1])
+    return mean, sem, final_mean, final_sem, final_sem * np.sqrt(d.shape[0])
+
+
+def reference_history(result, production_steps=0):
+    """The full acceptance history main_algorithm_1.py writes: the initial (0, 0.0)
+    (:234-235), the (total_mcmc_steps, 0.0) point appended after training (:362-363),
+    then the testing-phase entries."""
+    return [0, production_steps] + result.mcmc_steps_history, [0.0, 0.0] + result.p_acc_history
+
+
+def write_outputs(directory, bmc, local_snapshots, result=None, history=None, runs=None):
+    """acceptance_rate_data.csv (main_algorithm_1.py:434-440, written when `history` =
+    (mcmc_steps_history, p_acc_history) is given) and, per run,
+    mc_runs/run_XXX/{sampled_data.csv, mc_run_configs.npy, mc_run_testing_configs.npy}
+    (:499-547).  local_snapshots: the Snapshots of every phase whose samples went to
+    mc_run.local_samples, in order (equilibration, production); the testing phase's
+    snapshots are appended from `result`."""
+    import os
+
+    os.makedirs(directory, exist_ok=True)
+    if history is not None:
+        io.write_acceptance_rate(os.path.join(directory, "acceptance_rate_data.csv"), history[0], history[1])
+    runs = range(bmc.C) if runs is None else runs
+    for r in runs:
+        local = []
+        for s in local_snapshots:
+            local += s.tuples(bmc, r)
+        testing = []
+        if result is not None:
+            t = result.local_sample_tuples(bmc, r)
+            local += t
+            testing = [x[6] for x in t]
+        io.write_run_dir(os.path.join(directory, "mc_runs", f"run_{r + 1:03d}"), local, testing)

@@ -416,6 +416,160 @@ def analysis_case():
     print("analysis: ok", np.bincount([{"A": 0, "B": 1, "Outside": 2}[c] for c in out["f64_cls"].ravel()]))
 
 
+def driver_case(NF, MC):
+    """The Algorithm-1 driver's phases (main_algorithm_1.py:138-186 setup, 202-210
+    equilibration, 240-253 production, 375-424 testing, 443-455 well statistics, 467-471
+    free energy) restated with small sizes around the reference's own MonteCarlo
+    objects and hybrid utils: N=3, 4 runs (even runs start left, odd right), a seeded
+    flow.  Test configurations alternate between flow samples (+HALF_BOX, float32;
+    mostly rejected) and float32 jitters of the run's current state chosen so that the
+    MH decision is far from both ratio = 1 and the uniform draw (accepted or rejected
+    decisively), so a float32 log_prob that is not bit-identical cannot flip it."""
+    import copy
+    import importlib.util
+    import tempfile
+
+    from oracle import flow as OF
+
+    spec = importlib.util.spec_from_file_location("hyb_utils", os.path.join(LINK, "hybrid_NF_MCMC", "utils.py"))
+    U = importlib.util.module_from_spec(spec)
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        spec.loader.exec_module(U)
+    N, RUNS, SEED = 3, 4, 42
+    EQ, ADJ, SF = 600, 200, 50
+    PROD, ATTEMPTS, INTERVAL = 300, 9, 200
+    HB = ((N / 0.03) ** (1 / 2)) / 2
+    dims = OF.FlowDims(N=N, L=2, H=32, nb=1, K=5, B=HB)
+    flow_seed = 91
+    sd = OF.random_state_dict(dims, seed=flow_seed, final_std=0.05)
+    model = build_ref_model(NF, dims)
+    model.load_state_dict(sd, strict=True)
+    model.eval()
+    runs = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        for i in range(RUNS):
+            np.random.seed(i + SEED)
+            init = MC.initialise_low_left if i % 2 == 0 else MC.initialise_low_right
+            particles, box = init(num_particles=N, rho=0.03, aspect_ratio=1.0, visualise=False, checking=False)
+            runs.append(MC.MonteCarlo(particles=particles, sim_box=box, temperature=1.0, num_particles=N,
+                                      num_wells=2, V0_list=[-10.0, -10.5], r0=1.2, k=15,
+                                      initial_max_displacement=0.65, target_acceptance=0.5, timing=False,
+                                      checking=False, logger=None, seed=i + SEED, device=torch.device("cpu")))
+    out = {"init": np.array([np.asarray(m.particles, np.float64) for m in runs])}
+    for m in runs:
+        m.local_samples, m.testing_samples = [], []
+    with contextlib.redirect_stdout(io.StringIO()):
+        for m in runs:  # equilibration
+            for step in range(1, EQ + 1):
+                m.particle_displacement()
+                if step % ADJ == 0:
+                    m.adjust_displacement()
+                if step % SF == 0:
+                    m.local_samples.append(m.sample(step))
+    total = 0
+    p_hist, s_hist = [0.0], [0]
+    gmc = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        for m in runs:  # production
+            for step in range(1, PROD + 1):
+                m.particle_displacement()
+                total += 1
+                if step % SF == 0:
+                    s_ = m.sample(step)
+                    m.local_samples.append(s_)
+                    gmc.append(s_[6])
+    out["global_samples_nf"] = np.array([np.array([p - np.array([HB, HB]) for p in c]) for c in gmc])
+    out["total_after_production"] = np.int64(total)
+    p_hist.append(0.0)
+    s_hist.append(total)
+    for m in runs:
+        m.set_nf_model(model)
+    torch.manual_seed(5)
+    with torch.no_grad():
+        flow_cfgs = (model.sample(ATTEMPTS * RUNS).reshape(-1, N, 2).numpy() + HB)
+    test_cfgs = np.zeros((ATTEMPTS * RUNS, N, 2), np.float32)
+
+    def log_ratio_and_u(m, cfg):
+        E = m.energy_calculator
+        keep = (E.total_energy, E.total_virial)
+        enn, _ = E.calculate_total_energy_virial(cfg)
+        E.total_energy, E.total_virial = keep
+        nll = lambda x: -OF.log_prob(sd, torch.tensor((np.asarray(x, np.float64) - m.half_width).reshape(1, -1),
+                                                      dtype=torch.float), dims).item()
+        lr = -m.beta * (enn - keep[0]) - (nll(cfg) - nll(m.particles))
+        return lr, copy.deepcopy(m.rng).random()
+
+    big_attempts = big_accepts = 0
+    acc = np.zeros((RUNS, ATTEMPTS), np.int8)
+    with contextlib.redirect_stdout(io.StringIO()):
+        for r, m in enumerate(runs):  # testing phase (run-major, as the reference)
+            for a in range(ATTEMPTS):
+                for step in range(1, INTERVAL + 1):
+                    m.particle_displacement()
+                    total += 1
+                    if step % SF == 0:
+                        s_ = m.sample(step)
+                        m.local_samples.append(s_)
+                        m.testing_samples.append(s_[6])
+                if a % 3 == 0:
+                    cfg = flow_cfgs[a * RUNS + r].astype(np.float32)
+                else:  # a jitter of the state (a % 3 == 1) or of its mirror image in the other well
+                    cur = np.asarray(m.particles, np.float64)
+                    if a % 3 == 2:
+                        cur = cur + np.array([m.sim_box.box_size_x / 2, 0.0])
+                    cfg = None
+                    for sigma in (0.05, 0.02, 0.01, 0.005):
+                        for s in range(200):
+                            cand = np.mod(cur + np.random.default_rng(1000 * r + 10 * a + s).normal(0, sigma, cur.shape),
+                                          m.sim_box.box_size_x).astype(np.float32)
+                            lr, u = log_ratio_and_u(m, cand)
+                            if abs(lr) > 0.02 and (lr > 0 or abs(np.exp(lr) - u) > 0.02):
+                                cfg = cand
+                                break
+                        if cfg is not None:
+                            break
+                    assert cfg is not None
+                test_cfgs[a * RUNS + r] = cfg
+                ok = m.nf_big_move(test_cfgs[a * RUNS + r])
+                big_attempts += 1
+                big_accepts += int(ok)
+                acc[r, a] = int(ok)
+                p_hist.append(big_accepts / big_attempts)
+                s_hist.append(total)
+    out["test_configs"] = test_cfgs
+    out["accepts"] = acc
+    out["p_acc_history"] = np.array(p_hist)
+    out["mcmc_steps_history"] = np.array(s_hist)
+    dF_all = []
+    for r, m in enumerate(runs):
+        k = f"run{r}"
+        out[k + "_local"] = np.array([[float(v) for v in s_[:6]] for s_ in m.local_samples])
+        cfgs = np.array([s_[6] for s_ in m.local_samples])
+        out[k + "_configs"] = cfgs
+        tc = np.array(m.testing_samples)
+        out[k + "_testing"] = tc
+        ax, pa, pb, dF, _ = U.calculate_well_statistics(tc, 0, HB, 1.2)
+        out[k + "_avg_x"] = np.array(ax, np.float64)
+        out[k + "_p_a"] = np.array(pa)
+        out[k + "_p_b"] = np.array(pb)
+        out[k + "_dF"] = np.array(dF, np.float64)
+        out[k + "_final"] = np.asarray(m.particles)
+        out[k + "_counters"] = np.array([m.attempts_displacement, m.accepted_displacement])
+        out[k + "_max_disp"] = np.float64(m.max_displacement)
+        dF_all.append(dF)
+    with tempfile.TemporaryDirectory() as td, contextlib.redirect_stdout(io.StringIO()):
+        _, _, fm, fs, fstd = U.plot_avg_free_energy(dF_all, td, color="C2")
+        import json
+        d = json.load(open(os.path.join(td, "avg_free_energy_data.json")))
+    out["mean_deltaF"] = np.array(d["mean_deltaF"])
+    out["sem_deltaF"] = np.array(d["sem_deltaF"])
+    out["final"] = np.array([fm, fs, fstd])
+    out["params"] = np.array([N, RUNS, SEED, EQ, ADJ, SF, PROD, ATTEMPTS, INTERVAL, flow_seed])
+    out["half_box"] = np.float64(HB)
+    np.savez_compressed(os.path.join(HERE, "driver.npz"), **out)
+    print("driver: ok accepts", acc.sum(), "of", acc.size, "dtypes", [out[f"run{r}_testing"].dtype for r in range(RUNS)])
+
+
 def train_case(NF):
     """Algorithm-2 training pieces (main_algorithm_2.py:314-331) on a small flow in
     train mode: forward_kld / reverse_kld losses, their parameter gradients, the
@@ -511,6 +665,9 @@ def main(only=None):
     if only == "train":
         train_case(NF)
         return
+    if only == "driver":
+        driver_case(NF, MC)
+        return
     flow_case(NF, "tiny", OF.FlowDims(N=4, L=2, H=32, nb=1, K=5, B=OF.half_box(4)), 1, 64, True)
     flow_case(NF, "n16", OF.FlowDims(N=16, L=3, H=64, nb=2, K=8, B=OF.half_box(16)), 2, 48, False)
     flow_case(NF, "n64", OF.FlowDims(N=64, L=2, H=128, nb=2, K=32, B=OF.half_box(64)), 3, 16, False)
@@ -522,6 +679,7 @@ def main(only=None):
     local_case(NF, MC)
     analysis_case()
     train_case(NF)
+    driver_case(NF, MC)
 
 
 if __name__ == "__main__":
