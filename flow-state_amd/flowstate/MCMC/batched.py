@@ -180,6 +180,12 @@ class BatchedMonteCarlo:
             self._moved = True
         return sxy, sew, log
 
+    def invalidate_nll(self):
+        """The cached old NLL is stale (the flow's weights changed): the next big move
+        re-derives it from the current state, as nf_big_move does on every call
+        (monte_carlo.py:251-261), and recomputes the energy a reject writes back (:299-301)."""
+        self._moved = True
+
     def adjust_displacement(self):
         """MonteCarlo.adjust_displacement (monte_carlo.py:375-403) for every chain."""
         _lib.check(_lib.load().fs_adjust_displacement(self.C, _lib.ptr(self.max_disp), _lib.ptr(self.attempts),

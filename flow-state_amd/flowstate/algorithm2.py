@@ -1,0 +1,144 @@
+"""One update cycle of the Algorithm-2 driver (hybrid_NF_MCMC/main_algorithm_2.py:393-570)
+over batched runs, optionally sharded over ranks.
+
+A cycle is
+  production   UPDATE_NUM_SAMPLES / (NUM_MC_RUNS / SAMPLING_FREQUENCY) local moves per
+               run with sample() every SAMPLING_FREQUENCY steps; the sampled
+               configurations (run-major, minus HALF_BOX) are the training set
+               (:399-417, cumulative or not :420-425);
+  training     one epoch over the set: DataLoader(batch_size, shuffle=True) batches, a
+               fresh Adam, loss = ALPHA * forward_kld(batch) + (1 - ALPHA) *
+               reverse_kld(BATCH_SIZE), skipped when not finite (:433-452);
+  refeeding    model.eval(); one flow proposal per run (model.sample(NUM_MC_RUNS) +
+               HALF_BOX) offered through nf_big_move (:476-540).
+
+Device mapping: production and refeeding are one batched call each over all runs (the
+refeed is the fused fs_nf_mh_step: in-kernel base draws -> sampling pass -> density
+pass -> energies -> accept); training runs through PyTorch-ROCm autograd with the
+fused spline kernels, the full-size batches replaying one captured HIP graph
+(train.GraphedTrainStep), the partial last batch eager with the same optimizer.
+
+Several ranks: each owns a contiguous block of runs (global run order = rank order, so
+the gathered training set is in the reference's run-major order).  The training set
+is all-gathered and every rank trains the same replicated model with the same data
+order; rank 0's weights are then broadcast (42.9 MB at A2 / N=64) so that the replicas
+cannot drift.  The reference trains on one device (main_algorithm_2.py:437-452); this
+keeps its batch and BatchNorm semantics exactly (no per-rank batch statistics).
+"""
+import torch
+
+from . import algorithm1 as A1
+from . import parallel
+
+
+class Algorithm2:
+    def __init__(self, bmc, model, batch_size=256, lr=0.000543510751759681, weight_decay=9.5857178422352e-05,
+                 alpha=1.0, sampling_frequency=10, update_num_samples=1000, num_mc_runs=None, cumulative=False,
+                 graphed=True, group=None):
+        """bmc: this rank's BatchedMonteCarlo (its runs); model: the flow (the same
+        initial weights on every rank); num_mc_runs: NUM_MC_RUNS over all ranks
+        (default: bmc.C x world size).  Defaults are main_algorithm_2.py:32-64."""
+        self.bmc, self.model = bmc, model
+        self.batch_size, self.lr, self.wd, self.alpha = int(batch_size), float(lr), float(weight_decay), float(alpha)
+        self.sf = int(sampling_frequency)
+        self.group = group
+        self.world = parallel.world_size(group)
+        runs = bmc.C * self.world if num_mc_runs is None else int(num_mc_runs)
+        self.production_runs = int(update_num_samples / (runs / self.sf))  # :402
+        self.cumulative = bool(cumulative)
+        self.training_data = None
+        self.total_mcmc_steps = 0
+        self.loss_history = []
+        self.p_acc_history = []
+        self.mcmc_steps_history = []
+        self.graphed = bool(graphed) and next(model.parameters()).is_cuda
+        self._step = None
+
+    # ------------------------------------------------------------------
+    def production(self):
+        """:399-417 — returns this rank's Snapshots; sets the (gathered) training set."""
+        snap, local = A1.production(self.bmc, self.production_runs, self.sf)
+        self.total_mcmc_steps += self.production_runs * self.bmc.C * self.world
+        data = parallel.all_gather_configs(local.contiguous(), group=self.group)
+        data = data.to(torch.float32).reshape(data.shape[0], -1)  # get_dataloader: float32 (M, N*dim)
+        if self.cumulative and self.training_data is not None:
+            self.training_data = torch.cat([self.training_data, data], 0)
+        else:
+            self.training_data = data
+        return snap
+
+    def _batches(self, n):
+        """The index batches DataLoader(TensorDataset(data), batch_size, shuffle=True)
+        yields (same draws from the default generator)."""
+        from torch.utils.data import DataLoader, TensorDataset
+
+        dl = DataLoader(TensorDataset(torch.arange(n)), batch_size=self.batch_size, shuffle=True)
+        return [b[0] for b in dl]
+
+    def train(self):
+        """:430-452 — one epoch with a fresh Adam; returns the mean loss (reference:
+        cycle_loss / len(dataloader), NaN / inf losses included)."""
+        m = self.model
+        m.train()
+        data = self.training_data.to(next(m.parameters()).device)
+        batches = self._batches(data.shape[0])
+        losses = []
+        if self.graphed:
+            if self._step is None:
+                from .normflows.train import GraphedTrainStep
+
+                self._step = GraphedTrainStep(m, self.batch_size, self.lr, self.wd, alpha=self.alpha,
+                                              example=data[batches[0].to(data.device)] if
+                                              batches[0].numel() == self.batch_size else None)
+            self._step.reset_optimizer()
+            for b in batches:
+                x = data[b.to(data.device)]
+                losses.append((self._step.step(x) if b.numel() == self.batch_size else self._step.eager_step(x))
+                              .detach().reshape(()).clone())
+        else:
+            opt = torch.optim.Adam(m.parameters(), lr=self.lr, weight_decay=self.wd)
+            for b in batches:
+                x = data[b.to(data.device)]
+                opt.zero_grad()
+                energy_loss, _ = m.reverse_kld(self.batch_size)
+                sample_loss = m.forward_kld(x)
+                loss = self.alpha * sample_loss + (1 - self.alpha) * energy_loss
+                if bool(~(torch.isnan(loss) | torch.isinf(loss))):
+                    loss.backward()
+                    opt.step()
+                losses.append(loss.detach().reshape(()))
+            m.invalidate_packed()
+        if self.world > 1:
+            parallel.broadcast_state(m, src=0, group=self.group)
+            m.invalidate_packed()
+        total = 0.0
+        for v in torch.stack(losses).tolist() if losses else []:
+            total += v  # cycle_loss += loss.item(), in batch order
+        avg = total / len(batches) if batches else float("nan")
+        self.loss_history.append(avg)
+        return avg
+
+    def refeed(self):
+        """:476-540 — model.eval(), one NF-proposed MH step per run (fused HIP step);
+        returns (accepted runs on this rank (C,) u8, global acceptance p_acc_update)."""
+        self.model.eval()
+        if self.bmc.model is not self.model:
+            self.bmc.set_model(self.model)
+        self.bmc.invalidate_nll()  # nf_big_move re-derives the old NLL with the current weights (:251-261)
+        acc = self.bmc.step().clone()
+        n = acc.to(torch.int64).sum().reshape(1)
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(n, group=self.group)
+        p = int(n.item()) / (self.bmc.C * self.world)
+        self.p_acc_history.append(p)
+        self.mcmc_steps_history.append(self.total_mcmc_steps)
+        return acc, p
+
+    def cycle(self):
+        """One update cycle: production -> training -> refeeding."""
+        snap = self.production()
+        loss = self.train()
+        acc, p = self.refeed()
+        return snap, loss, acc, p

@@ -135,6 +135,11 @@ class NormalizingFlow(nn.Module):
         """Device packed parameter image (rebuilt when parameters/buffers change)."""
         return self._cache.get(self._layers())
 
+    def invalidate_packed(self):
+        """Force a repack on the next pass: for writes that bypass the tensor version
+        counters (HIP-graph replays of a training step, train.GraphedTrainStep)."""
+        self._cache.key = None
+
     def dims(self):
         return self.flows[0].dims(L=len(self.flows))
 

@@ -33,6 +33,10 @@ class GraphedTrainStep:
         if dev.type != "cuda":
             raise ValueError("GraphedTrainStep needs the model on the GPU")
         self.model = model
+        if hasattr(model.q0, "device") and torch.device(model.q0.device) != dev:
+            # UniformParticle keeps its construction device (Uniform.py:5-18) when the
+            # model is moved; host draws cannot be captured, so draw on the GPU
+            model.q0.device = dev
         self.batch_size = int(batch_size)
         self.alpha = float(alpha)
         D = model.flows[0].num_input_channels
@@ -84,6 +88,22 @@ class GraphedTrainStep:
         finally:
             AF._defer_nan = False
 
+    def reset_optimizer(self):
+        """A fresh Adam (main_algorithm_2.py:437 builds one per cycle): moments and step
+        counts zeroed in place, so the captured graph keeps its buffers."""
+        with torch.no_grad():
+            for p in self.params:
+                for v in self.opt.state[p].values():
+                    if torch.is_tensor(v):
+                        v.zero_()
+
+    def eager_step(self, batch):
+        """One step on a batch of another size (the epoch's last, partial batch) with the
+        same optimizer state, outside the graph; returns the loss tensor."""
+        loss = self._eager_step(batch)
+        self.model.invalidate_packed()
+        return loss
+
     def _eager_step(self, x):
         self.opt.zero_grad(set_to_none=False)
         energy_loss, _ = self.model.reverse_kld(self.batch_size)
@@ -98,6 +118,7 @@ class GraphedTrainStep:
         """One training step on `batch` (B, D); returns the loss tensor (device scalar)."""
         self.x.copy_(batch)
         self.graph.replay()
+        self.model.invalidate_packed()  # replayed writes do not bump tensor versions
         if bool(self.nan_flag):
             raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
         return self.loss

@@ -23,6 +23,15 @@ def env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def world_size(group=None):
+    """Ranks in `group` (1 without an initialised process group)."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size(group)
+
+
 def shard(chains_per_rank, rank, master_seed=MASTER_SEED):
     """(chain_offset, seeds) of this rank's chains."""
     c0 = rank * chains_per_rank

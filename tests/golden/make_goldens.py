@@ -639,6 +639,64 @@ def train_case(NF):
     print("train: ok", float(out["fkld"]), float(out["rkld"]), float(out["step_loss"]))
 
 
+def train_cycle_case(NF):
+    """One Algorithm-2 training epoch as main_algorithm_2.py:430-452 runs it: the
+    reference's get_dataloader (utils.py:49-59, shuffle=True, batch 256, a partial last
+    batch), a fresh Adam, loss = ALPHA * forward_kld + (1 - ALPHA) * reverse_kld(256)
+    with the base draws taken from the default generator, cycle_loss / len(dataloader).
+    ALPHA = 1 and 0.5, torch.manual_seed(23) before the epoch; N=3, L=2, H=32, nb=2, K=15."""
+    import importlib.util
+
+    from oracle import flow as OF
+    spec = importlib.util.spec_from_file_location("hyb_utils", os.path.join(LINK, "hybrid_NF_MCMC", "utils.py"))
+    U = importlib.util.module_from_spec(spec)
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        spec.loader.exec_module(U)
+    dims = OF.FlowDims(N=3, L=2, H=32, nb=2, K=15, B=OF.half_box(3))
+    sd = OF.random_state_dict(dims, seed=17, final_std=0.05)
+    rng = np.random.default_rng(3)
+    data = (rng.random((600, dims.N, 2)) * 2 - 1) * dims.B * 0.9  # centred float64 configurations
+    real_zeros = torch.zeros
+
+    def zeros_cpu(*a, **k):
+        if k.get("device") == "cuda":
+            k["device"] = "cpu"
+        return real_zeros(*a, **k)
+
+    out = {"data": data}
+    torch.zeros = zeros_cpu
+    try:
+        for alpha in (1.0, 0.5):
+            model = build_ref_model(NF, dims)
+            model.load_state_dict(sd, strict=True)
+            model.p = NF.Energy.DoubleWellLJ(dims.D, dims.N, 1.0, dims.B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+            model.train()
+            torch.manual_seed(23)
+            with contextlib.redirect_stdout(io.StringIO()):
+                dl = U.get_dataloader(data, dims.N, 2, torch.device("cpu"), batch_size=256, shuffle=True)
+            opt = torch.optim.Adam(model.parameters(), lr=0.000543510751759681, weight_decay=9.5857178422352e-05)
+            cycle_loss, losses = 0.0, []
+            for batch in dl:
+                opt.zero_grad()
+                energy_loss, z = model.reverse_kld(256)
+                sample_loss = model.forward_kld(batch[0])
+                loss = alpha * sample_loss + (1 - alpha) * energy_loss
+                if ~(torch.isnan(loss) | torch.isinf(loss)):
+                    loss.backward()
+                    opt.step()
+                cycle_loss += loss.item()
+                losses.append(loss.item())
+            tag = f"a{int(alpha * 10)}"
+            out[tag + "_losses"] = np.array(losses)
+            out[tag + "_avg"] = np.float64(cycle_loss / len(dl))
+            for k, v in model.state_dict().items():
+                out[tag + "/" + k] = v.numpy()
+    finally:
+        torch.zeros = real_zeros
+    np.savez_compressed(os.path.join(HERE, "train_cycle.npz"), **out)
+    print("train_cycle: ok", out["a10_losses"], out["a5_losses"])
+
+
 def pcg_case():
     seeds = np.arange(42, 42 + 64)
     st = np.zeros((64, 4), np.uint64)
@@ -668,6 +726,9 @@ def main(only=None):
     if only == "driver":
         driver_case(NF, MC)
         return
+    if only == "train_cycle":
+        train_cycle_case(NF)
+        return
     flow_case(NF, "tiny", OF.FlowDims(N=4, L=2, H=32, nb=1, K=5, B=OF.half_box(4)), 1, 64, True)
     flow_case(NF, "n16", OF.FlowDims(N=16, L=3, H=64, nb=2, K=8, B=OF.half_box(16)), 2, 48, False)
     flow_case(NF, "n64", OF.FlowDims(N=64, L=2, H=128, nb=2, K=32, B=OF.half_box(64)), 3, 16, False)
@@ -680,6 +741,7 @@ def main(only=None):
     analysis_case()
     train_case(NF)
     driver_case(NF, MC)
+    train_cycle_case(NF)
 
 
 if __name__ == "__main__":

@@ -65,3 +65,24 @@ def test_graphed_step_skips_non_finite_loss():
     assert torch.isnan(loss).item()
     for k, v in before.items():
         assert torch.equal(m.state_dict()[k], v), k
+
+
+def test_graphed_step_updates_inference_image():
+    """Graph replays write parameters / BN statistics without bumping tensor versions;
+    the eval-mode HIP passes must still see the trained weights."""
+    from flowstate.normflows.train import GraphedTrainStep
+
+    m, f = build("cuda")
+    x = torch.from_numpy(f["x"]).cuda()
+    m.eval()
+    lp0 = m.log_prob(x)  # packs the initial weights
+    g = GraphedTrainStep(m, 64, 1e-2, 0.0, alpha=1.0, example=x)
+    for i in range(3):
+        g.step(x.roll(i, 0))
+    m.eval()
+    lp1 = m.log_prob(x)
+    fresh, _ = build("cuda")
+    fresh.load_state_dict(m.state_dict())
+    fresh.eval()
+    assert not torch.equal(lp0, lp1)
+    assert torch.equal(lp1, fresh.log_prob(x))
