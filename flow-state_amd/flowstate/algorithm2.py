@@ -15,8 +15,8 @@ A cycle is
 Device mapping: production and refeeding are one batched call each over all runs (the
 refeed is the fused fs_nf_mh_step: in-kernel base draws -> sampling pass -> density
 pass -> energies -> accept); training runs through PyTorch-ROCm autograd with the
-fused spline kernels, the full-size batches replaying one captured HIP graph
-(train.GraphedTrainStep), the partial last batch eager with the same optimizer.
+fused spline kernels, the full-size batches and the partial last batch replaying captured HIP graphs
+(train.GraphedTrainStep, one per batch size, sharing one Adam state).
 
 Several ranks: each owns a contiguous block of runs (global run order = rank order, so
 the gathered training set is in the reference's run-major order).  The training set
@@ -87,14 +87,15 @@ class Algorithm2:
             if self._step is None:
                 from .normflows.train import GraphedTrainStep
 
+                tail = data.shape[0] % self.batch_size  # the partial last batch gets its own graph
                 self._step = GraphedTrainStep(m, self.batch_size, self.lr, self.wd, alpha=self.alpha,
-                                              example=data[batches[0].to(data.device)] if
-                                              batches[0].numel() == self.batch_size else None)
+                                              extra_batch_sizes=(tail,) if tail else ())
+            tail = data.shape[0] % self.batch_size
+            if tail:
+                self._step.add_batch_size(tail)  # cumulative training sets change the tail
             self._step.reset_optimizer()
             for b in batches:
-                x = data[b.to(data.device)]
-                losses.append((self._step.step(x) if b.numel() == self.batch_size else self._step.eager_step(x))
-                              .detach().reshape(()).clone())
+                losses.append(self._step.step(data[b.to(data.device)]).detach().reshape(()).clone())
         else:
             opt = torch.optim.Adam(m.parameters(), lr=self.lr, weight_decay=self.wd)
             for b in batches:

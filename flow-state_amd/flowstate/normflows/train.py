@@ -27,8 +27,20 @@ import torch
 from . import autograd_flow as AF
 
 
+class _Captured:
+    """One captured step for one batch size: its static input, loss and NaN flag."""
+
+    def __init__(self, graph, x, loss, nan_flag):
+        self.graph, self.x, self.loss, self.nan_flag = graph, x, loss, nan_flag
+
+
 class GraphedTrainStep:
-    def __init__(self, model, batch_size, lr, weight_decay=0.0, alpha=1.0, warmup=3, example=None):
+    def __init__(self, model, batch_size, lr, weight_decay=0.0, alpha=1.0, warmup=3, example=None,
+                 extra_batch_sizes=()):
+        """Captures the step for `batch_size` (reverse_kld always draws `batch_size`
+        samples, as the reference's reverse_kld(BATCH_SIZE)) and for every size in
+        extra_batch_sizes (e.g. the epoch's partial last batch); all graphs share the
+        parameters, gradients and one Adam state."""
         dev = next(model.parameters()).device
         if dev.type != "cuda":
             raise ValueError("GraphedTrainStep needs the model on the GPU")
@@ -39,54 +51,73 @@ class GraphedTrainStep:
             model.q0.device = dev
         self.batch_size = int(batch_size)
         self.alpha = float(alpha)
-        D = model.flows[0].num_input_channels
-        self.x = torch.zeros((self.batch_size, D), device=dev) if example is None else example.clone().to(dev)
+        self.D = model.flows[0].num_input_channels
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.opt = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay, capturable=True)
         model.train()
+        self.graphs = {}
+        for bs in [self.batch_size] + [int(b) for b in extra_batch_sizes if int(b) != self.batch_size]:
+            ex = example if (example is not None and example.shape[0] == bs) else None
+            self.graphs[bs] = self._capture(bs, ex, warmup, dev)
+        main = self.graphs[self.batch_size]
+        self.x, self.graph, self.loss, self.nan_flag = main.x, main.graph, main.loss, main.nan_flag
+
+    def _capture(self, bs, example, warmup, dev):
+        model = self.model
+        x = torch.zeros((bs, self.D), device=dev) if example is None else example.clone().to(dev)
         # warm up on a side stream (allocator, hipBLASLt heuristics, Adam state), then put
         # the parameters, BatchNorm buffers and optimizer state back: capturing must not
         # change the model
         saved = [t.detach().clone() for t in list(model.parameters()) + list(model.buffers())]
+        saved_opt = [[v.detach().clone() if torch.is_tensor(v) else v for v in self.opt.state[p].values()]
+                     for p in self.params] if self.opt.state else None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                self._eager_step(self.x)
+                self._eager_step(x)
         torch.cuda.current_stream().wait_stream(s)
         with torch.no_grad():
             for t, v in zip(list(model.parameters()) + list(model.buffers()), saved):
                 t.copy_(v)
-            for p in self.params:
-                for v in self.opt.state[p].values():
+            for i, p in enumerate(self.params):
+                for j, v in enumerate(self.opt.state[p].values()):
                     if torch.is_tensor(v):
-                        v.zero_()
+                        v.copy_(saved_opt[i][j]) if saved_opt else v.zero_()
         # snapshots of everything the optimizer step mutates
-        self._state_tensors = []
-        for p in self.params:
-            st = self.opt.state[p]
-            self._state_tensors += [p] + [v for v in st.values() if torch.is_tensor(v)]
-        self._backup = [t.detach().clone() for t in self._state_tensors]
-        self.graph = torch.cuda.CUDAGraph()
+        if not hasattr(self, "_state_tensors"):
+            self._state_tensors = []
+            for p in self.params:
+                st = self.opt.state[p]
+                self._state_tensors += [p] + [v for v in st.values() if torch.is_tensor(v)]
+            self._backup = [t.detach().clone() for t in self._state_tensors]
+        graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=False)
         AF._defer_nan = True
         try:
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(graph):  # own pool: graphs replay in any order
                 self.opt.zero_grad(set_to_none=False)
                 energy_loss, _ = model.reverse_kld(self.batch_size)
-                sample_loss = model.forward_kld(self.x)
-                self.loss = self.alpha * sample_loss + (1 - self.alpha) * energy_loss
-                self.loss.backward()
-                self.finite = ~(torch.isnan(self.loss) | torch.isinf(self.loss))
+                sample_loss = model.forward_kld(x)
+                loss = self.alpha * sample_loss + (1 - self.alpha) * energy_loss
+                loss.backward()
+                finite = ~(torch.isnan(loss) | torch.isinf(loss))
                 for b, t in zip(self._backup, self._state_tensors):
                     b.copy_(t.detach())
                 self.opt.step()
                 with torch.no_grad():
                     for b, t in zip(self._backup, self._state_tensors):
-                        t.copy_(torch.where(self.finite, t, b))
-                self.nan_flag = AF.reduce_nan_flags(dev)
+                        t.copy_(torch.where(finite, t, b))
+                nan_flag = AF.reduce_nan_flags(dev)
         finally:
             AF._defer_nan = False
+        return _Captured(graph, x, loss, nan_flag)
+
+    def add_batch_size(self, bs, warmup=3):
+        """Capture one more batch size (warm-up steps are undone, as at construction)."""
+        bs = int(bs)
+        if bs not in self.graphs:
+            self.graphs[bs] = self._capture(bs, None, warmup, next(self.model.parameters()).device)
 
     def reset_optimizer(self):
         """A fresh Adam (main_algorithm_2.py:437 builds one per cycle): moments and step
@@ -115,10 +146,14 @@ class GraphedTrainStep:
         return loss
 
     def step(self, batch):
-        """One training step on `batch` (B, D); returns the loss tensor (device scalar)."""
-        self.x.copy_(batch)
-        self.graph.replay()
+        """One training step on `batch` (B, D); returns the loss tensor (device scalar).
+        A batch size without a captured graph runs eagerly with the same optimizer."""
+        c = self.graphs.get(int(batch.shape[0]))
+        if c is None:
+            return self.eager_step(batch)
+        c.x.copy_(batch)
+        c.graph.replay()
         self.model.invalidate_packed()  # replayed writes do not bump tensor versions
-        if bool(self.nan_flag):
+        if bool(c.nan_flag):
             raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
-        return self.loss
+        return c.loss

@@ -27,6 +27,7 @@ for step in "$@"; do
     pmc_local_wait) run pmc_local_wait 400 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc_local_wait -o run --output-format csv -- python tools/bench_local.py --steps 2 --no-cpu-baseline ;;
     bench_hybrid) run bench_hybrid 400 python tools/bench_hybrid.py ;;
     bench_train) run bench_train 400 python tools/bench_train.py ;;
+    bench_a2) run bench_a2 400 python tools/bench_a2.py ;;
     prof_train) run rocprof_train 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- python tools/bench_train.py && rm -f gpurun_out/prof_train/run_kernel_trace.csv ;;
     phases) run phases 300 python tools/flow_phases.py ;;
     prof_local) run rocprof_local 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_local -o run --output-format csv -- python tools/bench_local.py --steps 3 --no-cpu-baseline ;;
