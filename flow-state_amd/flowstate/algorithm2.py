@@ -29,6 +29,7 @@ import torch
 
 from . import algorithm1 as A1
 from . import parallel
+from .normflows.train import step_loss
 
 
 class Algorithm2:
@@ -101,9 +102,7 @@ class Algorithm2:
             for b in batches:
                 x = data[b.to(data.device)]
                 opt.zero_grad()
-                energy_loss, _ = m.reverse_kld(self.batch_size)
-                sample_loss = m.forward_kld(x)
-                loss = self.alpha * sample_loss + (1 - self.alpha) * energy_loss
+                loss = step_loss(m, x, self.batch_size, self.alpha)
                 if bool(~(torch.isnan(loss) | torch.isinf(loss))):
                     loss.backward()
                     opt.step()

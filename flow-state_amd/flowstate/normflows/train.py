@@ -27,6 +27,27 @@ import torch
 from . import autograd_flow as AF
 
 
+def step_loss(model, x, n_reverse, alpha):
+    """loss = ALPHA * forward_kld(x) + (1 - ALPHA) * reverse_kld(n_reverse)
+    (main_algorithm_2.py:316-318).  With ALPHA = 1 (the reference's setting) the
+    reverse term only contributes its value (0 * e: NaN / inf when e is, so the skip
+    rule sees it) and its BatchNorm statistics, so it runs without autograd: its
+    gradient 0 * de/dtheta is exactly zero whenever the loss is finite.  Likewise the
+    forward term when ALPHA = 0."""
+    if alpha == 1.0:
+        with torch.no_grad():
+            energy_loss, _ = model.reverse_kld(n_reverse)
+        return model.forward_kld(x) + 0.0 * energy_loss
+    if alpha == 0.0:
+        energy_loss, _ = model.reverse_kld(n_reverse)
+        with torch.no_grad():
+            sample_loss = model.forward_kld(x)
+        return 0.0 * sample_loss + energy_loss
+    energy_loss, _ = model.reverse_kld(n_reverse)
+    sample_loss = model.forward_kld(x)
+    return alpha * sample_loss + (1 - alpha) * energy_loss
+
+
 class _Captured:
     """One captured step for one batch size: its static input, loss and NaN flag."""
 
@@ -84,22 +105,24 @@ class GraphedTrainStep:
                 for j, v in enumerate(self.opt.state[p].values()):
                     if torch.is_tensor(v):
                         v.copy_(saved_opt[i][j]) if saved_opt else v.zero_()
-        # snapshots of everything the optimizer step mutates
+        # snapshots of everything the optimizer step mutates: parameters and Adam state
+        # live in a few flat buffers, so the skip-on-non-finite snapshot / restore is 4
+        # copies + 4 selects instead of ~4 per parameter tensor (~8k graph nodes at A2)
         if not hasattr(self, "_state_tensors"):
-            self._state_tensors = []
-            for p in self.params:
-                st = self.opt.state[p]
-                self._state_tensors += [p] + [v for v in st.values() if torch.is_tensor(v)]
+            # parameters the step never reaches (the fork's unused preprocessing weights)
+            # keep grad None and are skipped by Adam, as in the reference: leave them out
+            used = [p for p in self.params if p.grad is not None]
+            self.opt.param_groups[0]["params"] = used
+            self.params = used
+            self._state_tensors = self._flatten()
             self._backup = [t.detach().clone() for t in self._state_tensors]
         graph = torch.cuda.CUDAGraph()
-        self.opt.zero_grad(set_to_none=False)
+        self._zero_grad()
         AF._defer_nan = True
         try:
             with torch.cuda.graph(graph):  # own pool: graphs replay in any order
-                self.opt.zero_grad(set_to_none=False)
-                energy_loss, _ = model.reverse_kld(self.batch_size)
-                sample_loss = model.forward_kld(x)
-                loss = self.alpha * sample_loss + (1 - self.alpha) * energy_loss
+                self._zero_grad()
+                loss = step_loss(model, x, self.batch_size, self.alpha)
                 loss.backward()
                 finite = ~(torch.isnan(loss) | torch.isinf(loss))
                 for b, t in zip(self._backup, self._state_tensors):
@@ -113,6 +136,53 @@ class GraphedTrainStep:
             AF._defer_nan = False
         return _Captured(graph, x, loss, nan_flag)
 
+    def _bind_grads(self):
+        """(Re)attach the flat gradient views (a zero_grad(set_to_none=True) elsewhere
+        drops them; the captured graphs keep using the views regardless)."""
+        for p, g in zip(self.params, self._grad_views):
+            if p.grad is not g:
+                p.grad = g
+
+    def _zero_grad(self):
+        if getattr(self, "_flat_grad", None) is not None:
+            self._flat_grad.zero_()  # one fill for every parameter's gradient
+        else:
+            self.opt.zero_grad(set_to_none=False)
+
+    @torch.no_grad()
+    def _flatten(self):
+        """Re-home the parameters and the optimizer's state tensors as views of one flat
+        buffer each (values unchanged); returns the buffers."""
+        ps = self.params
+        sizes = [p.numel() for p in ps]
+        offs = [0]
+        for n in sizes:
+            offs.append(offs[-1] + n)
+        flat = torch.cat([p.detach().reshape(-1) for p in ps])
+        for p, o, n in zip(ps, offs, sizes):
+            p.data = flat[o:o + n].view_as(p)
+        # gradients too: AccumulateGrad adds into an existing .grad in place, so the views
+        # stay the gradient storage and zeroing them is one fill
+        self._flat_grad = torch.zeros_like(flat)
+        self._grad_views = [self._flat_grad[o:o + n].view_as(p) for p, o, n in zip(ps, offs, sizes)]
+        self._bind_grads()
+        bufs = [flat]
+        for k, v0 in list(self.opt.state[ps[0]].items()):
+            if not torch.is_tensor(v0):
+                continue
+            vals = [self.opt.state[p][k] for p in ps]
+            if v0.dim() == 0:  # capturable Adam's per-parameter step counts
+                buf = torch.stack(vals)
+                for i, p in enumerate(ps):
+                    self.opt.state[p][k] = buf[i]
+            else:
+                buf = torch.cat([v.reshape(-1) for v in vals])
+                for p, o, n in zip(ps, offs, sizes):
+                    self.opt.state[p][k] = buf[o:o + n].view_as(p)
+            bufs.append(buf)
+        self.model.invalidate_packed()
+        return bufs
+
     def add_batch_size(self, bs, warmup=3):
         """Capture one more batch size (warm-up steps are undone, as at construction)."""
         bs = int(bs)
@@ -123,23 +193,21 @@ class GraphedTrainStep:
         """A fresh Adam (main_algorithm_2.py:437 builds one per cycle): moments and step
         counts zeroed in place, so the captured graph keeps its buffers."""
         with torch.no_grad():
-            for p in self.params:
-                for v in self.opt.state[p].values():
-                    if torch.is_tensor(v):
-                        v.zero_()
+            for b in self._state_tensors[1:]:
+                b.zero_()
 
     def eager_step(self, batch):
         """One step on a batch of another size (the epoch's last, partial batch) with the
         same optimizer state, outside the graph; returns the loss tensor."""
+        if getattr(self, "_flat_grad", None) is not None:
+            self._bind_grads()
         loss = self._eager_step(batch)
         self.model.invalidate_packed()
         return loss
 
     def _eager_step(self, x):
-        self.opt.zero_grad(set_to_none=False)
-        energy_loss, _ = self.model.reverse_kld(self.batch_size)
-        sample_loss = self.model.forward_kld(x)
-        loss = self.alpha * sample_loss + (1 - self.alpha) * energy_loss
+        self._zero_grad()
+        loss = step_loss(self.model, x, self.batch_size, self.alpha)
         if bool(~(torch.isnan(loss) | torch.isinf(loss))):
             loss.backward()
             self.opt.step()

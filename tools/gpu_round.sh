@@ -28,6 +28,7 @@ for step in "$@"; do
     bench_hybrid) run bench_hybrid 400 python tools/bench_hybrid.py ;;
     bench_train) run bench_train 400 python tools/bench_train.py ;;
     bench_a2) run bench_a2 400 python tools/bench_a2.py ;;
+    prof_graph) run rocprof_graph 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_graph -o run --output-format csv -- python tools/prof_train_graph.py; python tools/trace_window.py gpurun_out/prof_graph/run_kernel_trace.csv 10 > gpurun_out/graph_window.json; head -c 3000 gpurun_out/graph_window.json; rm -f gpurun_out/prof_graph/run_kernel_trace.csv ;;
     prof_train) run rocprof_train 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- python tools/bench_train.py && rm -f gpurun_out/prof_train/run_kernel_trace.csv ;;
     phases) run phases 300 python tools/flow_phases.py ;;
     prof_local) run rocprof_local 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_local -o run --output-format csv -- python tools/bench_local.py --steps 3 --no-cpu-baseline ;;
