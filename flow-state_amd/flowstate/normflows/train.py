@@ -134,7 +134,7 @@ class GraphedTrainStep:
                 nan_flag = AF.reduce_nan_flags(dev)
         finally:
             AF._defer_nan = False
-        return _Captured(graph, x, loss, nan_flag)
+        return _Captured(graph, x, loss.detach(), nan_flag)  # keep no autograd graph alive
 
     def _bind_grads(self):
         """(Re)attach the flat gradient views (a zero_grad(set_to_none=True) elsewhere
@@ -211,7 +211,7 @@ class GraphedTrainStep:
         if bool(~(torch.isnan(loss) | torch.isinf(loss))):
             loss.backward()
             self.opt.step()
-        return loss
+        return loss.detach()
 
     def step(self, batch):
         """One training step on `batch` (B, D); returns the loss tensor (device scalar).
