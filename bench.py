@@ -34,6 +34,9 @@ from flowstate import parallel  # noqa: E402
 from flowstate.models import A1, build_flow, half_box  # noqa: E402
 
 PEAK_F32_TFLOPS = 157.3  # MI355X dense FP32 (MFMA = vector rate), MI355X_MICROARCH.md
+PEAK_F64_TFLOPS = 78.6   # MI355X FP64 vector
+ENERGY_BYTES = lambda N: 4 * 2 * N + 16  # noqa: E731  float32 proposal in, E and W out
+ENERGY_FLOP = lambda N: 30 * N * (N - 1) // 2 + 40 * N  # noqa: E731
 
 
 def flops_per_pass(N, L, H, nb, K):
@@ -272,6 +275,14 @@ def main():
                      "frac": achieved / PEAK_F32_TFLOPS, "traffic": _pmc_traffic(),
                      "kernel": "flow_pass_kernel<256,32,*> (propose + log_prob)",
                      "algorithmic_flop_per_launch": fpp * C},
+        # the LJ + double-well kernel the north star asks about: HBM rate of its algorithmic
+        # bytes (float32 proposal in, E / W out) and fp64 rate (~30 FLOP per
+        # pair + ~40 per particle), against the fp64 vector peak that bounds it
+        "energy_kernel": {"ms": t_en, "bytes_per_chain": ENERGY_BYTES(N), "flop_per_chain": ENERGY_FLOP(N),
+                          "achieved_gbs": ENERGY_BYTES(N) * C / (t_en * 1e-3) / 1e9,
+                          "achieved_fp64_tflops": ENERGY_FLOP(N) * C / (t_en * 1e-3) / 1e12,
+                          "peak_fp64_tflops": PEAK_F64_TFLOPS,
+                          "frac": ENERGY_FLOP(N) * C / (t_en * 1e-3) / 1e12 / PEAK_F64_TFLOPS},
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)

@@ -46,6 +46,7 @@ struct LocalArgs {
     double *samples_xy, *samples_ew;
     uint8_t *accept_log;
     unsigned long long *n_accept;
+    PairThresh T;  // squared-distance / min-image thresholds (physics_device.h)
 };
 
 constexpr int kLocalWaves = 4;
@@ -122,7 +123,6 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
     constexpr int G = 64 / LPC;          // chains per wave
     constexpr int SLOTS = LPC * PPL;     // LDS slots per chain and array
     __shared__ double lds[kLocalWaves][4][G * SLOTS];
-    __shared__ double res[kLocalWaves][G][4];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane / LPC, gl = lane % LPC;
     const int sb = g * SLOTS;            // this chain's slot base
@@ -175,32 +175,58 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
             nx = np_remainder(ox + d0, P.Lx);
             ny = np_remainder(oy + d1, P.Ly);
         }
-        // pair terms of particle p against this lane's particles (np.delete order: j - (j > p))
+        // pair terms of particle p against this lane's particles (np.delete order: j - (j > p)).
+        // Only terms inside the cutoff are non-zero (about 1 % at rho = 0.03): they alone are
+        // written to LDS, at their compacted index, and flagged in a 64-bit mask per row
         bool ho = false, hn = false;
+        uint64_t mo = 0, mn = 0;
 #pragma unroll
         for (int q = 0; q < PPL; ++q) {
             const int j = gl + LPC * q;
             if (j < N && j != p) {
-                double ro, rn;
+                const int t = j - (j > p ? 1 : 0);
+                bool io, in;
+                double ro = 0.0, rn = 0.0;
                 if (f32) {
                     const float fx = (float)xj[q], fy = (float)yj[q];
-                    ro = dist_f32((float)ox, (float)oy, fx, fy, P.Lx, P.Ly, iLx, iLy);
-                    rn = dist_f32((float)nx, (float)ny, fx, fy, P.Lx, P.Ly, iLx, iLy);
+                    const float so = sqdist_f32((float)ox, (float)oy, fx, fy, P.Lx, P.Ly, a.T, iLx, iLy);
+                    const float sn = sqdist_f32((float)nx, (float)ny, fx, fy, P.Lx, P.Ly, a.T, iLx, iLy);
+                    ho |= so <= a.T.core32;
+                    hn |= sn <= a.T.core32;
+                    io = so <= a.T.cut32;
+                    in = sn <= a.T.cut32;
+                    if (io) ro = r_of_sq(so);
+                    if (in) rn = r_of_sq(sn);
                 } else {
-                    ro = dist_f64(ox, oy, xj[q], yj[q], P.Lx, P.Ly, iLx, iLy);
-                    rn = dist_f64(nx, ny, xj[q], yj[q], P.Lx, P.Ly, iLx, iLy);
+                    const double so = sqdist_f64(ox, oy, xj[q], yj[q], P.Lx, P.Ly, a.T, iLx, iLy);
+                    const double sn = sqdist_f64(nx, ny, xj[q], yj[q], P.Lx, P.Ly, a.T, iLx, iLy);
+                    ho |= so <= a.T.core64;
+                    hn |= sn <= a.T.core64;
+                    io = so <= a.T.cut64;
+                    in = sn <= a.T.cut64;
+                    if (io) ro = r_of_sq(so);
+                    if (in) rn = r_of_sq(sn);
                 }
-                ho |= ro < P.r_core;
-                hn |= rn < P.r_core;
-                double eo, wo, en, wn;
-                lj_pair(ro, P.r_cut, e_cut, eo, wo);
-                lj_pair(rn, P.r_cut, e_cut, en, wn);
-                const int tt = sb + j - (j > p ? 1 : 0);
-                lds[wid][0][tt] = eo;
-                lds[wid][1][tt] = wo;
-                lds[wid][2][tt] = en;
-                lds[wid][3][tt] = wn;
+                if (io) {
+                    double e, w;
+                    lj_pair(ro, P.r_cut, e_cut, e, w);
+                    lds[wid][0][sb + t] = e;
+                    lds[wid][1][sb + t] = w;
+                    mo |= 1ull << t;
+                }
+                if (in) {
+                    double e, w;
+                    lj_pair(rn, P.r_cut, e_cut, e, w);
+                    lds[wid][2][sb + t] = e;
+                    lds[wid][3][sb + t] = w;
+                    mn |= 1ull << t;
+                }
             }
+        }
+#pragma unroll
+        for (int o = 1; o < LPC; o <<= 1) {
+            mo |= __shfl_xor(mo, o, LPC);
+            mn |= __shfl_xor(mn, o, LPC);
         }
         const bool hit_old = (__ballot(ho) & gmask) != 0;
         const bool hit_new = (__ballot(hn) & gmask) != 0;
@@ -210,48 +236,31 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // numpy pairwise sums of the four compacted rows: eno, viro, enn, virn
-        double sums[4];
-        if (n < 8) {
-            double r = 0.0;
-            if (gl < 4)
-                for (int k = 0; k < n; ++k) r += lds[wid][gl][sb + k];
+        // numpy pairwise sums of the four compacted rows (eno, viro, enn, virn), lane gl < 4
+        // summing row gl over its flagged terms only: the terms left out are +0.0 and no
+        // term or partial sum is -0.0, so adding them changes nothing (x + 0 == x)
+        double r = 0.0;
+        if (gl < 4) {
+            const uint64_t m = gl < 2 ? mo : mn;
+            const double *row = &lds[wid][gl][sb];
+            if (n < 8) {
+                for (uint64_t b = m; b; b &= b - 1) r += row[__builtin_ctzll(b)];
+            } else {
+                const uint64_t body = nfull >= 64 ? ~0ull : ((1ull << nfull) - 1);
+                double acc[8];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) sums[q] = bcast<LPC>(r, q);
-        } else if constexpr (LPC == 64) {
-            // lanes 8*arr + k: partial sum k of array arr, tree by xor-shuffles, tail on lane 8*arr
-            double r = 0.0;
-            if (gl < 32) {
-                const int arr = gl >> 3, k = gl & 7;
-                r = lds[wid][arr][k];
-                for (int b = 8; b < nfull; b += 8) r += lds[wid][arr][b + k];
-            }
-            r += __shfl_xor(r, 1, 64);
-            r += __shfl_xor(r, 2, 64);
-            r += __shfl_xor(r, 4, 64);
-            if (gl < 32 && (gl & 7) == 0)
-                for (int i = nfull; i < n; ++i) r += lds[wid][gl >> 3][i];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) sums[q] = bcast<LPC>(r, 8 * q);
-        } else {
-            for (int ak = gl; ak < 32; ak += LPC) {  // LPC >= 8
-                const int arr = ak >> 3, k = ak & 7;
-                double r = lds[wid][arr][sb + k];
-                for (int b = 8; b < nfull; b += 8) r += lds[wid][arr][sb + b + k];
-                r += __shfl_xor(r, 1, LPC);
-                r += __shfl_xor(r, 2, LPC);
-                r += __shfl_xor(r, 4, LPC);
-                if (k == 0) {
-                    for (int i = nfull; i < n; ++i) r += lds[wid][arr][sb + i];
-                    res[wid][g][arr] = r;
+                for (int k = 0; k < 8; ++k) {  // partial k: terms k, k+8, k+16, ... in order
+                    acc[k] = 0.0;
+                    for (uint64_t b = m & body & (0x0101010101010101ull << k); b; b &= b - 1)
+                        acc[k] += row[__builtin_ctzll(b)];
                 }
+                r = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+                for (uint64_t b = m & ~body; b; b &= b - 1) r += row[__builtin_ctzll(b)];
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int q = 0; q < 4; ++q) sums[q] = res[wid][g][q];
         }
+        double sums[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sums[q] = bcast<LPC>(r, q);
         double eno = sums[0], viro = sums[1], enn = sums[2], virn = sums[3];
         if (P.num_wells > 0) {  // V = 0; V += term(well 0); V += term(well 1)  (potential.py:96-112)
             double vo = 0.0 + bcast<LPC>(dw, 0), vn = 0.0 + bcast<LPC>(dw, 2);
@@ -348,12 +357,13 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
     LocalArgs a{*p,       C,         N,        state,      is_f32,     E,          W,
                 pcg,      pcg_buf,   max_disp, attempts,   accepted,   prev,       n_moves,
                 step0,    adjust_every, target, sample_every, fs_local_samples_per_chain(step0, n_moves, sample_every),
-                samples_xy, samples_ew, accept_log, n_accept};
-    // lanes per chain x particles per lane (FS_LOCAL_LAYOUT=LPCxPPL overrides, for A/B runs)
-    // measured at 65536 chains x 1000 moves: 8 lanes per chain is fastest at every N
-    // (N=64: 1.90 G moves/s with 8x8 vs 1.11 G with 64x1; N=32: 2.68 G; N=16: 3.50 G)
-    int lpc = 8;
-    int ppl = N > 32 ? 8 : N > 16 ? 4 : N > 8 ? 2 : 1;
+                samples_xy, samples_ew, accept_log, n_accept, fs_pair_thresh(*p)};
+    // lanes per chain x particles per lane (FS_LOCAL_LAYOUT=LPCxPPL overrides, for A/B runs).
+    // Measured at 65536 chains x 1000 moves (sparse in-cutoff sums): N=64 8x8 2.41 G moves/s
+    // (16x4 1.88 G, 64x1 1.06 G, 4x16 1.69 G: register-limited); N=32 4x8 4.04 G (8x4 3.20 G);
+    // N=16 4x4 5.52 G (8x2 4.78 G).  More chains per wave amortise the per-move work.
+    int lpc = N > 32 ? 8 : N > 8 ? 4 : 8;
+    int ppl = N > 32 ? 8 : N > 16 ? 8 : N > 8 ? 4 : 1;
     if (const char *e = getenv("FS_LOCAL_LAYOUT")) {
         int l = 0, q = 0;
         if (sscanf(e, "%dx%d", &l, &q) == 2 && l * q >= N) {
@@ -368,7 +378,8 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
         hipLaunchKernelGGL((local_moves_kernel<L, Q>), grid, block, 0, st, a);        \
         return hipGetLastError();                                                     \
     }
-    FS_LCASE(8, 1) FS_LCASE(8, 2) FS_LCASE(8, 4) FS_LCASE(8, 8) FS_LCASE(64, 1) FS_LCASE(16, 4)
+    FS_LCASE(8, 1) FS_LCASE(8, 2) FS_LCASE(8, 4) FS_LCASE(8, 8) FS_LCASE(64, 1) FS_LCASE(16, 4) FS_LCASE(4, 16)
+    FS_LCASE(4, 8) FS_LCASE(4, 4)
 #undef FS_LCASE
     return hipErrorInvalidValue;
 }

@@ -6,6 +6,9 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
+
+#include "../../include/flowstate.h"
 
 #pragma clang fp contract(off)
 
@@ -22,32 +25,88 @@ __device__ __forceinline__ double rint_div(double d, double L, double invL) {
     return k;
 }
 
-// minimum-image distance (simulation_box.py:31-56) with numpy's promotion rules
-__device__ __forceinline__ double dist_f32(float ax, float ay, float bx, float by, double Lx, double Ly,
-                                           double iLx, double iLy) {
-    // plain operators under fp contract(off): HIP's __f*_rn helpers are defined in a
-    // header outside this pragma and carry the `contract` flag, which lets the backend
-    // fuse t0*t0 + t1*t1 into an FMA (a different float32 rounding than sdot's)
-    const float d0 = ax - bx, d1 = ay - by;
-    const double w0 = (double)d0 - Lx * rint_div((double)d0, Lx, iLx);
-    const double w1 = (double)d1 - Ly * rint_div((double)d1, Ly, iLy);
-    const float t0 = (float)w0, t1 = (float)w1;
-    const float s0 = t0 * t0, s1 = t1 * t1;
-    const float s = s0 + s1;  // OpenBLAS sdot
-    // correctly rounded float32 sqrt (np.sqrt on float32): the double sqrt of a float
-    // rounded once more to float is exact-rounded (53 >= 2*24+2 bits); the device
-    // f32 sqrt instruction is only faithful
-    return (double)(float)__dsqrt_rn((double)s);
+// ---------------------------------------------------------------------------
+// Squared-distance thresholds.  The reference compares r = sqrt(s) (float32: the
+// correctly rounded float sqrt of the float32 sdot; float64: sqrt of the ddot) with
+// r_cut (inclusive) and r_core; correctly rounded sqrt is monotone, so each comparison
+// is exactly one comparison of s with a host-computed threshold, and the sqrt is only
+// taken for pairs inside the cutoff (about 1 % of pairs at rho = 0.03).  Likewise the
+// minimum-image round: for |d| <= L, rint(d / L) is sign(d) if fl(|d| / L) > 0.5
+// (round-half-even keeps 0.5 at 0), else 0, i.e. one comparison with h = the largest
+// double with fl(h / L) <= 0.5.
+struct PairThresh {
+    double cut64, core64;  // s <= cut64 <=> sqrt(s) <= r_cut; s <= core64 <=> sqrt(s) < r_core
+    double hx, hy;         // min-image half-box thresholds
+    float cut32, core32;   // the same for the float32 path
+};
+
+template <class P>
+static inline uint64_t fs_bisect_u64(P pred, uint64_t lo, uint64_t hi) {  // pred(lo), !pred(hi)
+    while (hi - lo > 1) {
+        const uint64_t m = lo + (hi - lo) / 2;
+        if (pred(m)) lo = m; else hi = m;
+    }
+    return lo;
 }
 
-__device__ __forceinline__ double dist_f64(double ax, double ay, double bx, double by, double Lx, double Ly,
-                                           double iLx, double iLy) {
-    const double d0 = ax - bx, d1 = ay - by;
-    const double t0 = d0 - Lx * rint_div(d0, Lx, iLx);
-    const double t1 = d1 - Ly * rint_div(d1, Ly, iLy);
-    const double s0 = t0 * t0;
-    return __dsqrt_rn(fma(t1, t1, s0));  // OpenBLAS ddot (FMA kernel)
+static inline double fs_u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
+static inline float fs_u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+// largest non-negative double / float x with pred(x); -1 if pred(0) is false
+template <class P>
+static inline double fs_max_true_f64(P pred) {
+    if (!pred(0.0)) return -1.0;
+    return fs_u2d(fs_bisect_u64([&](uint64_t u) { return pred(fs_u2d(u)); }, 0, 0x7ff0000000000000ull));
 }
+template <class P>
+static inline float fs_max_true_f32(P pred) {
+    if (!pred(0.0f)) return -1.0f;
+    return fs_u2f((uint32_t)fs_bisect_u64([&](uint64_t u) { return pred(fs_u2f((uint32_t)u)); }, 0, 0x7f800000ull));
+}
+
+static inline PairThresh fs_pair_thresh(const fs_phys &p) {
+    PairThresh t;
+    t.cut64 = fs_max_true_f64([&](double s) { return sqrt(s) <= p.r_cut; });
+    t.core64 = fs_max_true_f64([&](double s) { return sqrt(s) < p.r_core; });
+    t.cut32 = fs_max_true_f32([&](float s) { return (double)(float)sqrt((double)s) <= p.r_cut; });
+    t.core32 = fs_max_true_f32([&](float s) { return (double)(float)sqrt((double)s) < p.r_core; });
+    t.hx = fs_max_true_f64([&](double a) { return a / p.Lx <= 0.5; });
+    t.hy = fs_max_true_f64([&](double a) { return a / p.Ly <= 0.5; });
+    return t;
+}
+
+// d - L * rint(d / L) as simulation_box.py:35-39 computes it
+__device__ __forceinline__ double wrap_min_image(double d, double L, double h, double invL) {
+    const double a = fabs(d);
+    if (a <= L) return a > h ? d - copysign(L, d) : d;
+    return d - L * rint_div(d, L, invL);
+}
+
+// squared minimum-image distances (simulation_box.py:31-56) with numpy's promotion rules.
+// float32 state: float32 delta, wrapped in float64 (box lengths are np.float64), back to
+// float32, then the float32 sdot t0*t0 + t1*t1 as OpenBLAS computes it -- plain operators
+// under fp contract(off): HIP's __f*_rn helpers carry the `contract` flag, which would let
+// the backend fuse the sdot into an FMA.  float64 state: the ddot with its FMA.
+// The distance itself is the correctly rounded sqrt of s (r_of_sq): for float32 the double
+// sqrt rounded once more to float is exact-rounded (53 >= 2*24+2 bits), whereas the
+// device f32 sqrt instruction is only faithful.
+__device__ __forceinline__ float sqdist_f32(float ax, float ay, float bx, float by, double Lx, double Ly,
+                                            const PairThresh &T, double iLx, double iLy) {
+    const float d0 = ax - bx, d1 = ay - by;
+    const float t0 = (float)wrap_min_image((double)d0, Lx, T.hx, iLx);
+    const float t1 = (float)wrap_min_image((double)d1, Ly, T.hy, iLy);
+    const float s0 = t0 * t0, s1 = t1 * t1;
+    return s0 + s1;
+}
+__device__ __forceinline__ double sqdist_f64(double ax, double ay, double bx, double by, double Lx, double Ly,
+                                             const PairThresh &T, double iLx, double iLy) {
+    const double t0 = wrap_min_image(ax - bx, Lx, T.hx, iLx);
+    const double t1 = wrap_min_image(ay - by, Ly, T.hy, iLy);
+    const double s0 = t0 * t0;
+    return fma(t1, t1, s0);
+}
+__device__ __forceinline__ double r_of_sq(float s) { return (double)(float)__dsqrt_rn((double)s); }
+__device__ __forceinline__ double r_of_sq(double s) { return __dsqrt_rn(s); }
 
 // x^6 rounded once from a double-double product (tracks the correctly rounded pow)
 __device__ __forceinline__ double pow6(double x) {

@@ -39,27 +39,32 @@ __device__ double pairwise_lds(const double *a, int n) {
     return res;
 }
 
+// Two chains per wave (one per 32-lane half).  Lane l of a half owns pair rows l and
+// N-2-l, so every lane evaluates N pair terms (the triangle is folded); each row is
+// still summed in numpy's pairwise order and the rows are accumulated in row order.
 template <bool F32>
-__global__ void __launch_bounds__(256) energy_kernel(fs_phys p, const void *__restrict__ pos, int64_t C, int N,
-                                                     double *__restrict__ E, double *__restrict__ W,
+__global__ void __launch_bounds__(256) energy_kernel(fs_phys p, PairThresh T, const void *__restrict__ pos, int64_t C,
+                                                     int N, double *__restrict__ E, double *__restrict__ W,
                                                      uint8_t *__restrict__ ov, uint64_t *__restrict__ nbr,
                                                      const uint8_t *__restrict__ is_f32) {
-    __shared__ double sx[4][64], sy[4][64], se[4][64], sw[4][64], sv[4][64];
+    __shared__ double sx[4][2][64], sy[4][2][64], se[4][2][64], sw[4][2][64], sv[4][2][64];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t c = (int64_t)blockIdx.x * 4 + wid;
-    if (c >= C) return;  // whole wave leaves; no block-level barrier below
+    const int hh = lane >> 5, hl = lane & 31;
+    const int64_t c = ((int64_t)blockIdx.x * 4 + wid) * 2 + hh;
+    if (c >= C) return;  // a whole half leaves; only wave-level barriers below
     // float64 storage holding a chain whose reference state is float32 (after an accepted
     // big move, monte_carlo.py:296): the float32 distance path on the exact float values
     const bool as_f32 = F32 || (is_f32 && is_f32[c]);
-    if (lane < N) {
+    double *X = sx[wid][hh], *Y = sy[wid][hh];
+    for (int q = hl; q < N; q += 32) {
         if (F32) {
-            const float *q = (const float *)pos + c * 2 * N;
-            sx[wid][lane] = q[2 * lane];
-            sy[wid][lane] = q[2 * lane + 1];
+            const float *src = (const float *)pos + c * 2 * N;
+            X[q] = src[2 * q];
+            Y[q] = src[2 * q + 1];
         } else {
-            const double *q = (const double *)pos + c * 2 * N;
-            sx[wid][lane] = q[2 * lane];
-            sy[wid][lane] = q[2 * lane + 1];
+            const double *src = (const double *)pos + c * 2 * N;
+            X[q] = src[2 * q];
+            Y[q] = src[2 * q + 1];
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -68,81 +73,98 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, const void *__re
     const double sr6c = pow6(1.0 / p.r_cut);
     const double e_cut = 4.0 * (sr6c * sr6c - sr6c);
     const double iLx = 1.0 / p.Lx, iLy = 1.0 / p.Ly;
-    const int i = lane;
-    const int n = (i < N - 1) ? N - 1 - i : 0;
-    const double xi = sx[wid][i < N ? i : 0], yi = sy[wid][i < N ? i : 0];
     bool hit = false;
-    uint64_t mask = 0;
-    auto pair = [&](int t, double &e, double &w) {
-        const int j = i + 1 + t;
-        const double r = as_f32 ? dist_f32((float)xi, (float)yi, (float)sx[wid][j], (float)sy[wid][j], p.Lx, p.Ly,
-                                           iLx, iLy)
-                                : dist_f64(xi, yi, sx[wid][j], sy[wid][j], p.Lx, p.Ly, iLx, iLy);
-        hit |= r < p.r_core;
-        if (r <= p.r_cut) mask |= (uint64_t)1 << j;
-        lj_pair(r, p.r_cut, e_cut, e, w);
-    };
-    // row sum in numpy's pairwise order (loops_utils.h pairwise_sum, n <= 128)
-    double re = 0.0, rw = 0.0;
-    if (n < 8) {
-        for (int t = 0; t < n; ++t) {
-            double e, w;
-            pair(t, e, w);
-            re += e;
-            rw += w;
-        }
-    } else {
-        double ae[8], aw[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pair(j, ae[j], aw[j]);
-        const int nfull = n - (n % 8);
-        for (int t0 = 8; t0 < nfull; t0 += 8) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                double e, w;
-                pair(t0 + j, e, w);
-                ae[j] += e;
-                aw[j] += w;
+    // pair (i, j): e, w of lennard_jones_energy_virial (potential.py:3-29); the sqrt only
+    // inside the cutoff (PairThresh)
+    auto pair = [&](int i, int j, double &e, double &w, uint64_t &mask) {
+        e = 0.0;
+        w = 0.0;
+        if (as_f32) {
+            const float s = sqdist_f32((float)X[i], (float)Y[i], (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy);
+            hit |= s <= T.core32;
+            if (s <= T.cut32) {
+                mask |= (uint64_t)1 << j;
+                lj_pair(r_of_sq(s), p.r_cut, e_cut, e, w);
+            }
+        } else {
+            const double s = sqdist_f64(X[i], Y[i], X[j], Y[j], p.Lx, p.Ly, T, iLx, iLy);
+            hit |= s <= T.core64;
+            if (s <= T.cut64) {
+                mask |= (uint64_t)1 << j;
+                lj_pair(r_of_sq(s), p.r_cut, e_cut, e, w);
             }
         }
-        re = ((ae[0] + ae[1]) + (ae[2] + ae[3])) + ((ae[4] + ae[5]) + (ae[6] + ae[7]));
-        rw = ((aw[0] + aw[1]) + (aw[2] + aw[3])) + ((aw[4] + aw[5]) + (aw[6] + aw[7]));
-        for (int t = nfull; t < n; ++t) {
-            double e, w;
-            pair(t, e, w);
-            re += e;
-            rw += w;
+    };
+    // row i (pairs j > i) summed in numpy's pairwise order (loops_utils.h pairwise_sum, n <= 128)
+    auto row = [&](int i) {
+        const int n = N - 1 - i;
+        double re = 0.0, rw = 0.0;
+        uint64_t mask = 0;
+        if (n < 8) {
+            for (int t = 0; t < n; ++t) {
+                double e, w;
+                pair(i, i + 1 + t, e, w, mask);
+                re += e;
+                rw += w;
+            }
+        } else {
+            double ae[8], aw[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pair(i, i + 1 + j, ae[j], aw[j], mask);
+            const int nfull = n - (n % 8);
+            for (int t0 = 8; t0 < nfull; t0 += 8) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    double e, w;
+                    pair(i, i + 1 + t0 + j, e, w, mask);
+                    ae[j] += e;
+                    aw[j] += w;
+                }
+            }
+            re = ((ae[0] + ae[1]) + (ae[2] + ae[3])) + ((ae[4] + ae[5]) + (ae[6] + ae[7]));
+            rw = ((aw[0] + aw[1]) + (aw[2] + aw[3])) + ((aw[4] + aw[5]) + (aw[6] + aw[7]));
+            for (int t = nfull; t < n; ++t) {
+                double e, w;
+                pair(i, i + 1 + t, e, w, mask);
+                re += e;
+                rw += w;
+            }
         }
-    }
+        se[wid][hh][i] = re;
+        sw[wid][hh][i] = rw;
+        if (nbr) nbr[c * N + i] = mask;
+    };
+    const int ra = hl, rb = N - 2 - hl;
+    if (ra <= N - 2) row(ra);
+    if (rb > ra) row(rb);
+    if (nbr && hl == 0 && N >= 1) nbr[c * N + N - 1] = 0;  // the last row has no j > i
     // external double well per particle (potential.py:89-112)
-    double v = 0.0;
-    if (lane < N) {
+    for (int q = hl; q < N; q += 32) {
+        double v = 0.0;
         const double cy = p.Ly / 2.0;
         for (int k = 0; k < p.num_wells && k < 2; ++k) {
             const double cx = (k == 0) ? p.Lx / 4.0 : 3.0 * p.Lx / 4.0;
-            double dx = xi - cx, dy = yi - cy;
+            double dx = X[q] - cx, dy = Y[q] - cy;
             dx -= p.Lx * rint_div(dx, p.Lx, iLx);
             dy -= p.Ly * rint_div(dy, p.Ly, iLy);
             const double r = sqrt(dx * dx + dy * dy);
             const double tr = 0.5 * (1.0 + tanh(p.k * (r - p.r0)));
             v += p.V0[k] * (1.0 - tr);
         }
+        sv[wid][hh][q] = v;
     }
-    se[wid][lane] = re;
-    sw[wid][lane] = rw;
-    sv[wid][lane] = v;
-    if (nbr && lane < N) nbr[c * N + lane] = mask;
-    const bool any_hit = __ballot(hit) != 0;
+    const uint64_t half = hh ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+    const bool any_hit = (__ballot(hit) & half) != 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane == 0) {
+    if (hl == 0) {
         double te = 0.0, tw = 0.0;
         for (int k = 0; k < N - 1; ++k) {  // Python-float accumulation over rows
-            te += se[wid][k];
-            tw += sw[wid][k];
+            te += se[wid][hh][k];
+            tw += sw[wid][hh][k];
         }
-        if (p.num_wells > 0) te += pairwise_lds(sv[wid], N);
+        if (p.num_wells > 0) te += pairwise_lds(sv[wid][hh], N);
         if (any_hit) {
             te = INFINITY;
             tw = INFINITY;
@@ -339,11 +361,13 @@ using namespace fs;
 hipError_t fs_energy_impl(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int N, double *E,
                           double *W, uint8_t *overlap, uint64_t *nbr, hipStream_t st, const uint8_t *chain_is_f32) {
     if (C <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((C + 3) / 4));
+    const dim3 grid((unsigned)((C + 7) / 8));
+    const PairThresh T = fs_pair_thresh(*p);
     if (pos_is_f32)
-        hipLaunchKernelGGL(energy_kernel<true>, grid, dim3(256), 0, st, *p, pos, C, N, E, W, overlap, nbr, nullptr);
+        hipLaunchKernelGGL(energy_kernel<true>, grid, dim3(256), 0, st, *p, T, pos, C, N, E, W, overlap, nbr,
+                           nullptr);
     else
-        hipLaunchKernelGGL(energy_kernel<false>, grid, dim3(256), 0, st, *p, pos, C, N, E, W, overlap, nbr,
+        hipLaunchKernelGGL(energy_kernel<false>, grid, dim3(256), 0, st, *p, T, pos, C, N, E, W, overlap, nbr,
                            chain_is_f32);
     return hipGetLastError();
 }

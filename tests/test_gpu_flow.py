@@ -127,3 +127,26 @@ def test_pack_tracks_weight_updates():
     sd2 = {k: v.clone() for k, v in sd.items()}
     sd2["flows.0.prqct.transform_net.final_layer.weight"] *= 2.0
     close(b.cpu().numpy(), OF.log_prob(sd2, torch.from_numpy(f["x"]), dims).numpy())
+
+
+@pytest.mark.parametrize("N", [1, 3])
+def test_layer_forward_inverse_like_reference_flowtest(N):
+    """The reference's own FlowTest.checkForwardInverse (flows/flow_test.py, used by
+    neural_spline/wrapper_test.py::test_circular_nsf) on the drop-in layer, in the
+    configuration the hot path uses (all coordinates circular, no context): dtype and
+    shape kept, inverse(forward(x)) == x, log-dets cancel."""
+    from flowstate.normflows.flows import CircularCoupledRationalQuadraticSpline
+
+    torch.manual_seed(N)
+    D, B = 2 * N, 5.0
+    flow = CircularCoupledRationalQuadraticSpline(D, 2, 32, range(D), num_bins=8, tail_bound=B).cuda().eval()
+    with torch.no_grad():  # leave the identity initialisation (wrapper.py:181-185)
+        for p in flow.parameters():
+            p.add_(0.1 * torch.randn_like(p))
+    inputs = 6 * torch.rand((3, D), device="cuda") - 3
+    out, ld = flow(inputs)
+    assert out.dtype == inputs.dtype and out.shape == inputs.shape and ld.shape == (3,)
+    back, ld_inv = flow.inverse(out)
+    assert back.dtype == inputs.dtype and back.shape == inputs.shape
+    torch.testing.assert_close(back, inputs, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(ld + ld_inv, torch.zeros_like(ld), atol=1e-3, rtol=1e-3)

@@ -76,3 +76,18 @@ def check_training(device, rtol_loss, rtol_grad, atol_grad):
 def test_training_step_matches_reference_cpu():
     torch.set_num_threads(4)
     check_training("cpu", rtol_loss=1e-6, rtol_grad=1e-4, atol_grad=1e-6)
+
+
+def test_torch_spline_forward_inverse_consistent():
+    """The reference's splines_test.py consistency check on the torch restatement used
+    on CPU tensors (autograd_flow.circular_rqs_torch)."""
+    from flowstate.normflows.autograd_flow import circular_rqs_torch
+
+    torch.manual_seed(0)
+    shape, K, B = (2, 3, 4), 10, 3.0
+    uw, uh, ud = torch.randn(*shape, K), torch.randn(*shape, K), torch.randn(*shape, K + 1)
+    x = torch.randn(*shape) * 2
+    y, ld = circular_rqs_torch(x, uw, uh, ud, B, False)
+    x2, ld2 = circular_rqs_torch(y, uw, uh, ud, B, True)
+    torch.testing.assert_close(x2, x, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(ld + ld2, torch.zeros_like(ld), atol=1e-3, rtol=1e-3)
