@@ -35,6 +35,8 @@ from flowstate.models import A1, build_flow, half_box  # noqa: E402
 
 PEAK_F32_TFLOPS = 157.3  # MI355X dense FP32 (MFMA = vector rate), MI355X_MICROARCH.md
 PEAK_F64_TFLOPS = 78.6   # MI355X FP64 vector
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense BF16 MFMA (spec, no sparsity), MI355X_MICROARCH.md
+SPLIT_PRODUCTS = {"bf16x6": 6, "bf16x3": 3}  # bf16 MFMAs per f32-equivalent product
 ENERGY_BYTES = lambda N: 4 * 2 * N + 16  # noqa: E731  float32 proposal in, E and W out
 ENERGY_FLOP = lambda N: 30 * N * (N - 1) // 2 + 40 * N  # noqa: E731
 
@@ -67,6 +69,45 @@ def synthetic_states(N, C, c0, seed=7):
     rng = np.random.default_rng(seed + c0)
     L = float(box.box_size_x)
     return np.mod(base[None] + rng.normal(0, 0.05, (C, N, 2)), L), L
+
+
+def alt_precisions(bmc, stepper, steps=3):
+    """The opt-in split-bf16 conditioner modes (NormalizingFlow.set_precision) on the same
+    chains right after the headline run: steps/s of the same fused step, the flow kernels'
+    f32-equivalent TFLOP/s against the emulated-f32 peak (bf16 dense peak / plane
+    products), and the largest relative log q difference to the f32 kernel on the same
+    4096 proposals.  Reported beside the headline, never as `value`."""
+    model, C, N = bmc.model, bmc.C, bmc.N
+    base = model.precision
+    x = stepper.centered[:4096].clone()
+    ref = model.log_prob(x).double()
+    fpp = flops_per_pass(N, **A1)
+    out = {}
+    for prec, nprod in SPLIT_PRODUCTS.items():
+        model.set_precision(prec)
+        lq = model.log_prob(x).double()
+        fin = torch.isfinite(ref)
+        rel = float(((lq - ref).abs() / ref.abs())[fin].max().item()) if bool(fin.any()) else 0.0
+        st = Stepper(bmc)
+        st.step(timed=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            st.step(timed=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        st.harvest()
+        t_prop, t_lp, t_en, t_acc = st.t / steps
+        ach = 2 * fpp * C / ((t_prop + t_lp) * 1e-3) / 1e12
+        peak = PEAK_BF16_TFLOPS / nprod
+        out[prec] = {"value": C * steps / dt, "unit": "steps/s", "steps": steps, "ms_per_step": dt / steps * 1e3,
+                     "kernel_ms": {"flow_propose": t_prop, "flow_log_prob": t_lp, "energy": t_en, "mh_accept": t_acc},
+                     "max_rel_log_q_vs_f32": rel,
+                     "roofline": {"bound": "mfma", "achieved": ach, "peak": peak,
+                                  "unit": "TFLOP/s (f32-equivalent)", "frac": ach / peak,
+                                  "kernel": f"flow_split_kernel<256,32,*,{3 if nprod == 6 else 2}>"}}
+    model.set_precision(base)
+    return out
 
 
 class Stepper:
@@ -189,6 +230,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--precision", default="f32", choices=["f32", "bf16x6", "bf16x3"],
+                    help="conditioner GEMM arithmetic of the headline run (f32 = the reference's)")
+    ap.add_argument("--no-alt-precision", action="store_true",
+                    help="skip the secondary measurement of the split-bf16 modes")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -209,7 +254,7 @@ def main():
 
     N, C = args.particles, args.chains
     c0, seeds = parallel.shard(C, rank)
-    model = synthetic_model(N, dev)
+    model = synthetic_model(N, dev).set_precision(args.precision)
     init, L = synthetic_states(N, C, c0)
     phys = Physics(L, L, temperature=1.0, num_wells=2, V0_list=(-10.0, -10.5), r0=1.2, k=15)
     bmc = BatchedMonteCarlo(model, init, phys, seeds, device=dev, chain_offset=c0)
@@ -249,6 +294,7 @@ def main():
     fpp = flops_per_pass(N, **A1)
     t_prop, t_lp, t_en, t_acc = (stepper.t / args.steps)  # ms per launch
     achieved = 2 * fpp * C / ((t_prop + t_lp) * 1e-3) / 1e12  # both flow passes (same kernel template)
+    peak = PEAK_F32_TFLOPS if args.precision == "f32" else PEAK_BF16_TFLOPS / SPLIT_PRODUCTS[args.precision]
     out = {
         "metric": "NF-proposed MH steps/sec, N=64 2D LJ, 65536 chains; acceptance-rate match",
         "value": value,
@@ -260,7 +306,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if args.precision == "f32" else f"f32 operands, {args.precision} split on bf16 MFMA",
         "data": "synthetic (FCC+jitter states, random-init A1 flow with perturbed final layers)",
         "config": {"workload": f"Algorithm-1 NF-proposed MH step, N={N}, {C} chains per GPU",
                    "particles": N, "chains_per_gpu": C, "flow": "A1: L=15 H=256 blocks=32 K=32",
@@ -271,8 +317,8 @@ def main():
                         "gathered_chain_rows": int(table.shape[0]),
                         "deltaF_mean_sem": parallel.free_energy_stats(table)[:2]},
         "kernel_ms": {"flow_propose": t_prop, "flow_log_prob": t_lp, "energy": t_en, "mh_accept": t_acc},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_F32_TFLOPS, "traffic": _pmc_traffic(),
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                     "frac": achieved / peak, "traffic": _pmc_traffic() if args.precision == "f32" else None,
                      "kernel": "flow_pass_kernel<256,32,*> (propose + log_prob)",
                      "algorithmic_flop_per_launch": fpp * C},
         # the LJ + double-well kernel the north star asks about: HBM rate of its algorithmic
@@ -284,6 +330,8 @@ def main():
                           "peak_fp64_tflops": PEAK_F64_TFLOPS,
                           "frac": ENERGY_FLOP(N) * C / (t_en * 1e-3) / 1e12 / PEAK_F64_TFLOPS},
     }
+    if world == 1 and not args.no_alt_precision and args.precision == "f32":
+        out["alt_precision"] = alt_precisions(bmc, stepper)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
     if rank == 0:

@@ -116,4 +116,79 @@ FS_HD LdsLayout lds_layout(int N, int H) {
     return l;
 }
 
+// ---------------------------------------------------------------------------
+// Split-bf16 image (fs_flow_dims.precision = 1: P = 3 planes, 6 products;
+// precision = 2: P = 2 planes, 3 products).  Every f32 weight w is stored as P
+// bf16 planes w = w_0 + w_1 (+ w_2), each the round-to-nearest-even bf16 of the
+// remainder of the previous ones.  GEMM A operands of v_mfma_f32_32x32x16_bf16
+// (the conditioner runs transposed: C^T = W . X^T, so the weights are the A
+// operand and the accumulator lane is the chain) are 1 KiB fragments
+// [tile (32 output rows)][k-step (16 inputs)][plane][lane][8 bf16]: lane l
+// (r = l & 31, h = l >> 5) holds W[32 tile + r][16 s + 8 h + j], j = 0..7.
+// Offsets are in floats (1 fragment = 256 floats).  The vector section (folded
+// BatchNorm, biases) and the unconditional knots are those of PackLayout, at
+// the same distance from each other (pack_vec_kernel writes both images).
+// ---------------------------------------------------------------------------
+FS_HD int split_planes(int precision) { return precision == 1 ? 3 : 2; }
+
+struct SplitLayout {
+    int P;            // planes
+    int kst_in;       // k-steps of the initial layer (ceil(2N/16))
+    int kst_h;        // k-steps of an H-input layer (H/16)
+    int nfw;          // transform features per wave (ceil(N/8)); wave w owns [w nfw, (w+1) nfw)
+    int64_t win;      // [H/32][kst_in][P] fragments
+    int64_t blocks;   // nb x { W0 [H/32][kst_h][P], W1 [...] }
+    int64_t block_stride;
+    int64_t wf;       // final layer: per feature j, 3 tiles (widths, heights, d_0..d_{K-1})
+    int64_t wt;       // per wave: one tile whose rows r < nfw are d_K of feature w nfw + r
+    int64_t vec;      // PackLayout's vector section
+    int64_t unc;      // PackLayout's unconditional knots
+    int64_t stride;
+};
+
+FS_HD SplitLayout split_layout(int N, int H, int nb, int K, int precision) {
+    SplitLayout s;
+    const PackLayout p = pack_layout(N, H, nb, K);
+    s.P = split_planes(precision);
+    s.kst_in = (2 * N + 15) / 16;
+    s.kst_h = H / 16;
+    s.nfw = (N + 7) / 8;
+    const int64_t frag = 256 * (int64_t)s.P;  // floats per (tile, k-step), all planes
+    const int64_t tiles_h = H / 32;
+    s.win = 0;
+    s.blocks = s.win + tiles_h * s.kst_in * frag;
+    s.block_stride = 2 * tiles_h * s.kst_h * frag;
+    s.wf = s.blocks + nb * s.block_stride;
+    s.wt = s.wf + (int64_t)N * 3 * s.kst_h * frag;
+    s.vec = s.wt + (int64_t)8 * s.kst_h * frag;
+    s.unc = s.vec + (p.unc - p.vec);
+    s.stride = rup(s.unc + (int64_t)N * 3 * (K + 1), 64);
+    return s;
+}
+
+// LDS of the split kernel: activations [64 chains][P planes][xw + 8] bf16 (a
+// chain's planes are adjacent, so every fragment address of a GEMM is one base
+// VGPR + a 16-bit immediate; the 16-byte pad per plane row keeps the 32 rows of
+// a ds_read_b128 fragment and the ds_write_b64 epilogue stores conflict-free),
+// then coordinates, tail values, log-det partials.  `plane` = bytes between the
+// planes of one chain, `xsb` = bytes between chains.
+struct SplitLds {
+    int xw, xsb, plane, coord, tail, ld, total, cstride, tstride;
+};
+
+FS_HD SplitLds split_lds(int N, int H, int P) {
+    SplitLds l;
+    const int in16 = (2 * N + 15) / 16 * 16;
+    l.xw = H > in16 ? H : in16;
+    l.plane = 2 * l.xw + 16;
+    l.xsb = P * l.plane;
+    l.cstride = 2 * N + 1;
+    l.tstride = 8 * ((N + 7) / 8) + 1;
+    l.coord = kRows * l.xsb;
+    l.tail = (int)rup(l.coord + kRows * l.cstride * 4, 16);
+    l.ld = (int)rup(l.tail + kRows * l.tstride * 4, 16);
+    l.total = l.ld + kWaves * kRows * 4 + 16;
+    return l;
+}
+
 }  // namespace fs

@@ -18,6 +18,16 @@ hipError_t fs_flow_pass_impl(const fs_flow_dims *d, const void *packed, int mode
                              uint64_t seed, uint64_t counter, int64_t row_offset, double half_width,
                              int32_t *err, hipStream_t st);
 
+// split-bf16 flow image and pass (flow_split_kernels.hip; fs_flow_dims.precision 1 or 2)
+namespace fs { struct FlowArgs; }
+bool fs_flow_split_supported(const fs_flow_dims *d, char *why, size_t n);
+int64_t fs_flow_split_packed_bytes(const fs_flow_dims *d);
+hipError_t fs_flow_split_pack(const fs_flow_dims *d, const float *raw, float *packed, hipStream_t st);
+hipError_t fs_flow_split_pass(const fs::FlowArgs &a, int mode, int precision, int N, int H, int K, hipStream_t st);
+// pack_vec_kernel of the f32 image (biases, folded BatchNorm, unconditional knots), launched
+// with dst shifted so that its vector section lands where the caller's image keeps it
+hipError_t fs_flow_pack_vec(float *dst, const float *raw_layer, const fs_flow_dims *d, hipStream_t st);
+
 hipError_t fs_energy_impl(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int N, double *E,
                           double *W, uint8_t *overlap, uint64_t *nbr, hipStream_t st,
                           const uint8_t *chain_is_f32 = nullptr);

@@ -19,7 +19,7 @@ FS_MH_HYBRID = 2
 
 class FlowDims(ctypes.Structure):
     _fields_ = [("N", ctypes.c_int32), ("L", ctypes.c_int32), ("H", ctypes.c_int32), ("nb", ctypes.c_int32),
-                ("K", ctypes.c_int32), ("reserved", ctypes.c_int32), ("tail_bound", ctypes.c_double)]
+                ("K", ctypes.c_int32), ("precision", ctypes.c_int32), ("tail_bound", ctypes.c_double)]
 
 
 class Phys(ctypes.Structure):

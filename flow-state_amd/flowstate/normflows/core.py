@@ -18,6 +18,7 @@ import torch.nn as nn
 
 from .. import _lib
 from .Energy import UniformParticle
+from .flows import PRECISIONS
 
 
 def _tensor_key(ts):
@@ -34,12 +35,12 @@ class _PackCache:
 
     def get(self, layers):
         tensors = [t for layer in layers for t in layer.raw_param_tensors()]
-        key = _tensor_key(tensors)
+        dims = layers[0].dims(L=len(layers))
+        key = (_tensor_key(tensors), int(dims.precision))
         if key == self.key:
             return self.packed
         dev = tensors[0].device
         _lib.require_device(tensors[0])
-        dims = layers[0].dims(L=len(layers))
         L = _lib.load()
         nraw = L.fs_flow_raw_floats(dims)
         nbytes = L.fs_flow_packed_bytes(dims)
@@ -130,6 +131,25 @@ class NormalizingFlow(nn.Module):
         b = float(self.q0.bound)
         if any(abs(f.tail_bound - b) > 0 for f in self.flows):
             raise NotImplementedError("q0.bound must equal the layers' tail_bound (main_algorithm_1.py:276-283)")
+
+    def set_precision(self, precision="f32"):
+        """Arithmetic of the conditioner GEMMs in the fused passes (flows.PRECISIONS):
+        "f32" (default: the reference's float32, exact-f32 MFMA products), "bf16x6" or
+        "bf16x3" (f32 operands split into bf16 planes on the bf16 matrix cores, DESIGN.md
+        'Precision modes').  The spline, base density and everything outside the
+        conditioner GEMMs are unchanged.  Returns self."""
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
+        for f in self.flows:
+            f._fs_precision = precision
+            if getattr(f, "_fs_cache", None) is not None:
+                f._fs_cache.key = None
+        self.invalidate_packed()
+        return self
+
+    @property
+    def precision(self):
+        return getattr(self.flows[0], "_fs_precision", "f32")
 
     def packed(self):
         """Device packed parameter image (rebuilt when parameters/buffers change)."""

@@ -18,6 +18,11 @@ from torch import nn
 from .. import _lib
 
 DEFAULT_MIN_DERIVATIVE = 1e-3  # splines.py:8
+# Conditioner GEMM arithmetic of the fused passes (fs_flow_dims.precision, include/flowstate.h):
+#   "f32"    the reference's float32 products and sums (exact-f32 MFMA), the default;
+#   "bf16x6" f32 operands as three bf16 planes, the six plane products above 2^-24 (f32-level error);
+#   "bf16x3" two planes, three products (16 significant bits per operand).
+PRECISIONS = {"f32": 0, "bf16x6": 1, "bf16x3": 2}
 
 
 def _alternating_mask(features, even):
@@ -161,6 +166,7 @@ class CircularCoupledRationalQuadraticSpline(nn.Module):
         d.H = self.num_hidden_channels
         d.nb = self.num_blocks
         d.K = self.num_bins
+        d.precision = PRECISIONS[getattr(self, "_fs_precision", "f32")]
         d.tail_bound = self.tail_bound
         return d
 

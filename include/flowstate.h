@@ -33,14 +33,18 @@ extern "C" {
 /* Flow hyper-parameters.  Mirrors the CircularCoupledRationalQuadraticSpline
  * stack built by main_algorithm_1.py:280-284 (wrapper.py:103-119):
  * N particles (D = 2N), L layers, H hidden units, nb residual blocks,
- * K spline bins, tail_bound = HALF_BOX. */
+ * K spline bins, tail_bound = HALF_BOX; precision selects the GEMM arithmetic
+ * (the reference's is float32: precision 0). */
 typedef struct {
     int32_t N;
     int32_t L;
     int32_t H;
     int32_t nb;
     int32_t K;
-    int32_t reserved;
+    int32_t precision;   /* conditioner GEMM arithmetic: 0 = f32 MFMA (exact f32 products, the
+                          * default); 1 = bf16x6 (f32 operands as 3 bf16 planes, 6 plane
+                          * products: f32-level error); 2 = bf16x3 (2 planes, 3 products:
+                          * 16-bit operands).  1 and 2 use their own packed image. */
     double tail_bound;
 } fs_flow_dims;
 

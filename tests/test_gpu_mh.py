@@ -47,10 +47,10 @@ def test_reference_traces_replay(N):
         assert mc.attempts_displacement == len(acc) and mc.accepted_displacement == sum(acc)
 
 
-def _fused_vs_oracle(N, dims_kw, C, steps, seed_w=11):
+def _fused_vs_oracle(N, dims_kw, C, steps, seed_w=11, precision="f32"):
     dims = OF.FlowDims(N=N, B=half_box(N), **dims_kw)
     sd = OF.random_state_dict(dims, seed=seed_w)
-    model = flow_from_state_dict(sd, N, bound=dims.B, **dims_kw)
+    model = flow_from_state_dict(sd, N, bound=dims.B, **dims_kw).set_precision(precision)
     L = float(np.sqrt(N / 0.03))
     phys = Physics(L, L)
     rng = np.random.default_rng(5)

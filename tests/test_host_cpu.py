@@ -99,8 +99,8 @@ def test_abi_rejects_invalid_arguments_before_touching_the_device():
     assert rc == -1 and b"K=7" in L.fs_last_error()
     rc = L.fs_pair_hist(one, 1, 4, 300, 5.0, one, 10, one, None)
     assert rc == -1
-    d = _lib.FlowDims(N=16, L=2, H=96, nb=1, K=8, reserved=0, tail_bound=5.0)
+    d = _lib.FlowDims(N=16, L=2, H=96, nb=1, K=8, precision=0, tail_bound=5.0)
     assert L.fs_flow_packed_bytes(d) == -1 and b"H=96" in L.fs_last_error()
-    rc = L.fs_nf_mh_step(_lib.FlowDims(N=16, L=2, H=64, nb=1, K=8, reserved=0, tail_bound=5.0), one, ph, 4, 0, 0, 0,
+    rc = L.fs_nf_mh_step(_lib.FlowDims(N=16, L=2, H=64, nb=1, K=8, precision=0, tail_bound=5.0), one, ph, 4, 0, 0, 0,
                          None, None, None, None, None, None, None, None, None, None, None, 0, one, None)
     assert rc == -1
