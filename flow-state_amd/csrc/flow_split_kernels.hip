@@ -47,6 +47,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define FS_SPLIT_XB 1  // activation-fragment buffers (k-steps read ahead)
 #endif
 
+
 // (H, K) instantiations of the split kernel
 #define FS_SPLIT_INSTANCES FS_SCASE(256, 32) FS_SCASE(256, 15) FS_SCASE(128, 32) FS_SCASE(128, 15) FS_SCASE(64, 8) FS_SCASE(32, 5)
 
@@ -118,9 +119,33 @@ __device__ __forceinline__ void sring_prologue(SRing<P, CTW, RD> &R, __amdgpu_bu
         if (u < kst) sring_slot<P, CTW, RD>(R.w[u], W, sec, kst, tile0, u);
 }
 
+// Per-feature vectors of an epilogue (folded BatchNorm scale a and shift c) for a wave's
+// tiles: lane half h holds features 32 tile + 8 g + 4 h + 0..3.  (Loading them inside
+// the preceding GEMM instead, to hide their L2 latency, costs 32 live VGPRs there and
+// spills: +27 % pass time.  Without the loads at all the epilogue phase shrinks only
+// from 12.2 % to 9.3 % of wave time: its cost is the VALU split and the LDS stores.)
+template <int CTW>
+struct EpiVec {
+    f32x4 a[CTW][4], c[CTW][4];
+};
+
+template <int CTW>
+__device__ __forceinline__ void load_epi(EpiVec<CTW> &e, const float *__restrict__ av, const float *__restrict__ cv,
+                                         int tile0) {
+    const int h = (threadIdx.x >> 5) & 1;
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f0 = 32 * (tile0 + ct) + 8 * g + 4 * h;
+            e.c[ct][g] = *(const f32x4 *)(cv + f0);
+            if (av) e.a[ct][g] = *(const f32x4 *)(av + f0);
+        }
+}
+
 // acc[ct][rt] (+)= W[tile0 + ct] . X^T[chain half rt0 + rt] over kst k-steps.
 // X planes: XP + q * plane + chain * xsb (bytes).  Weight ring slot = s % RD, the
-// activation fragments of step s + 2 are read right after the MFMAs of step s.
+// activation fragments of step s + XB are read right after the MFMAs of step s.
 template <int P, int CTW, int RTW, int RD, bool ACC>
 __device__ __forceinline__ void sgemm(const char *XP, int plane, int xsb, __amdgpu_buffer_rsrc_t W, int sec, int kst,
                                       int tile0, int rt0, SRing<P, CTW, RD> &R, f32x16 (&acc)[CTW][RTW]) {
@@ -221,27 +246,20 @@ __device__ __forceinline__ float tile_row(const f32x16 &lo, const f32x16 &hi, in
 
 // ResNet epilogue of a wave's tiles into the activation planes: relu(a * acc + c)
 // (eval BatchNorm folded, the block's deferred biases re-associated into c, resnet.py:37-50)
-// when RELU, else acc + c (the final layer's input).  a, c: per output feature [H].
+// when RELU, else acc + c (the final layer's input).  a, c: prefetched by the GEMM before.
 template <int P, int H, int CTW, int RTW, bool RELU>
 __device__ __forceinline__ void split_epilogue(char *XP, int plane, int xsb, int tile0, int rt0,
-                                               const float *__restrict__ av, const float *__restrict__ cv,
-                                               const f32x16 (&acc)[CTW][RTW]) {
-    const int h = (threadIdx.x >> 5) & 1;
+                                               const EpiVec<CTW> &e, const f32x16 (&acc)[CTW][RTW]) {
 #pragma unroll
     for (int ct = 0; ct < CTW; ++ct) {
         float a[16], c[16];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int f0 = 32 * (tile0 + ct) + 8 * g + 4 * h;
-            const f32x4 c4 = *(const f32x4 *)(cv + f0);
-            f32x4 a4 = {1.f, 1.f, 1.f, 1.f};
-            if (RELU) a4 = *(const f32x4 *)(av + f0);
+        for (int g = 0; g < 4; ++g)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                a[4 * g + j] = a4[j];
-                c[4 * g + j] = c4[j];
+                a[4 * g + j] = RELU ? e.a[ct][g][j] : 1.f;
+                c[4 * g + j] = e.c[ct][g][j];
             }
-        }
 #pragma unroll
         for (int rt = 0; rt < RTW; ++rt) {
             float v[16];
@@ -272,7 +290,7 @@ __device__ __forceinline__ void preset_bias(f32x16 (&acc)[1][2], const float *__
 template <int P, int K, bool INV, int RD>
 __device__ __forceinline__ float split_cond_spline(const char *XP, int plane, int xsb, __amdgpu_buffer_rsrc_t W,
                                                    int sec, int kst, const float *__restrict__ bf, float *CO, int cs,
-                                                   int p, float ud_tail, const FlowArgs &a, bool &nan_any) {
+                                                   int p, float ud_tail, const FlowArgs &a, bool &nan_any, Prof &pf) {
     const int lane = threadIdx.x & 63;
     const float x = CO[lane * cs + p];
     const bool inside = (x >= a.negB) && (x <= a.B);
@@ -288,6 +306,7 @@ __device__ __forceinline__ float split_cond_spline(const char *XP, int plane, in
             preset_bias(acc, bf + 32 * t);
             sgemm<P, 1, 2, RD, true>(XP, plane, xsb, W, sec, kst, t, 0, R, acc);
             lanes_to_chains(acc[0][0], acc[0][1]);
+            pf.mark(PH_FINAL_GEMM);
             float u[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) u[k] = tile_row(acc[0][0], acc[0][1], k);
@@ -295,6 +314,7 @@ __device__ __forceinline__ float split_cond_spline(const char *XP, int plane, in
                 knots_from_logits<K>(u, cw, kMinW, a.twoB, a.negB, a.B);
             else
                 knots_from_logits<K>(u, ch, kMinH, a.twoB, a.negB, a.B);
+            pf.mark(PH_SPLINE);
         }
         icw = cw[0], cw1 = cw[1], ich = ch[0], ch1 = ch[1];
 #pragma unroll
@@ -315,6 +335,7 @@ __device__ __forceinline__ float split_cond_spline(const char *XP, int plane, in
         preset_bias(acc, bf + 64);
         sgemm<P, 1, 2, RD, true>(XP, plane, xsb, W, sec, kst, 2, 0, R, acc);
         lanes_to_chains(acc[0][0], acc[0][1]);
+        pf.mark(PH_FINAL_GEMM);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const float dk = tile_row(acc[0][0], acc[0][1], k);
@@ -327,6 +348,7 @@ __device__ __forceinline__ float split_cond_spline(const char *XP, int plane, in
     float y, l;
     bool nd;
     rqs_eval<INV>(x, icw, cw1 - icw, ich, ch1 - ich, d0, d1, y, l, nd);
+    pf.mark(PH_SPLINE);
     if (inside) {
         CO[lane * cs + p] = y;
         nan_any |= nd;
@@ -349,7 +371,6 @@ __global__ void __launch_bounds__(kThreads, 2) flow_split_kernel(FlowArgs a) {
     // wave index as a scalar: every weight-fragment offset derived from it is an SGPR
     // (buffer-load soffset), never a per-lane value the compiler would waterfall
     const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int h = lane >> 5, r = lane & 31;
     char *XP = smem;
     const int plane = LL.plane, xsb = LL.xsb;
     float *CO = (float *)(smem + LL.coord);
@@ -392,6 +413,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_split_kernel(FlowArgs a) {
     bool nan_any = false;
     int off = 0;
     __syncthreads();
+    Prof pf;
 
     for (int s = 0; s < a.L; ++s) {
         const int layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
@@ -402,7 +424,9 @@ __global__ void __launch_bounds__(kThreads, 2) flow_split_kernel(FlowArgs a) {
         if (MODE != MODE_DENSITY) {
             off = (off + N) % D;  // Coupling.inverse rolls first (coupling.py:113-114)
             ld += uncond_spline<K, true>(Pl + SL.unc, CO, cs, N, D, off, a, nan_any);
+            pf.mark(PH_UNCOND);
             __syncthreads();
+            pf.mark(PH_BARRIER);
         }
         SRing<P, CTW, RD> R;
         if (active) sring_prologue<P, CTW, RD>(R, W, (int)(SL.win * 4), SL.kst_in, tile0);
@@ -421,37 +445,52 @@ __global__ void __launch_bounds__(kThreads, 2) flow_split_kernel(FlowArgs a) {
         for (int c = D + wid; c < 16 * SL.kst_in; c += kWaves)
 #pragma unroll
             for (int p = 0; p < P; ++p) *(uint16_t *)(XP + p * plane + lane * xsb + 2 * c) = 0;
+        pf.mark(PH_PF);
         __syncthreads();
+        pf.mark(PH_BARRIER);
 
         // ResidualNet (resnet.py:53-104), transposed; hr = residual stream without its
         // deferred biases (pack_vec_kernel re-associates them exactly as for the f32 kernel)
         f32x16 hr[CTW][RTW], acc[CTW][RTW];
+        EpiVec<CTW> ev;
         if (active) sgemm<P, CTW, RTW, RD, false>(XP, plane, xsb, W, (int)(SL.win * 4), SL.kst_in, tile0, rt0, R, hr);
-#ifndef FS_DIAG_NORES
+        pf.mark(PH_INIT_GEMM);
         for (int jb = 0; jb < a.nb; ++jb) {
             const float *VB = V + PL.v_blocks + (int64_t)4 * H * jb;
             const int w0 = (int)((SL.blocks + jb * SL.block_stride) * 4);
             const int w1 = w0 + (int)(SL.block_stride * 2);
             if (active) sring_prologue<P, CTW, RD>(R, W, w0, SL.kst_h, tile0);
             __syncthreads();  // every wave is done reading X
-            if (active) split_epilogue<P, H, CTW, RTW, true>(XP, plane, xsb, tile0, rt0, VB, VB + H, hr);
+            pf.mark(PH_BARRIER);
+            if (active) load_epi<CTW>(ev, VB, VB + H, tile0);
+            if (active) split_epilogue<P, H, CTW, RTW, true>(XP, plane, xsb, tile0, rt0, ev, hr);
+            pf.mark(PH_EPI);
             __syncthreads();
+            pf.mark(PH_BARRIER);
             if (active) {
                 sgemm<P, CTW, RTW, RD, false>(XP, plane, xsb, W, w0, SL.kst_h, tile0, rt0, R, acc);
                 sring_prologue<P, CTW, RD>(R, W, w1, SL.kst_h, tile0);
             }
+            pf.mark(PH_RES_GEMM);
             __syncthreads();
-            if (active) split_epilogue<P, H, CTW, RTW, true>(XP, plane, xsb, tile0, rt0, VB + 2 * H, VB + 3 * H, acc);
+            pf.mark(PH_BARRIER);
+            if (active) load_epi<CTW>(ev, VB + 2 * H, VB + 3 * H, tile0);
+            if (active) split_epilogue<P, H, CTW, RTW, true>(XP, plane, xsb, tile0, rt0, ev, acc);
+            pf.mark(PH_EPI);
             __syncthreads();
+            pf.mark(PH_BARRIER);
             if (active) sgemm<P, CTW, RTW, RD, true>(XP, plane, xsb, W, w1, SL.kst_h, tile0, rt0, R, hr);  // h += Lin1(t)
+            pf.mark(PH_RES_GEMM);
         }
-#endif
         // X <- h + the deferred biases: the final layer's input
         __syncthreads();
-        if (active) split_epilogue<P, H, CTW, RTW, false>(XP, plane, xsb, tile0, rt0, nullptr, V, hr);
+        pf.mark(PH_BARRIER);
+        if (active) load_epi<CTW>(ev, nullptr, V, tile0);
+        if (active) split_epilogue<P, H, CTW, RTW, false>(XP, plane, xsb, tile0, rt0, ev, hr);
+        pf.mark(PH_EPI);
         __syncthreads();
+        pf.mark(PH_BARRIER);
         // tail: d_K of this wave's features j0 + m (rows m < nfw of the wave's tail tile)
-#ifndef FS_DIAG_NOFINAL
         if (j0 < j1) {
             SRing<P, 1, RD> RT;
             f32x16 t[1][2];
@@ -462,20 +501,23 @@ __global__ void __launch_bounds__(kThreads, 2) flow_split_kernel(FlowArgs a) {
             for (int m = 0; m < (kMaxN + 7) / 8; ++m)
                 if (m < j1 - j0) TL[lane * ts + j0 + m] = tile_row(t[0][0], t[0][1], m) + V[PL.v_bt + j0 + m];
         }
+        pf.mark(PH_TAIL_GEMM);
         // final layer + conditional spline, feature by feature (TL column j: written by this wave only)
         for (int j = j0; j < j1; ++j) {
             const int p = (2 * j + 1 + off) % D;
             ld += split_cond_spline<P, K, MODE != MODE_DENSITY, RD>(
                 XP, plane, xsb, W, (int)((SL.wf + (int64_t)3 * j * SL.kst_h * 256 * P) * 4), SL.kst_h,
-                V + PL.v_bf + 96 * j, CO, cs, p, TL[lane * ts + j], a, nan_any);
+                V + PL.v_bf + 96 * j, CO, cs, p, TL[lane * ts + j], a, nan_any, pf);
         }
-#endif
         if (MODE == MODE_DENSITY) {
             ld += uncond_spline<K, false>(Pl + SL.unc, CO, cs, N, D, off, a, nan_any);
             off = (off + N) % D;  // Coupling.forward rolls last (coupling.py:100-101)
+            pf.mark(PH_UNCOND);
         }
         __syncthreads();
+        pf.mark(PH_BARRIER);
     }
+    pf.flush();
 
     // ---- outputs (as flow_pass_kernel)
     LDP[wid * kRows + lane] = ld;
@@ -584,6 +626,18 @@ static hipError_t launch_split_mode(const FlowArgs &a, int N, int H, int K, hipS
 
 #ifndef FS_SPLIT_NO_HOST  // (tools/split/unit_split.hip includes the device code only)
 using namespace fs;
+
+#ifdef FS_PROF
+// this translation unit's phase counters (tools/flow_phases.py --precision)
+extern "C" int fs_prof_read_split(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
 
 bool fs_flow_split_supported(const fs_flow_dims *d, char *why, size_t n) {
     bool ok = false;

@@ -18,27 +18,29 @@ PH = ["input", "periodic_features", "init_gemm", "epilogue", "resnet_gemm", "bar
 
 
 def main():
-    lib = _lib.load(os.path.join(REPO, "flow-state_amd", "flowstate", "lib", "libflowstate_prof.so"))
-    lib.fs_prof_read.restype = ctypes.c_int
-    lib.fs_prof_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    prec = sys.argv[1] if len(sys.argv) > 1 else "f32"  # f32 | bf16x6 | bf16x3 (flow_split_kernel)
+    lib = _lib.load(os.environ.get("FS_PROF_LIB") or os.path.join(REPO, "flow-state_amd", "flowstate", "lib", "libflowstate_prof.so"))
+    read = lib.fs_prof_read if prec == "f32" else lib.fs_prof_read_split
+    read.restype = ctypes.c_int
+    read.argtypes = [ctypes.c_void_p, ctypes.c_int]
     _lib._lib = lib  # route the Python classes through the prof build for this run
     from bench import synthetic_model, synthetic_states
     N, C = 64, int(os.environ.get("FS_CHAINS", "65536"))
-    model = synthetic_model(N, torch.device("cuda"))
+    model = synthetic_model(N, torch.device("cuda")).set_precision(prec)
     init, L = synthetic_states(N, C, 0)
     x = torch.from_numpy((init - L / 2).astype("float32").reshape(C, -1)).cuda()
     buf = (ctypes.c_ulonglong * 16)()
-    out = {}
+    out = {"precision": prec}
     for name, fn in (("density", lambda: model.log_prob(x)), ("sample", lambda: model.forward(x))):
         fn()
         torch.cuda.synchronize()
-        lib.fs_prof_read(buf, 1)
+        read(buf, 1)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
         fn()
         ev1.record()
         torch.cuda.synchronize()
-        lib.fs_prof_read(buf, 1)
+        read(buf, 1)
         tot = sum(buf[i] for i in range(len(PH)))
         out[name] = {"ms": ev0.elapsed_time(ev1), "share": {PH[i]: buf[i] / tot for i in range(len(PH))}}
     print(json.dumps(out, indent=1))

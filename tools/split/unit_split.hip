@@ -48,7 +48,9 @@ __global__ void __launch_bounds__(kThreads, 1) unit_kernel(const float *X, const
         sgemm<P, CTW, RTW, RD, false>(XP, plane, xsb, W, 0, kst, tile0, rt0, R, acc);
     }
     __syncthreads();
-    if (active) split_epilogue<P, H, CTW, RTW, false>(XP, plane, xsb, tile0, rt0, nullptr, zeros, acc);
+    EpiVec<CTW> ev;
+    load_epi<CTW>(ev, nullptr, zeros, tile0);
+    if (active) split_epilogue<P, H, CTW, RTW, false>(XP, plane, xsb, tile0, rt0, ev, acc);
     __syncthreads();
     for (int c = wid; c < H; c += kWaves) {
         float s = 0.f;
