@@ -1,7 +1,7 @@
 // MI355X (gfx950) kernels for the circular rational-quadratic-spline coupling
 // flow of the NF-proposed MH hot path.
 //
-// One workgroup = 4 waves = 64 chains (rows) carried through ALL L coupling
+// One workgroup = 8 waves = 64 chains (rows) carried through ALL L coupling
 // layers of a pass without touching HBM between layers:
 //   * the chain coordinates live in LDS (CO), the roll of every coupling
 //     (coupling.py:100-101, :113-114) is an index offset, never a copy;
