@@ -78,8 +78,10 @@ __device__ __forceinline__ void b_prologue(BRing<CT, PD> &br, __amdgpu_buffer_rs
 // g % PD; the loads of group g+PD are issued right after the MFMAs of group g
 // (sched_barrier keeps hipcc from sinking them next to their use).
 // ACC = true accumulates onto the incoming acc (the residual add of a ResidualBlock
-// done by the matrix cores instead of 16 VALU adds per tile).
-template <int XS, int RT, int CT, int PD, bool ACC = false>
+// done by the matrix cores instead of 16 VALU adds per tile).  TR = true computes the
+// transposed tile, acc^T = B^T . X^T (the packed weight fragment is a valid A operand
+// as it stands): accumulator lane = chain, registers = output columns.
+template <int XS, int RT, int CT, int PD, bool ACC = false, bool TR = false>
 __device__ __forceinline__ void gemm_run(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
                                          int rt0, int ct0, BRing<CT, PD> &br, f32x16 (&acc)[RT][CT]) {
     const int lane = threadIdx.x & 63;
@@ -110,8 +112,10 @@ __device__ __forceinline__ void gemm_run(const float *__restrict__ X, __amdgpu_b
                     for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
                         for (int rt = 0; rt < RT; ++rt)
-                            acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[s][rt][j], br.rb[s][ct][j],
-                                                                              acc[rt][ct], 0, 0, 0);
+                            acc[rt][ct] = TR ? __builtin_amdgcn_mfma_f32_32x32x2f32(br.rb[s][ct][j], ra[s][rt][j],
+                                                                                   acc[rt][ct], 0, 0, 0)
+                                             : __builtin_amdgcn_mfma_f32_32x32x2f32(ra[s][rt][j], br.rb[s][ct][j],
+                                                                                   acc[rt][ct], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
                 const int gn = g + PD;
                 if (gn < kg) {
@@ -126,12 +130,29 @@ __device__ __forceinline__ void gemm_run(const float *__restrict__ X, __amdgpu_b
     }
 }
 
-template <int XS, int RT, int CT, int PD>
+template <int XS, int RT, int CT, int PD, bool ACC = false, bool TR = false>
 __device__ __forceinline__ void gemm64(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
                                        int rt0, int ct0, f32x16 (&acc)[RT][CT]) {
     BRing<CT, PD> br;
     b_prologue<CT, PD>(br, W, sec, kg, ct0);
-    gemm_run<XS, RT, CT, PD>(X, W, sec, kg, rt0, ct0, br, acc);
+    gemm_run<XS, RT, CT, PD, ACC, TR>(X, W, sec, kg, rt0, ct0, br, acc);
+}
+
+// Transposed final-layer tile of both chain halves with the column biases preset in the
+// accumulators (register i of lane half h = column 8 (i >> 2) + 4 h + (i & 3)), turned
+// lane-per-chain by 16 v_permlane32_swap: row k of the result is tile_row(t[0][0], t[1][0], k).
+template <int XS>
+__device__ __forceinline__ void final_tile(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
+                                           int tile, const float *__restrict__ b, f32x16 (&t)[2][1]) {
+    const int h = (threadIdx.x >> 5) & 1;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *(const f32x4 *)(b + 8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[0][0][4 * g + j] = t[1][0][4 * g + j] = v[j];
+    }
+    gemm64<XS, 2, 1, 4, true, true>(X, W, sec, kg, 0, tile, t);
+    lanes_to_chains(t[0][0], t[1][0]);
 }
 
 #pragma clang fp contract(off)
@@ -179,15 +200,16 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
                                              int kg, const float *__restrict__ bf, float *STG, const float *TL,
                                              int tstride, float *CO, int cs, int p, int j, const FlowArgs &a,
                                              bool &nan_any, Prof &pf, int *tail_ctr, int tail_target) {
-    const int lane = threadIdx.x & 63, r = lane & 31;
+    const int lane = threadIdx.x & 63;
     float cw[K + 1], ch[K + 1];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         f32x16 acc[2][1];
-        gemm64<XS, 2, 1, 4>(X, W, sec, kg, 0, 3 * j + t, acc);
+        final_tile<XS>(X, W, sec, kg, 3 * j + t, bf + 32 * t, acc);
         pf.mark(PH_FINAL_GEMM);
         float u[K];
-        load_logits<K>(STG, acc[0][0], acc[1][0], bf[32 * t + r], u);
+#pragma unroll
+        for (int k = 0; k < K; ++k) u[k] = tile_row(acc[0][0], acc[1][0], k);
         if (t == 0)
             knots_from_logits<K>(u, cw, kMinW, a.twoB, a.negB, a.B);
         else
@@ -218,19 +240,13 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
     {
         f32x16 acc[2][1];
         pf.mark(PH_SPLINE);
-        gemm64<XS, 2, 1, 4>(X, W, sec, kg, 0, 3 * j + 2, acc);
+        final_tile<XS>(X, W, sec, kg, 3 * j + 2, bf + 64, acc);
         pf.mark(PH_FINAL_GEMM);
-        const float bias = bf[64 + r];
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            if (16 * half < K) {
-                stage_half(STG, acc[0][0], acc[1][0], bias, half);
-                wave_lds_sync();
-                const int b0 = bin - 16 * half, b1 = bin + 1 - 16 * half;
-                if (b0 >= 0 && b0 < 16) ud0 = STG[lane * 17 + b0];
-                if (b1 >= 0 && b1 < 16 && bin + 1 < K) ud1 = STG[lane * 17 + b1];
-                wave_lds_sync();
-            }
+        for (int k = 0; k < K; ++k) {
+            const float dk = tile_row(acc[0][0], acc[1][0], k);
+            if (k == bin) ud0 = dk;
+            if (k == bin + 1) ud1 = dk;
         }
     }
     const float d0 = kMinD + softplus_t(ud0);

@@ -217,33 +217,6 @@ __device__ __forceinline__ void store_tile(char *XP, int plane, int xsb, int til
         for (int p = 0; p < P; ++p) *(uint2 *)(row + p * plane + 16 * g) = pk[g][p];
 }
 
-// Lane-per-chain view of the two chain halves of a transposed 32-row tile: after the
-// swap, lane c (chain c) holds rows 8g + j in lo[4g + j] and rows 8g + 4 + j in hi[4g + j].
-// (inline asm with both operands read-write: with the builtin, hipcc 7.2 emitted swaps
-// whose second result it then treated as the unswapped input, handing several rows the
-// same register.  The compiler's hazard recognizer does not look into inline asm, so the
-// asm carries its own wait states: 24 before the first swap for a VGPR just written by a
-// 16-pass XDL op (the accumulators come straight from the MFMA chain; without them
-// row 0 of the second chain half read the value before the last MFMA), two before the
-// others for a VALU-written operand.)
-__device__ __forceinline__ void lanes_to_chains(f32x16 &t0, f32x16 &t1) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        float a = t0[i], b = t1[i];
-        if (i == 0)
-            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-        else
-            asm volatile("v_nop\n\tv_nop\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-        t0[i] = a;
-        t1[i] = b;
-    }
-}
-
-// row m of a swapped tile pair
-__device__ __forceinline__ float tile_row(const f32x16 &lo, const f32x16 &hi, int m) {
-    return ((m >> 2) & 1) ? hi[4 * (m >> 3) + (m & 3)] : lo[4 * (m >> 3) + (m & 3)];
-}
-
 // ResNet epilogue of a wave's tiles into the activation planes: relu(a * acc + c)
 // (eval BatchNorm folded, the block's deferred biases re-associated into c, resnet.py:37-50)
 // when RELU, else acc + c (the final layer's input).  a, c: prefetched by the GEMM before.
