@@ -231,6 +231,53 @@ def cpu_baseline(N, budget_s=15.0):
                       f"16 proposals, {dt:.1f} s wall on {threads} host threads ({os.cpu_count()} visible CPUs)"}
 
 
+def acceptance_match(bmc, stepper, n_chains=2048):
+    """Checker of the cpu_baseline leg (the metric's "acceptance-rate match"): one more
+    fused step of all chains, untimed, then the oracle's restatement of the reference
+    (oracle/, test infrastructure) re-derives the first n_chains decisions from the same
+    inputs: the old state (its NLL recomputed by the oracle), the cached old energy
+    (monte_carlo.py:243), the proposals the kernel made, and each chain's PCG64 state
+    before the step.  Reports both acceptance counts and the decisions that differ."""
+    from oracle import flow as OF
+    from oracle import physics as OP
+
+    N, S = bmc.N, min(n_chains, bmc.C)
+    dims = OF.FlowDims(N=N, B=half_box(N), **A1)
+    hw = bmc.phys.half_width
+    E0 = bmc.E_old[:S].cpu().numpy()
+    state0 = bmc.state[:S].cpu().numpy()
+    pcg0 = bmc.pcg[:S].cpu().numpy().view(np.uint64).copy()
+    stepper.step(timed=False)
+    torch.cuda.synchronize()
+    cfg = stepper.config[:S].cpu().numpy().reshape(S, N, 2)
+    cen = stepper.centered[:S].cpu()
+    lq_gpu = stepper.log_q[:S].cpu().numpy().astype(np.float64)
+    acc = bmc.accept[:S].cpu().numpy().astype(bool)
+    t0 = time.perf_counter()
+    sd = {k: v.detach().cpu() for k, v in bmc.model.state_dict().items()}
+    E_new = OP.total_energy_batch(cfg, OP.make_phys(N))[0]
+    lq = OF.log_prob(sd, cen.clone(), dims).numpy().astype(np.float64)
+    x_old = torch.from_numpy((state0 - hw).astype(np.float32).reshape(S, -1))
+    nll_old = -OF.log_prob(sd, x_old, dims).numpy().astype(np.float64)
+    acc_o, _ = OP.mh_accept(E0, E_new, nll_old, -lq, pcg0)
+    acc_o = acc_o.astype(bool)
+    # both float32 evaluations against the exact value (the oracle in float64) on a subset
+    S64 = min(256, S)
+    sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+    lq64 = OF.log_prob(sd64, cen[:S64].double(), dims).numpy()
+
+    def max_rel(a, b):
+        fin = np.isfinite(b)
+        return float((np.abs(a[fin] - b[fin]) / np.abs(b[fin])).max()) if fin.any() else 0.0
+
+    return {"chains": S, "steps": 1, "gpu_accepts": int(acc.sum()), "oracle_accepts": int(acc_o.sum()),
+            "mismatched_decisions": int((acc != acc_o).sum()),
+            "max_rel_log_q_gpu_vs_oracle_f32": max_rel(lq_gpu, lq),
+            "max_rel_log_q_vs_f64": {"chains": S64, "gpu_f32": max_rel(lq_gpu[:S64], lq64),
+                                     "oracle_f32": max_rel(lq[:S64], lq64)},
+            "oracle_s": time.perf_counter() - t0}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -338,10 +385,14 @@ def main():
                           "peak_fp64_tflops": PEAK_F64_TFLOPS,
                           "frac": ENERGY_FLOP(N) * C / (t_en * 1e-3) / 1e12 / PEAK_F64_TFLOPS},
     }
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        out["acceptance_match"] = acceptance_match(bmc, stepper)
     if world == 1 and not args.no_alt_precision and args.precision == "f32":
         out["alt_precision"] = alt_precisions(bmc, stepper)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
+        # vs_baseline stays null: BASELINE.md has no published number for this metric
+        out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -76,6 +76,36 @@ __device__ T pairwise_sum_dev(Load load, int64_t n) {
     }
 }
 
+// classify_particles' per-particle test (utils.py:104-141) in the array dtype T:
+// box = halfbox*2 for both axes, centres (box/4, box/2) and (3box/4, box/2), radius
+// r0*1.1, each a Python float rounded into T (numpy 2 weak scalars)
+template <typename T>
+struct WellTest {
+    T bx, by, lcx, lcy, rcx, rcy, rad2;
+    __device__ WellTest(double half_box, double r0) {
+        const double box = half_box * 2.0, radius = r0 * 1.1;
+        bx = (T)box;
+        by = (T)box;
+        lcx = (T)(box / 4.0);
+        lcy = (T)(box / 2.0);
+        rcx = (T)(3.0 * box / 4.0);
+        rcy = (T)(box / 2.0);
+        rad2 = (T)(radius * radius);  // radius ** 2 (Python float), compared in T
+    }
+    __device__ bool in_circle(T x, T y, T cx, T cy) const {
+        T dx = x - cx, dy = y - cy;
+        dx -= bx * (T)rint(dx / bx);
+        dy -= by * (T)rint(dy / by);
+        const T dx2 = dx * dx, dy2 = dy * dy;
+        return (dx2 + dy2) <= rad2;
+    }
+    // 0 = 'A' (left), 1 = 'B' (right), 2 = 'Outside'
+    __device__ int classify(T x, T y) const {
+        if (in_circle(x, y, lcx, lcy)) return 0;
+        return in_circle(x, y, rcx, rcy) ? 1 : 2;
+    }
+};
+
 // one wave per configuration, lane loop over particles
 template <typename T>
 __global__ void __launch_bounds__(256) classify_kernel(const T *__restrict__ pos, int64_t M, int N, double half_box,
@@ -84,27 +114,14 @@ __global__ void __launch_bounds__(256) classify_kernel(const T *__restrict__ pos
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t m = (int64_t)blockIdx.x * 4 + wid;
     if (m >= M) return;
-    // utils.py:105-112: box = halfbox*2, centres, radius = r0*1.1 (Python floats)
-    const double box = half_box * 2.0, radius = r0 * 1.1;
-    const T bx = (T)box, by = (T)box;
-    const T lcx = (T)(box / 4.0), lcy = (T)(box / 2.0), rcx = (T)(3.0 * box / 4.0), rcy = (T)(box / 2.0);
-    const T rad2 = (T)(radius * radius);  // radius ** 2 (Python float), compared in T
+    const WellTest<T> w(half_box, r0);
     const T *q = pos + m * (int64_t)N * 2;
-    auto in_circle = [&](T x, T y, T cx, T cy) {
-        T dx = x - cx, dy = y - cy;
-        dx -= bx * (T)rint(dx / bx);
-        dy -= by * (T)rint(dy / by);
-        const T dx2 = dx * dx, dy2 = dy * dy;
-        return (dx2 + dy2) <= rad2;
-    };
     bool allA = true, allB = true;
     for (int i = lane; i < N; i += 64) {
-        const T x = q[2 * i], y = q[2 * i + 1];
-        const bool a = in_circle(x, y, lcx, lcy);
-        const bool b = !a && in_circle(x, y, rcx, rcy);
-        if (cls) cls[m * N + i] = a ? 0 : (b ? 1 : 2);
-        allA &= a;
-        allB &= b;
+        const int k = w.classify(q[2 * i], q[2 * i + 1]);
+        if (cls) cls[m * N + i] = (uint8_t)k;
+        allA &= k == 0;
+        allB &= k == 1;
     }
     allA = __all(allA);
     allB = __all(allB);
@@ -114,6 +131,43 @@ __global__ void __launch_bounds__(256) classify_kernel(const T *__restrict__ pos
             const T s = pairwise_sum_dev<T>([&](int64_t i) { return q[2 * i]; }, N);
             avg_x[m] = (double)(s / (T)N);
         }
+    }
+}
+
+// calculate_well_statistics' all-in-A / all-in-B counts (utils.py:73-86) for the
+// batched engine's live chain states: state f64 [C][N][2] holding each chain's
+// values, classified in that chain's reference dtype (float32 after an accepted big
+// move, monte_carlo.py:296), one wave per chain.
+__global__ void __launch_bounds__(256) well_stats_kernel(const double *__restrict__ pos,
+                                                         const uint8_t *__restrict__ is_f32, int64_t C, int N,
+                                                         double half_box, double r0,
+                                                         long long *__restrict__ counts) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t c = (int64_t)blockIdx.x * 4 + wid;
+    if (c >= C) return;
+    const double *q = pos + c * (int64_t)N * 2;
+    bool allA = true, allB = true;
+    if (is_f32 && is_f32[c]) {
+        const WellTest<float> w(half_box, r0);
+        for (int i = lane; i < N; i += 64) {
+            const int k = w.classify((float)q[2 * i], (float)q[2 * i + 1]);
+            allA &= k == 0;
+            allB &= k == 1;
+        }
+    } else {
+        const WellTest<double> w(half_box, r0);
+        for (int i = lane; i < N; i += 64) {
+            const int k = w.classify(q[2 * i], q[2 * i + 1]);
+            allA &= k == 0;
+            allB &= k == 1;
+        }
+    }
+    allA = __all(allA);
+    allB = __all(allB);
+    if (lane == 0) {
+        counts[3 * c] += allA;
+        counts[3 * c + 1] += (!allA && allB);
+        counts[3 * c + 2] += 1;
     }
 }
 
@@ -191,6 +245,14 @@ hipError_t fs_classify_wells_impl(const void *pos, int f32, int64_t M, int N, do
     else
         hipLaunchKernelGGL(classify_kernel<double>, grid, dim3(256), 0, st, (const double *)pos, M, N, half_box, r0,
                            cls, state, avg_x);
+    return hipGetLastError();
+}
+
+hipError_t fs_well_stats_impl(const double *pos, const uint8_t *is_f32, int64_t C, int N, double half_box, double r0,
+                              int64_t *counts, hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    hipLaunchKernelGGL(well_stats_kernel, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, st, pos, is_f32, C, N, half_box,
+                       r0, (long long *)counts);
     return hipGetLastError();
 }
 

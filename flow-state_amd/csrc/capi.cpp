@@ -10,8 +10,8 @@ hipError_t fs_pcg64_seed_impl(const uint64_t *seeds, int64_t C, uint64_t *state,
 hipError_t fs_pcg64_random_impl(uint64_t *state, int64_t C, double *out, hipStream_t st);
 hipError_t fs_hist2d_impl(const double *pos, int64_t C, int N, double shift, const double *edges, int nb,
                           int64_t *hist, hipStream_t st);
-hipError_t fs_well_stats_impl(const fs_phys *p, const double *pos, int64_t C, int N, int64_t *counts,
-                              hipStream_t st);
+hipError_t fs_well_stats_impl(const double *pos, const uint8_t *is_f32, int64_t C, int N, double half_box, double r0,
+                              int64_t *counts, hipStream_t st);
 
 static thread_local char g_err[512] = "";
 
@@ -239,9 +239,11 @@ int fs_hist2d(const double *pos, int64_t C, int32_t N, double shift, const doubl
     return hip_rc(fs_hist2d_impl(pos, C, N, shift, edges, nbins, hist, (hipStream_t)stream), "fs_hist2d");
 }
 
-int fs_well_stats(const fs_phys *p, const double *pos, int64_t C, int32_t N, int64_t *counts, void *stream) {
-    REQUIRE(p && pos && counts && C >= 0 && N >= 1, "fs_well_stats: invalid arguments");
-    return hip_rc(fs_well_stats_impl(p, pos, C, N, counts, (hipStream_t)stream), "fs_well_stats");
+int fs_well_stats(const double *pos, const uint8_t *state_is_f32, int64_t C, int32_t N, double half_box, double r0,
+                  int64_t *counts, void *stream) {
+    REQUIRE(pos && counts && C >= 0 && N >= 1 && half_box > 0, "fs_well_stats: invalid arguments");
+    return hip_rc(fs_well_stats_impl(pos, state_is_f32, C, N, half_box, r0, counts, (hipStream_t)stream),
+                  "fs_well_stats");
 }
 
 int fs_rqs_forward(int64_t M, int32_t K, int32_t inverse, const float *x, const float *uw, const float *uh,

@@ -636,12 +636,8 @@ __global__ void pack_vec_kernel(float *__restrict__ dst, const float *__restrict
 template <int H, int K, int MODE>
 static hipError_t launch_pass_t(const FlowArgs &a, int N, hipStream_t st) {
     auto kfn = flow_pass_kernel<H, K, MODE>;
-    static bool attr_set = false;  // per instantiation
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::atomic<unsigned long long> attr_set{0};  // per instantiation, bit d = device d
+    if (hipError_t e = fs_set_max_lds_once((const void *)kfn, attr_set); e != hipSuccess) return e;
     const int64_t blocks = (a.nrows + kRows - 1) / kRows;
     hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kThreads), lds_layout(N, H).total, st, a);
     return hipGetLastError();

@@ -575,12 +575,8 @@ __global__ void pack_split_linear_kernel(uint16_t *__restrict__ dst, const float
 template <int H, int K, int MODE, int P>
 static hipError_t launch_split_t(const FlowArgs &a, int N, hipStream_t st) {
     auto kfn = flow_split_kernel<H, K, MODE, P>;
-    static bool attr_set = false;  // per instantiation
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::atomic<unsigned long long> attr_set{0};  // per instantiation, bit d = device d
+    if (hipError_t e = fs_set_max_lds_once((const void *)kfn, attr_set); e != hipSuccess) return e;
     const int64_t blocks = (a.nrows + kRows - 1) / kRows;
     hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kThreads), split_lds(N, H, P).total, st, a);
     return hipGetLastError();

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <atomic>
 #include <stdio.h>
 #include <string.h>
 
@@ -58,3 +60,16 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
                                hipStream_t st);
 
 void fs_set_error(const char *fmt, ...);
+
+// Raise a kernel's dynamic-LDS limit to the full 160 KiB once per device: the
+// attribute belongs to the current device, and the library runs on whichever device
+// the caller made current (flowstate._lib.on_device).  `done` is one bit per device.
+inline hipError_t fs_set_max_lds_once(const void *kfn, std::atomic<unsigned long long> &done) {
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+    const unsigned long long bit = dev < 64 ? 1ull << dev : 0ull;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+    hipError_t e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    if (e == hipSuccess && bit) done.fetch_or(bit, std::memory_order_release);
+    return e;
+}

@@ -329,31 +329,6 @@ __global__ void hist2d_kernel(const double *__restrict__ pos, int64_t C, int N, 
     atomicAdd(&hist[bx * nb + by], 1ull);
 }
 
-__global__ void well_stats_kernel(fs_phys p, const double *__restrict__ pos, int64_t C, int N,
-                                  long long *__restrict__ counts) {
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    const double bx = p.Lx, by = p.Ly;
-    const double rad = p.r0 * 1.1, rad2 = rad * rad;
-    bool allA = true, allB = true;
-    for (int i = 0; i < N; ++i) {
-        const double x = pos[(c * N + i) * 2], y = pos[(c * N + i) * 2 + 1];
-        auto in = [&](double cx, double cy) {
-            double dx = x - cx, dy = y - cy;
-            dx -= bx * rint(dx / bx);
-            dy -= by * rint(dy / by);
-            return (dx * dx + dy * dy) <= rad2;
-        };
-        const bool inA = in(bx / 4, by / 2);
-        const bool inB = !inA && in(3 * bx / 4, by / 2);
-        allA &= inA;
-        allB &= inB;
-    }
-    counts[3 * c] += allA;
-    counts[3 * c + 1] += (!allA && allB);
-    counts[3 * c + 2] += 1;
-}
-
 }  // namespace fs
 
 using namespace fs;
@@ -405,13 +380,6 @@ hipError_t fs_hist2d_impl(const double *pos, int64_t C, int N, double shift, con
     return hipGetLastError();
 }
 
-hipError_t fs_well_stats_impl(const fs_phys *p, const double *pos, int64_t C, int N, int64_t *counts,
-                              hipStream_t st) {
-    if (C <= 0) return hipSuccess;
-    hipLaunchKernelGGL(well_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, *p, pos, C, N,
-                       (long long *)counts);
-    return hipGetLastError();
-}
 
 hipError_t fs_center_impl(const double *state, int64_t n, double hw, float *out, hipStream_t st) {
     if (n <= 0) return hipSuccess;

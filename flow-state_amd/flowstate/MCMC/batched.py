@@ -28,11 +28,25 @@ state and recomputes the energy on reject, as nf_big_move does on every call
 values are exactly those numbers.  The flow model is optional until the first
 big move (the reference equilibrates before set_nf_model).
 """
+import functools
+
 import numpy as np
 import torch
 
 from .. import _lib
 from .energy_calculator import make_phys, total_energy
+
+
+def _on_own_device(fn):
+    """Run a method with the engine's device current: the library launches on the
+    current device's stream (flowstate._lib.require_device)."""
+
+    @functools.wraps(fn)
+    def wrapped(self, *args, **kwargs):
+        with _lib.on_device(self.device):
+            return fn(self, *args, **kwargs)
+
+    return wrapped
 
 
 class Physics:
@@ -50,8 +64,31 @@ class Physics:
         return self.box_x / 2  # MonteCarlo.half_width (monte_carlo.py:66)
 
 
+def _splitmix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
+def default_proposal_seed(seeds, chain_offset=0):
+    """Seed of the in-kernel proposal stream when none is given.
+
+    The stream is keyed (proposal_seed, step, global chain = chain_offset + c), so two
+    engines share proposals exactly when they share this seed and chain indices.  The
+    default derives it from the chains' own PCG64 seeds: the base seed
+    seeds[0] - chain_offset (the driver's MASTER_SEED under seed = i + MASTER_SEED,
+    main_algorithm_1.py:139) mixed by splitmix64.  Ranks of one job (same base seed,
+    disjoint chain_offset) therefore draw one consistent global stream, independent of
+    the number of ranks, while jobs with different master seeds draw independent ones.
+    Engines that reuse the same seeds for the same global chains draw the same
+    proposals, as the same chains should."""
+    base = (int(np.asarray(seeds, dtype=np.uint64).reshape(-1)[0]) - int(chain_offset)) & 0xFFFFFFFFFFFFFFFF
+    return _splitmix64(base ^ 0x70726F706F736531) & 0x7FFFFFFFFFFFFFFF
+
+
 class BatchedMonteCarlo:
-    def __init__(self, model, particles, physics, seeds, device=None, proposal_seed=1234,
+    def __init__(self, model, particles, physics, seeds, device=None, proposal_seed=None,
                  correct_sign=False, state_is_f32=None, chain_offset=0, initial_max_displacement=0.5,
                  target_acceptance=0.5):
         self.model = None
@@ -59,8 +96,17 @@ class BatchedMonteCarlo:
         if device is None:
             device = next(model.parameters()).device if model is not None else "cuda"
         dev = torch.device(device)
-        _lib.require_device(torch.empty(0, device=dev))
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else dev
         self.device = dev
+        with _lib.on_device(dev):
+            _lib.require_device(torch.empty(0, device=dev))
+            self._init_state(model, particles, seeds, proposal_seed, correct_sign, state_is_f32, chain_offset,
+                             initial_max_displacement, target_acceptance)
+
+    def _init_state(self, model, particles, seeds, proposal_seed, correct_sign, state_is_f32, chain_offset,
+                    initial_max_displacement, target_acceptance):
+        dev = self.device
         p = torch.as_tensor(np.asarray(particles) if not torch.is_tensor(particles) else particles)
         if p.dim() == 2:
             p = p[None]
@@ -71,12 +117,14 @@ class BatchedMonteCarlo:
         self.state_is_f32 = torch.full((self.C,), int(bool(state_is_f32)), dtype=torch.uint8, device=dev)
         self.correct_sign = bool(correct_sign)
         self.flags = _lib.FS_MH_CORRECT_SIGN if correct_sign else 0
-        self.proposal_seed = int(proposal_seed)
         self.chain_offset = int(chain_offset)
         self.step_count = 0
-        seeds = torch.as_tensor(np.asarray(seeds, dtype=np.uint64).view(np.int64), device=dev)
-        if seeds.numel() != self.C:
+        seeds_np = np.asarray(seeds, dtype=np.uint64).reshape(-1)
+        if seeds_np.size != self.C:
             raise ValueError("one seed per chain")
+        self.proposal_seed = default_proposal_seed(seeds_np, self.chain_offset) if proposal_seed is None \
+            else int(proposal_seed)
+        seeds = torch.as_tensor(seeds_np.view(np.int64), device=dev)
         self.pcg = torch.empty((self.C, 4), dtype=torch.int64, device=dev)
         L = _lib.load()
         _lib.check(L.fs_pcg64_seed(_lib.ptr(seeds), self.C, _lib.ptr(self.pcg), _lib.stream_ptr()), "fs_pcg64_seed")
@@ -96,6 +144,7 @@ class BatchedMonteCarlo:
         if model is not None:
             self.set_model(model)
 
+    @_on_own_device
     def set_model(self, model):
         """MonteCarlo.set_nf_model (monte_carlo.py:229-233)."""
         if 2 * self.N != model.flows[0].num_input_channels:
@@ -109,6 +158,7 @@ class BatchedMonteCarlo:
         """fl32(pos - half_width) as nf_big_move feeds the flow (monte_carlo.py:251-258)."""
         return (pos - self.phys.half_width).to(torch.float32).reshape(pos.shape[0], -1).contiguous()
 
+    @_on_own_device
     def _energy_of_state(self):
         """Total energy / virial in the reference dtype of each chain's state
         (EnergyCalculator.__init__, energy_calculator.py:46)."""
@@ -134,6 +184,7 @@ class BatchedMonteCarlo:
         return self._ws
 
     # ------------------------------------------------------------------
+    @_on_own_device
     def step(self, n=1):
         """n fused NF-MH steps for all chains (stream-ordered, no host sync)."""
         self._need_model()
@@ -154,6 +205,7 @@ class BatchedMonteCarlo:
             self._moved = False
         return self.accept
 
+    @_on_own_device
     def local_moves(self, n, adjust_every=0, sample_every=0, step0=0, log_accepts=False):
         """n MonteCarlo.particle_displacement calls per chain (monte_carlo.py:146-223),
         numbered step0+1 .. step0+n like the driver's loop counter
@@ -186,6 +238,7 @@ class BatchedMonteCarlo:
         (monte_carlo.py:251-261), and recomputes the energy a reject writes back (:299-301)."""
         self._moved = True
 
+    @_on_own_device
     def adjust_displacement(self):
         """MonteCarlo.adjust_displacement (monte_carlo.py:375-403) for every chain."""
         _lib.check(_lib.load().fs_adjust_displacement(self.C, _lib.ptr(self.max_disp), _lib.ptr(self.attempts),
@@ -197,19 +250,28 @@ class BatchedMonteCarlo:
         if int(self.err.item()) & 1:
             raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
 
+    @_on_own_device
     def nf_big_move(self, configs):
-        """Batched nf_big_move with supplied proposals (C, N, 2) float32 box coords."""
+        """Batched nf_big_move with supplied proposals (C, N, 2) box coords.
+
+        The proposals keep their dtype, as in the reference (monte_carlo.py:245-296):
+        float32 (the drivers' proposals, main_algorithm_1.py:340-343) or float64.  The
+        energy is computed in that dtype, the flow sees fl32(config - half_width)
+        either way (:251-258), and an accepted chain's state takes the config's dtype."""
         cfg = torch.as_tensor(configs, device=self.device)
-        if cfg.dtype != torch.float32:
-            raise ValueError("proposals are float32 (main_algorithm_1.py:340-343)")
+        if cfg.dtype not in (torch.float32, torch.float64):
+            raise ValueError(f"proposals must be float32 or float64, got {cfg.dtype}")
         cfg = cfg.reshape(self.C, self.N, 2).contiguous()
+        cfg64 = None
+        if cfg.dtype == torch.float64:
+            cfg64, cfg = cfg, cfg.to(torch.float32)
         self._need_model()
         stale = self._moved
         if stale:  # old NLL of the current state (monte_carlo.py:251-261); energy for a reject (:299-301)
             self.nll_old = -(self.model.log_prob(self._centered_f32(self.state)).to(torch.float64))
             E_cur, W_cur = self._energy_of_state()
-        E_new, W_new, _ = total_energy(cfg, self.phys.c)
-        lq = self.model.log_prob(self._centered_f32(cfg.to(torch.float64)))
+        E_new, W_new, _ = total_energy(cfg if cfg64 is None else cfg64, self.phys.c)
+        lq = self.model.log_prob(self._centered_f32(cfg.to(torch.float64) if cfg64 is None else cfg64))
         L = _lib.load()
         _lib.check(L.fs_mh_accept(self.phys.c, self.C, self.N, _lib.ptr(self.E_old), _lib.ptr(self.W_old),
                                   _lib.ptr(self.nll_old), _lib.ptr(E_new), _lib.ptr(W_new), _lib.ptr(lq),
@@ -217,6 +279,10 @@ class BatchedMonteCarlo:
                                   _lib.ptr(cfg), _lib.ptr(self.accept), _lib.ptr(self.attempts),
                                   _lib.ptr(self.accepted), _lib.ptr(self.n_accept), self.flags,
                                   _lib.stream_ptr()), "fs_mh_accept")
+        if cfg64 is not None:  # the kernel stored the float32 copy: accepted chains take the float64 config
+            acc = (self.accept != 0)
+            self.state.copy_(torch.where(acc[:, None, None], cfg64, self.state))
+            self.state_is_f32.copy_(torch.where(acc, torch.zeros_like(self.state_is_f32), self.state_is_f32))
         if stale:
             rej = self.accept == 0
             self.E_old = torch.where(rej, E_cur, self.E_old)
@@ -233,6 +299,7 @@ class BatchedMonteCarlo:
         a = self.attempts.sum().item()
         return self.accepted.sum().item() / a if a else 0.0
 
+    @_on_own_device
     def histogram2d(self, bins=100):
         """Density histogram of the current states (utils.py:488-495): counts (bins-1, bins-1)."""
         B = self.phys.half_width
@@ -242,10 +309,15 @@ class BatchedMonteCarlo:
                                          _lib.ptr(hist), _lib.stream_ptr()), "fs_hist2d")
         return hist.reshape(bins - 1, bins - 1)
 
-    def well_counts(self, counts=None):
-        """(C, 3) int64: all-in-A, all-in-B, samples (utils.py:61-141) accumulated into counts."""
+    @_on_own_device
+    def well_counts(self, counts=None, half_box=None, r0=None):
+        """(C, 3) int64: all-in-A, all-in-B, samples (utils.py:61-141) accumulated into counts.
+        half_box is the driver's HALF_BOX (default box_x / 2), r0 the well radius parameter
+        (default the physics' r0); each chain is classified in its state's dtype."""
         if counts is None:
             counts = torch.zeros((self.C, 3), dtype=torch.int64, device=self.device)
-        _lib.check(_lib.load().fs_well_stats(self.phys.c, _lib.ptr(self.state), self.C, self.N, _lib.ptr(counts),
+        _lib.check(_lib.load().fs_well_stats(_lib.ptr(self.state), _lib.ptr(self.state_is_f32), self.C, self.N,
+                                             float(half_box if half_box is not None else self.phys.half_width),
+                                             float(self.phys.r0 if r0 is None else r0), _lib.ptr(counts),
                                              _lib.stream_ptr()), "fs_well_stats")
         return counts

@@ -24,7 +24,13 @@ def make_phys(box_x, box_y, num_wells=2, V0_list=(-10.0, -10.5), r0=1.2, k=15.0,
 
 def total_energy(pos, phys, with_neighbours=False):
     """pos: device tensor (C, N, 2) float32/float64 box coordinates.
-    Returns E (C,) f64, W (C,) f64, overlap (C,) u8[, nbr (C, N) u64 bitmasks]."""
+    Returns E (C,) f64, W (C,) f64, overlap (C,) u8[, nbr (C, N) u64 bitmasks].
+    Runs on pos's device."""
+    with _lib.on_device(pos):
+        return _total_energy_here(pos, phys, with_neighbours)
+
+
+def _total_energy_here(pos, phys, with_neighbours):
     _lib.require_device(pos)
     if pos.dim() != 3 or pos.shape[2] != 2 or pos.dtype not in (torch.float32, torch.float64):
         raise ValueError("pos must be (C, N, 2) float32/float64")

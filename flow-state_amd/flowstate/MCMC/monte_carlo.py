@@ -91,8 +91,11 @@ class MonteCarlo:
         """monte_carlo.py:235-303: returns True if the NF proposal was accepted."""
         if self.nf_model is None:
             raise RuntimeError("set_nf_model() first")
-        cfg = np.asarray(config, dtype=np.float32).reshape(1, self.num_particles, 2)
-        acc = self._b.nf_big_move(torch.from_numpy(cfg))
+        cfg = np.asarray(config)
+        if cfg.dtype not in (np.float32, np.float64):
+            cfg = cfg.astype(np.float64)  # numpy promotes ints / Python floats to float64
+        cfg = np.ascontiguousarray(cfg).reshape(1, self.num_particles, 2)
+        acc = self._b.nf_big_move(torch.from_numpy(cfg))  # energy and accepted state in the config's dtype
         return bool(acc[0].item())
 
     def sample(self, cycle_number):

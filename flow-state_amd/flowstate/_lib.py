@@ -3,6 +3,7 @@
 This is the product's only route to compute: there is no CPU fallback.  If the
 HIP library is missing (not built) or no HIP device is present, calls raise.
 """
+import contextlib
 import ctypes
 import os
 
@@ -69,7 +70,7 @@ _SIGS = {
                                     _P, _P]),
     "fs_rdf_mean": (ctypes.c_int, [_P, _I64, ctypes.c_int32, _P, _P, _P]),
     "fs_hist2d": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_double, _P, ctypes.c_int32, _P, _P]),
-    "fs_well_stats": (ctypes.c_int, [_PH, _P, _I64, ctypes.c_int32, _P, _P]),
+    "fs_well_stats": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double, _P, _P]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -101,11 +102,33 @@ def check(rc, what=""):
 
 
 def require_device(*tensors):
+    """Every tensor is on the CURRENT HIP device.  The library launches on the stream
+    passed in (stream_ptr(): the current device's current stream) and never switches
+    devices itself, so a tensor on another device would be a cross-device access and
+    unordered against torch's work on that device.  Public entry points enter the
+    device of their tensors first (on_device), so this only fires on a mixed call."""
     if not torch.cuda.is_available():
         raise FlowStateError("flowstate needs a HIP device (MI355X); none is visible")
+    cur = None
     for t in tensors:
-        if t is not None and not t.is_cuda:
+        if t is None:
+            continue
+        if not t.is_cuda:
             raise FlowStateError("flowstate kernels take device tensors; got a CPU tensor")
+        if cur is None:
+            cur = torch.cuda.current_device()
+        if t.device.index != cur:
+            raise FlowStateError(
+                f"tensor on {t.device} but the current HIP device is cuda:{cur}: flowstate launches on the "
+                "current device's stream; use `with torch.cuda.device(...)` or torch.cuda.set_device()")
+
+
+def on_device(where):
+    """Context entering the HIP device of a tensor / torch.device (no-op for CPU or None)."""
+    dev = where.device if torch.is_tensor(where) else (torch.device(where) if where is not None else None)
+    if dev is None or dev.type != "cuda" or dev.index is None:
+        return contextlib.nullcontext()
+    return torch.cuda.device(dev)
 
 
 def ptr(t):

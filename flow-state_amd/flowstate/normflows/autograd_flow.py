@@ -119,9 +119,11 @@ class _CircularRQS(torch.autograd.Function):
         lad = torch.empty_like(x)
         flag = torch.zeros(1, dtype=torch.int32, device=x.device)
         L = _lib.load()
-        _lib.check(L.fs_rqs_forward(M, K, int(inverse), _lib.ptr(x), _lib.ptr(uw), _lib.ptr(uh), _lib.ptr(ud),
-                                    float(B), _lib.ptr(out), _lib.ptr(lad), _lib.ptr(flag), _lib.stream_ptr()),
-                   "fs_rqs_forward")
+        with _lib.on_device(x):
+            _lib.require_device(x, uw, uh, ud)
+            _lib.check(L.fs_rqs_forward(M, K, int(inverse), _lib.ptr(x), _lib.ptr(uw), _lib.ptr(uh), _lib.ptr(ud),
+                                        float(B), _lib.ptr(out), _lib.ptr(lad), _lib.ptr(flag), _lib.stream_ptr()),
+                       "fs_rqs_forward")
         _nan_flags.append(flag[0] != 0)
         ctx.save_for_backward(x, uw, uh, ud)
         ctx.B, ctx.inverse = float(B), int(inverse)
@@ -140,9 +142,11 @@ class _CircularRQS(torch.autograd.Function):
         guh = torch.empty_like(uh)
         gud = torch.empty_like(ud)
         L = _lib.load()
-        _lib.check(L.fs_rqs_backward(M, K, ctx.inverse, _lib.ptr(x), _lib.ptr(uw), _lib.ptr(uh), _lib.ptr(ud),
-                                     ctx.B, _lib.ptr(go), _lib.ptr(gl), _lib.ptr(gx), _lib.ptr(guw),
-                                     _lib.ptr(guh), _lib.ptr(gud), _lib.stream_ptr()), "fs_rqs_backward")
+        with _lib.on_device(x):
+            _lib.require_device(x, go, gl)
+            _lib.check(L.fs_rqs_backward(M, K, ctx.inverse, _lib.ptr(x), _lib.ptr(uw), _lib.ptr(uh), _lib.ptr(ud),
+                                         ctx.B, _lib.ptr(go), _lib.ptr(gl), _lib.ptr(gx), _lib.ptr(guw),
+                                         _lib.ptr(guh), _lib.ptr(gud), _lib.stream_ptr()), "fs_rqs_backward")
         return gx, guw, guh, gud, None, None
 
 

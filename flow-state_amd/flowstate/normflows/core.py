@@ -40,7 +40,11 @@ class _PackCache:
         if key == self.key:
             return self.packed
         dev = tensors[0].device
-        _lib.require_device(tensors[0])
+        with _lib.on_device(dev):
+            return self._pack(tensors, dims, key, dev)
+
+    def _pack(self, tensors, dims, key, dev):
+        _lib.require_device(*tensors)
         L = _lib.load()
         nraw = L.fs_flow_raw_floats(dims)
         nbytes = L.fs_flow_packed_bytes(dims)
@@ -83,7 +87,13 @@ def _raise_on_nan(err):
 
 def _run_stack(layers, x, direction, cache=None, base_log_prob=None):
     """Run the coupling stack in one launch.  direction: 'forward' (sampling,
-    layers 0..L-1) or 'inverse' (density, layers L-1..0).  Returns (out, log_det)."""
+    layers 0..L-1) or 'inverse' (density, layers L-1..0).  Returns (out, log_det).
+    Runs on x's device (its current stream); the parameters must live there too."""
+    with _lib.on_device(x):
+        return _run_stack_here(layers, x, direction, cache, base_log_prob)
+
+
+def _run_stack_here(layers, x, direction, cache, base_log_prob):
     _check_stack(layers)
     cache = cache or getattr(layers[0], "_fs_cache", None)
     if cache is None:
@@ -92,6 +102,7 @@ def _run_stack(layers, x, direction, cache=None, base_log_prob=None):
     D = layers[0].num_input_channels
     x = _prepare_input(x, D)
     packed = cache.get(layers)
+    _lib.require_device(packed)
     dims = layers[0].dims(L=len(layers))
     B = x.shape[0]
     out = torch.empty_like(x)

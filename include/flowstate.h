@@ -241,11 +241,16 @@ int64_t fs_local_samples_per_chain(int64_t step0, int64_t n_moves, int32_t sampl
 int fs_hist2d(const double *pos, int64_t C, int32_t N, double shift, const double *edges,
               int32_t nbins, int64_t *hist, void *stream);
 
-/* classify_particles / calculate_well_statistics (utils.py:61-141): for each
- * chain, all particles within 1.1*r0 of the left well (A) or all within the
- * right well (B); counts[c][0] += all_A, counts[c][1] += all_B, counts[c][2] += 1. */
-int fs_well_stats(const fs_phys *p, const double *pos, int64_t C, int32_t N, int64_t *counts,
-                  void *stream);
+/* classify_particles / calculate_well_statistics (utils.py:61-141) over the
+ * batched engine's live states: for each chain, all particles within 1.1*r0 of
+ * the left well (A) or all within the right well (B), wells at (box/4, box/2)
+ * and (3box/4, box/2) with box = 2*half_box on both axes (utils.py:105-110).
+ * pos [C][N][2] float64 holds each chain's values; a chain with
+ * state_is_f32[c] != 0 is classified in float32 arithmetic (its reference
+ * dtype), others in float64; state_is_f32 may be NULL (all float64).
+ * counts[c][0] += all_A, counts[c][1] += all_B, counts[c][2] += 1. */
+int fs_well_stats(const double *pos, const uint8_t *state_is_f32, int64_t C, int32_t N, double half_box,
+                  double r0, int64_t *counts, void *stream);
 
 /* classify_particles (utils.py:104-141) + the per-configuration part of
  * calculate_well_statistics (utils.py:61-101) for M configurations

@@ -132,3 +132,42 @@ def test_batched_step_seed_sharding_independent_of_batch():
     np.testing.assert_array_equal(full.state[:128].cpu().numpy(), lo.state.cpu().numpy())
     np.testing.assert_array_equal(full.state[128:].cpu().numpy(), hi.state.cpu().numpy())
     assert full.accepted.sum().item() > 0
+
+
+def test_nf_big_move_float64_proposals():
+    """nf_big_move keeps the proposal's dtype (monte_carlo.py:245-296): a float64 config
+    is scored in float64 (energy), the flow still sees fl32(config - half_width)
+    (:251-258), and an accepted chain's state becomes that float64 config."""
+    N, C = 16, 256
+    dims_kw = dict(L=2, H=32, nb=1, K=8)
+    dims = OF.FlowDims(N=N, B=half_box(N), **dims_kw)
+    sd = OF.random_state_dict(dims, seed=4)
+    model = flow_from_state_dict(sd, N, bound=dims.B, **dims_kw)
+    L = float(np.sqrt(N / 0.03))
+    rng = np.random.default_rng(9)
+    init = np.mod(OP.fcc_lattice(N)[None] + rng.normal(0, 0.05, (C, N, 2)), L)
+    seeds = np.arange(42, 42 + C, dtype=np.uint64)
+    bmc = BatchedMonteCarlo(model, init, Physics(L, L), seeds)
+    # proposals: jittered lattices (some overlap-free, so both branches are taken)
+    cfg = np.mod(OP.fcc_lattice(N)[None] + rng.normal(0, 0.3, (C, N, 2)), L)
+    E_o = OP.total_energy_batch(init, OP.make_phys(N))[0]
+    E_new = OP.total_energy_batch(cfg, OP.make_phys(N))[0]
+    x_old = torch.from_numpy((init - L / 2).astype(np.float32).reshape(C, -1))
+    x_new = torch.from_numpy((cfg - L / 2).astype(np.float32).reshape(C, -1))
+    nll_o = -OF.log_prob(sd, x_old, dims).numpy().astype(np.float64)
+    nll_n = -OF.log_prob(sd, x_new, dims).numpy().astype(np.float64)
+    acc_o, _ = OP.mh_accept(E_o, E_new, nll_o, nll_n, OP.pcg64_seed_many(seeds))
+    acc = bmc.nf_big_move(torch.from_numpy(cfg)).cpu().numpy()
+    np.testing.assert_array_equal(acc, acc_o)
+    a = acc.astype(bool)
+    assert 0 < a.sum() < C
+    np.testing.assert_array_equal(bmc.state.cpu().numpy()[a], cfg[a])  # float64 values, not rounded to f32
+    assert not bmc.state_is_f32.cpu().numpy()[a].any()
+    np.testing.assert_allclose(bmc.E_old.cpu().numpy(), np.where(a, E_new, E_o), rtol=1e-12)
+    # the per-chain drop-in returns the state in the config's dtype
+    mc = MonteCarlo(particles=init[0], sim_box=SimulationBox(L, L), temperature=1.0, num_particles=N,
+                    num_wells=2, V0_list=[-10.0, -10.5], r0=1.2, k=15, seed=42)
+    mc.set_nf_model(model)
+    ok = mc.nf_big_move(cfg[0])
+    assert ok == bool(acc_o[0])
+    assert mc.particles.dtype == np.float64

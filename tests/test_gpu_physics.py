@@ -147,8 +147,42 @@ def test_hist2d_and_well_stats():
     _lib.check(_lib.load().fs_hist2d(_lib.ptr(tpos), C, N, B, _lib.ptr(tedges), 99,
                                      _lib.ptr(hist), _lib.stream_ptr()))
     np.testing.assert_array_equal(hist.cpu().numpy().reshape(99, 99), want.astype(np.int64))
-    ph = Physics(L, L)
     counts = torch.zeros((C, 3), dtype=torch.int64, device="cuda")
-    _lib.check(_lib.load().fs_well_stats(ph.c, _lib.ptr(tpos), C, N, _lib.ptr(counts), _lib.stream_ptr()))
+    _lib.check(_lib.load().fs_well_stats(_lib.ptr(tpos), None, C, N, B, 1.2, _lib.ptr(counts), _lib.stream_ptr()))
     c = counts.cpu().numpy()
     assert c[0].tolist() == [1, 0, 1] and c[1].tolist() == [0, 1, 1] and c[2:, :2].sum() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("half_box_scale", [1.0, 0.8])
+def test_well_stats_matches_classify_particles(half_box_scale):
+    """fs_well_stats = calculate_well_statistics' all-in-A / all-in-B (utils.py:61-141)
+    with box = 2*half_box on both axes and each chain in its own dtype: checked against
+    the oracle's classify (pinned to the reference in test_oracle_analysis.py), also for
+    a half_box that is not box_x / 2 (the driver passes HALF_BOX explicitly)."""
+    from oracle import analysis as OA
+    N, C = 16, 512
+    L = float(np.sqrt(N / 0.03))
+    hb = L / 2 * half_box_scale
+    rng = np.random.default_rng(7)
+    box = 2 * hb
+    # most chains packed near one well, a spread around the radius
+    centre = np.where(rng.random(C)[:, None] < 0.5, box / 4, 3 * box / 4)
+    pos = np.empty((C, N, 2))
+    pos[..., 0] = centre + rng.normal(0, 0.6, (C, N))
+    pos[..., 1] = box / 2 + rng.normal(0, 0.6, (C, N))
+    is_f32 = (rng.random(C) < 0.5).astype(np.uint8)
+    pos[is_f32 == 1] = pos[is_f32 == 1].astype(np.float32)
+    counts = torch.zeros((C, 3), dtype=torch.int64, device="cuda")
+    tpos, tf32 = torch.from_numpy(pos).cuda(), torch.from_numpy(is_f32).cuda()  # alive across the launch
+    _lib.check(_lib.load().fs_well_stats(_lib.ptr(tpos), _lib.ptr(tf32), C, N, hb, 1.2,
+                                         _lib.ptr(counts), _lib.stream_ptr()))
+    got = counts.cpu().numpy()
+    want = np.zeros((C, 3), np.int64)
+    for dt, sel in ((np.float32, is_f32 == 1), (np.float64, is_f32 == 0)):
+        _, st, _ = OA.classify(pos[sel].astype(dt), hb, 1.2)
+        want[sel, 0] = st == 1
+        want[sel, 1] = st == 2
+    want[:, 2] = 1
+    np.testing.assert_array_equal(got, want)
+    assert 0 < want[:, 0].sum() < C and 0 < want[:, 1].sum() < C

@@ -104,3 +104,44 @@ def test_abi_rejects_invalid_arguments_before_touching_the_device():
     rc = L.fs_nf_mh_step(_lib.FlowDims(N=16, L=2, H=64, nb=1, K=8, precision=0, tail_bound=5.0), one, ph, 4, 0, 0, 0,
                          None, None, None, None, None, None, None, None, None, None, None, 0, one, None)
     assert rc == -1
+
+
+class _FakeDeviceTensor:
+    """Stands in for a tensor on cuda:1 (this container has no GPU)."""
+
+    is_cuda = True
+    device = torch.device("cuda", 1)
+
+
+def test_require_device_rejects_tensor_on_non_current_device(monkeypatch):
+    """The library launches on the current device's stream and never switches device,
+    so a tensor on another device must raise, not launch (flowstate._lib.require_device)."""
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 0)
+    with pytest.raises(_lib.FlowStateError, match="current HIP device is cuda:0"):
+        _lib.require_device(_FakeDeviceTensor())
+    with pytest.raises(_lib.FlowStateError, match="CPU tensor"):
+        _lib.require_device(torch.zeros(1))
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 1)
+    _lib.require_device(_FakeDeviceTensor(), None)  # on the current device: accepted
+
+
+def test_on_device_context():
+    import contextlib
+    assert isinstance(_lib.on_device(torch.zeros(1)), contextlib.nullcontext)
+    assert isinstance(_lib.on_device(None), contextlib.nullcontext)
+    assert isinstance(_lib.on_device("cuda"), contextlib.nullcontext)  # no index: stay on the current device
+    assert isinstance(_lib.on_device(torch.device("cuda", 1)), torch.cuda.device)
+
+
+def test_default_proposal_seed_contract():
+    """Ranks of one job share one global proposal stream (same base seed, disjoint
+    chain_offset); jobs with different master seeds get different streams."""
+    from flowstate.MCMC.batched import default_proposal_seed
+    C = 256
+    s0 = default_proposal_seed(np.arange(42, 42 + C, dtype=np.uint64), 0)
+    s1 = default_proposal_seed(np.arange(42 + C, 42 + 2 * C, dtype=np.uint64), C)
+    assert s0 == s1
+    other = default_proposal_seed(np.arange(1042, 1042 + C, dtype=np.uint64), 0)
+    assert other != s0
+    assert 0 <= s0 < 2 ** 63 and 0 <= other < 2 ** 63
