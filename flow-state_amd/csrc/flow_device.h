@@ -17,6 +17,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr float kMinW = 1e-3f;  // splines.py:6-8
 constexpr float kMinH = 1e-3f;
 constexpr float kMinD = 1e-3f;
+constexpr double kMinWd = 1e-3;  // the same minima, exact (knots_from_logits)
+constexpr double kMinHd = 1e-3;
 
 enum { MODE_DENSITY = 0, MODE_SAMPLE = 1, MODE_PROPOSE = 2 };
 
@@ -35,6 +37,7 @@ struct FlowArgs {
     int N, L, nb, K;
     int add_base;
     float B, twoB, negB;  // fl32(tail_bound), fl32(2*tail_bound), -fl32(tail_bound)
+    double Bd, twoBd;     // tail_bound, 2*tail_bound (the knots' double-precision affine)
     float scale_pf;       // fl32(pi / tail_bound)          (wrapper.py:151-154, nn.py:125-126)
     float sqrtH;          // fl32(sqrt(H))                 (coupling.py:340-342)
     float base_lp;        // fl32(-D * log(fl32(2B)))      (Uniform.py:70)
@@ -126,32 +129,38 @@ __device__ __forceinline__ float softplus_t(float x) {  // F.softplus(beta=1, th
     return x > 20.f ? x : log1pf(expf(x));
 }
 
-// softmax -> min-width affine -> cumsum (double accumulation, torch CPU) ->
-// scale to [-B, B] with pinned ends (splines.py:117-127 / :131-143).  K is a
-// compile-time constant so every array below stays in registers.
+// softmax -> min-width affine -> cumsum -> scale to [-B, B] with pinned ends
+// (splines.py:117-127 / :131-143).  The reference rounds each op to float32 (its
+// cumsum accumulates in double, torch CPU); here the normalisation, the affines and
+// the cumsum run in double from the float32 exponentials, and each knot is rounded to
+// float32 once.  A float32 1/sum is a scale error shared by every width, which the
+// cumsum carries up to 2B (~1 ulp of B at the top knot) - the largest error term of
+// the float32 spline; in double the knots are within ~0.5 ulp of the exact ones, so
+// the pass is closer to the exact function than the reference's own float32
+// (tools/acc_layers.py, tools/acc_uncond.py).  K is a compile-time constant so every
+// array below stays in registers.
 template <int K>
-__device__ __forceinline__ void knots_from_logits(const float (&u)[K], float (&kn)[K + 1], float minb,
-                                                  float twoB, float negB, float B) {
+__device__ __forceinline__ void knots_from_logits(const float (&u)[K], float (&kn)[K + 1], double minb,
+                                                  const FlowArgs &a) {
     float m = u[0];
 #pragma unroll
     for (int k = 1; k < K; ++k) m = fmaxf(m, u[k]);
     float e[K];
-    float s = 0.f;
+    double s = 0.0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {  // logits carry log2(e) (folded at pack time): one v_exp_f32 each
         e[k] = __builtin_amdgcn_exp2f(u[k] - m);
-        s += e[k];
+        s += (double)e[k];
     }
-    const float c1 = (float)(1.0 - 1e-3 * (double)K);
-    const float c1inv = c1 / s;
+    const double sc = (1.0 - minb * (double)K) / s;
     double cs = 0.0;
-    kn[0] = negB;
+    kn[0] = a.negB;
 #pragma unroll
-    for (int k = 0; k < K - 1; ++k) {  // fused affines: a rounding or two from torch's op-by-op, << 1e-5
-        cs += (double)__builtin_fmaf(e[k], c1inv, minb);
-        kn[k + 1] = __builtin_fmaf(twoB, (float)cs, negB);
+    for (int k = 0; k < K - 1; ++k) {
+        cs += __builtin_fma((double)e[k], sc, minb);
+        kn[k + 1] = (float)__builtin_fma(a.twoBd, cs, -a.Bd);
     }
-    kn[K] = B;
+    kn[K] = a.B;
 }
 
 // rational_quadratic_spline forward (splines.py:202-222) / inverse (:162-201)

@@ -211,9 +211,9 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
 #pragma unroll
         for (int k = 0; k < K; ++k) u[k] = tile_row(acc[0][0], acc[1][0], k);
         if (t == 0)
-            knots_from_logits<K>(u, cw, kMinW, a.twoB, a.negB, a.B);
+            knots_from_logits<K>(u, cw, kMinWd, a);
         else
-            knots_from_logits<K>(u, ch, kMinH, a.twoB, a.negB, a.B);
+            knots_from_logits<K>(u, ch, kMinHd, a);
         pf.mark(PH_SPLINE);
     }
     const float x = CO[lane * cs + p];
@@ -598,33 +598,33 @@ __global__ void pack_vec_kernel(float *__restrict__ dst, const float *__restrict
     }
     for (int i = tid; i < PL.ntt * 32; i += nthr) V[PL.v_bt + i] = (i < N) ? src[R.bf + (int64_t)i * P + 3 * K] : 0.f;
     // unconditional knots (PiecewiseRationalQuadraticCDF, coupling.py:227-259): batch independent
-    const float B = (float)tail_bound, twoB = (float)(2.0 * tail_bound), negB = (float)(-tail_bound);
+    const float B = (float)tail_bound, negB = (float)(-tail_bound);
     const int K1 = K + 1;
     for (int f = tid; f < N; f += nthr) {
         float *T = dst + PL.unc + (int64_t)f * 3 * K1;
+        // batch independent, so computed in double and rounded once (the conditional
+        // knots' rationale, knots_from_logits in flow_device.h)
         for (int which = 0; which < 2; ++which) {
             const float *u = src + (which == 0 ? R.uw : R.uh) + (int64_t)f * K;
-            float m = u[0];
-            for (int k = 1; k < K; ++k) m = fmaxf(m, u[k]);
-            float s = 0.f;
-            for (int k = 0; k < K; ++k) s += expf(u[k] - m);
-            const float inv = 1.f / s;
-            const float c1 = (float)(1.0 - 1e-3 * (double)K);
+            double m = u[0];
+            for (int k = 1; k < K; ++k) m = fmax(m, (double)u[k]);
+            double s = 0.0;
+            for (int k = 0; k < K; ++k) s += exp((double)u[k] - m);
+            const double mn = which == 0 ? kMinWd : kMinHd;
+            const double sc = (1.0 - mn * (double)K) / s;
             double cum = 0.0;
             float *kn = T + which * K1;
             kn[0] = negB;
-            for (int k = 0; k < K; ++k) {
-                const float p = expf(u[k] - m) * inv;
-                const float w = (which == 0 ? kMinW : kMinH) + c1 * p;
-                cum += (double)w;
-                kn[k + 1] = twoB * (float)cum + negB;
+            for (int k = 0; k < K - 1; ++k) {
+                cum += mn + sc * exp((double)u[k] - m);
+                kn[k + 1] = (float)(2.0 * tail_bound * cum - tail_bound);
             }
             kn[K] = B;
         }
         const float *ud = src + R.ud + (int64_t)f * K1;
-        for (int k = 0; k < K1; ++k) {
-            const float x = ud[k];
-            T[2 * K1 + k] = kMinD + (x > 20.f ? x : log1pf(expf(x)));
+        for (int k = 0; k < K1; ++k) {  // min_derivative + softplus (threshold 20), rounded once
+            const double x = ud[k];
+            T[2 * K1 + k] = (float)(1e-3 + (x > 20.0 ? x : log1p(exp(x))));
         }
     }
 }
@@ -758,6 +758,8 @@ static void fill_args(FlowArgs &a, const fs_flow_dims *d, const void *packed, in
     a.B = (float)tb;
     a.twoB = (float)(2.0 * tb);
     a.negB = (float)(-tb);
+    a.Bd = tb;
+    a.twoBd = 2.0 * tb;
     a.scale_pf = (float)(M_PI / tb);
     a.sqrtH = (float)sqrt((double)d->H);
     // UniformParticle.log_prob: -D * torch.log(torch.tensor(2*B)) in float32

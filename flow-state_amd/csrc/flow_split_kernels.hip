@@ -284,9 +284,9 @@ __device__ __forceinline__ float split_cond_spline(const char *XP, int plane, in
 #pragma unroll
             for (int k = 0; k < K; ++k) u[k] = tile_row(acc[0][0], acc[0][1], k);
             if (t == 0)
-                knots_from_logits<K>(u, cw, kMinW, a.twoB, a.negB, a.B);
+                knots_from_logits<K>(u, cw, kMinWd, a);
             else
-                knots_from_logits<K>(u, ch, kMinH, a.twoB, a.negB, a.B);
+                knots_from_logits<K>(u, ch, kMinHd, a);
             pf.mark(PH_SPLINE);
         }
         icw = cw[0], cw1 = cw[1], ich = ch[0], ch1 = ch[1];

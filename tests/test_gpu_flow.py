@@ -69,11 +69,12 @@ def test_a1_log_prob_matches_oracle(N):
 
 def test_a1_log_prob_on_flow_samples_within_reference_f32_envelope():
     """The bench's inputs: proposals drawn by the flow itself (sampling pass), A1, N=64.
-    There the reference's own float32 log_prob is ~1e-5 relative from the exact value
-    (float64 restatement), so "within 1e-5 of the reference" is below float32 noise; the
-    bound checked is that the HIP pass is as close to the float64 value as the
-    reference's float32 arithmetic is: its worst / median relative error at most twice
-    the reference's, and within 1e-5 of the float64 value at the median."""
+    There the reference's own float32 log_prob is up to ~2e-5 relative from the exact
+    value (float64 restatement), so "within 1e-5 of the reference" is below float32
+    noise there.  The bound checked is against the exact value: the HIP pass (spline
+    knots normalised in double, flow_device.h knots_from_logits) is within 1e-5 of it
+    everywhere, and closer to it than the reference's float32 arithmetic, at the worst
+    chain and at the median (measured: ~3x closer)."""
     N = 64
     dims = OF.FlowDims(N=N, B=half_box(N), **A1)
     sd = OF.random_state_dict(dims, seed=7)
@@ -89,9 +90,9 @@ def test_a1_log_prob_on_flow_samples_within_reference_f32_envelope():
     assert np.isfinite(exact).all()
     e_gpu = np.abs(got - exact) / np.abs(exact)
     e_ref = np.abs(ref32 - exact) / np.abs(exact)
-    assert e_gpu.max() <= 2 * e_ref.max(), (e_gpu.max(), e_ref.max())
-    assert np.median(e_gpu) <= 2 * np.median(e_ref), (np.median(e_gpu), np.median(e_ref))
-    assert np.median(e_gpu) <= 1e-5
+    assert e_gpu.max() <= 1e-5, e_gpu.max()
+    assert e_gpu.max() <= e_ref.max(), (e_gpu.max(), e_ref.max())
+    assert np.median(e_gpu) <= 0.5 * np.median(e_ref), (np.median(e_gpu), np.median(e_ref))
 
 
 def test_a1_forward_inverse_roundtrip_full_batch():
