@@ -11,10 +11,10 @@
 //     fragments (one dwordx4 per lane feeds 4 MFMAs), the residual stream h in
 //     the accumulator registers of the wave that owns its columns;
 //   * bias / eval-BatchNorm / ReLU / residual add are fused GEMM epilogues;
-//   * the final layer is computed feature by feature (3 x 32 columns: widths,
-//     heights, derivatives d_0..d_{K-1}; d_K of every feature in a separate
-//     "tail" GEMM) and fed straight into the spline through a per-wave LDS
-//     transpose: one lane = one chain for softmax / cumsum / bin search /
+//   * the final layer is computed feature by feature: widths and heights as two
+//     transposed 32-column tiles turned lane-per-chain by v_permlane32_swap, then
+//     only the two derivative logits each chain's bin needs (per-lane dot products
+//     with gathered rows); one lane = one chain for softmax / cumsum / bin search /
 //     rational-quadratic map / log-det (splines.py:16-222);
 //   * the unconditional spline (coupling.py:176-265) uses knots precomputed at
 //     pack time (they are batch independent).
@@ -157,100 +157,119 @@ __device__ __forceinline__ void final_tile(const float *__restrict__ X, __amdgpu
 
 #pragma clang fp contract(off)
 
-// Stage columns [16*half, 16*half+16) of a 32-column accumulator tile (64 rows,
-// + column bias) into the wave's [64][17] LDS buffer: lane r then reads chain
-// r's 16 values (odd stride: conflict-free lane-per-row reads).
-__device__ __forceinline__ void stage_half(float *STG, const f32x16 &t0, const f32x16 &t1, float bias, int half) {
-    const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
-    if ((r >> 4) == half) {
-        const int c = r & 15;
+// Derivative-row gathers of cond_spline: QB quads (16-byte pieces of rows bin and
+// bin + 1) per batch, two batches in flight.
+template <int QB>
+struct DRows {
+    f32x4 a[QB], b[QB];
+};
+
+template <int QB, int K>
+__device__ __forceinline__ void drows_issue(DRows<QB> &g, __amdgpu_buffer_rsrc_t W, int voff, int dsec, int q0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            STG[acc_row(0, i, h) * 17 + c] = t0[i] + bias;
-            STG[acc_row(1, i, h) * 17 + c] = t1[i] + bias;
-        }
+    for (int i = 0; i < QB; ++i) {
+        g.a[i] = ldb_frag(W, voff, dsec + (q0 + i) * (K + 1) * 16);
+        g.b[i] = ldb_frag(W, voff + 16, dsec + (q0 + i) * (K + 1) * 16);
     }
 }
 
-// widths / heights logits of one feature, already scaled by log2(e) / sqrt(H) (folded
-// into the packed final-layer columns and biases)
-template <int K>
-__device__ __forceinline__ void load_logits(float *STG, const f32x16 &t0, const f32x16 &t1, float bias,
-                                            float (&u)[K]) {
-    const int lane = threadIdx.x & 63;
+// u0 += row_bin . h, u1 += row_bin+1 . h over QB quads; even and odd k accumulate in
+// the two halves of a float2 (v_pk_fma_f32 straight on the loaded register pairs)
+template <int QB>
+__device__ __forceinline__ void drows_dot(const DRows<QB> &g, const float *xr, int q0, f32x2 &u0, f32x2 &u1) {
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        if (16 * half < K) {
-            stage_half(STG, t0, t1, bias, half);
-            wave_lds_sync();
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (16 * half + k < K) u[16 * half + k] = STG[lane * 17 + k];
-            wave_lds_sync();
-        }
+    for (int i = 0; i < QB; ++i) {
+        const f32x4 hv = *(const f32x4 *)(xr + 4 * (q0 + i));
+        u0 = __builtin_elementwise_fma(g.a[i].xy, hv.xy, u0);
+        u1 = __builtin_elementwise_fma(g.b[i].xy, hv.xy, u1);
+        u0 = __builtin_elementwise_fma(g.a[i].zw, hv.zw, u0);
+        u1 = __builtin_elementwise_fma(g.b[i].zw, hv.zw, u1);
     }
 }
 
-// Final layer + conditional spline of transform feature j for the 64 chains
-// of the wave (lane = chain): three single-tile GEMMs (widths, heights,
-// derivatives d_0..d_{K-1}; d_K from the tail block TL), each transposed
-// through LDS right away so only one 64x32 accumulator pair is live.
-template <int XS, int K, bool INV>
+// Final layer + conditional spline of transform feature j for the 64 chains of the
+// wave (lane = chain).  Widths and heights: two transposed single-tile GEMMs (all K
+// logits of each feed the softmax / cumsum).  Derivatives: the reference computes
+// all K+1 logits (coupling.py:327-342) but the spline reads only d_bin and d_bin+1
+// (splines.py:157-158), so each lane takes the dot products of its chain's hidden
+// vector (its X row) with those two rows of the final layer, gathered from the
+// [H/4][K+1][4] `wd` section.  That replaces the 32-column derivative tile and the
+// d_K tail GEMM: 9 % of the pass's MFMA work.  The bin comes from the knots of the
+// searched tile (cumwidths in the density direction, cumheights when inverting), so
+// that tile runs first and the first gathers are in flight during the other tile's GEMM.
+template <int XS, int H, int K, bool INV>
 __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec,
-                                             int kg, const float *__restrict__ bf, float *STG, const float *TL,
-                                             int tstride, float *CO, int cs, int p, int j, const FlowArgs &a,
-                                             bool &nan_any, Prof &pf, int *tail_ctr, int tail_target) {
+                                             int kg, const float *__restrict__ bf, int dsec,
+                                             const float *__restrict__ bd, float *CO, int cs, int p, int j,
+                                             const FlowArgs &a, bool &nan_any, Prof &pf) {
+    constexpr int NQ = H / 4;                   // quads of the hidden vector
+    constexpr int QB = NQ >= 8 ? 4 : NQ / 2;    // quads per gather batch
     const int lane = threadIdx.x & 63;
-    float cw[K + 1], ch[K + 1];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    const float x = CO[lane * cs + p];
+    const bool inside = (x >= a.negB) && (x <= a.B);
+    constexpr int TS = INV ? 1 : 0;  // searched tile: 0 widths, 1 heights
+    float ks[K + 1];
+    {
         f32x16 acc[2][1];
-        final_tile<XS>(X, W, sec, kg, 3 * j + t, bf + 32 * t, acc);
+        final_tile<XS>(X, W, sec, kg, 2 * j + TS, bf + 32 * TS, acc);
         pf.mark(PH_FINAL_GEMM);
         float u[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) u[k] = tile_row(acc[0][0], acc[1][0], k);
-        if (t == 0)
-            knots_from_logits<K>(u, cw, kMinWd, a);
-        else
-            knots_from_logits<K>(u, ch, kMinHd, a);
-        pf.mark(PH_SPLINE);
+        knots_from_logits<K>(u, ks, INV ? kMinHd : kMinWd, a);
     }
-    const float x = CO[lane * cs + p];
-    const bool inside = (x >= a.negB) && (x <= a.B);
     // searchsorted (splines.py:11-13): knots are non-decreasing, so the last k
-    // with x >= knot[k] is the bin; carry the gathered values along the scan
+    // with x >= knot[k] is the bin; the gathered knots ride along the scan
     // (register-resident, no dynamically indexed array)
     int bin = 0;
-    float icw = cw[0], cw1 = cw[1], ich = ch[0], ch1 = ch[1];
+    float s0 = ks[0], s1 = ks[1];
 #pragma unroll
     for (int k = 1; k < K; ++k) {
-        if (x >= (INV ? ch[k] : cw[k])) {
+        if (x >= ks[k]) {
             bin = k;
-            icw = cw[k];
-            cw1 = cw[k + 1];
-            ich = ch[k];
-            ch1 = ch[k + 1];
+            s0 = ks[k];
+            s1 = ks[k + 1];
         }
     }
-    while (__hip_atomic_load(tail_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < tail_target)
-        __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    float ud0 = 0.f, ud1 = TL[lane * tstride + j];  // d_K unless bin + 1 < K
+    // d_bin, d_bin+1 = bias + row . h  (bin + 1 <= K: row K is the circular-tail d_K)
+    const int voff = bin * 16;
+    DRows<QB> g0, g1;
+    drows_issue<QB, K>(g0, W, voff, dsec, 0);  // in flight during the other tile's GEMM
+    f32x2 ud0 = {bd[bin], 0.f}, ud1 = {bd[bin + 1], 0.f};
+    pf.mark(PH_SPLINE);
+    float o0, o1;
     {
         f32x16 acc[2][1];
-        pf.mark(PH_SPLINE);
-        final_tile<XS>(X, W, sec, kg, 3 * j + 2, bf + 64, acc);
+        final_tile<XS>(X, W, sec, kg, 2 * j + 1 - TS, bf + 32 * (1 - TS), acc);
         pf.mark(PH_FINAL_GEMM);
+        float u[K], ko[K + 1];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const float dk = tile_row(acc[0][0], acc[1][0], k);
-            if (k == bin) ud0 = dk;
-            if (k == bin + 1) ud1 = dk;
+        for (int k = 0; k < K; ++k) u[k] = tile_row(acc[0][0], acc[1][0], k);
+        knots_from_logits<K>(u, ko, INV ? kMinWd : kMinHd, a);
+        o0 = ko[0];
+        o1 = ko[1];
+#pragma unroll
+        for (int k = 1; k < K; ++k) {
+            if (k == bin) {
+                o0 = ko[k];
+                o1 = ko[k + 1];
+            }
         }
     }
-    const float d0 = kMinD + softplus_t(ud0);
-    const float d1 = kMinD + softplus_t(ud1);
+    pf.mark(PH_SPLINE);
+    const float *xr = X + lane * XS;
+#pragma unroll 1
+    for (int q0 = 0; q0 < NQ; q0 += 2 * QB) {
+        drows_issue<QB, K>(g1, W, voff, dsec, q0 + QB);
+        drows_dot<QB>(g0, xr, q0, ud0, ud1);
+        if (q0 + 2 * QB < NQ) drows_issue<QB, K>(g0, W, voff, dsec, q0 + 2 * QB);
+        drows_dot<QB>(g1, xr, q0 + QB, ud0, ud1);
+    }
+    pf.mark(PH_FINAL_GEMM);
+    const float icw = INV ? o0 : s0, cw1 = INV ? o1 : s1;
+    const float ich = INV ? s0 : o0, ch1 = INV ? s1 : o1;
+    const float d0 = kMinD + softplus_t(ud0.x + ud0.y);
+    const float d1 = kMinD + softplus_t(ud1.x + ud1.y);
     float y, l;
     bool nd;
     rqs_eval<INV>(x, icw, cw1 - icw, ich, ch1 - ich, d0, d1, y, l, nd);
@@ -278,14 +297,13 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
     const int N = a.N, D = 2 * N;
     const LdsLayout LL = lds_layout(N, H);
     const PackLayout PL = pack_layout(N, H, a.nb, a.K);
-    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar feature / offset math)
     const int h = lane >> 5, r = lane & 31;
     float *X = (float *)(smem + LL.x);
     float *CO = (float *)(smem + LL.coord);
-    float *STG = (float *)(smem + LL.stg) + wid * kRows * 17;
-    float *TL = (float *)(smem + LL.tail);
     float *LDP = (float *)(smem + LL.ld);
-    const int cs = LL.cstride, ts = LL.tstride;
+    const int cs = LL.cstride;
     const int64_t row0 = (int64_t)blockIdx.x * kRows;
     const bool row_valid = row0 + lane < a.nrows;
 
@@ -322,7 +340,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
     const bool gact = gw < NUg;
     const int gct0 = gw * CTg;
     int *gbar = (int *)(smem + LL.ld + kWaves * kRows * 4);  // one arrival counter per row group
-    int gphase = 0, tail_target = 0;
+    int gphase = 0;
     if (tid < 4) gbar[tid] = 0;
 #ifdef FS_PRIO_HI
     if (wid >= 4) __builtin_amdgcn_s_setprio(1);  // second-dispatched half wins VALU arbitration
@@ -445,31 +463,17 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
         pf.mark(PH_EPI);
         __syncthreads();
         pf.mark(PH_BARRIER);
-        // tail block (d_K of every transform feature -> TL) on waves 4-7, one
-        // 32-row half tile each; waves 0-3 start their features at once, which puts
-        // the two waves of every SIMD about half a GEMM apart for the final phase
-        // (one's spline VALU runs under the other's MFMAs).  TL readers wait on
-        // the tail counter (cond_spline).
-        tail_target += 4;
-        if (wid >= 4) {
-            for (int piece = wid - 4; piece < 2 * PL.ntt; piece += 4) {
-                const int q = piece >> 1, rt = piece & 1;
-                f32x16 t[1][1];
-                gemm64<XS, 1, 1, 4>(X, W, (int)(PL.wt * 4), PL.kg_h, rt, q, t);
-                const float bt = V[PL.v_bt + 32 * q + r];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) TL[acc_row(rt, i, h) * ts + 32 * q + r] = t[0][0][i] + bt;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-            if (lane == 0) __hip_atomic_fetch_add(gbar + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        pf.mark(PH_TAIL_GEMM);
+#ifdef FS_STAGGER
+        // waves 4-7 start the final phase FS_STAGGER x 64 x 127 cycles late (A/B experiment)
+        if (wid >= 4)
+            for (int z = 0; z < FS_STAGGER; ++z) __builtin_amdgcn_s_sleep(127);
+#endif
         // final layer + conditional spline, feature by feature
         for (int j = wid; j < N; j += kWaves) {
             const int p = (2 * j + 1 + off) % D;
-            ld += cond_spline<XS, K, MODE != MODE_DENSITY>(X, W, (int)(PL.wf * 4), PL.kg_h,
-                                                        V + PL.v_bf + 96 * j, STG, TL, ts, CO, cs, p, j, a,
-                                                        nan_any, pf, gbar + 2, tail_target);
+            ld += cond_spline<XS, H, K, MODE != MODE_DENSITY>(
+                X, W, (int)(PL.wf * 4), PL.kg_h, V + PL.v_bf + 96 * j, (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
+                V + PL.v_bd + j * (K + 1), CO, cs, p, j, a, nan_any, pf);
         }
         if (MODE == MODE_DENSITY) {
             ld += uncond_spline<K, false>(P + PL.unc, CO, cs, N, D, off, a, nan_any);
@@ -517,8 +521,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
 // ---------------------------------------------------------------------------
 // Packing kernels
 // ---------------------------------------------------------------------------
-// kind 0: plain linear W[nout][kin];  kind 1: final layer main (feature tiles);
-// kind 2: final layer tail (d_K per feature)
+// kind 0: plain linear W[nout][kin];  kind 1: final layer widths / heights (2 tiles per feature)
 __global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restrict__ src, int kin, int kg,
                                    int ntiles, int nout, int kind, int K, float wh_scale) {
     const int64_t total = (int64_t)ntiles * kg * 256;
@@ -537,15 +540,29 @@ __global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restr
         if (kind == 0) {
             const int col = 32 * tile + c;
             row = col < nout ? col : -1;
-        } else if (kind == 1) {
-            const int feat = tile / 3, t = tile % 3;
-            if (c < K) row = (int64_t)feat * P + t * K + c;
-            if (t < 2) sc = wh_scale;  // widths / heights: / sqrt(H) (coupling.py:340-342) and * log2(e) folded in
         } else {
-            const int feat = 32 * tile + c;
-            if (feat < nout) row = (int64_t)feat * P + 3 * K;
+            const int feat = tile / 2, t = tile % 2;
+            if (c < K) row = (int64_t)feat * P + t * K + c;
+            sc = wh_scale;  // / sqrt(H) (coupling.py:340-342) and * log2(e) folded in
         }
-        dst[idx] = (row >= 0 && k < kin) ? (sc == 1.f ? src[row * kin + k] : src[row * kin + k] * sc) : 0.f;
+        dst[idx] = (row >= 0 && k < kin) ? src[row * kin + k] * sc : 0.f;
+    }
+}
+
+// derivative rows d_0..d_K of every feature (final-layer rows 2K..3K, unscaled) as
+// [N][H/4][K+1][4]: cond_spline's per-lane gathers
+__global__ void pack_deriv_kernel(float *__restrict__ dst, const float *__restrict__ src, int N, int H, int K) {
+    const int K1 = K + 1, P = 3 * K + 1;
+    const int64_t total = (int64_t)N * H * K1;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int i = idx & 3;
+        const int64_t t = idx >> 2;
+        const int b = (int)(t % K1);
+        const int64_t fq = t / K1;
+        const int q = (int)(fq % (H / 4));
+        const int feat = (int)(fq / (H / 4));
+        dst[idx] = src[((int64_t)feat * P + 2 * K + b) * H + 4 * q + i];
     }
 }
 
@@ -597,6 +614,8 @@ __global__ void pack_vec_kernel(float *__restrict__ dst, const float *__restrict
                                          : src[R.bf + (int64_t)feat * P + t * K + c]) : 0.f;
     }
     for (int i = tid; i < PL.ntt * 32; i += nthr) V[PL.v_bt + i] = (i < N) ? src[R.bf + (int64_t)i * P + 3 * K] : 0.f;
+    // derivative biases d_0..d_K per feature (cond_spline's gathers)
+    for (int i = tid; i < N * (K + 1); i += nthr) V[PL.v_bd + i] = src[R.bf + (int64_t)(i / (K + 1)) * P + 2 * K + i % (K + 1)];
     // unconditional knots (PiecewiseRationalQuadraticCDF, coupling.py:227-259): batch independent
     const float B = (float)tail_bound, negB = (float)(-tail_bound);
     const int K1 = K + 1;
@@ -739,8 +758,13 @@ hipError_t fs_flow_pack_impl(const fs_flow_dims *d, const float *raw, float *pac
             lin(o, B + RawLayout::w0(H), H, PL.kg_h, H / 32, H, 0);
             lin(o + PL.block_stride / 2, B + RawLayout::w1(H), H, PL.kg_h, H / 32, H, 0);
         }
-        lin(dst + PL.wf, src + R.wf, H, PL.kg_h, 3 * N, 0, 1);
-        lin(dst + PL.wt, src + R.wf, H, PL.kg_h, PL.ntt, N, 2);
+        lin(dst + PL.wf, src + R.wf, H, PL.kg_h, 2 * N, 0, 1);
+        {
+            const int64_t tot = (int64_t)N * H * (K + 1);
+            int blocks = (int)((tot + 255) / 256);
+            if (blocks > 4096) blocks = 4096;
+            hipLaunchKernelGGL(pack_deriv_kernel, dim3(blocks), dim3(256), 0, st, dst + PL.wd, src + R.wf, N, H, K);
+        }
         hipLaunchKernelGGL(pack_vec_kernel, dim3(16), dim3(256), 0, st, dst, src, N, H, nb, K, d->tail_bound);
     }
     return hipGetLastError();

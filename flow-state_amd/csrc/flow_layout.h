@@ -54,17 +54,23 @@ FS_HD RawLayout raw_layout(int N, int H, int nb, int K) {
 // columns, k-group = 8 reduction indices; lane l (h = l>>5, c = l&31) holds
 // W[col = 32*tile + c][k = 8*g + 4*h + j] for j = 0..3 -> one 16-byte load per
 // lane feeds four v_mfma_f32_32x32x2_f32 steps (k = 8g+j and 8g+4+j).
+// The derivative rows of the final layer (d_0..d_K of every transform feature,
+// coupling.py:327-342) are NOT a GEMM operand: a chain's spline reads only d_bin and
+// d_bin+1 (splines.py:157-158), so the f32 kernel gathers those two rows per lane and
+// takes their dot products with the chain's hidden vector.  They are stored
+// [feature][quad q = k/4][row 0..K][4] (`wd`): for one quad the 64 lanes of a wave
+// read 16-byte pieces of one (K+1)*16-byte stretch, offset by their bins.
 struct PackLayout {
     int kg_in;       // k-groups of the initial layer (ceil(2N/8))
     int kg_h;        // k-groups of an H-input layer (H/8)
-    int ntt;         // tail tiles (ceil(N/32)): the last derivative d_K of every feature
+    int ntt;         // ceil(N/32) (v_bt: the split image's d_K biases)
     int64_t win;     // [H/32][kg_in][64][4]
     int64_t blocks;  // nb x { W0 [H/32][kg_h][64][4], W1 [...] }
     int64_t block_stride;
-    int64_t wf;      // final layer, per feature j: 3 tiles (widths, heights, d_0..d_{K-1})
-    int64_t wt;      // tail block: column n = d_K of feature n
-    int64_t vec;     // s_h[H]; nb x {a0,c0',a1,c1'}[H]; bf[N][3][32]; bt[ntt*32] (see pack_vec_kernel)
-    int64_t v_blocks, v_bf, v_bt;
+    int64_t wf;      // final layer, per feature j: 2 tiles (widths, heights)
+    int64_t wd;      // final layer derivative rows, per feature j: [H/4][K+1][4]
+    int64_t vec;     // s_h[H]; nb x {a0,c0',a1,c1'}[H]; bf[N][3][32]; bt[ntt*32]; bd[N][K+1] (pack_vec_kernel)
+    int64_t v_blocks, v_bf, v_bt, v_bd;
     int64_t unc;     // unconditional knots: [N][3][K+1] = cumwidths, cumheights, derivatives
     int64_t stride;
 };
@@ -79,12 +85,13 @@ FS_HD PackLayout pack_layout(int N, int H, int nb, int K) {
     p.blocks = rup(p.win + tiles_h * p.kg_in * 256, 64);
     p.block_stride = 2 * tiles_h * p.kg_h * 256;
     p.wf = rup(p.blocks + nb * p.block_stride, 64);
-    p.wt = rup(p.wf + (int64_t)N * 3 * p.kg_h * 256, 64);
-    p.vec = rup(p.wt + (int64_t)p.ntt * p.kg_h * 256, 64);
+    p.wd = rup(p.wf + (int64_t)N * 2 * p.kg_h * 256, 64);
+    p.vec = rup(p.wd + (int64_t)N * H * (K + 1), 64);
     p.v_blocks = H;
     p.v_bf = p.v_blocks + 4 * (int64_t)H * nb;
     p.v_bt = p.v_bf + (int64_t)N * 96;
-    p.unc = rup(p.vec + p.v_bt + p.ntt * 32, 64);
+    p.v_bd = p.v_bt + p.ntt * 32;
+    p.unc = rup(p.vec + p.v_bd + (int64_t)N * (K + 1), 64);
     p.stride = rup(p.unc + (int64_t)N * 3 * (K + 1), 64);
     return p;
 }
@@ -97,8 +104,8 @@ FS_HD PackLayout pack_layout(int N, int H, int nb, int K) {
 FS_HD int flow_xw(int H) { return H < 2 * kMaxN ? 2 * kMaxN : H; }
 
 struct LdsLayout {
-    int x, coord, stg, tail, ld, total;  // byte offsets
-    int xw, xs, cstride, tstride;
+    int x, coord, ld, total;  // byte offsets
+    int xw, xs, cstride;
 };
 
 FS_HD LdsLayout lds_layout(int N, int H) {
@@ -106,12 +113,9 @@ FS_HD LdsLayout lds_layout(int N, int H) {
     l.xw = flow_xw(H);
     l.xs = l.xw + 4;
     l.cstride = 2 * N + 1;                 // odd stride: lane-per-row reads are conflict-free
-    l.tstride = ((N + 31) / 32) * 32 + 1;
     l.x = 0;
     l.coord = l.x + kRows * l.xs * 4;
-    l.stg = (int)rup(l.coord + kRows * l.cstride * 4, 16);
-    l.tail = l.stg + kWaves * kRows * 17 * 4;  // per-wave [64][17] half-tile transpose buffer
-    l.ld = (int)rup(l.tail + kRows * l.tstride * 4, 16);
+    l.ld = (int)rup(l.coord + kRows * l.cstride * 4, 16);
     l.total = l.ld + kWaves * kRows * 4 + 16;
     return l;
 }
