@@ -46,6 +46,16 @@ def flops_per_pass(N, L, H, nb, K):
     return 2 * L * (2 * N * H + 2 * nb * H * H + H * N * (3 * K + 1))
 
 
+def mfma_flops_per_pass(N, L, H, nb, K):
+    """FLOP per chain per pass the f32 kernel actually issues to the matrix cores: the
+    initial layer (2N inputs padded to k-groups of 8), the ResNet GEMMs, and per transform
+    feature the widths and heights tiles (32 columns each).  The derivative logits are not
+    a GEMM: a chain's spline reads only d_bin and d_bin+1 (splines.py:157-158), which the
+    kernel takes as two per-lane dot products (VALU, 4*H FLOP per feature)."""
+    kin = (2 * N + 7) // 8 * 8
+    return 2 * L * (kin * H + 2 * nb * H * H + N * 2 * 32 * H)
+
+
 def synthetic_model(N, device):
     """Random-init A1 flow (no checkpoint exists offline): reference init order under
     torch.manual_seed(0), then final layers N(0, 0.01) and unconditional spline
@@ -108,6 +118,30 @@ def alt_precisions(bmc, stepper, steps=3):
                                   "kernel": f"flow_split_kernel<256,32,*,{3 if nprod == 6 else 2}>"}}
     model.set_precision(base)
     return out
+
+
+def given_proposal(bmc, stepper, steps=3):
+    """SURVEY §8(d) secondary: the nf_big_move equivalent, i.e. proposals supplied as
+    box-coordinate float32 configs (pre-generated as main_algorithm_1.py:340-343 does,
+    outside the timed region), then per step: their energy, log q by the density pass,
+    and the MH accept (BatchedMonteCarlo.nf_big_move).  The old NLL and energy are the
+    cached values (pure NF chains).  Reported beside the headline, never as `value`."""
+    C = bmc.C
+    batches = []
+    for _ in range(2):
+        stepper.step(timed=False)  # a fused step leaves its proposals in stepper.config
+        batches.append(stepper.config.clone().view(C, bmc.N, 2))
+    bmc.nf_big_move(batches[0])
+    torch.cuda.synchronize()
+    acc0 = int(bmc.n_accept.item())
+    t0 = time.perf_counter()
+    for i in range(steps):
+        bmc.nf_big_move(batches[i % 2])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"value": C * steps / dt, "unit": "steps/s", "steps": steps, "ms_per_step": dt / steps * 1e3,
+            "acceptance_rate": (int(bmc.n_accept.item()) - acc0) / (C * steps),
+            "what": "energy + density pass + accept of supplied float32 proposals (proposal generation excluded)"}
 
 
 class Stepper:
@@ -292,6 +326,8 @@ def main():
                     help="conditioner GEMM arithmetic of the headline run (f32 = the reference's)")
     ap.add_argument("--no-alt-precision", action="store_true",
                     help="skip the secondary measurement of the split-bf16 modes")
+    ap.add_argument("--no-given-proposal", action="store_true",
+                    help="skip the secondary nf_big_move-equivalent measurement (supplied proposals)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -349,6 +385,8 @@ def main():
     fpp = flops_per_pass(N, **A1)
     t_prop, t_lp, t_en, t_acc = (stepper.t / args.steps)  # ms per launch
     achieved = 2 * fpp * C / ((t_prop + t_lp) * 1e-3) / 1e12  # both flow passes (same kernel template)
+    mfpp = mfma_flops_per_pass(N, **A1)
+    mfma_ach = 2 * mfpp * C / ((t_prop + t_lp) * 1e-3) / 1e12
     peak = PEAK_F32_TFLOPS if args.precision == "f32" else PEAK_BF16_TFLOPS / SPLIT_PRODUCTS[args.precision]
     out = {
         "metric": "NF-proposed MH steps/sec, N=64 2D LJ, 65536 chains; acceptance-rate match",
@@ -375,7 +413,11 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": _pmc_traffic() if args.precision == "f32" else None,
                      "kernel": "flow_pass_kernel<256,32,*> (propose + log_prob)",
-                     "algorithmic_flop_per_launch": fpp * C},
+                     "algorithmic_flop_per_launch": fpp * C,
+                     # what the matrix cores actually execute (the derivative logits are
+                     # two per-lane dot products instead of a 33-column GEMM)
+                     "executed_mfma": {"flop_per_launch": mfpp * C, "achieved": mfma_ach,
+                                       "frac": mfma_ach / peak} if args.precision == "f32" else None},
         # the LJ + double-well kernel the north star asks about: HBM rate of its algorithmic
         # bytes (float32 proposal in, E / W out) and fp64 rate (~30 FLOP per
         # pair + ~40 per particle), against the fp64 vector peak that bounds it
@@ -389,6 +431,8 @@ def main():
         out["acceptance_match"] = acceptance_match(bmc, stepper)
     if world == 1 and not args.no_alt_precision and args.precision == "f32":
         out["alt_precision"] = alt_precisions(bmc, stepper)
+    if world == 1 and not args.no_given_proposal:
+        out["given_proposal"] = given_proposal(bmc, stepper)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
         # vs_baseline stays null: BASELINE.md has no published number for this metric
