@@ -22,7 +22,24 @@ from .flows import PRECISIONS
 
 
 def _tensor_key(ts):
-    return tuple((t.data_ptr(), t._version, str(t.device)) for t in ts)
+    # every in-place update bumps _version; .to() / .data = ... move data_ptr (UVA: pointers
+    # of different devices never coincide)
+    return tuple([t._version for t in ts]), tuple([t.data_ptr() for t in ts])
+
+
+# Module-structure generation: bumped whenever any module registers (or re-assigns) a
+# parameter, buffer or submodule, so the per-stack tensor list below is re-derived only
+# then (walking the A1 stack's ~5.9k tensors costs milliseconds of host time per pass).
+_STRUCT_GEN = [0]
+
+
+def _bump_struct_gen(*_args):
+    _STRUCT_GEN[0] += 1
+
+
+nn.modules.module.register_module_parameter_registration_hook(_bump_struct_gen)
+nn.modules.module.register_module_buffer_registration_hook(_bump_struct_gen)
+nn.modules.module.register_module_module_registration_hook(_bump_struct_gen)
 
 
 class _PackCache:
@@ -32,9 +49,18 @@ class _PackCache:
         self.key = None
         self.packed = None
         self.raw = None
+        self._tensors = None
+        self._struct = None
+
+    def _tensor_list(self, layers):
+        struct = (_STRUCT_GEN[0], tuple(map(id, layers)))
+        if self._tensors is None or struct != self._struct:
+            self._tensors = [t for layer in layers for t in layer.raw_param_tensors()]
+            self._struct = struct
+        return self._tensors
 
     def get(self, layers):
-        tensors = [t for layer in layers for t in layer.raw_param_tensors()]
+        tensors = self._tensor_list(layers)
         dims = layers[0].dims(L=len(layers))
         key = (_tensor_key(tensors), int(dims.precision))
         if key == self.key:

@@ -113,6 +113,58 @@ def test_fused_step_matches_oracle_a1_n16():
     assert flips <= 1, (flips, n)
 
 
+def test_fused_step_config2_full_size():
+    """BASELINE config 2 at its own size: Algorithm 1, N=16, 4096 chains, A1 flow, float32.
+    Every chain re-derived by the oracle (energies, log q, accept decisions)."""
+    flips, acc, n = _fused_vs_oracle(16, A1, C=4096, steps=1)
+    assert acc > 0
+    assert flips <= max(1, n // 2000), (flips, n)
+
+
+def test_fused_step_config3_full_batch_subset():
+    """BASELINE config 3 at its own size (N=64, 65536 chains, A1 flow): two fused steps
+    of the whole batch on the device; the oracle re-derives a spread subset of chains
+    from the kernel's own proposals (CPU cost), and the whole batch is checked for the
+    size-independent invariants (finite accepted energies, state = accepted configs,
+    counters consistent)."""
+    N, C = 64, 65536
+    dims = OF.FlowDims(N=N, B=half_box(N), **A1)
+    sd = OF.random_state_dict(dims, seed=3)
+    model = flow_from_state_dict(sd, N, bound=dims.B, **A1)
+    L = float(np.sqrt(N / 0.03))
+    rng = np.random.default_rng(9)
+    init = np.mod(OP.fcc_lattice(N)[None] + rng.normal(0, 0.05, (C, N, 2)), L)
+    bmc = BatchedMonteCarlo(model, init, Physics(L, L), np.arange(42, 42 + C, dtype=np.uint64))
+    sub = np.linspace(0, C - 1, 96).astype(np.int64)
+    tot = 0
+    for _ in range(2):
+        E0 = bmc.E_old.cpu().numpy()[sub]
+        nll0 = bmc.nll_old.cpu().numpy()[sub]
+        state0 = bmc.state.cpu().numpy()
+        pcg0 = bmc.pcg.cpu().numpy().view(np.uint64)[sub].copy()
+        bmc.step()
+        ws = bmc._ws
+        nbytes = C * 2 * N * 4
+        cfg = ws.view(torch.uint8)[:nbytes].view(torch.float32).reshape(C, N, 2).cpu().numpy()
+        cen = ws.view(torch.uint8)[(nbytes + 255) // 256 * 256:][:nbytes].view(torch.float32).reshape(C, 2 * N)
+        acc = bmc.accept.cpu().numpy().astype(bool)
+        tot += int(acc.sum())
+        # whole batch: accepted chains hold their proposal, rejected ones their old state
+        st = bmc.state.cpu().numpy()
+        np.testing.assert_array_equal(st[acc], cfg[acc].astype(np.float64))
+        np.testing.assert_array_equal(st[~acc], state0[~acc])
+        assert np.isfinite(bmc.E_old.cpu().numpy()[acc]).all()
+        # subset: the oracle's decisions from the same inputs
+        E_new = OP.total_energy_batch(cfg[sub], OP.make_phys(N))[0]
+        lq = OF.log_prob(sd, cen[sub].cpu().clone(), dims).numpy().astype(np.float64)
+        acc_o, _ = OP.mh_accept(E0, E_new, nll0, -lq, pcg0)
+        assert int((acc_o.astype(bool) != acc[sub]).sum()) <= 1
+        np.testing.assert_allclose(bmc.E_old.cpu().numpy()[sub][acc[sub]], E_new[acc[sub]], rtol=1e-12)
+    bmc.check_errors()
+    assert int(bmc.n_accept.item()) == tot
+    assert (bmc.attempts.cpu().numpy() == 2).all()
+
+
 def test_batched_step_seed_sharding_independent_of_batch():
     """Chain c's trajectory depends only on (seed_c, proposal stream row c): running the
     first half of the chains alone reproduces them exactly (the multi-GPU contract)."""

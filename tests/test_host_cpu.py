@@ -145,3 +145,27 @@ def test_default_proposal_seed_contract():
     other = default_proposal_seed(np.arange(1042, 1042 + C, dtype=np.uint64), 0)
     assert other != s0
     assert 0 <= s0 < 2 ** 63 and 0 <= other < 2 ** 63
+
+
+def test_pack_cache_tracks_versions_and_structure():
+    """The packed image's key (normflows/core.py _PackCache): in-place updates bump a
+    tensor's version, re-assigned parameters / buffers bump the module-structure
+    generation, so a cached tensor list is never stale (no device work here)."""
+    from flowstate.normflows import core as C
+
+    m = build_flow(4, 2, 32, 1, 5).eval()
+    layers = list(m.flows)
+    cache = C._PackCache()
+    t0 = cache._tensor_list(layers)
+    k0 = C._tensor_key(t0)
+    assert cache._tensor_list(layers) is t0  # no walk while nothing was re-registered
+    with torch.no_grad():
+        layers[0].prqct.transform_net.final_layer.weight.add_(1.0)
+    assert C._tensor_key(cache._tensor_list(layers)) != k0
+    fl = layers[1].prqct.transform_net.final_layer
+    fl.weight = torch.nn.Parameter(fl.weight.detach().clone())
+    t1 = cache._tensor_list(layers)
+    assert t1 is not t0 and any(t is fl.weight for t in t1)
+    bn = layers[0].prqct.transform_net.blocks[0].batch_norm_layers[0]
+    bn.running_mean = torch.zeros_like(bn.running_mean)
+    assert any(t is bn.running_mean for t in cache._tensor_list(layers))
