@@ -144,6 +144,14 @@ int fs_mh_accept(const fs_phys *p, int64_t C, int32_t N, double *E_old, double *
                   "fs_mh_accept");
 }
 
+int fs_metropolis_judge(double beta, int64_t C, int64_t M, const double *E_ref, const double *E_new, uint64_t *pcg,
+                        uint8_t *accept, int64_t *n_accept, void *stream) {
+    REQUIRE(E_ref && E_new && pcg && C >= 0 && M >= 0, "fs_metropolis_judge: invalid arguments");
+    REQUIRE(beta == beta, "fs_metropolis_judge: beta is NaN");
+    return hip_rc(fs_metropolis_judge_impl(beta, C, M, E_ref, E_new, pcg, accept, n_accept, (hipStream_t)stream),
+                  "fs_metropolis_judge");
+}
+
 int64_t fs_nf_mh_step_ws_bytes(const fs_flow_dims *d, int64_t C) {
     if (check_dims(d) != FS_OK || C < 0) return -1;
     const int64_t D = 2 * d->N;

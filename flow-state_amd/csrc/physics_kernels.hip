@@ -299,6 +299,39 @@ __global__ void __launch_bounds__(256) mh_accept_kernel(fs_phys p, int64_t C, in
     }
 }
 
+// Energy-only Metropolis of supplied proposals against a reference energy, without moving
+// the chain: judge_normalizing_flow (monte_carlo.py:305-329, reference = the chain's
+// energy) and bulk_judge_normalizing_flow (:331-370, M proposals per chain against one
+// reference energy), both through metropolis_acceptance_particle_move (:191-223):
+// E_new <= E_ref accepts and E_new = +-inf rejects without a draw, otherwise
+// Generator.random() < exp(-beta (E_new - E_ref)) (a NaN energy draws and rejects).
+// One thread per chain walks its M proposals in order (one PCG64 stream).
+__global__ void __launch_bounds__(256) metropolis_judge_kernel(double beta, int64_t C, int64_t M,
+                                                               const double *__restrict__ E_ref,
+                                                               const double *__restrict__ E_new,
+                                                               uint64_t *__restrict__ pcg, uint8_t *__restrict__ accept,
+                                                               int64_t *__restrict__ n_accept) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double eo = E_ref[c];
+    int64_t n = 0;
+    for (int64_t m = 0; m < M; ++m) {
+        const double en = E_new[c * M + m];
+        int acc;
+        if (en <= eo) {
+            acc = 1;
+        } else if (isinf(en)) {
+            acc = 0;
+        } else {
+            const double bf = exp(-beta * (en - eo));
+            acc = pcg64_next_double(pcg + 4 * c) < bf ? 1 : 0;
+        }
+        if (accept) accept[c * M + m] = (uint8_t)acc;
+        n += acc;
+    }
+    if (n_accept) n_accept[c] = n;
+}
+
 // (float32)(particles - half_width): the NF coordinates of the current state
 // (monte_carlo.py:251-257)
 __global__ void center_kernel(const double *__restrict__ state, int64_t n, double hw, float *__restrict__ out) {
@@ -356,6 +389,14 @@ hipError_t fs_mh_accept_impl(const fs_phys *p, int64_t C, int N, double *E_old, 
     hipLaunchKernelGGL(mh_accept_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, *p, C, N, E_old,
                        W_old, nll_old, E_new, W_new, log_q_new, pcg, state, state_is_f32, config, accept,
                        attempts, accepted, n_accept, flags, log_q_old, E_cur, W_cur);
+    return hipGetLastError();
+}
+
+hipError_t fs_metropolis_judge_impl(double beta, int64_t C, int64_t M, const double *E_ref, const double *E_new,
+                                   uint64_t *pcg, uint8_t *accept, int64_t *n_accept, hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    hipLaunchKernelGGL(metropolis_judge_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, beta, C, M,
+                       E_ref, E_new, pcg, accept, n_accept);
     return hipGetLastError();
 }
 

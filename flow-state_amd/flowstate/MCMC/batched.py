@@ -250,6 +250,71 @@ class BatchedMonteCarlo:
         if int(self.err.item()) & 1:
             raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
 
+    # ------------------------------------------------------------------ judging
+    @_on_own_device
+    def metropolis_judge(self, E_ref, E_new):
+        """metropolis_acceptance_particle_move (monte_carlo.py:191-223) for M energies per
+        chain against one reference energy each, judged in order on the chain's own PCG64
+        stream: E_new <= E_ref accepts and an infinite E_new rejects without a draw, else
+        Generator.random() < exp(-beta (E_new - E_ref)).  E_ref (C,), E_new (C, M) float64.
+        Returns accept (C, M) uint8; nothing else changes but the PCG64 states."""
+        E_ref = torch.as_tensor(E_ref, dtype=torch.float64, device=self.device).reshape(-1).contiguous()
+        E_new = torch.as_tensor(E_new, dtype=torch.float64, device=self.device).contiguous()
+        if E_ref.numel() != self.C or E_new.dim() != 2 or E_new.shape[0] != self.C:
+            raise ValueError(f"E_ref must be ({self.C},) and E_new ({self.C}, M)")
+        M = int(E_new.shape[1])
+        acc = torch.empty((self.C, M), dtype=torch.uint8, device=self.device)
+        _lib.check(_lib.load().fs_metropolis_judge(float(self.phys.c.beta), self.C, M, _lib.ptr(E_ref),
+                                                   _lib.ptr(E_new), _lib.ptr(self.pcg), _lib.ptr(acc), None,
+                                                   _lib.stream_ptr()), "fs_metropolis_judge")
+        return acc
+
+    def _proposal_energies(self, configs, M):
+        """Total energy / virial of C x M supplied configurations, each in its own dtype
+        (float32 or float64, as calculate_total_energy_virial computes it): (C, M) each."""
+        cfg = torch.as_tensor(configs, device=self.device)
+        if cfg.dtype not in (torch.float32, torch.float64):
+            raise ValueError(f"proposals must be float32 or float64, got {cfg.dtype}")
+        if cfg.numel() != self.C * M * self.N * 2:
+            raise ValueError(f"expected {self.C} x {M} configurations of ({self.N}, 2)")
+        E, W, _ = total_energy(cfg.reshape(self.C * M, self.N, 2).contiguous(), self.phys.c)
+        return E.reshape(self.C, M), W.reshape(self.C, M)
+
+    @_on_own_device
+    def judge_normalizing_flow(self, configs):
+        """MonteCarlo.judge_normalizing_flow (monte_carlo.py:305-329), batched: the
+        energy-only Metropolis verdict on one supplied proposal per chain (C, N, 2) against
+        the chain's current total energy (:313), without accepting it.  As the reference:
+        attempts_displacement += 1 (:309), the energy bookkeeping is restored (:327-328),
+        the state is untouched, and the PCG64 stream advances when a draw is taken.
+        Returns accept (C,) uint8."""
+        E_new, _ = self._proposal_energies(configs, 1)
+        acc = self.metropolis_judge(self.E_old, E_new)[:, 0]
+        self.attempts += 1
+        return acc
+
+    @_on_own_device
+    def bulk_judge_normalizing_flow(self, configs, ref_energy):
+        """MonteCarlo.bulk_judge_normalizing_flow (monte_carlo.py:331-370), batched: M
+        supplied proposals per chain, configs (C, M, N, 2), each judged in order against
+        ref_energy (scalar or (C,)) on the chain's PCG64 stream.  Returns (accepted (C,)
+        int64, M).  Kept from the reference: every calculate_total_energy_virial call there
+        overwrites the calculator's running totals (energy_calculator.py:121-203) and this
+        method does not restore them, so afterwards a chain's running energy / virial are
+        those of its last proposal (the next big move's ratio uses that value, :243, and a
+        reject re-derives the energy of the state, :299-301, as after local moves)."""
+        cfg = torch.as_tensor(configs, device=self.device)
+        M = int(cfg.numel() // (self.C * self.N * 2)) if cfg.numel() else 0
+        ref = torch.as_tensor(ref_energy, dtype=torch.float64, device=self.device).reshape(-1)
+        ref = ref.expand(self.C).contiguous() if ref.numel() == 1 else ref
+        if M == 0:
+            return torch.zeros(self.C, dtype=torch.int64, device=self.device), 0
+        E_new, W_new = self._proposal_energies(cfg, M)
+        acc = self.metropolis_judge(ref, E_new)
+        self.E_old, self.W_old = E_new[:, -1].contiguous(), W_new[:, -1].contiguous()
+        self._moved = True
+        return acc.sum(dim=1, dtype=torch.int64), M
+
     @_on_own_device
     def nf_big_move(self, configs):
         """Batched nf_big_move with supplied proposals (C, N, 2) box coords.

@@ -4,8 +4,9 @@ Keeps the reference constructor and the attributes/methods the Algorithm-1
 driver touches around ``nf_big_move`` (main_algorithm_1.py:168-186, 372-422).
 Each instance is a 1-chain ``BatchedMonteCarlo`` created with the chain (its
 device state exists before set_nf_model, as the reference equilibrates first).
-``particle_displacement`` / ``adjust_displacement`` / ``nf_big_move`` follow
-monte_carlo.py:146-223, 375-403 and 235-303 on the same numpy PCG64 stream as
+``particle_displacement`` / ``adjust_displacement`` / ``nf_big_move`` /
+``judge_normalizing_flow`` / ``bulk_judge_normalizing_flow`` follow
+monte_carlo.py:146-223, 375-403, 235-303 and 305-370 on the same numpy PCG64 stream as
 ``np.random.default_rng(seed)`` — bit-exact trajectories.  One call = one kernel
 launch, so drivers with many chains should use ``BatchedMonteCarlo.local_moves``.
 """
@@ -91,12 +92,62 @@ class MonteCarlo:
         """monte_carlo.py:235-303: returns True if the NF proposal was accepted."""
         if self.nf_model is None:
             raise RuntimeError("set_nf_model() first")
+        cfg = self._as_config(config).reshape(1, self.num_particles, 2)
+        acc = self._b.nf_big_move(torch.from_numpy(cfg))  # energy and accepted state in the config's dtype
+        return bool(acc[0].item())
+
+    def _log(self, message, level="info"):
+        """monte_carlo.py:129-146: the logger's method for `level`, else print."""
+        if self.logger:
+            getattr(self.logger, level if level in ("debug", "warning", "error") else "info")(message)
+        else:
+            print(message)
+
+    @staticmethod
+    def _as_config(config):
         cfg = np.asarray(config)
         if cfg.dtype not in (np.float32, np.float64):
             cfg = cfg.astype(np.float64)  # numpy promotes ints / Python floats to float64
-        cfg = np.ascontiguousarray(cfg).reshape(1, self.num_particles, 2)
-        acc = self._b.nf_big_move(torch.from_numpy(cfg))  # energy and accepted state in the config's dtype
-        return bool(acc[0].item())
+        return np.ascontiguousarray(cfg)
+
+    def metropolis_acceptance_particle_move(self, old_energy, new_energy):
+        """monte_carlo.py:191-223 on the chain's PCG64 stream (a draw only when
+        new_energy > old_energy and finite)."""
+        acc = self._b.metropolis_judge(torch.tensor([float(old_energy)], dtype=torch.float64),
+                                       torch.tensor([[float(new_energy)]], dtype=torch.float64))
+        return bool(acc[0, 0].item())
+
+    def judge_normalizing_flow(self, config):
+        """monte_carlo.py:305-329: the Metropolis verdict on `config` against the current
+        total energy, without accepting it (attempts_displacement += 1)."""
+        cfg = self._as_config(config).reshape(1, self.num_particles, 2)
+        return bool(self._b.judge_normalizing_flow(torch.from_numpy(cfg))[0].item())
+
+    def bulk_judge_normalizing_flow(self, configs, ref_energy):
+        """monte_carlo.py:331-370: (accepted_moves, attempted_moves) of `configs` judged in
+        order against ref_energy; the running total energy / virial are left at the last
+        configuration's, as the reference's calculator is (BatchedMonteCarlo
+        .bulk_judge_normalizing_flow)."""
+        cfgs = [self._as_config(c).reshape(self.num_particles, 2) for c in configs]
+        M = len(cfgs)
+        if M == 0:
+            accepted = 0
+        else:
+            b = self._b
+            E = torch.empty((1, M), dtype=torch.float64, device=b.device)
+            W = torch.empty_like(E)
+            for dt in (np.float32, np.float64):  # each configuration's energy in its own dtype
+                idx = [m for m, c in enumerate(cfgs) if c.dtype == dt]
+                if idx:
+                    e, w = b._proposal_energies(torch.from_numpy(np.stack([cfgs[m] for m in idx])[None]), len(idx))
+                    E[:, idx], W[:, idx] = e, w
+            acc = b.metropolis_judge(torch.tensor([float(ref_energy)], dtype=torch.float64), E)
+            accepted = int(acc.sum().item())
+            b.E_old, b.W_old = E[:, -1].contiguous(), W[:, -1].contiguous()
+            b._moved = True
+        self._log(f"Bulk judge normalizing flow: {accepted} accepted moves out of {M} attempted moves "
+                  f"(reference energy: {ref_energy:.3f}).", level="info")
+        return accepted, M
 
     def sample(self, cycle_number):
         """monte_carlo.py:416-444."""

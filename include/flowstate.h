@@ -161,6 +161,18 @@ int fs_mh_accept(const fs_phys *p, int64_t C, int32_t N, double *E_old, double *
                  uint8_t *accept, int64_t *attempts, int64_t *accepted,
                  unsigned long long *n_accept, int flags, void *stream);
 
+/* Energy-only Metropolis judgement of supplied proposals, no state change:
+ * MonteCarlo.judge_normalizing_flow (monte_carlo.py:305-329; M = 1, E_ref = the
+ * chain's total energy) and bulk_judge_normalizing_flow (:331-370; M proposals per
+ * chain against one reference energy), both via metropolis_acceptance_particle_move
+ * (:191-223): E_new <= E_ref accepts and an infinite E_new rejects without a draw;
+ * otherwise accept iff Generator.random() < exp(-beta*(E_new - E_ref)).  Chain c's
+ * proposals are judged in order m = 0..M-1 on its PCG64 stream pcg[c] (advanced).
+ * E_ref [C], E_new [C][M] float64; accept [C][M] u8 and n_accept [C] (accepted
+ * count per chain) out, each nullable. */
+int fs_metropolis_judge(double beta, int64_t C, int64_t M, const double *E_ref, const double *E_new,
+                        uint64_t *pcg, uint8_t *accept, int64_t *n_accept, void *stream);
+
 /* Fused batched NF-MH step over C chains: fs_flow_propose -> fs_flow_log_prob
  * (density pass on `centered`) -> fs_energy_lj_dw (config, float32) ->
  * fs_mh_accept.  chain_offset: global index of chain 0 (proposal stream row), so a

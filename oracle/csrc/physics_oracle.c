@@ -317,6 +317,33 @@ void oracle_mh_accept(long C, const double *E_old, const double *E_new, const do
     }
 }
 
+/*
+ * judge_normalizing_flow / bulk_judge_normalizing_flow (MCMC/monte_carlo.py:305-370)
+ * through metropolis_acceptance_particle_move (:191-223): for chain c, proposals
+ * m = 0..M-1 in order against E_ref[c]: new <= old -> accept (no draw); isinf(new)
+ * -> reject (no draw); else Generator.random() < exp(-beta*(new - old)).
+ * E_new is [C][M]; pcg [C][4] advanced; accept [C][M] (0/1).
+ */
+void oracle_metropolis_judge(long C, long M, const double *E_ref, const double *E_new, double beta,
+                             uint64_t *pcg, uint8_t *accept)
+{
+    for (long c = 0; c < C; c++) {
+        for (long m = 0; m < M; m++) {
+            double en = E_new[c * M + m], eo = E_ref[c];
+            int acc;
+            if (en <= eo) {
+                acc = 1;
+            } else if (isinf(en)) {
+                acc = 0;
+            } else {
+                double bf = exp(-beta * (en - eo));
+                acc = oracle_pcg64_next_double(&pcg[4 * c]) < bf;
+            }
+            accept[c * M + m] = (uint8_t)acc;
+        }
+    }
+}
+
 /* ------------------------------------------------------------------ */
 /* Local moves: MonteCarlo.particle_displacement (monte_carlo.py:146-189),  */
 /* metropolis_acceptance_particle_move (:191-223), adjust_displacement     */

@@ -72,6 +72,9 @@ def lib():
         L.oracle_mh_accept.argtypes = [
             ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_double, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_metropolis_judge.restype = None
+        L.oracle_metropolis_judge.argtypes = [ctypes.c_long, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_local_moves.restype = None
         L.oracle_local_moves.argtypes = [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(Phys), ctypes.c_double,
@@ -157,6 +160,18 @@ def mh_accept(E_old, E_new, nll_old, nll_new, pcg, beta=1.0, correct_sign=False)
     lib().oracle_mh_accept(C, _ptr(E_old), _ptr(E_new), _ptr(nll_old), _ptr(nll_new), beta,
                            _ptr(pcg), int(bool(correct_sign)), _ptr(acc), _ptr(u))
     return acc, u
+
+
+def metropolis_judge(E_ref, E_new, pcg, beta=1.0):
+    """judge / bulk_judge_normalizing_flow decisions (monte_carlo.py:191-223, 305-370):
+    E_ref (C,), E_new (C, M); pcg (C, 4) u64 advanced in place; returns accept (C, M) u8."""
+    E_ref = np.ascontiguousarray(E_ref, np.float64).reshape(-1)
+    E_new = np.ascontiguousarray(E_new, np.float64).reshape(len(E_ref), -1)
+    assert pcg.dtype == np.uint64 and pcg.flags.c_contiguous and pcg.shape == (len(E_ref), 4)
+    acc = np.empty(E_new.shape, np.uint8)
+    lib().oracle_metropolis_judge(E_new.shape[0], E_new.shape[1], _ptr(E_ref), _ptr(E_new), beta, _ptr(pcg),
+                                  _ptr(acc))
+    return acc
 
 
 class LocalChain:

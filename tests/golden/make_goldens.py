@@ -18,6 +18,9 @@ Fixtures:
   mh_trace.npz      reference MonteCarlo.nf_big_move traces (accept mask,
                     energies, NLLs, final PCG64 state) for given proposals
   pcg64.npz         numpy default_rng(seed) states and first draws, seeds 42..105
+  judge_trace.npz   reference judge_normalizing_flow / bulk_judge_normalizing_flow /
+                    metropolis_acceptance_particle_move on a scripted op sequence
+                    (with nf_big_move after a bulk judge), results + energies + PCG64
 """
 import contextlib
 import hashlib
@@ -697,6 +700,94 @@ def train_cycle_case(NF):
     print("train_cycle: ok", out["a10_losses"], out["a5_losses"])
 
 
+def judge_case(NF, MC):
+    """Reference judge_normalizing_flow / bulk_judge_normalizing_flow /
+    metropolis_acceptance_particle_move (monte_carlo.py:191-223, 305-370) on a scripted
+    sequence per chain, with an nf_big_move after a bulk judge (the stale running energy
+    it leaves behind enters that move's ratio, :243).  Per op: the verdict (bool, or the
+    accepted count for bulk), the calculator's total energy / virial and the attempt
+    counter afterwards; per chain the final particles and PCG64 state."""
+    from oracle import flow as OF
+    out = {}
+    for N, chains in ((16, 3), (64, 2)):
+        dims = OF.FlowDims(N=N, L=2, H=32, nb=1, K=8, B=OF.half_box(N))
+        sd = OF.random_state_dict(dims, seed=7 + N)
+        model = build_ref_model(NF, dims)
+        model.load_state_dict(sd, strict=True)
+        model.eval()
+        for c in range(chains):
+            rng = np.random.default_rng(500 + 10 * N + c)
+            with contextlib.redirect_stdout(io.StringIO()):
+                particles, box = MC.initialise_fcc(num_particles=N, rho=0.03, aspect_ratio=1.0)
+                mc = MC.MonteCarlo(particles=particles, sim_box=box, temperature=1.0, num_particles=N,
+                                   num_wells=2, V0_list=[-10.0, -10.5], r0=1.2, k=15,
+                                   initial_max_displacement=0.65, target_acceptance=0.5,
+                                   timing=False, checking=False, logger=None, seed=42 + c,
+                                   device=torch.device("cpu"))
+                mc.set_nf_model(model)
+            L = box.box_size_x
+
+            def near(scale, dt):
+                x = np.mod(np.asarray(mc.particles, np.float64) + rng.normal(0, scale, (N, 2)), L)
+                return x.astype(dt)
+
+            def overlap(dt):
+                x = near(0.02, dt)
+                x[1] = x[0]
+                return x
+
+            ops, cfgs, res, Es, Ws, att = [], [], [], [], [], []
+            script = [("judge", np.float32, 0.05), ("judge", np.float64, 0.6), ("judge_ov", np.float32, 0),
+                      ("metro", -5.0, -4.0), ("metro", -4.0, -5.0), ("metro", 1.0, np.inf),
+                      ("metro", np.inf, np.inf), ("metro", 2.0, np.nan), ("metro", -3.0, -2.999),
+                      ("bulk", np.float32, 6), ("big", np.float32, 0.05), ("judge", np.float32, 0.4),
+                      ("bulk", np.float64, 5), ("judge", np.float64, 0.05), ("big", np.float32, 0.02)]
+            for op in script:
+                kind = op[0]
+                with contextlib.redirect_stdout(io.StringIO()):
+                    if kind in ("judge", "judge_ov"):
+                        x = overlap(op[1]) if kind == "judge_ov" else near(op[2], op[1])
+                        r = float(mc.judge_normalizing_flow(x))
+                        cfgs.append(x.astype(np.float64)[None]); ops.append((0, int(op[1] == np.float32), 1, 0.0, 0.0))
+                    elif kind == "metro":
+                        r = float(mc.metropolis_acceptance_particle_move(op[1], op[2]))
+                        cfgs.append(np.zeros((0, N, 2))); ops.append((1, 0, 0, op[1], op[2]))
+                    elif kind == "bulk":
+                        M = op[2]
+                        xs = [near(0.03 * (m + 1), op[1]) for m in range(M - 1)] + [overlap(op[1])]
+                        xs = xs[:2] + [xs[-1]] + xs[2:-1]  # an overlapping one in the middle
+                        ref = mc.energy_calculator.total_energy - 0.3
+                        a, t = mc.bulk_judge_normalizing_flow(xs, ref)
+                        assert t == M
+                        r = float(a)
+                        cfgs.append(np.stack(xs).astype(np.float64)); ops.append((2, int(op[1] == np.float32), M, ref, 0.0))
+                    else:  # big
+                        x = near(op[2], op[1])
+                        r = float(mc.nf_big_move(x))
+                        cfgs.append(x.astype(np.float64)[None]); ops.append((3, 1, 1, 0.0, 0.0))
+                res.append(r)
+                Es.append(mc.energy_calculator.total_energy)
+                Ws.append(mc.energy_calculator.total_virial)
+                att.append(mc.attempts_displacement)
+            key = f"N{N}_c{c}"
+            st = mc.rng.bit_generator.state["state"]
+            out[key + "_init"] = np.asarray(particles, np.float64)
+            out[key + "_ops"] = np.array(ops, np.float64)  # kind, is_f32, M, a, b
+            out[key + "_cfgs"] = np.concatenate(cfgs)
+            out[key + "_result"] = np.array(res)
+            out[key + "_E"] = np.array(Es)
+            out[key + "_W"] = np.array(Ws)
+            out[key + "_attempts"] = np.array(att, np.int64)
+            out[key + "_final"] = np.asarray(mc.particles, np.float64)
+            out[key + "_final_f32"] = np.bool_(np.asarray(mc.particles).dtype == np.float32)
+            out[key + "_pcg_state"] = np.array([st["state"] >> 64, st["state"] & (2**64 - 1),
+                                                st["inc"] >> 64, st["inc"] & (2**64 - 1)], np.uint64)
+            print(f"judge {key}: results {res}")
+        out[f"N{N}_flow_seed"] = np.int64(7 + N)
+        out[f"N{N}_chains"] = np.int64(chains)
+    np.savez_compressed(os.path.join(HERE, "judge_trace.npz"), **out)
+
+
 def pcg_case():
     seeds = np.arange(42, 42 + 64)
     st = np.zeros((64, 4), np.uint64)
@@ -729,6 +820,9 @@ def main(only=None):
     if only == "train_cycle":
         train_cycle_case(NF)
         return
+    if only == "judge":
+        judge_case(NF, MC)
+        return
     flow_case(NF, "tiny", OF.FlowDims(N=4, L=2, H=32, nb=1, K=5, B=OF.half_box(4)), 1, 64, True)
     flow_case(NF, "n16", OF.FlowDims(N=16, L=3, H=64, nb=2, K=8, B=OF.half_box(16)), 2, 48, False)
     flow_case(NF, "n64", OF.FlowDims(N=64, L=2, H=128, nb=2, K=32, B=OF.half_box(64)), 3, 16, False)
@@ -742,6 +836,7 @@ def main(only=None):
     train_case(NF)
     driver_case(NF, MC)
     train_cycle_case(NF)
+    judge_case(NF, MC)
 
 
 if __name__ == "__main__":
