@@ -144,6 +144,22 @@ int fs_mh_accept(const fs_phys *p, int64_t C, int32_t N, double *E_old, double *
                   "fs_mh_accept");
 }
 
+int fs_min_image(const fs_phys *p, const void *pos1, int64_t stride1, const void *pos2, int pos_is_f32, int64_t n,
+                 double *delta, double *r, void *stream) {
+    REQUIRE(p && pos1 && pos2 && n >= 0 && (stride1 == 0 || stride1 == 1), "fs_min_image: invalid arguments");
+    REQUIRE(p->Lx > 0 && p->Ly > 0, "fs_min_image: box lengths must be positive");
+    return hip_rc(fs_min_image_impl(p, pos1, stride1, pos2, pos_is_f32, n, delta, r, (hipStream_t)stream),
+                  "fs_min_image");
+}
+
+int fs_particle_energy(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int32_t N,
+                       const int32_t *particle, double *E, double *W, void *stream) {
+    REQUIRE(p && pos && particle && E && W && C >= 0, "fs_particle_energy: invalid arguments");
+    REQUIRE(N >= 2 && N <= fs::kMaxN, "fs_particle_energy: N=%d outside [2, %d]", N, fs::kMaxN);
+    return hip_rc(fs_particle_energy_impl(p, pos, pos_is_f32, C, N, particle, E, W, (hipStream_t)stream),
+                  "fs_particle_energy");
+}
+
 int fs_metropolis_judge(double beta, int64_t C, int64_t M, const double *E_ref, const double *E_new, uint64_t *pcg,
                         uint8_t *accept, int64_t *n_accept, void *stream) {
     REQUIRE(E_ref && E_new && pcg && C >= 0 && M >= 0, "fs_metropolis_judge: invalid arguments");

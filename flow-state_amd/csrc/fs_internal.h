@@ -39,6 +39,10 @@ hipError_t fs_mh_accept_impl(const fs_phys *p, int64_t C, int N, double *E_old, 
                              int64_t *attempts, int64_t *accepted, unsigned long long *n_accept, int flags,
                              hipStream_t st, const float *log_q_old = nullptr, const double *E_cur = nullptr,
                              const double *W_cur = nullptr);
+hipError_t fs_min_image_impl(const fs_phys *p, const void *a, int64_t sa, const void *b, int f32, int64_t n,
+                            double *delta, double *r, hipStream_t st);
+hipError_t fs_particle_energy_impl(const fs_phys *p, const void *pos, int f32, int64_t C, int N, const int32_t *part,
+                                   double *E, double *W, hipStream_t st);
 hipError_t fs_metropolis_judge_impl(double beta, int64_t C, int64_t M, const double *E_ref, const double *E_new,
                                    uint64_t *pcg, uint8_t *accept, int64_t *n_accept, hipStream_t st);
 hipError_t fs_adjust_displacement_impl(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,

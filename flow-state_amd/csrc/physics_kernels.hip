@@ -299,6 +299,116 @@ __global__ void __launch_bounds__(256) mh_accept_kernel(fs_phys p, int64_t C, in
     }
 }
 
+// SimulationBox.minimum_image / compute_distance (simulation_box.py:31-56) for n pairs
+// (a[i * sa], b[i]), sa = 0 broadcasts one first position (compute_distances, :58-65):
+// delta = the wrapped displacement in the positions' dtype (float32: wrapped in float64
+// against the np.float64 box lengths, rounded back), r = np.linalg.norm(delta) (the
+// float32 sdot / float64 ddot, correctly rounded sqrt), both widened to float64.
+template <bool F32>
+__global__ void min_image_kernel(fs_phys p, PairThresh T, const void *__restrict__ a, int64_t sa,
+                                 const void *__restrict__ b, int64_t n, double *__restrict__ delta,
+                                 double *__restrict__ r) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double iLx = 1.0 / p.Lx, iLy = 1.0 / p.Ly;
+    double t0, t1, rr;
+    if (F32) {
+        const float *A = (const float *)a + 2 * i * sa, *B = (const float *)b + 2 * i;
+        const float u0 = (float)wrap_min_image((double)(A[0] - B[0]), p.Lx, T.hx, iLx);
+        const float u1 = (float)wrap_min_image((double)(A[1] - B[1]), p.Ly, T.hy, iLy);
+        t0 = u0;
+        t1 = u1;
+        rr = r_of_sq(sqdist_f32(A[0], A[1], B[0], B[1], p.Lx, p.Ly, T, iLx, iLy));
+    } else {
+        const double *A = (const double *)a + 2 * i * sa, *B = (const double *)b + 2 * i;
+        t0 = wrap_min_image(A[0] - B[0], p.Lx, T.hx, iLx);
+        t1 = wrap_min_image(A[1] - B[1], p.Ly, T.hy, iLy);
+        rr = r_of_sq(sqdist_f64(A[0], A[1], B[0], B[1], p.Lx, p.Ly, T, iLx, iLy));
+    }
+    if (delta) {
+        delta[2 * i] = t0;
+        delta[2 * i + 1] = t1;
+    }
+    if (r) r[i] = rr;
+}
+
+// EnergyCalculator.calculate_particle_energy_virial (energy_calculator.py:48-108): the
+// energy / virial of particle part[c] of chain c with the np.delete-compacted others
+// (pair t <-> particle t + (t >= part)), +inf for both if any r < 0.5, else np.sum of the
+// LJ terms (numpy's pairwise order) + the particle's double-well term.  One thread per
+// chain (an API call, not the local-move hot loop, which has its own kernel).
+template <bool F32>
+__global__ void particle_energy_kernel(fs_phys p, PairThresh T, const void *__restrict__ pos, int64_t C, int N,
+                                       const int32_t *__restrict__ part, double *__restrict__ E,
+                                       double *__restrict__ W) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const int pi = part[c];
+    const double iLx = 1.0 / p.Lx, iLy = 1.0 / p.Ly;
+    const double sr6c = pow6(1.0 / p.r_cut);
+    const double e_cut = 4.0 * (sr6c * sr6c - sr6c);
+    auto X = [&](int j) {
+        return F32 ? (double)((const float *)pos)[(c * N + j) * 2] : ((const double *)pos)[(c * N + j) * 2];
+    };
+    auto Y = [&](int j) {
+        return F32 ? (double)((const float *)pos)[(c * N + j) * 2 + 1] : ((const double *)pos)[(c * N + j) * 2 + 1];
+    };
+    bool hit = false;
+    auto term = [&](int t, double &e, double &w) {
+        const int j = t + (t >= pi ? 1 : 0);
+        e = 0.0;
+        w = 0.0;
+        if (F32) {
+            const float s = sqdist_f32((float)X(pi), (float)Y(pi), (float)X(j), (float)Y(j), p.Lx, p.Ly, T, iLx, iLy);
+            hit |= s <= T.core32;
+            if (s <= T.cut32) lj_pair(r_of_sq(s), p.r_cut, e_cut, e, w);
+        } else {
+            const double s = sqdist_f64(X(pi), Y(pi), X(j), Y(j), p.Lx, p.Ly, T, iLx, iLy);
+            hit |= s <= T.core64;
+            if (s <= T.cut64) lj_pair(r_of_sq(s), p.r_cut, e_cut, e, w);
+        }
+    };
+    const int n = N - 1;
+    double re = 0.0, rw = 0.0;
+    if (n < 8) {
+        for (int t = 0; t < n; ++t) {
+            double e, w;
+            term(t, e, w);
+            re += e;
+            rw += w;
+        }
+    } else {
+        double ae[8], aw[8];
+        for (int j = 0; j < 8; ++j) term(j, ae[j], aw[j]);
+        const int nfull = n - (n % 8);
+        for (int t0 = 8; t0 < nfull; t0 += 8)
+            for (int j = 0; j < 8; ++j) {
+                double e, w;
+                term(t0 + j, e, w);
+                ae[j] += e;
+                aw[j] += w;
+            }
+        re = ((ae[0] + ae[1]) + (ae[2] + ae[3])) + ((ae[4] + ae[5]) + (ae[6] + ae[7]));
+        rw = ((aw[0] + aw[1]) + (aw[2] + aw[3])) + ((aw[4] + aw[5]) + (aw[6] + aw[7]));
+        for (int t = nfull; t < n; ++t) {
+            double e, w;
+            term(t, e, w);
+            re += e;
+            rw += w;
+        }
+    }
+    if (hit) {
+        E[c] = INFINITY;
+        W[c] = INFINITY;
+        return;
+    }
+    double v = 0.0;
+    for (int k = 0; k < p.num_wells && k < 2; ++k)
+        v += dw_term(X(pi), Y(pi), k, p.Lx, p.Ly, p.V0[k], p.r0, p.k, iLx, iLy);
+    E[c] = p.num_wells > 0 ? re + v : re;
+    W[c] = rw;
+}
+
 // Energy-only Metropolis of supplied proposals against a reference energy, without moving
 // the chain: judge_normalizing_flow (monte_carlo.py:305-329, reference = the chain's
 // energy) and bulk_judge_normalizing_flow (:331-370, M proposals per chain against one
@@ -389,6 +499,30 @@ hipError_t fs_mh_accept_impl(const fs_phys *p, int64_t C, int N, double *E_old, 
     hipLaunchKernelGGL(mh_accept_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, *p, C, N, E_old,
                        W_old, nll_old, E_new, W_new, log_q_new, pcg, state, state_is_f32, config, accept,
                        attempts, accepted, n_accept, flags, log_q_old, E_cur, W_cur);
+    return hipGetLastError();
+}
+
+hipError_t fs_min_image_impl(const fs_phys *p, const void *a, int64_t sa, const void *b, int f32, int64_t n,
+                            double *delta, double *r, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const PairThresh T = fs_pair_thresh(*p);
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (f32)
+        hipLaunchKernelGGL(min_image_kernel<true>, grid, dim3(256), 0, st, *p, T, a, sa, b, n, delta, r);
+    else
+        hipLaunchKernelGGL(min_image_kernel<false>, grid, dim3(256), 0, st, *p, T, a, sa, b, n, delta, r);
+    return hipGetLastError();
+}
+
+hipError_t fs_particle_energy_impl(const fs_phys *p, const void *pos, int f32, int64_t C, int N, const int32_t *part,
+                                   double *E, double *W, hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    const PairThresh T = fs_pair_thresh(*p);
+    const dim3 grid((unsigned)((C + 255) / 256));
+    if (f32)
+        hipLaunchKernelGGL(particle_energy_kernel<true>, grid, dim3(256), 0, st, *p, T, pos, C, N, part, E, W);
+    else
+        hipLaunchKernelGGL(particle_energy_kernel<false>, grid, dim3(256), 0, st, *p, T, pos, C, N, part, E, W);
     return hipGetLastError();
 }
 

@@ -72,6 +72,21 @@ class EnergyCalculator:
         self.total_energy, self.total_virial = float(E.item()), float(W.item())
         return self.total_energy, self.total_virial
 
+    def calculate_particle_energy_virial(self, positions, particle_index):
+        """energy_calculator.py:48-108: (energy, virial) of one particle with the others
+        (+inf both on a hard-core overlap); the running totals are not touched."""
+        a = np.asarray(positions)
+        a = a if a.dtype in (np.float32, np.float64) else a.astype(np.float64)
+        t = torch.as_tensor(np.ascontiguousarray(a), device=self.device).reshape(1, self.num_particles, 2)
+        part = torch.tensor([int(particle_index)], dtype=torch.int32, device=t.device)
+        E = torch.empty(1, dtype=torch.float64, device=t.device)
+        W = torch.empty_like(E)
+        with _lib.on_device(t):
+            _lib.check(_lib.load().fs_particle_energy(self.phys, _lib.ptr(t), int(t.dtype == torch.float32), 1,
+                                                      self.num_particles, _lib.ptr(part), _lib.ptr(E), _lib.ptr(W),
+                                                      _lib.stream_ptr()), "fs_particle_energy")
+        return float(E.item()), float(W.item())
+
     def update_total_energy_virial(self, energy_dif, virial_dif):
         self.total_energy += energy_dif
         self.total_virial += virial_dif

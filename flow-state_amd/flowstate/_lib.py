@@ -52,6 +52,8 @@ _SIGS = {
     "fs_energy_lj_dw": (ctypes.c_int, [_PH, _P, ctypes.c_int, _I64, ctypes.c_int32, _P, _P, _P, _P, _P]),
     "fs_pcg64_seed": (ctypes.c_int, [_P, _I64, _P, _P]),
     "fs_pcg64_random": (ctypes.c_int, [_P, _I64, _P, _P]),
+    "fs_min_image": (ctypes.c_int, [_PH, _P, _I64, _P, ctypes.c_int, _I64, _P, _P, _P]),
+    "fs_particle_energy": (ctypes.c_int, [_PH, _P, ctypes.c_int, _I64, ctypes.c_int32, _P, _P, _P, _P]),
     "fs_metropolis_judge": (ctypes.c_int, [ctypes.c_double, _I64, _I64] + [_P] * 5 + [_P]),
     "fs_mh_accept": (ctypes.c_int, [_PH, _I64, ctypes.c_int32] + [_P] * 14 + [ctypes.c_int, _P]),
     "fs_nf_mh_step_ws_bytes": (_I64, [_D, _I64]),

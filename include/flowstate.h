@@ -133,6 +133,24 @@ int fs_flow_propose(const fs_flow_dims *d, const void *packed, int64_t B, uint64
 int fs_energy_lj_dw(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int32_t N,
                     double *E, double *W, uint8_t *overlap, uint64_t *nbr, void *stream);
 
+/* SimulationBox.minimum_image / compute_distance / compute_distances
+ * (simulation_box.py:31-65) for n pairs (pos1[i * stride1], pos2[i]) of [2] positions,
+ * float32 (pos_is_f32=1) or float64 (both the same dtype, numpy's promotion done by the
+ * caller; box lengths np.float64 as initialise_fcc makes them); stride1 = 0 broadcasts
+ * one first position.  delta [n][2] = the wrapped displacement (np.round half-even; in
+ * the positions' dtype, widened), r [n] = np.linalg.norm(delta) (float32 sdot / float64
+ * ddot with a correctly rounded sqrt), each nullable. */
+int fs_min_image(const fs_phys *p, const void *pos1, int64_t stride1, const void *pos2, int pos_is_f32, int64_t n,
+                 double *delta, double *r, void *stream);
+
+/* EnergyCalculator.calculate_particle_energy_virial (energy_calculator.py:48-108) for one
+ * particle per chain: pos [C][N][2] (float32 or float64), particle [C] int32.  E, W [C]
+ * float64: +inf both on any r < 0.5 to the other particles, else the np.sum (pairwise
+ * order, np.delete-compacted others) of the LJ terms, E plus the particle's double-well
+ * term. */
+int fs_particle_energy(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int32_t N,
+                       const int32_t *particle, double *E, double *W, void *stream);
+
 /* np.random.default_rng(seed) (SeedSequence + PCG64 init, monte_carlo.py:92-95)
  * for C seeds -> state [C][4] u64 = {state_hi, state_lo, inc_hi, inc_lo}. */
 int fs_pcg64_seed(const uint64_t *seeds, int64_t C, uint64_t *state, void *stream);

@@ -92,6 +92,22 @@ double oracle_min_image_dist(const void *pos, int dtype_f32, int i, int j, doubl
     return min_image_dist_f64(p[2 * i], p[2 * i + 1], p[2 * j], p[2 * j + 1], Lx, Ly);
 }
 
+/* minimum_image (simulation_box.py:31-46): the wrapped displacement in the dtype */
+void oracle_min_image(const void *a, const void *b, int dtype_f32, double Lx, double Ly, double delta[2])
+{
+    if (dtype_f32) {
+        const float *p = (const float *)a, *q = (const float *)b;
+        float d0 = p[0] - q[0], d1 = p[1] - q[1];
+        delta[0] = (float)((double)d0 - Lx * rint((double)d0 / Lx));
+        delta[1] = (float)((double)d1 - Ly * rint((double)d1 / Ly));
+    } else {
+        const double *p = (const double *)a, *q = (const double *)b;
+        double d0 = p[0] - q[0], d1 = p[1] - q[1];
+        delta[0] = d0 - Lx * rint(d0 / Lx);
+        delta[1] = d1 - Ly * rint(d1 / Ly);
+    }
+}
+
 /* ------------------------------------------------------------------ */
 /* physics parameters                                                  */
 /* ------------------------------------------------------------------ */
@@ -447,6 +463,11 @@ static int particle_energy(const double *xy, int f32, int N, int p, const oracle
  * f32); E/W: running totals; counters: attempts/accepted; every adjust_every
  * moves (0 = never) adjust_displacement with prev_* bookkeeping.
  * accept_log (nullable): per-move 0/1. */
+int oracle_particle_energy(const double *xy, int f32, int N, int p, const oracle_phys *ph, double *E, double *W)
+{
+    return particle_energy(xy, f32, N, p, ph, E, W);
+}
+
 void oracle_local_moves(double *xy, int f32, int N, const oracle_phys *ph, double beta, uint64_t s[6],
                         double *max_disp, double target_acc, double *E, double *W, int64_t *attempts,
                         int64_t *accepted, int64_t *prev_att, int64_t *prev_acc, int n_moves, int adjust_every,

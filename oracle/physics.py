@@ -72,6 +72,13 @@ def lib():
         L.oracle_mh_accept.argtypes = [
             ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_double, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_min_image.restype = None
+        L.oracle_min_image.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_void_p]
+        L.oracle_particle_energy.restype = ctypes.c_int
+        L.oracle_particle_energy.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.POINTER(Phys), ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_double)]
         L.oracle_metropolis_judge.restype = None
         L.oracle_metropolis_judge.argtypes = [ctypes.c_long, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]
@@ -160,6 +167,26 @@ def mh_accept(E_old, E_new, nll_old, nll_new, pcg, beta=1.0, correct_sign=False)
     lib().oracle_mh_accept(C, _ptr(E_old), _ptr(E_new), _ptr(nll_old), _ptr(nll_new), beta,
                            _ptr(pcg), int(bool(correct_sign)), _ptr(acc), _ptr(u))
     return acc, u
+
+
+def min_image(a, b, phys):
+    """SimulationBox.minimum_image (simulation_box.py:31-46) of two (2,) positions of one dtype."""
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    assert a.dtype == b.dtype and a.dtype in (np.float32, np.float64)
+    d = np.empty(2, np.float64)
+    lib().oracle_min_image(_ptr(a), _ptr(b), int(a.dtype == np.float32), phys.Lx, phys.Ly, _ptr(d))
+    return d.astype(a.dtype)
+
+
+def particle_energy(pos, p, phys):
+    """EnergyCalculator.calculate_particle_energy_virial (energy_calculator.py:48-108)."""
+    pos = np.ascontiguousarray(pos)
+    xy = np.ascontiguousarray(pos, np.float64)
+    E = ctypes.c_double()
+    W = ctypes.c_double()
+    lib().oracle_particle_energy(_ptr(xy), int(pos.dtype == np.float32), pos.shape[0], int(p), ctypes.byref(phys),
+                                 ctypes.byref(E), ctypes.byref(W))
+    return E.value, W.value
 
 
 def metropolis_judge(E_ref, E_new, pcg, beta=1.0):

@@ -21,6 +21,8 @@ Fixtures:
   judge_trace.npz   reference judge_normalizing_flow / bulk_judge_normalizing_flow /
                     metropolis_acceptance_particle_move on a scripted op sequence
                     (with nf_big_move after a bulk judge), results + energies + PCG64
+  box_trace.npz     reference SimulationBox.minimum_image / compute_distance(s) and
+                    EnergyCalculator.calculate_particle_energy_virial outputs
 """
 import contextlib
 import hashlib
@@ -788,6 +790,49 @@ def judge_case(NF, MC):
     np.savez_compressed(os.path.join(HERE, "judge_trace.npz"), **out)
 
 
+def box_case(MC):
+    """Reference SimulationBox.minimum_image / compute_distance / compute_distances
+    (simulation_box.py:31-65) and EnergyCalculator.calculate_particle_energy_virial
+    (energy_calculator.py:48-108) on float32 and float64 configurations with
+    boundary-straddling pairs, exact half-box separations and a hard-core overlap."""
+    from energy_calculator import EnergyCalculator
+    out = {}
+    for N in (16, 64):
+        with contextlib.redirect_stdout(io.StringIO()):
+            base, box = MC.initialise_fcc(num_particles=N, rho=0.03, aspect_ratio=1.0)
+        L = box.box_size_x
+        rng = np.random.default_rng(77 + N)
+        for dt in (np.float32, np.float64):
+            tag = f"N{N}_{'f32' if dt == np.float32 else 'f64'}"
+            x = np.mod(np.asarray(base, np.float64) + rng.normal(0, 0.6, (N, 2)), L)
+            x[1] = [0.05, x[1, 1]]
+            x[2] = [L - 0.05, x[1, 1]]  # straddles x = 0 with particle 1
+            x[3] = [x[4, 0] + L / 2, x[4, 1]]  # exact half-box separation (round half to even)
+            x[5] = [x[6, 0] + 0.3, x[6, 1]]  # hard-core overlap (r < 0.5)
+            x = np.mod(x, L).astype(dt)
+            ii = rng.integers(0, N, 64)
+            jj = rng.integers(0, N, 64)
+            ii[:4], jj[:4] = [1, 3, 5, 2], [2, 4, 6, 1]
+            deltas = np.stack([box.minimum_image(x[i], x[j]) for i, j in zip(ii, jj)])
+            dist = np.array([box.compute_distance(x[i], x[j]) for i, j in zip(ii, jj)])
+            rows = np.stack([box.compute_distances(x[i], np.delete(x, i, axis=0)) for i in range(N)])
+            with contextlib.redirect_stdout(io.StringIO()):
+                ec = EnergyCalculator(num_particles=N, initial_particles=x, simulation_box=box, num_wells=2,
+                                      V0_list=[-10.0, -10.5], r0=1.2, k=15, timing=False, checking=False)
+            pe = np.array([ec.calculate_particle_energy_virial(x, p) for p in range(N)], np.float64)
+            out[tag + "_x"] = x
+            out[tag + "_ij"] = np.stack([ii, jj], 1)
+            out[tag + "_delta"] = deltas
+            out[tag + "_delta_dtype_f32"] = np.bool_(deltas.dtype == np.float32)
+            out[tag + "_dist"] = np.asarray(dist)
+            out[tag + "_dist_dtype_f32"] = np.bool_(np.asarray(dist).dtype == np.float32)
+            out[tag + "_rows"] = rows
+            out[tag + "_particle_ew"] = pe
+            out[tag + "_L"] = np.float64(L)
+            print(f"box {tag}: inf rows {int(np.isinf(pe[:, 0]).sum())}, dtypes {deltas.dtype}/{np.asarray(dist).dtype}")
+    np.savez_compressed(os.path.join(HERE, "box_trace.npz"), **out)
+
+
 def pcg_case():
     seeds = np.arange(42, 42 + 64)
     st = np.zeros((64, 4), np.uint64)
@@ -823,6 +868,9 @@ def main(only=None):
     if only == "judge":
         judge_case(NF, MC)
         return
+    if only == "box":
+        box_case(MC)
+        return
     flow_case(NF, "tiny", OF.FlowDims(N=4, L=2, H=32, nb=1, K=5, B=OF.half_box(4)), 1, 64, True)
     flow_case(NF, "n16", OF.FlowDims(N=16, L=3, H=64, nb=2, K=8, B=OF.half_box(16)), 2, 48, False)
     flow_case(NF, "n64", OF.FlowDims(N=64, L=2, H=128, nb=2, K=32, B=OF.half_box(64)), 3, 16, False)
@@ -837,6 +885,7 @@ def main(only=None):
     driver_case(NF, MC)
     train_cycle_case(NF)
     judge_case(NF, MC)
+    box_case(MC)
 
 
 if __name__ == "__main__":

@@ -69,3 +69,23 @@ def test_oracle_replays_reference_judge_traces(N):
             assert attempts == f[k + "_attempts"][i]
         np.testing.assert_array_equal(pcg[0], f[k + "_pcg_state"])
         np.testing.assert_array_equal(xy, f[k + "_final"])
+
+
+@pytest.mark.parametrize("tag", ["N16_f32", "N16_f64", "N64_f32", "N64_f64"])
+def test_oracle_box_and_particle_energy(tag):
+    """oracle min_image / min_image_dist / particle_energy vs the reference's
+    SimulationBox and EnergyCalculator.calculate_particle_energy_virial
+    (tests/golden/box_trace.npz): bit-exact displacements and distances, energies
+    within 1e-12 (both +inf on the hard core)."""
+    f = np.load(os.path.join(G, "box_trace.npz"))
+    x = f[tag + "_x"]
+    N = x.shape[0]
+    phys = OP.make_phys(N)
+    assert phys.Lx == float(f[tag + "_L"])
+    for (i, j), d, r in zip(f[tag + "_ij"], f[tag + "_delta"], f[tag + "_dist"]):
+        np.testing.assert_array_equal(OP.min_image(x[i], x[j], phys), d)
+        assert OP.min_image_dist(x, int(i), int(j), phys) == r
+    for p in range(N):
+        E, W = OP.particle_energy(x, p, phys)
+        Er, Wr = f[tag + "_particle_ew"][p]
+        assert _close(E, Er) and _close(W, Wr), (p, E, Er)
