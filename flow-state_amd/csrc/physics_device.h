@@ -38,6 +38,10 @@ struct PairThresh {
     double cut64, core64;  // s <= cut64 <=> sqrt(s) <= r_cut; s <= core64 <=> sqrt(s) < r_core
     double hx, hy;         // min-image half-box thresholds
     float cut32, core32;   // the same for the float32 path
+    // float32 path: for a float d, (double)|d| > hx <=> |d| > hx32 and (double)|d| <= Lx <=>
+    // |d| <= Lx32 (each the largest float not above the double), so the common minimum-image
+    // case needs no float64 compare
+    float hx32, hy32, Lx32, Ly32;
 };
 
 template <class P>
@@ -72,6 +76,10 @@ static inline PairThresh fs_pair_thresh(const fs_phys &p) {
     t.core32 = fs_max_true_f32([&](float s) { return (double)(float)sqrt((double)s) < p.r_core; });
     t.hx = fs_max_true_f64([&](double a) { return a / p.Lx <= 0.5; });
     t.hy = fs_max_true_f64([&](double a) { return a / p.Ly <= 0.5; });
+    t.hx32 = fs_max_true_f32([&](float a) { return (double)a <= t.hx; });
+    t.hy32 = fs_max_true_f32([&](float a) { return (double)a <= t.hy; });
+    t.Lx32 = fs_max_true_f32([&](float a) { return (double)a <= p.Lx; });
+    t.Ly32 = fs_max_true_f32([&](float a) { return (double)a <= p.Ly; });
     return t;
 }
 
@@ -95,6 +103,22 @@ __device__ __forceinline__ float sqdist_f32(float ax, float ay, float bx, float 
     const float d0 = ax - bx, d1 = ay - by;
     const float t0 = (float)wrap_min_image((double)d0, Lx, T.hx, iLx);
     const float t1 = (float)wrap_min_image((double)d1, Ly, T.hy, iLy);
+    const float s0 = t0 * t0, s1 = t1 * t1;
+    return s0 + s1;
+}
+// the same for float32 coordinates without a float64 compare or branch in the common case
+// (|d| <= L): the wrap subtraction stays in float64 (exact there, rounded once), and the
+// rare |d| > L takes wrap_min_image's general path
+__device__ __forceinline__ float wrap32(float d, double L, float h32, float L32, double h, double invL) {
+    const float a = fabsf(d);
+    float t = a > h32 ? (float)((double)d - copysign(L, (double)d)) : d;
+    if (__builtin_expect(a > L32, 0)) t = (float)wrap_min_image((double)d, L, h, invL);
+    return t;
+}
+__device__ __forceinline__ float sqdist32(float ax, float ay, float bx, float by, double Lx, double Ly,
+                                         const PairThresh &T, double iLx, double iLy) {
+    const float t0 = wrap32(ax - bx, Lx, T.hx32, T.Lx32, T.hx, iLx);
+    const float t1 = wrap32(ay - by, Ly, T.hy32, T.Ly32, T.hy, iLy);
     const float s0 = t0 * t0, s1 = t1 * t1;
     return s0 + s1;
 }

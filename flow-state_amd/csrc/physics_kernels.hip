@@ -13,6 +13,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "flow_layout.h"
 #include "fs_internal.h"
 #include "physics_device.h"
@@ -47,7 +49,9 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, PairThresh T, co
                                                      int N, double *__restrict__ E, double *__restrict__ W,
                                                      uint8_t *__restrict__ ov, uint64_t *__restrict__ nbr,
                                                      const uint8_t *__restrict__ is_f32) {
-    __shared__ double sx[4][2][64], sy[4][2][64], se[4][2][64], sw[4][2][64], sv[4][2][64];
+    using CT = typename std::conditional<F32, float, double>::type;  // coordinates in LDS, stored dtype
+    __shared__ CT sx[4][2][64], sy[4][2][64];
+    __shared__ double se[4][2][64], sw[4][2][64], sv[4][2][64];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int hh = lane >> 5, hl = lane & 31;
     const int64_t c = ((int64_t)blockIdx.x * 4 + wid) * 2 + hh;
@@ -55,7 +59,7 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, PairThresh T, co
     // float64 storage holding a chain whose reference state is float32 (after an accepted
     // big move, monte_carlo.py:296): the float32 distance path on the exact float values
     const bool as_f32 = F32 || (is_f32 && is_f32[c]);
-    double *X = sx[wid][hh], *Y = sy[wid][hh];
+    CT *X = sx[wid][hh], *Y = sy[wid][hh];
     for (int q = hl; q < N; q += 32) {
         if (F32) {
             const float *src = (const float *)pos + c * 2 * N;
@@ -80,7 +84,8 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, PairThresh T, co
         e = 0.0;
         w = 0.0;
         if (as_f32) {
-            const float s = sqdist_f32((float)X[i], (float)Y[i], (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy);
+            const float s = F32 ? sqdist32((float)X[i], (float)Y[i], (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy)
+                                : sqdist_f32((float)X[i], (float)Y[i], (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy);
             hit |= s <= T.core32;
             if (s <= T.cut32) {
                 mask |= (uint64_t)1 << j;

@@ -64,6 +64,35 @@ def test_energy_matches_oracle_random(dtype, N):
     assert 0 < fin.sum() < C
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("N", [16, 64])
+def test_energy_clustered_states(dtype, N):
+    """Dense clusters (lattice spacing 0.7-0.9 < r_cut, > r_core): every particle has tens
+    of pairs inside the cutoff, so the kernel's queue of in-cutoff pair terms fills and
+    drains several times per row; energies, virials and neighbour masks against the oracle."""
+    rng = np.random.default_rng(100 + N)
+    L = float(np.sqrt(N / 0.03))
+    C = 512
+    side = int(np.ceil(np.sqrt(N)))
+    g = np.stack(np.meshgrid(np.arange(side), np.arange(side), indexing="ij"), -1).reshape(-1, 2)[:N].astype(float)
+    sp = rng.uniform(0.7, 0.9, (C, 1, 1))
+    pos = g[None] * sp + rng.uniform(0, L, (C, 1, 2)) + rng.normal(0, 0.02, (C, N, 2))
+    pos = np.mod(pos, L).astype(dtype)
+    Eo, Wo, ovo = OP.total_energy_batch(pos, OP.make_phys(N))
+    E, W, ov, nbr = total_energy(torch.from_numpy(pos).cuda(), gphys(N), with_neighbours=True)
+    E, W, ov = E.cpu().numpy(), W.cpu().numpy(), ov.cpu().numpy()
+    np.testing.assert_array_equal(ov, ovo)
+    assert (ov == 0).all()
+    np.testing.assert_allclose(E, Eo, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(W, Wo, rtol=1e-12, atol=1e-12)
+    words = nbr.cpu().numpy().view(np.uint64)
+    for c in range(0, C, 64):
+        _, _, _, cut = OP.total_energy(pos[c], OP.make_phys(N), with_cutoff=True)
+        got = ((words[c][:, None] >> np.arange(N, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+        np.testing.assert_array_equal(got, np.triu(cut, 1))
+        assert got.sum() > 4 * N  # dense: many in-cutoff pairs per row
+
+
 def test_pcg64_seed_and_draws_bit_exact():
     f = np.load(os.path.join(G, "pcg64.npz"))
     seeds = torch.from_numpy(f["seeds"].astype(np.uint64).view(np.int64)).cuda()
