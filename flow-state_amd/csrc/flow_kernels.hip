@@ -32,6 +32,19 @@
 
 namespace fs {
 
+// timing-only A/B builds (wrong results): FS_TIMING_NO_EPI_VALU stores the accumulators
+// without the BatchNorm / ReLU arithmetic, FS_TIMING_NO_GROUP_BARRIER drops the row-group
+// barriers of the residual blocks
+#ifdef FS_TIMING_NO_EPI_VALU
+#define FS_EPI(v, a, b) (v)
+#else
+#define FS_EPI(v, a, b) fmaxf(fmaf((v), (a), (b)), 0.f)
+#endif
+#ifdef FS_TIMING_NO_GROUP_BARRIER
+#define FS_GROUP_BARRIER(c, ph) ((void)0)
+#else
+#define FS_GROUP_BARRIER(c, ph) group_barrier((c), (ph))
+#endif
 #ifndef FS_RPD
 #define FS_RPD 3  // weight-fragment ring depth of the ResNet GEMMs
 #endif
@@ -216,7 +229,13 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
         float u[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) u[k] = tile_row(acc[0][0], acc[1][0], k);
+#ifdef FS_TIMING_NO_KNOTS  // timing-only A/B build (wrong results): the knot arithmetic removed
+#pragma unroll
+        for (int k = 0; k < K; ++k) ks[k] = u[k];
+        ks[K] = a.B;
+#else
         knots_from_logits<K>(u, ks, INV ? kMinHd : kMinWd, a);
+#endif
     }
     // searchsorted (splines.py:11-13): knots are non-decreasing, so the last k
     // with x >= knot[k] is the bin; the gathered knots ride along the scan
@@ -245,7 +264,13 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
         float u[K], ko[K + 1];
 #pragma unroll
         for (int k = 0; k < K; ++k) u[k] = tile_row(acc[0][0], acc[1][0], k);
+#ifdef FS_TIMING_NO_KNOTS
+#pragma unroll
+        for (int k = 0; k < K; ++k) ko[k] = u[k];
+        ko[K] = a.B;
+#else
         knots_from_logits<K>(u, ko, INV ? kMinWd : kMinHd, a);
+#endif
         o0 = ko[0];
         o1 = ko[1];
 #pragma unroll
@@ -258,6 +283,7 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
     }
     pf.mark(PH_SPLINE);
     const float *xr = X + lane * XS;
+#ifndef FS_TIMING_NO_GATHER  // timing-only A/B build: the derivative dot products removed
 #pragma unroll 1
     for (int q0 = 0; q0 < NQ; q0 += 2 * QB) {
         drows_issue<QB, K>(g1, W, voff, dsec, q0 + QB);
@@ -265,6 +291,9 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
         if (q0 + 2 * QB < NQ) drows_issue<QB, K>(g0, W, voff, dsec, q0 + 2 * QB);
         drows_dot<QB>(g1, xr, q0 + QB, ud0, ud1);
     }
+#else
+    drows_dot<QB>(g0, xr, 0, ud0, ud1);
+#endif
     pf.mark(PH_FINAL_GEMM);
     const float icw = INV ? o0 : s0, cw1 = INV ? o1 : s1;
     const float ich = INV ? s0 : o0, ch1 = INV ? s1 : o1;
@@ -403,7 +432,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
             const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4);
             const int w1 = w0 + (int)(PL.block_stride * 2);
             pf.mark(PH_EPI);
-            group_barrier(gbar + grp, gphase);
+            FS_GROUP_BARRIER(gbar + grp, gphase);
             pf.mark(PH_BARRIER);
             if (gact) {
 #pragma unroll
@@ -411,18 +440,18 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
                     const int col = 32 * (gct0 + ct) + r;
 #pragma unroll
                     for (int i = 0; i < 16; ++i)
-                        X[acc_row(grp, i, h) * XS + col] = fmaxf(fmaf(hr[0][ct][i], ev[0][ct], ev[1][ct]), 0.f);
+                        X[acc_row(grp, i, h) * XS + col] = FS_EPI(hr[0][ct][i], ev[0][ct], ev[1][ct]);
                 }
             }
             pf.mark(PH_EPI);
-            group_barrier(gbar + grp, gphase);
+            FS_GROUP_BARRIER(gbar + grp, gphase);
             pf.mark(PH_BARRIER);
             if (gact) {
                 gemm_run<XS, 1, CTg, FS_RPD>(X, W, w0, PL.kg_h, grp, gct0, br, acc);
                 b_prologue<CTg, FS_RPD>(br, W, w1, PL.kg_h, gct0);  // next GEMM's first weight groups
             }
             pf.mark(PH_RES_GEMM);
-            group_barrier(gbar + grp, gphase);
+            FS_GROUP_BARRIER(gbar + grp, gphase);
             pf.mark(PH_BARRIER);
             if (gact) {
 #pragma unroll
@@ -430,11 +459,11 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
                     const int col = 32 * (gct0 + ct) + r;
 #pragma unroll
                     for (int i = 0; i < 16; ++i)
-                        X[acc_row(grp, i, h) * XS + col] = fmaxf(fmaf(acc[0][ct][i], ev[2][ct], ev[3][ct]), 0.f);
+                        X[acc_row(grp, i, h) * XS + col] = FS_EPI(acc[0][ct][i], ev[2][ct], ev[3][ct]);
                 }
             }
             pf.mark(PH_EPI);
-            group_barrier(gbar + grp, gphase);
+            FS_GROUP_BARRIER(gbar + grp, gphase);
             pf.mark(PH_BARRIER);
             float evn[4][CTg];
             if (jb + 1 < a.nb) load_ev(jb + 1, evn);
@@ -449,7 +478,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
                     for (int ct = 0; ct < CTg; ++ct) ev[q][ct] = evn[q][ct];
             pf.mark(PH_RES_GEMM);
         }
-        group_barrier(gbar + grp, gphase);
+        FS_GROUP_BARRIER(gbar + grp, gphase);
         pf.mark(PH_BARRIER);
         if (gact) {  // X <- h (+ the deferred biases) for the final layer
 #pragma unroll
