@@ -310,7 +310,7 @@ __global__ void __launch_bounds__(256) mh_accept_kernel(fs_phys p, int64_t C, in
 // against the np.float64 box lengths, rounded back), r = np.linalg.norm(delta) (the
 // float32 sdot / float64 ddot, correctly rounded sqrt), both widened to float64.
 template <bool F32>
-__global__ void min_image_kernel(fs_phys p, PairThresh T, const void *__restrict__ a, int64_t sa,
+__global__ void __launch_bounds__(256) min_image_kernel(fs_phys p, PairThresh T, const void *__restrict__ a, int64_t sa,
                                  const void *__restrict__ b, int64_t n, double *__restrict__ delta,
                                  double *__restrict__ r) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -343,7 +343,7 @@ __global__ void min_image_kernel(fs_phys p, PairThresh T, const void *__restrict
 // LJ terms (numpy's pairwise order) + the particle's double-well term.  One thread per
 // chain (an API call, not the local-move hot loop, which has its own kernel).
 template <bool F32>
-__global__ void particle_energy_kernel(fs_phys p, PairThresh T, const void *__restrict__ pos, int64_t C, int N,
+__global__ void __launch_bounds__(64) particle_energy_kernel(fs_phys p, PairThresh T, const void *__restrict__ pos, int64_t C, int N,
                                        const int32_t *__restrict__ part, double *__restrict__ E,
                                        double *__restrict__ W) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -523,11 +523,11 @@ hipError_t fs_particle_energy_impl(const fs_phys *p, const void *pos, int f32, i
                                    double *E, double *W, hipStream_t st) {
     if (C <= 0) return hipSuccess;
     const PairThresh T = fs_pair_thresh(*p);
-    const dim3 grid((unsigned)((C + 255) / 256));
+    const dim3 grid((unsigned)((C + 63) / 64));
     if (f32)
-        hipLaunchKernelGGL(particle_energy_kernel<true>, grid, dim3(256), 0, st, *p, T, pos, C, N, part, E, W);
+        hipLaunchKernelGGL(particle_energy_kernel<true>, grid, dim3(64), 0, st, *p, T, pos, C, N, part, E, W);
     else
-        hipLaunchKernelGGL(particle_energy_kernel<false>, grid, dim3(256), 0, st, *p, T, pos, C, N, part, E, W);
+        hipLaunchKernelGGL(particle_energy_kernel<false>, grid, dim3(64), 0, st, *p, T, pos, C, N, part, E, W);
     return hipGetLastError();
 }
 
