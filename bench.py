@@ -116,6 +116,26 @@ def alt_precisions(bmc, stepper, steps=3):
                      "roofline": {"bound": "mfma", "achieved": ach, "peak": peak,
                                   "unit": "TFLOP/s (f32-equivalent)", "frac": ach / peak,
                                   "kernel": f"flow_split_kernel<256,32,*,{3 if nprod == 6 else 2}>"}}
+    # proposals drawn through the bf16x6 image, log q (the parity-relevant value) by the
+    # f32 kernel: the proposal pass only produces the draws, whose stream differs from the
+    # reference's anyway (in-kernel Philox vs torch's generator)
+    model.set_precision("bf16x6")
+    img = (model.dims(), model.packed())
+    model.set_precision("f32")
+    st = Stepper(bmc, propose_image=img)
+    st.step(timed=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st.step(timed=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st.harvest()
+    t_prop, t_lp, t_en, t_acc = st.t / steps
+    out["propose_bf16x6_log_prob_f32"] = {
+        "value": C * steps / dt, "unit": "steps/s", "steps": steps, "ms_per_step": dt / steps * 1e3,
+        "kernel_ms": {"flow_propose": t_prop, "flow_log_prob": t_lp, "energy": t_en, "mh_accept": t_acc},
+        "what": "proposal pass on the bf16x6 image, density pass (log q) on the f32 kernel"}
     model.set_precision(base)
     return out
 
@@ -147,11 +167,13 @@ def given_proposal(bmc, stepper, steps=3):
 class Stepper:
     """The fs_nf_mh_step kernel sequence, launched piecewise with HIP events."""
 
-    def __init__(self, bmc):
+    def __init__(self, bmc, propose_image=None):
         self.b = bmc
         self.L = _lib.load()
         self.dims = bmc.model.dims()
         self.packed = bmc.model.packed()
+        # (dims, packed) of another precision's image for the proposal pass only
+        self.pdims, self.ppacked = propose_image if propose_image else (self.dims, self.packed)
         C, D = bmc.C, 2 * bmc.N
         dev = bmc.device
         self.config = torch.empty((C, D), dtype=torch.float32, device=dev)
@@ -169,7 +191,7 @@ class Stepper:
         if timed:
             self.events.append(ev)
             ev[0].record()
-        _lib.check(L.fs_flow_propose(self.dims, p(self.packed), b.C, b.proposal_seed, b.step_count, b.chain_offset,
+        _lib.check(L.fs_flow_propose(self.pdims, p(self.ppacked), b.C, b.proposal_seed, b.step_count, b.chain_offset,
                                      b.phys.half_width, p(self.config), p(self.centered), None, p(b.err), st))
         if timed:
             ev[1].record()
