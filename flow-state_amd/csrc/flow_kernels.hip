@@ -386,7 +386,9 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
             __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
         if (MODE != MODE_DENSITY) {
             off = (off + N) % D;  // Coupling.inverse rolls first (coupling.py:113-114)
+#ifndef FS_TIMING_NO_UNC  // timing-only A/B build (wrong results): no unconditional spline
             ld += uncond_spline<K, true>(P + PL.unc, CO, cs, N, D, off, a, nan_any);
+#endif
             pf.mark(PH_UNCOND);
             __syncthreads();
             pf.mark(PH_BARRIER);
@@ -395,8 +397,13 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
         for (int f = wid; f < N; f += kWaves) {
             const float v = CO[lane * cs + (2 * f + off) % D];
             const float sv = a.scale_pf * v;
+#ifdef FS_TIMING_NO_PF  // timing-only A/B build (wrong results): no cos / sin
+            X[lane * XS + f] = sv;
+            X[lane * XS + N + f] = sv;
+#else
             X[lane * XS + f] = cosf(sv);
             X[lane * XS + N + f] = sinf(sv);
+#endif
         }
         for (int c = D + wid; c < 8 * PL.kg_in; c += kWaves) X[lane * XS + c] = 0.f;
         pf.mark(PH_PF);
@@ -498,14 +505,20 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
             for (int z = 0; z < FS_STAGGER; ++z) __builtin_amdgcn_s_sleep(127);
 #endif
         // final layer + conditional spline, feature by feature
+#ifdef FS_TIMING_NO_FINAL  // timing-only A/B build (wrong results): no final layer / conditional spline
+        for (int j = wid; j < 0; j += kWaves) {
+#else
         for (int j = wid; j < N; j += kWaves) {
+#endif
             const int p = (2 * j + 1 + off) % D;
             ld += cond_spline<XS, H, K, MODE != MODE_DENSITY>(
                 X, W, (int)(PL.wf * 4), PL.kg_h, V + PL.v_bf + 96 * j, (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
                 V + PL.v_bd + j * (K + 1), CO, cs, p, j, a, nan_any, pf);
         }
         if (MODE == MODE_DENSITY) {
+#ifndef FS_TIMING_NO_UNC
             ld += uncond_spline<K, false>(P + PL.unc, CO, cs, N, D, off, a, nan_any);
+#endif
             off = (off + N) % D;  // Coupling.forward rolls last (coupling.py:100-101)
             pf.mark(PH_UNCOND);
         }
