@@ -477,6 +477,39 @@ __global__ void hist2d_kernel(const double *__restrict__ pos, int64_t C, int N, 
     atomicAdd(&hist[bx * nb + by], 1ull);
 }
 
+// The same histogram with a private LDS copy per workgroup (uint32 counters, edges in LDS),
+// one workgroup per CU walking the points grid-stride, and one global atomic per non-empty
+// bin at the end: the points of many chains land in the same bins (the wells, the lattice),
+// which serialises global atomics.  nb <= kHistLdsBins (LDS budget).
+constexpr int kHistLdsBins = 120;
+__global__ void __launch_bounds__(1024) hist2d_lds_kernel(const double *__restrict__ pos, int64_t n, double shift,
+                                                          const double *__restrict__ edges, int nb,
+                                                          unsigned long long *__restrict__ hist) {
+    __shared__ unsigned int h[kHistLdsBins * kHistLdsBins];
+    __shared__ double e[kHistLdsBins + 1];
+    for (int i = threadIdx.x; i < nb * nb; i += blockDim.x) h[i] = 0u;
+    for (int i = threadIdx.x; i <= nb; i += blockDim.x) e[i] = edges[i];
+    __syncthreads();
+    auto bin_of = [&](double v) {  // np.searchsorted(edges, v, 'right') - 1, last edge inclusive
+        int lo = 0, hi = nb + 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (e[mid] <= v) lo = mid + 1;
+            else hi = mid;
+        }
+        int b = lo;
+        if (v == e[nb]) b -= 1;
+        return b - 1;
+    };
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        const int bx = bin_of(pos[2 * t] - shift), by = bin_of(pos[2 * t + 1] - shift);
+        if (bx >= 0 && bx < nb && by >= 0 && by < nb) atomicAdd(&h[bx * nb + by], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nb * nb; i += blockDim.x)
+        if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
+}
+
 }  // namespace fs
 
 using namespace fs;
@@ -555,8 +588,17 @@ hipError_t fs_hist2d_impl(const double *pos, int64_t C, int N, double shift, con
                           int64_t *hist, hipStream_t st) {
     const int64_t n = C * N;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(hist2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pos, C, N, shift,
-                       edges, nb, (unsigned long long *)hist);
+    if (nb <= kHistLdsBins) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const int64_t want = (n + 1023) / 1024;
+        const unsigned blocks = (unsigned)(want < cus ? (want > 0 ? want : 1) : cus);
+        hipLaunchKernelGGL(hist2d_lds_kernel, dim3(blocks), dim3(1024), 0, st, pos, n, shift, edges, nb,
+                           (unsigned long long *)hist);
+    } else {
+        hipLaunchKernelGGL(hist2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pos, C, N, shift,
+                           edges, nb, (unsigned long long *)hist);
+    }
     return hipGetLastError();
 }
 

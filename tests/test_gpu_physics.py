@@ -182,6 +182,27 @@ def test_hist2d_and_well_stats():
     assert c[0].tolist() == [1, 0, 1] and c[1].tolist() == [0, 1, 1] and c[2:, :2].sum() == 0
 
 
+@pytest.mark.parametrize("nedges", [100, 151])
+def test_hist2d_clustered_large(nedges):
+    """fs_hist2d on 16384 chains x 64 particles crowded into few bins (lattice + jitter,
+    many chains per bin): the LDS-privatised kernel (nb <= 120) and the global-atomic one
+    (nb = 150) against np.histogram2d."""
+    N, C = 64, 16384
+    L = float(np.sqrt(N / 0.03))
+    B = L / 2
+    rng = np.random.default_rng(5)
+    pos = np.mod(OP.fcc_lattice(N)[None] + rng.normal(0, 0.3, (C, N, 2)), L)
+    pos[:64, 0] = [L, L]  # on the right / top edge after centring: the last bin is right-inclusive
+    pos[64:128, 0] = [L + 1.0, 0.5]  # outside the edges: dropped
+    edges = np.linspace(-B, B, nedges)
+    want, _, _ = np.histogram2d((pos - B).reshape(-1, 2)[:, 0], (pos - B).reshape(-1, 2)[:, 1], bins=[edges, edges])
+    hist = torch.zeros((nedges - 1) ** 2, dtype=torch.int64, device="cuda")
+    _lib.check(_lib.load().fs_hist2d(_lib.ptr(torch.from_numpy(pos).cuda()), C, N, B,
+                                     _lib.ptr(torch.from_numpy(edges).cuda()), nedges - 1, _lib.ptr(hist),
+                                     _lib.stream_ptr()))
+    np.testing.assert_array_equal(hist.cpu().numpy().reshape(nedges - 1, nedges - 1), want.astype(np.int64))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("half_box_scale", [1.0, 0.8])
 def test_well_stats_matches_classify_particles(half_box_scale):
