@@ -15,7 +15,7 @@ from flowstate import _lib  # noqa: E402
 from bench import synthetic_model  # noqa: E402
 
 N, C = 64, 65536
-model = synthetic_model(N, torch.device("cuda"))
+model = synthetic_model(N, torch.device("cuda")).set_precision(os.environ.get("FS_PREC", "f32"))
 dims, packed = model.dims(), model.packed()
 x = ((torch.rand((C, 2 * N), device="cuda") * 2 - 1) * 23.0).contiguous()
 lq = torch.empty(C, device="cuda")
