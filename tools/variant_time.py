@@ -46,6 +46,20 @@ for arg in sys.argv[1:]:
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
         res[mode] = round(min(ts), 3)
+    if os.environ.get("FS_CHECK"):  # bit-compare the density pass and the proposals with the base build
+        Lb = _lib.load()
+        outs = []
+        for LL in (Lb, L):
+            q = torch.empty(C, device="cuda")
+            cf = torch.empty_like(x)
+            LL.fs_flow_log_prob(dims, _lib.ptr(packed), _lib.ptr(x), C, _lib.ptr(q), None, _lib.ptr(err),
+                                _lib.stream_ptr())
+            LL.fs_flow_propose(dims, _lib.ptr(packed), C, 77, 3, 0, 23.0, _lib.ptr(cf), _lib.ptr(cen), None,
+                               _lib.ptr(err), _lib.stream_ptr())
+            torch.cuda.synchronize()
+            outs.append((q.clone(), cf.clone()))
+        res["log_q_bit_identical"] = bool(torch.equal(outs[0][0], outs[1][0]))
+        res["proposals_bit_identical"] = bool(torch.equal(outs[0][1], outs[1][1]))
     out[arg] = res
     print(arg, res, flush=True)
 print(json.dumps(out))
