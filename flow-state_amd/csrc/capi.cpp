@@ -105,7 +105,7 @@ int fs_flow_propose(const fs_flow_dims *d, const void *packed, int64_t B, uint64
                     int32_t *err, void *stream) {
     int rc = check_dims(d);
     if (rc) return rc;
-    REQUIRE(packed && B >= 0 && (config || centered || x_out), "fs_flow_propose: invalid arguments");
+    REQUIRE(B >= 0 && (B == 0 || (packed && (config || centered || x_out))), "fs_flow_propose: invalid arguments");
     return hip_rc(fs_flow_pass_impl(d, packed, 2, nullptr, B, x_out, nullptr, 0, config, centered, seed, counter,
                                     row_offset, half_width, err, (hipStream_t)stream),
                   "fs_flow_propose");
@@ -113,7 +113,7 @@ int fs_flow_propose(const fs_flow_dims *d, const void *packed, int64_t B, uint64
 
 int fs_energy_lj_dw(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int32_t N, double *E, double *W,
                     uint8_t *overlap, uint64_t *nbr, void *stream) {
-    REQUIRE(p && pos && E && C >= 0, "fs_energy_lj_dw: invalid arguments");
+    REQUIRE(p && C >= 0 && (C == 0 || (pos && E)), "fs_energy_lj_dw: invalid arguments");
     REQUIRE(N >= 1 && N <= fs::kMaxN, "fs_energy_lj_dw: N=%d outside [1, %d]", N, fs::kMaxN);
     REQUIRE(p->Lx > 0 && p->Ly > 0, "fs_energy_lj_dw: box must be positive");
     return hip_rc(fs_energy_impl(p, pos, pos_is_f32, C, N, E, W, overlap, nbr, (hipStream_t)stream),
@@ -121,12 +121,12 @@ int fs_energy_lj_dw(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C
 }
 
 int fs_pcg64_seed(const uint64_t *seeds, int64_t C, uint64_t *state, void *stream) {
-    REQUIRE(seeds && state && C >= 0, "fs_pcg64_seed: invalid arguments");
+    REQUIRE(C >= 0 && (C == 0 || (seeds && state)), "fs_pcg64_seed: invalid arguments");
     return hip_rc(fs_pcg64_seed_impl(seeds, C, state, (hipStream_t)stream), "fs_pcg64_seed");
 }
 
 int fs_pcg64_random(uint64_t *state, int64_t C, double *out, void *stream) {
-    REQUIRE(state && out && C >= 0, "fs_pcg64_random: invalid arguments");
+    REQUIRE(C >= 0 && (C == 0 || (state && out)), "fs_pcg64_random: invalid arguments");
     return hip_rc(fs_pcg64_random_impl(state, C, out, (hipStream_t)stream), "fs_pcg64_random");
 }
 
@@ -134,7 +134,7 @@ int fs_mh_accept(const fs_phys *p, int64_t C, int32_t N, double *E_old, double *
                  const double *E_new, const double *W_new, const float *log_q_new, uint64_t *pcg, double *state,
                  uint8_t *state_is_f32, const float *config, uint8_t *accept, int64_t *attempts, int64_t *accepted,
                  unsigned long long *n_accept, int flags, void *stream) {
-    REQUIRE(p && E_old && nll_old && E_new && log_q_new && pcg && accept && C >= 0,
+    REQUIRE(p && C >= 0 && (C == 0 || (E_old && nll_old && E_new && log_q_new && pcg && accept)),
             "fs_mh_accept: invalid arguments");
     REQUIRE(N >= 1 && N <= fs::kMaxN, "fs_mh_accept: N=%d outside [1, %d]", N, fs::kMaxN);
     REQUIRE((state == nullptr) == (config == nullptr), "fs_mh_accept: state and config go together");
@@ -146,7 +146,7 @@ int fs_mh_accept(const fs_phys *p, int64_t C, int32_t N, double *E_old, double *
 
 int fs_min_image(const fs_phys *p, const void *pos1, int64_t stride1, const void *pos2, int pos_is_f32, int64_t n,
                  double *delta, double *r, void *stream) {
-    REQUIRE(p && pos1 && pos2 && n >= 0 && (stride1 == 0 || stride1 == 1), "fs_min_image: invalid arguments");
+    REQUIRE(p && n >= 0 && (n == 0 || (pos1 && pos2)) && (stride1 == 0 || stride1 == 1), "fs_min_image: invalid arguments");
     REQUIRE(p->Lx > 0 && p->Ly > 0, "fs_min_image: box lengths must be positive");
     return hip_rc(fs_min_image_impl(p, pos1, stride1, pos2, pos_is_f32, n, delta, r, (hipStream_t)stream),
                   "fs_min_image");
@@ -154,7 +154,7 @@ int fs_min_image(const fs_phys *p, const void *pos1, int64_t stride1, const void
 
 int fs_particle_energy(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int32_t N,
                        const int32_t *particle, double *E, double *W, void *stream) {
-    REQUIRE(p && pos && particle && E && W && C >= 0, "fs_particle_energy: invalid arguments");
+    REQUIRE(p && C >= 0 && (C == 0 || (pos && particle && E && W)), "fs_particle_energy: invalid arguments");
     REQUIRE(N >= 2 && N <= fs::kMaxN, "fs_particle_energy: N=%d outside [2, %d]", N, fs::kMaxN);
     return hip_rc(fs_particle_energy_impl(p, pos, pos_is_f32, C, N, particle, E, W, (hipStream_t)stream),
                   "fs_particle_energy");
@@ -162,7 +162,7 @@ int fs_particle_energy(const fs_phys *p, const void *pos, int pos_is_f32, int64_
 
 int fs_metropolis_judge(double beta, int64_t C, int64_t M, const double *E_ref, const double *E_new, uint64_t *pcg,
                         uint8_t *accept, int64_t *n_accept, void *stream) {
-    REQUIRE(E_ref && E_new && pcg && C >= 0 && M >= 0, "fs_metropolis_judge: invalid arguments");
+    REQUIRE(C >= 0 && M >= 0 && (C == 0 || (E_ref && pcg && (M == 0 || E_new))), "fs_metropolis_judge: invalid arguments");
     REQUIRE(beta == beta, "fs_metropolis_judge: beta is NaN");
     return hip_rc(fs_metropolis_judge_impl(beta, C, M, E_ref, E_new, pcg, accept, n_accept, (hipStream_t)stream),
                   "fs_metropolis_judge");
@@ -182,8 +182,9 @@ int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, i
                   unsigned long long *n_accept, int32_t *err, int flags, void *ws, void *stream) {
     int rc = check_dims(d);
     if (rc) return rc;
-    REQUIRE(packed && p && E_old && nll_old && pcg && accept && ws && C >= 0, "fs_nf_mh_step: invalid arguments");
+    REQUIRE(p && C >= 0 && (C == 0 || (packed && E_old && nll_old && pcg && accept && ws)), "fs_nf_mh_step: invalid arguments");
     REQUIRE(((uintptr_t)ws & 255) == 0, "fs_nf_mh_step: workspace must be 256-byte aligned");
+    if (C == 0) return FS_OK;
     const int64_t D = 2 * d->N;
     char *w = (char *)ws;
     float *config = (float *)w;
@@ -234,8 +235,8 @@ int fs_local_moves(const fs_phys *p, int64_t C, int32_t N, double *state, const 
                    int64_t *accepted, int64_t *prev_counts, int64_t n_moves, int64_t step0, int32_t adjust_every,
                    double target_acceptance, int32_t sample_every, double *samples_xy, double *samples_ew,
                    uint8_t *accept_log, unsigned long long *n_accept, void *stream) {
-    REQUIRE(p && state && E && pcg && pcg_buf && max_disp && attempts && accepted && C >= 0 && n_moves >= 0 &&
-                step0 >= 0,
+    REQUIRE(p && C >= 0 && n_moves >= 0 && step0 >= 0 &&
+                (C == 0 || (state && E && pcg && pcg_buf && max_disp && attempts && accepted)),
             "fs_local_moves: invalid arguments");
     REQUIRE(N >= 1 && N <= fs::kMaxN, "fs_local_moves: N=%d outside [1, %d]", N, fs::kMaxN);
     REQUIRE(adjust_every <= 0 || (prev_counts && target_acceptance > 0.0),
@@ -250,7 +251,7 @@ int fs_local_moves(const fs_phys *p, int64_t C, int32_t N, double *state, const 
 
 int fs_adjust_displacement(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,
                            int64_t *prev_counts, double target_acceptance, void *stream) {
-    REQUIRE(max_disp && attempts && accepted && prev_counts && C >= 0 && target_acceptance > 0.0,
+    REQUIRE(C >= 0 && target_acceptance > 0.0 && (C == 0 || (max_disp && attempts && accepted && prev_counts)),
             "fs_adjust_displacement: invalid arguments");
     return hip_rc(fs_adjust_displacement_impl(C, max_disp, attempts, accepted, prev_counts, target_acceptance,
                                               (hipStream_t)stream),
@@ -259,20 +260,20 @@ int fs_adjust_displacement(int64_t C, double *max_disp, const int64_t *attempts,
 
 int fs_hist2d(const double *pos, int64_t C, int32_t N, double shift, const double *edges, int32_t nbins,
               int64_t *hist, void *stream) {
-    REQUIRE(pos && edges && hist && C >= 0 && N >= 1 && nbins >= 1, "fs_hist2d: invalid arguments");
+    REQUIRE(edges && hist && C >= 0 && N >= 1 && nbins >= 1 && (C == 0 || pos), "fs_hist2d: invalid arguments");
     return hip_rc(fs_hist2d_impl(pos, C, N, shift, edges, nbins, hist, (hipStream_t)stream), "fs_hist2d");
 }
 
 int fs_well_stats(const double *pos, const uint8_t *state_is_f32, int64_t C, int32_t N, double half_box, double r0,
                   int64_t *counts, void *stream) {
-    REQUIRE(pos && counts && C >= 0 && N >= 1 && half_box > 0, "fs_well_stats: invalid arguments");
+    REQUIRE(C >= 0 && N >= 1 && half_box > 0 && (C == 0 || (pos && counts)), "fs_well_stats: invalid arguments");
     return hip_rc(fs_well_stats_impl(pos, state_is_f32, C, N, half_box, r0, counts, (hipStream_t)stream),
                   "fs_well_stats");
 }
 
 int fs_rqs_forward(int64_t M, int32_t K, int32_t inverse, const float *x, const float *uw, const float *uh,
                    const float *ud, double tail_bound, float *out, float *lad, int32_t *nan_flag, void *stream) {
-    REQUIRE(M >= 0 && x && uw && uh && ud && out && lad && tail_bound > 0, "fs_rqs_forward: invalid arguments");
+    REQUIRE(M >= 0 && tail_bound > 0 && (M == 0 || (x && uw && uh && ud && out && lad)), "fs_rqs_forward: invalid arguments");
     REQUIRE(K == 5 || K == 8 || K == 15 || K == 32, "fs_rqs_forward: K=%d not instantiated (5, 8, 15, 32)", K);
     return hip_rc(fs_rqs_forward_impl(M, K, inverse, x, uw, uh, ud, (float)tail_bound, out, lad, nan_flag,
                                       (hipStream_t)stream),
@@ -282,7 +283,7 @@ int fs_rqs_forward(int64_t M, int32_t K, int32_t inverse, const float *x, const 
 int fs_rqs_backward(int64_t M, int32_t K, int32_t inverse, const float *x, const float *uw, const float *uh,
                     const float *ud, double tail_bound, const float *g_out, const float *g_lad, float *gx,
                     float *guw, float *guh, float *gud, void *stream) {
-    REQUIRE(M >= 0 && x && uw && uh && ud && gx && guw && guh && gud && tail_bound > 0,
+    REQUIRE(M >= 0 && tail_bound > 0 && (M == 0 || (x && uw && uh && ud && gx && guw && guh && gud)),
             "fs_rqs_backward: invalid arguments");
     REQUIRE(K == 5 || K == 8 || K == 15 || K == 32, "fs_rqs_backward: K=%d not instantiated (5, 8, 15, 32)", K);
     return hip_rc(fs_rqs_backward_impl(M, K, inverse, x, uw, uh, ud, (float)tail_bound, g_out, g_lad, gx, guw, guh,
@@ -292,14 +293,14 @@ int fs_rqs_backward(int64_t M, int32_t K, int32_t inverse, const float *x, const
 
 int fs_classify_wells(const void *pos, int pos_is_f32, int64_t M, int32_t N, double half_box, double r0,
                       uint8_t *cls, uint8_t *state, double *avg_x, void *stream) {
-    REQUIRE(pos && M >= 0 && N >= 1 && half_box > 0.0, "fs_classify_wells: invalid arguments");
+    REQUIRE(M >= 0 && N >= 1 && half_box > 0.0 && (M == 0 || pos), "fs_classify_wells: invalid arguments");
     return hip_rc(fs_classify_wells_impl(pos, pos_is_f32, M, N, half_box, r0, cls, state, avg_x, (hipStream_t)stream),
                   "fs_classify_wells");
 }
 
 int fs_pair_hist(const void *pos, int pos_is_f32, int64_t M, int32_t N, double bound, const double *edges,
                  int32_t nbins, int32_t *counts, void *stream) {
-    REQUIRE(pos && edges && counts && M >= 0 && N >= 1 && bound > 0.0, "fs_pair_hist: invalid arguments");
+    REQUIRE(edges && M >= 0 && N >= 1 && bound > 0.0 && (M == 0 || (pos && counts)), "fs_pair_hist: invalid arguments");
     REQUIRE(N <= 256 && nbins >= 1 && nbins <= 128, "fs_pair_hist: N <= 256 and 1 <= nbins <= 128 (got %d, %d)", N,
             nbins);
     return hip_rc(fs_pair_hist_impl(pos, pos_is_f32, M, N, bound, edges, nbins, counts, (hipStream_t)stream),
