@@ -313,3 +313,33 @@ int fs_rdf_mean(const int32_t *counts, int64_t M, int32_t nbins, const double *d
 }
 
 }  // extern "C"
+
+int fs_linear_f32(int64_t M, int64_t N, int64_t K, const float *A, int64_t sam, int64_t sak, const float *B,
+                  int64_t sbk, int64_t sbn, const float *bias, const float *R, int64_t ldr, float *C, int64_t ldc,
+                  float *rowsum_a, void *stream) {
+    REQUIRE(M >= 0 && N >= 0 && K >= 0 && (M == 0 || N == 0 || (C && (K == 0 || (A && B)))) && ldc >= N && (!R || ldr >= N),
+            "fs_linear_f32: invalid arguments");
+    REQUIRE(M <= 32LL * 65535 && N <= 32LL * 65535, "fs_linear_f32: M, N at most %lld", 32LL * 65535);
+    fs::GemmArgs g{M, N, K, A, sam, sak, B, sbk, sbn, bias, R, ldr, C, ldc, rowsum_a};
+    return hip_rc(fs_linear_f32_impl(g, (hipStream_t)stream), "fs_linear_f32");
+}
+
+int fs_bn_relu_train_fwd(int64_t Bn, int32_t H, const float *x, const float *gamma, const float *beta,
+                         float *running_mean, float *running_var, int64_t *num_batches, double momentum, double eps,
+                         float *y, float *mean, float *invstd, void *stream) {
+    REQUIRE(Bn >= 2 && H >= 1 && x && gamma && beta && y && mean && invstd && eps > 0.0,
+            "fs_bn_relu_train_fwd: invalid arguments");
+    REQUIRE((running_mean == nullptr) == (running_var == nullptr), "fs_bn_relu_train_fwd: running stats go together");
+    return hip_rc(fs_bn_relu_train_fwd_impl(Bn, H, x, gamma, beta, running_mean, running_var, num_batches,
+                                            (float)momentum, (float)eps, y, mean, invstd, (hipStream_t)stream),
+                  "fs_bn_relu_train_fwd");
+}
+
+int fs_bn_relu_train_bwd(int64_t Bn, int32_t H, const float *x, const float *y, const float *dy, const float *gamma,
+                         const float *mean, const float *invstd, float *dx, float *dgamma, float *dbeta, void *stream) {
+    REQUIRE(Bn >= 2 && H >= 1 && x && y && dy && gamma && mean && invstd && dx,
+            "fs_bn_relu_train_bwd: invalid arguments");
+    return hip_rc(fs_bn_relu_train_bwd_impl(Bn, H, x, y, dy, gamma, mean, invstd, dx, dgamma, dbeta,
+                                            (hipStream_t)stream),
+                  "fs_bn_relu_train_bwd");
+}

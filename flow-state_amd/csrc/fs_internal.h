@@ -79,3 +79,28 @@ inline hipError_t fs_set_max_lds_once(const void *kfn, std::atomic<unsigned long
     if (e == hipSuccess && bit) done.fetch_or(bit, std::memory_order_release);
     return e;
 }
+
+// training conditioner pieces (train_kernels.hip): C = A . B (+ bias) (+ R), A[m][k] at
+// A[m sam + k sak], B[k][n] at B[k sbk + n sbn]; rowsum_a (nullable) = sum_k A[m][k]
+namespace fs {
+struct GemmArgs {
+    int64_t M, N, K;
+    const float *A;
+    int64_t sam, sak;
+    const float *B;
+    int64_t sbk, sbn;
+    const float *bias;
+    const float *R;
+    int64_t ldr;
+    float *C;
+    int64_t ldc;
+    float *rowsum_a;
+};
+}  // namespace fs
+hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st);
+hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,
+                                     float *rm, float *rv, int64_t *nbt, float momentum, float eps, float *y,
+                                     float *mean, float *invstd, hipStream_t st);
+hipError_t fs_bn_relu_train_bwd_impl(int64_t B, int H, const float *x, const float *y, const float *dy,
+                                     const float *gamma, const float *mean, const float *invstd, float *dx,
+                                     float *dgamma, float *dbeta, hipStream_t st);

@@ -590,7 +590,7 @@ hipError_t fs_hist2d_impl(const double *pos, int64_t C, int N, double shift, con
     if (n <= 0) return hipSuccess;
     if (nb <= kHistLdsBins) {
         int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const int64_t want = (n + 1023) / 1024;
         const unsigned blocks = (unsigned)(want < cus ? (want > 0 ? want : 1) : cus);
         hipLaunchKernelGGL(hist2d_lds_kernel, dim3(blocks), dim3(1024), 0, st, pos, n, shift, edges, nb,

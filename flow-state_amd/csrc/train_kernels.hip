@@ -1,0 +1,237 @@
+// Conditioner pieces of the Algorithm-2 training step (SURVEY §8(f) row 4,
+// hybrid_NF_MCMC/main_algorithm_2.py:314-331) on the A2 shapes: batch 256, H = 128.
+//
+// gemm_f32_kernel: C = A . B (+ bias[n]) (+ R), exact f32 (v_mfma_f32_32x32x2_f32), A and B
+// strided so that one kernel serves nn.Linear's forward (X W^T), its input gradient (dY W)
+// and its weight gradient (dY^T X).  hipBLASLt runs a 256 x 128 x 128 product as one or two
+// 128 x 256 macro tiles on one or two CUs (19 us); here every 32 x 32 output tile is one
+// workgroup whose SPLIT waves share the reduction dimension and add their partial tiles in a
+// fixed order (deterministic), so the same product spreads over 32 workgroups.
+// The optional rowsum_a output (= sum_k A[m][k], written by the workgroups of the first
+// column tile) is nn.Linear's bias gradient when A = dY^T.
+//
+// bn_relu_train_*: BatchNorm1d in train mode followed by ReLU (resnet.py:35-51, the
+// block's batch_norm_layers[i] then the activation), forward and backward.  A workgroup
+// owns 16 feature columns over the whole batch, so the batch statistics are workgroup
+// reductions in a fixed order: two-pass mean / biased variance, running statistics
+// updated as torch does (momentum, unbiased variance), num_batches_tracked += 1.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "fs_internal.h"
+
+namespace fs {
+
+typedef float t4 __attribute__((ext_vector_type(4)));
+typedef float t16 __attribute__((ext_vector_type(16)));
+
+
+// lane (r = lane & 31, h = lane >> 5) supplies A[m0 + r][kb + 4h + j] and B[kb + 4h + j][n0 + r]
+// for MFMA step j = 0..3 of the 8-wide k-block kb (A and B use the same k order).
+template <bool CONTIG>
+__device__ __forceinline__ t4 load4(const float *p, int64_t stride, int64_t k0, int64_t K, bool ok) {
+    t4 v = {0.f, 0.f, 0.f, 0.f};
+    if (!ok) return v;  // no address outside the operand is formed (an empty operand may be NULL)
+    if (CONTIG && k0 + 3 < K) {
+        v = *(const t4 *)(p + k0);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (k0 + j < K) v[j] = p[(k0 + j) * stride];
+    }
+    return v;
+}
+
+template <int SPLIT, bool AK, bool BK>
+__global__ __launch_bounds__(64 * SPLIT) void gemm_f32_kernel(GemmArgs g) {
+    __shared__ t16 part[SPLIT > 1 ? SPLIT - 1 : 1][64];
+    __shared__ float rs_part[SPLIT][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t m0 = (int64_t)blockIdx.x * 32, n0 = (int64_t)blockIdx.y * 32;
+    const bool aok = m0 + r < g.M, bok = n0 + r < g.N;
+    const float *Ap = aok ? g.A + (m0 + r) * g.sam : g.A;
+    const float *Bp = bok ? g.B + (n0 + r) * g.sbn : g.B;
+    const bool rows = g.rowsum_a != nullptr && blockIdx.y == 0;
+    t16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    float rs = 0.f;
+    const int64_t step = 8 * SPLIT;
+    int64_t kb = 8 * w;
+    t4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+    if (kb < g.K) {
+        a = load4<AK>(Ap, g.sak, kb + 4 * h, g.K, aok);
+        b = load4<BK>(Bp, g.sbk, kb + 4 * h, g.K, bok);
+    }
+    for (; kb < g.K; kb += step) {
+        t4 an = a, bn = b;
+        if (kb + step < g.K) {  // next k-block in flight under this one's MFMAs
+            an = load4<AK>(Ap, g.sak, kb + step + 4 * h, g.K, aok);
+            bn = load4<BK>(Bp, g.sbk, kb + step + 4 * h, g.K, bok);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
+        if (rows) rs += ((a[0] + a[1]) + a[2]) + a[3];
+        a = an;
+        b = bn;
+    }
+    if (SPLIT > 1) {
+        if (w > 0) part[w - 1][lane] = acc;
+        if (rows) rs_part[w][lane] = rs;
+        __syncthreads();
+        if (w > 0) return;
+#pragma unroll 1
+        for (int p = 0; p < SPLIT - 1; ++p) acc += part[p][lane];
+        if (rows) {
+#pragma unroll
+            for (int p = 1; p < SPLIT; ++p) rs += rs_part[p][lane];
+        }
+    }
+    if (rows) {  // the two k-halves of row m0 + r live in lanes r and r + 32
+        rs += __shfl_xor(rs, 32);
+        if (h == 0 && aok) g.rowsum_a[m0 + r] = rs;
+    }
+    const int64_t col = n0 + r;
+    if (!bok) return;
+    const float bias = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
+        if (row < g.M) {
+            float v = acc[i] + bias;
+            if (g.R) v = v + g.R[row * g.ldr + col];
+            g.C[row * g.ldc + col] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// BatchNorm1d (train) + ReLU.  Workgroup = 16 columns x 16 row groups.
+constexpr int kBnCols = 16, kBnRg = 16;
+
+__device__ __forceinline__ float wg_colsum(float v, float (*red)[kBnCols], int c, int rg) {
+    red[rg][c] = v;
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < kBnRg; ++q) s += red[q][c];
+    __syncthreads();
+    return s;
+}
+
+__global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_fwd_kernel(
+    int64_t B, int H, const float *__restrict__ x, const float *__restrict__ gamma, const float *__restrict__ beta,
+    float *running_mean, float *running_var, int64_t *num_batches, float momentum, float eps, float *__restrict__ y,
+    float *__restrict__ mean_out, float *__restrict__ invstd_out) {
+    __shared__ float red[kBnRg][kBnCols];
+    const int c = threadIdx.x % kBnCols, rg = threadIdx.x / kBnCols;
+    const int col = blockIdx.x * kBnCols + c;
+    const bool ok = col < H;
+    const float *xc = x + (ok ? col : 0);
+    float s = 0.f;
+    if (ok)
+        for (int64_t i = rg; i < B; i += kBnRg) s += xc[i * H];
+    const float mean = wg_colsum(s, red, c, rg) / (float)B;
+    float q = 0.f;
+    if (ok)
+        for (int64_t i = rg; i < B; i += kBnRg) {
+            const float d = xc[i * H] - mean;
+            q += d * d;
+        }
+    const float var = wg_colsum(q, red, c, rg) / (float)B;
+    const float invstd = 1.f / sqrtf(var + eps);
+    if (!ok) return;
+    const float gm = gamma[col], bt = beta[col];
+    for (int64_t i = rg; i < B; i += kBnRg) {
+        const float v = gm * ((xc[i * H] - mean) * invstd) + bt;
+        y[i * H + col] = v > 0.f ? v : 0.f;
+    }
+    if (rg == 0) {
+        mean_out[col] = mean;
+        invstd_out[col] = invstd;
+        if (running_mean) {
+            running_mean[col] = (1.f - momentum) * running_mean[col] + momentum * mean;
+            running_var[col] = (1.f - momentum) * running_var[col] + momentum * (var * (float)B / (float)(B - 1));
+        }
+        if (num_batches && col == 0) *num_batches += 1;
+    }
+}
+
+// dz = dy * (y > 0); dbeta = sum dz; dgamma = sum dz xhat;
+// dx = gamma invstd (dz - dbeta / B - xhat dgamma / B)   (torch's batch_norm_backward_elemt)
+__global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
+    int64_t B, int H, const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ dy,
+    const float *__restrict__ gamma, const float *__restrict__ mean, const float *__restrict__ invstd,
+    float *__restrict__ dx, float *__restrict__ dgamma, float *__restrict__ dbeta) {
+    __shared__ float red[kBnRg][kBnCols];
+    const int c = threadIdx.x % kBnCols, rg = threadIdx.x / kBnCols;
+    const int col = blockIdx.x * kBnCols + c;
+    const bool ok = col < H;
+    const int64_t o = ok ? col : 0;
+    const float mu = mean[o], is = invstd[o];
+    float sd = 0.f, sdx = 0.f;
+    if (ok)
+        for (int64_t i = rg; i < B; i += kBnRg) {
+            const float dz = y[i * H + o] > 0.f ? dy[i * H + o] : 0.f;
+            sd += dz;
+            sdx += dz * ((x[i * H + o] - mu) * is);
+        }
+    const float db = wg_colsum(sd, red, c, rg);
+    const float dg = wg_colsum(sdx, red, c, rg);
+    if (!ok) return;
+    const float gm = gamma[col];
+    const float mdb = db / (float)B, mdg = dg / (float)B;
+    for (int64_t i = rg; i < B; i += kBnRg) {
+        const float dz = y[i * H + col] > 0.f ? dy[i * H + col] : 0.f;
+        const float xh = (x[i * H + col] - mu) * is;
+        dx[i * H + col] = (dz - mdb - xh * mdg) * (is * gm);
+    }
+    if (rg == 0) {
+        if (dgamma) dgamma[col] = dg;
+        if (dbeta) dbeta[col] = db;
+    }
+}
+
+}  // namespace fs
+
+using namespace fs;
+
+hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st) {
+    if (g.M <= 0 || (g.N <= 0 && !g.rowsum_a)) return hipSuccess;
+    // one column tile even when N = 0, so that rowsum_a is still written
+    const dim3 grid((unsigned)((g.M + 31) / 32), (unsigned)(g.N > 0 ? (g.N + 31) / 32 : 1));
+    const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0;
+    const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0;
+    // enough waves per tile that each walks at most ~16 k-blocks
+    const int split = g.K > 8 * 4 * 16 ? 8 : 4;
+#define FS_G(S, A, B)                                                                           \
+    if (split == S && ak == A && bk == B) {                                                     \
+        hipLaunchKernelGGL((gemm_f32_kernel<S, A, B>), grid, dim3(64 * S), 0, st, g);           \
+        return hipGetLastError();                                                               \
+    }
+    FS_G(4, true, true) FS_G(4, true, false) FS_G(4, false, true) FS_G(4, false, false)
+    FS_G(8, true, true) FS_G(8, true, false) FS_G(8, false, true) FS_G(8, false, false)
+#undef FS_G
+    return hipErrorInvalidValue;
+}
+
+hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,
+                                     float *rm, float *rv, int64_t *nbt, float momentum, float eps, float *y,
+                                     float *mean, float *invstd, hipStream_t st) {
+    if (B <= 0 || H <= 0) return hipSuccess;
+    hipLaunchKernelGGL(bn_relu_train_fwd_kernel, dim3((unsigned)((H + kBnCols - 1) / kBnCols)),
+                       dim3(kBnCols * kBnRg), 0, st, B, H, x, gamma, beta, rm, rv, nbt, momentum, eps, y, mean,
+                       invstd);
+    return hipGetLastError();
+}
+
+hipError_t fs_bn_relu_train_bwd_impl(int64_t B, int H, const float *x, const float *y, const float *dy,
+                                     const float *gamma, const float *mean, const float *invstd, float *dx,
+                                     float *dgamma, float *dbeta, hipStream_t st) {
+    if (B <= 0 || H <= 0) return hipSuccess;
+    hipLaunchKernelGGL(bn_relu_train_bwd_kernel, dim3((unsigned)((H + kBnCols - 1) / kBnCols)),
+                       dim3(kBnCols * kBnRg), 0, st, B, H, x, y, dy, gamma, mean, invstd, dx, dgamma, dbeta);
+    return hipGetLastError();
+}

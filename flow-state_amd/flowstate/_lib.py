@@ -67,6 +67,11 @@ _SIGS = {
                        + [_P] * 4),
     "fs_rqs_backward": (ctypes.c_int, [_I64, ctypes.c_int32, ctypes.c_int32] + [_P] * 4 + [ctypes.c_double]
                         + [_P] * 7),
+    "fs_linear_f32": (ctypes.c_int, [_I64, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _P, _I64, _P, _I64,
+                                     _P, _P]),
+    "fs_bn_relu_train_fwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 6 + [ctypes.c_double, ctypes.c_double]
+                             + [_P] * 4),
+    "fs_bn_relu_train_bwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 10),
     "fs_classify_wells": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
                                           _P, _P, _P, _P]),
     "fs_pair_hist": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, _P, ctypes.c_int32,

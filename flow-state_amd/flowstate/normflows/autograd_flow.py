@@ -174,11 +174,127 @@ def circular_rqs_torch(x, uw, uh, ud, B, inverse):
     return torch.where(inside, o, x), torch.where(inside, l, torch.zeros_like(l))
 
 
+class _Linear(torch.autograd.Function):
+    """nn.Linear (+ an optional residual added to the output) through fs_linear_f32
+    (csrc/train_kernels.hip): y = x W^T + b (+ r); backward dx = dy W, dW = dy^T x and
+    db = column sums of dy (from the same launch)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, r):
+        from .. import _lib
+
+        x = x.contiguous()
+        M, K = x.shape
+        N = w.shape[0]
+        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        L = _lib.load()
+        _lib.require_device(x, w, b, r)
+        _lib.check(L.fs_linear_f32(M, N, K, _lib.ptr(x), K, 1, _lib.ptr(w), 1, K, _lib.ptr(b), _lib.ptr(r),
+                                   N, _lib.ptr(y), N, None, _lib.stream_ptr()), "fs_linear_f32")
+        ctx.save_for_backward(x, w)
+        ctx.has_r = r is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .. import _lib
+
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        M, K = x.shape
+        N = w.shape[0]
+        L = _lib.load()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            _lib.check(L.fs_linear_f32(M, K, N, _lib.ptr(gy), N, 1, _lib.ptr(w), K, 1, None, None, 0, _lib.ptr(gx),
+                                       K, None, _lib.stream_ptr()), "fs_linear_f32")
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            gw = torch.empty_like(w)
+            gb = torch.empty((N,), dtype=torch.float32, device=x.device)
+            _lib.check(L.fs_linear_f32(N, K, M, _lib.ptr(gy), 1, N, _lib.ptr(x), K, 1, None, None, 0, _lib.ptr(gw),
+                                       K, _lib.ptr(gb), _lib.stream_ptr()), "fs_linear_f32")
+        return gx, gw, gb, (gy if ctx.has_r and ctx.needs_input_grad[3] else None)
+
+
+class _BnRelu(torch.autograd.Function):
+    """relu(BatchNorm1d(x)) in train mode through fs_bn_relu_train_fwd / _bwd: batch
+    statistics, the module's running statistics and num_batches_tracked updated in the
+    same launch (torch.nn.BatchNorm1d.forward, momentum form)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bn):
+        from .. import _lib
+
+        x = x.contiguous()
+        M, H = x.shape
+        y = torch.empty_like(x)
+        mean = torch.empty((H,), dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        L = _lib.load()
+        _lib.require_device(x, gamma, beta)
+        _lib.check(L.fs_bn_relu_train_fwd(M, H, _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta),
+                                          _lib.ptr(bn.running_mean), _lib.ptr(bn.running_var),
+                                          _lib.ptr(bn.num_batches_tracked), float(bn.momentum), float(bn.eps),
+                                          _lib.ptr(y), _lib.ptr(mean), _lib.ptr(invstd), _lib.stream_ptr()),
+                   "fs_bn_relu_train_fwd")
+        ctx.save_for_backward(x, y, gamma, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .. import _lib
+
+        x, y, gamma, mean, invstd = ctx.saved_tensors
+        gy = gy.contiguous()
+        M, H = x.shape
+        gx = torch.empty_like(x)
+        gg = torch.empty_like(gamma)
+        gb = torch.empty_like(gamma)
+        _lib.check(_lib.load().fs_bn_relu_train_bwd(M, H, _lib.ptr(x), _lib.ptr(y), _lib.ptr(gy), _lib.ptr(gamma),
+                                                    _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(gx), _lib.ptr(gg),
+                                                    _lib.ptr(gb), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
+        return gx, gg, gb, None
+
+
+def _fused_ok(net, t):
+    """The fused train-mode conditioner applies: f32 device activations, every BatchNorm
+    in train mode with affine parameters, running statistics and a momentum, batch >= 2
+    (torch raises on a batch of one in train mode: that case keeps torch's modules)."""
+    if not (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.shape[0] >= 2):
+        return False
+    for blk in net.blocks:
+        for bn in blk.batch_norm_layers:
+            if not (bn.training and bn.affine and bn.track_running_stats and bn.momentum is not None
+                    and bn.running_mean is not None):
+                return False
+    return True
+
+
+def _conditioner_fused(net, t):
+    """ResidualNet.forward (resnet.py:82-104, blocks :35-51) in train mode: every Linear
+    on fs_linear_f32 (the block's residual add fused into its second Linear), every
+    BatchNorm + ReLU pair on fs_bn_relu_train_fwd."""
+    li = net.initial_layer
+    t = _Linear.apply(t, li.weight, li.bias, None)
+    for blk in net.blocks:
+        bn0, bn1 = blk.batch_norm_layers
+        l0, l1 = blk.linear_layers
+        u = _BnRelu.apply(t, bn0.weight, bn0.bias, bn0)
+        u = _Linear.apply(u, l0.weight, l0.bias, None)
+        u = _BnRelu.apply(u, bn1.weight, bn1.bias, bn1)
+        t = _Linear.apply(u, l1.weight, l1.bias, t)
+    lf = net.final_layer
+    return _Linear.apply(t, lf.weight, lf.bias, None)
+
+
 def conditioner(net, ident, B):
     """ResidualNet.forward with PeriodicFeaturesElementwise (fork: cos/sin of all identity
     features, nn.py:120-137); BatchNorm modules in their current train/eval mode."""
     scale = np.pi / B
     t = torch.cat([torch.cos(scale * ident), torch.sin(scale * ident)], dim=-1)
+    if _fused_ok(net, t):
+        return _conditioner_fused(net, t)
     t = net.initial_layer(t)
     for blk in net.blocks:
         u = blk.batch_norm_layers[0](t)

@@ -225,6 +225,31 @@ int fs_rqs_backward(int64_t M, int32_t K, int32_t inverse, const float *x, const
                     const float *ud, double tail_bound, const float *g_out, const float *g_lad, float *gx,
                     float *guw, float *guh, float *gud, void *stream);
 
+/* Conditioner pieces of the training step (ResidualNet in train mode, NF/normflows/
+ * nets/resnet.py:7-104; nn.Linear / nn.BatchNorm1d semantics).
+ * fs_linear_f32: C[m][n] = sum_k A[m][k] B[k][n] (+ bias[n]) (+ R[m][n]) in f32, with
+ * A[m][k] at A[m*sam + k*sak], B[k][n] at B[k*sbk + n*sbn], R (ld ldr) and C (ld ldc)
+ * row-major; bias, R nullable.  rowsum_a (nullable) [M] = sum_k A[m][k] (the bias
+ * gradient when A = dY^T).  nn.Linear forward: A = X, B = W^T; input gradient: A = dY,
+ * B = W; weight gradient: A = dY^T, B = X (replaces torch.addmm / mm, at::linear). */
+int fs_linear_f32(int64_t M, int64_t N, int64_t K, const float *A, int64_t sam, int64_t sak, const float *B,
+                  int64_t sbk, int64_t sbn, const float *bias, const float *R, int64_t ldr, float *C, int64_t ldc,
+                  float *rowsum_a, void *stream);
+
+/* BatchNorm1d (training mode) followed by ReLU over x [Bn][H] (row-major):
+ * batch mean / biased variance, y = relu(gamma (x - mean) invstd + beta),
+ * running_mean / running_var updated with `momentum` (unbiased variance) and
+ * *num_batches += 1 when non-NULL (torch.nn.BatchNorm1d.forward); mean, invstd [H]
+ * saved for the backward.  Bn >= 2. */
+int fs_bn_relu_train_fwd(int64_t Bn, int32_t H, const float *x, const float *gamma, const float *beta,
+                         float *running_mean, float *running_var, int64_t *num_batches, double momentum, double eps,
+                         float *y, float *mean, float *invstd, void *stream);
+
+/* Gradients of the above: dx [Bn][H], dgamma, dbeta [H] (nullable) from dy = dL/dy and
+ * the forward's x, y, mean, invstd. */
+int fs_bn_relu_train_bwd(int64_t Bn, int32_t H, const float *x, const float *y, const float *dy, const float *gamma,
+                         const float *mean, const float *invstd, float *dx, float *dgamma, float *dbeta, void *stream);
+
 /* ------------------------------------------------------------------ */
 /* Local moves (MCMC/monte_carlo.py)                                   */
 /* ------------------------------------------------------------------ */
