@@ -343,3 +343,69 @@ int fs_bn_relu_train_bwd(int64_t Bn, int32_t H, const float *x, const float *y, 
                                             (hipStream_t)stream),
                   "fs_bn_relu_train_bwd");
 }
+
+static int check_coupling(const fs_coupling *c, const char *what) {
+    REQUIRE(c && c->rows >= 0 && c->D >= 2 && c->D % 2 == 0 && c->hidden >= 1 && c->tail_bound > 0.0,
+            "%s: invalid coupling description", what);
+    REQUIRE(c->K == 5 || c->K == 8 || c->K == 15 || c->K == 32, "%s: K=%d not instantiated (5, 8, 15, 32)", what,
+            c->K);
+    REQUIRE(c->rows == 0 || (c->identity_features && c->transform_features), "%s: feature indices are NULL", what);
+    return FS_OK;
+}
+
+int fs_coupling_features_fwd(const fs_coupling *c, const float *x, float *t, void *stream) {
+    int rc = check_coupling(c, "fs_coupling_features_fwd");
+    if (rc) return rc;
+    REQUIRE(c->rows == 0 || (x && t), "fs_coupling_features_fwd: invalid arguments");
+    return hip_rc(fs_coupling_features_fwd_impl(c, x, t, (hipStream_t)stream), "fs_coupling_features_fwd");
+}
+
+int fs_coupling_density_fwd(const fs_coupling *c, const float *x, const float *params, const float *uw,
+                            const float *uh, const float *ud, const float *lq_in, float *out, float *lq_out,
+                            void *stream) {
+    int rc = check_coupling(c, "fs_coupling_density_fwd");
+    if (rc) return rc;
+    REQUIRE(c->rows == 0 || (x && params && uw && uh && ud && out && lq_out),
+            "fs_coupling_density_fwd: invalid arguments");
+    REQUIRE(x != out, "fs_coupling_density_fwd: out must not alias x");
+    return hip_rc(fs_coupling_density_fwd_impl(c, x, params, uw, uh, ud, lq_in, out, lq_out, (hipStream_t)stream),
+                  "fs_coupling_density_fwd");
+}
+
+int fs_coupling_density_bwd(const fs_coupling *c, const float *x, const float *params, const float *uw,
+                            const float *uh, const float *ud, const float *g_out, const float *g_lq, float *gx,
+                            float *g_params, float *g_u, void *stream) {
+    int rc = check_coupling(c, "fs_coupling_density_bwd");
+    if (rc) return rc;
+    REQUIRE(c->rows == 0 || (x && params && uw && uh && ud && gx && g_params && g_u),
+            "fs_coupling_density_bwd: invalid arguments");
+    return hip_rc(fs_coupling_density_bwd_impl(c, x, params, uw, uh, ud, g_out, g_lq, gx, g_params, g_u,
+                                               (hipStream_t)stream),
+                  "fs_coupling_density_bwd");
+}
+
+int fs_coupling_features_bwd(const fs_coupling *c, const float *x, const float *g_t, float *gx, void *stream) {
+    int rc = check_coupling(c, "fs_coupling_features_bwd");
+    if (rc) return rc;
+    REQUIRE(c->rows == 0 || (x && g_t && gx), "fs_coupling_features_bwd: invalid arguments");
+    return hip_rc(fs_coupling_features_bwd_impl(c, x, g_t, gx, (hipStream_t)stream), "fs_coupling_features_bwd");
+}
+
+int fs_coupling_sample_pre(const fs_coupling *c, const float *z, const float *uw, const float *uh, const float *ud,
+                           float *t, float *out, float *lad_u, int32_t *nan_flag, void *stream) {
+    int rc = check_coupling(c, "fs_coupling_sample_pre");
+    if (rc) return rc;
+    REQUIRE(c->rows == 0 || (z && uw && uh && ud && t && out && lad_u), "fs_coupling_sample_pre: invalid arguments");
+    REQUIRE(z != out, "fs_coupling_sample_pre: out must not alias z");
+    return hip_rc(fs_coupling_sample_pre_impl(c, z, uw, uh, ud, t, out, lad_u, nan_flag, (hipStream_t)stream),
+                  "fs_coupling_sample_pre");
+}
+
+int fs_coupling_sample_post(const fs_coupling *c, const float *params, const float *lad_u, const float *lq_in,
+                            float *out, float *lq_out, int32_t *nan_flag, void *stream) {
+    int rc = check_coupling(c, "fs_coupling_sample_post");
+    if (rc) return rc;
+    REQUIRE(c->rows == 0 || (params && lad_u && out && lq_out), "fs_coupling_sample_post: invalid arguments");
+    return hip_rc(fs_coupling_sample_post_impl(c, params, lad_u, lq_in, out, lq_out, nan_flag, (hipStream_t)stream),
+                  "fs_coupling_sample_post");
+}

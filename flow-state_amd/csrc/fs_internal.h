@@ -104,3 +104,18 @@ hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const flo
 hipError_t fs_bn_relu_train_bwd_impl(int64_t B, int H, const float *x, const float *y, const float *dy,
                                      const float *gamma, const float *mean, const float *invstd, float *dx,
                                      float *dgamma, float *dbeta, hipStream_t st);
+hipError_t fs_coupling_density_fwd_impl(const fs_coupling *cp, const float *x, const float *params, const float *uw,
+                                        const float *uh, const float *ud, const float *lq_in, float *out, float *lq_out,
+                                        hipStream_t st);
+hipError_t fs_coupling_features_fwd_impl(const fs_coupling *cp, const float *x, float *t, hipStream_t st);
+hipError_t fs_coupling_density_bwd_impl(const fs_coupling *cp, const float *x, const float *params, const float *uw,
+                                        const float *uh, const float *ud, const float *g_out, const float *g_lq,
+                                        float *gx, float *g_params, float *g_u, hipStream_t st);
+hipError_t fs_coupling_sample_pre_impl(const fs_coupling *cp, const float *z, const float *uw, const float *uh,
+                                       const float *ud, float *t, float *out, float *lad_u, int32_t *nan_flag,
+                                       hipStream_t st);
+hipError_t fs_coupling_sample_post_impl(const fs_coupling *cp, const float *params, const float *lad_u,
+                                        const float *lq_in, float *out, float *lq_out, int32_t *nan_flag,
+                                        hipStream_t st);
+hipError_t fs_coupling_features_bwd_impl(const fs_coupling *cp, const float *x, const float *g_t, float *gx,
+                                         hipStream_t st);

@@ -75,23 +75,14 @@ __device__ __forceinline__ int find_bin(float x, const float *knots) {
     return b < 0 ? 0 : (b > K - 1 ? K - 1 : b);
 }
 
+// one element: x inside [-B, B] (callers route the outside identity themselves)
 template <int K, bool INV>
-__global__ void rqs_forward_kernel(int64_t M, const float *__restrict__ x, const float *__restrict__ uw,
-                                   const float *__restrict__ uh, const float *__restrict__ ud, float B,
-                                   float *__restrict__ out, float *__restrict__ lad, int32_t *__restrict__ nan_flag) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= M) return;
-    const float xv = x[i];
-    if (!(xv >= -B && xv <= B)) {
-        out[i] = xv;
-        lad[i] = 0.f;
-        return;
-    }
+__device__ __forceinline__ void rqs_point(float xv, const float *uw, const float *uh, const float *dd, float B,
+                                          float &out, float &lad, int32_t *nan_flag) {
     Knots<K> W, Hh;
-    build_knots<K>(uw + i * K, B, W);
-    build_knots<K>(uh + i * K, B, Hh);
+    build_knots<K>(uw, B, W);
+    build_knots<K>(uh, B, Hh);
     const int b = find_bin<K>(xv, INV ? Hh.c : W.c);
-    const float *dd = ud + i * (K + 1);
     const float d0 = kMin + softplus(dd[b]), d1 = kMin + softplus(dd[b + 1]);
     const float icw = W.c[b], ibw = W.c[b + 1] - W.c[b];
     const float ich = Hh.c[b], ih = Hh.c[b + 1] - Hh.c[b];
@@ -113,12 +104,27 @@ __global__ void rqs_forward_kernel(int64_t M, const float *__restrict__ x, const
     const float A = d1 * th * th + 2.f * s * t + d0 * (1.f - th) * (1.f - th);
     const float l = logf(s * s * A) - 2.f * logf(den);
     if (INV) {
-        out[i] = th * ibw + icw;
-        lad[i] = -l;
+        out = th * ibw + icw;
+        lad = -l;
     } else {
-        out[i] = ich + ih * (s * th * th + d0 * t) / den;
-        lad[i] = l;
+        out = ich + ih * (s * th * th + d0 * t) / den;
+        lad = l;
     }
+}
+
+template <int K, bool INV>
+__global__ void rqs_forward_kernel(int64_t M, const float *__restrict__ x, const float *__restrict__ uw,
+                                   const float *__restrict__ uh, const float *__restrict__ ud, float B,
+                                   float *__restrict__ out, float *__restrict__ lad, int32_t *__restrict__ nan_flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const float xv = x[i];
+    if (!(xv >= -B && xv <= B)) {
+        out[i] = xv;
+        lad[i] = 0.f;
+        return;
+    }
+    rqs_point<K, INV>(xv, uw + i * K, uh + i * K, ud + i * (K + 1), B, out[i], lad[i], nan_flag);
 }
 
 // knot adjoints (g_c over c[0..K]) -> unnormalised-parameter adjoints
@@ -140,32 +146,14 @@ __device__ __forceinline__ void knots_backward(const Knots<K> &kn, const float *
     for (int j = 0; j < K; ++j) gu[j] = kn.p[j] * (c1 * gw[j] - dot);
 }
 
+// adjoints of one element inside [-B, B]: gx, guw[K], guh[K], gud[K+1]
 template <int K, bool INV>
-__global__ void rqs_backward_kernel(int64_t M, const float *__restrict__ x, const float *__restrict__ uw,
-                                    const float *__restrict__ uh, const float *__restrict__ ud, float B,
-                                    const float *__restrict__ g_out, const float *__restrict__ g_lad,
-                                    float *__restrict__ gx, float *__restrict__ guw, float *__restrict__ guh,
-                                    float *__restrict__ gud) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= M) return;
-    const float xv = x[i];
-    const float go = g_out ? g_out[i] : 0.f, gl = g_lad ? g_lad[i] : 0.f;
-    if (!(xv >= -B && xv <= B)) {
-        gx[i] = go;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            guw[i * K + k] = 0.f;
-            guh[i * K + k] = 0.f;
-        }
-#pragma unroll
-        for (int k = 0; k <= K; ++k) gud[i * (K + 1) + k] = 0.f;
-        return;
-    }
+__device__ __forceinline__ void rqs_point_bwd(float xv, const float *uw, const float *uh, const float *dd, float B,
+                                              float go, float gl, float &gx, float *guw, float *guh, float *gud) {
     Knots<K> W, Hh;
-    build_knots<K>(uw + i * K, B, W);
-    build_knots<K>(uh + i * K, B, Hh);
+    build_knots<K>(uw, B, W);
+    build_knots<K>(uh, B, Hh);
     const int b = find_bin<K>(xv, INV ? Hh.c : W.c);
-    const float *dd = ud + i * (K + 1);
     const float e0 = dd[b], e1 = dd[b + 1];
     const float d0 = kMin + softplus(e0), d1 = kMin + softplus(e1);
     const float icw = W.c[b], ibw = W.c[b + 1] - W.c[b];
@@ -250,27 +238,269 @@ __global__ void rqs_backward_kernel(int64_t M, const float *__restrict__ x, cons
     // s = h_b / w_b
     g_ih += g_s / ibw;
     g_ibw -= g_s * s / ibw;
-    gx[i] = g_x;
+    gx = g_x;
     float gcw[K + 1], gch[K + 1];
 #pragma unroll
     for (int k = 0; k <= K; ++k) {
         gcw[k] = (k == b) ? (g_icw - g_ibw) : ((k == b + 1) ? g_ibw : 0.f);
         gch[k] = (k == b) ? (g_ich - g_ih) : ((k == b + 1) ? g_ih : 0.f);
     }
-    float gu[K];
-    knots_backward<K>(W, gcw, B, gu);
-#pragma unroll
-    for (int k = 0; k < K; ++k) guw[i * K + k] = gu[k];
-    knots_backward<K>(Hh, gch, B, gu);
-#pragma unroll
-    for (int k = 0; k < K; ++k) guh[i * K + k] = gu[k];
+    knots_backward<K>(W, gcw, B, guw);
+    knots_backward<K>(Hh, gch, B, guh);
 #pragma unroll
     for (int k = 0; k <= K; ++k) {
         float g = 0.f;
         if (k == b) g = g_d0 * softplus_grad(e0);
         if (k == b + 1) g = g_d1 * softplus_grad(e1);
-        gud[i * (K + 1) + k] = g;
+        gud[k] = g;
     }
+}
+
+
+template <int K, bool INV>
+__global__ void rqs_backward_kernel(int64_t M, const float *__restrict__ x, const float *__restrict__ uw,
+                                    const float *__restrict__ uh, const float *__restrict__ ud, float B,
+                                    const float *__restrict__ g_out, const float *__restrict__ g_lad,
+                                    float *__restrict__ gx, float *__restrict__ guw, float *__restrict__ guh,
+                                    float *__restrict__ gud) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const float xv = x[i];
+    const float go = g_out ? g_out[i] : 0.f, gl = g_lad ? g_lad[i] : 0.f;
+    if (!(xv >= -B && xv <= B)) {
+        gx[i] = go;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            guw[i * K + k] = 0.f;
+            guh[i * K + k] = 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k <= K; ++k) gud[i * (K + 1) + k] = 0.f;
+        return;
+    }
+    float a[K], b[K], d[K + 1];
+    rqs_point_bwd<K, INV>(xv, uw + i * K, uh + i * K, ud + i * (K + 1), B, go, gl, gx[i], a, b, d);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        guw[i * K + k] = a[k];
+        guh[i * K + k] = b[k];
+    }
+#pragma unroll
+    for (int k = 0; k <= K; ++k) gud[i * (K + 1) + k] = d[k];
+}
+
+
+// ---------------------------------------------------------------------------
+// One coupling layer of the training path around its conditioner: the feature gather,
+// periodic features (nn.py:120-137), the conditional and unconditional splines, the
+// half-roll and the log-det sums (coupling.py:71-134, wrapper.py:269-275) in one launch
+// per side of the conditioner instead of ~30 torch kernels.  One wave per sample row,
+// lane = feature j (j += 64); log-det sums are wave reductions read from lane 0.
+struct CouplingArgs {
+    int64_t rows;
+    int D, n, split;
+    const int64_t *id, *tr;
+    float bound, scale, sq;
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return __shfl(v, 0);
+}
+
+template <int K>
+__device__ __forceinline__ void cond_params(const float *p, float sq, float *w, float *h) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        w[k] = p[k] / sq;  // params[..., :K] / sqrt(H) (coupling.py:340-342)
+        h[k] = p[K + k] / sq;
+    }
+}
+
+// density direction forward (Coupling.forward), after the conditioner: both splines,
+// rolled output, lq_out = lq_in + (sum lad_cond + sum lad_uncond)
+template <int K>
+__global__ __launch_bounds__(256) void coupling_density_fwd_kernel(CouplingArgs c, const float *__restrict__ x,
+                                                                   const float *__restrict__ params,
+                                                                   const float *__restrict__ uw,
+                                                                   const float *__restrict__ uh,
+                                                                   const float *__restrict__ ud,
+                                                                   const float *__restrict__ lq_in, float *out,
+                                                                   float *lq_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= c.rows) return;
+    const float *xr = x + row * c.D;
+    float sc = 0.f, su = 0.f;
+    for (int j = lane; j < c.n; j += 64) {
+        const int pi = (int)c.id[j], pt = (int)c.tr[j];
+        const float xi = xr[pi], xt = xr[pt];
+        float yt = xt, lt = 0.f;
+        if (xt >= -c.bound && xt <= c.bound) {
+            const float *p = params + (row * c.n + j) * (3 * K + 1);
+            float w[K], h[K];
+            cond_params<K>(p, c.sq, w, h);
+            rqs_point<K, false>(xt, w, h, p + 2 * K, c.bound, yt, lt, nullptr);
+        }
+        float yi = xi, li = 0.f;
+        if (xi >= -c.bound && xi <= c.bound)
+            rqs_point<K, false>(xi, uw + j * K, uh + j * K, ud + j * (K + 1), c.bound, yi, li, nullptr);
+        out[row * c.D + (pt + c.D - c.split) % c.D] = yt;
+        out[row * c.D + (pi + c.D - c.split) % c.D] = yi;
+        sc += lt;
+        su += li;
+    }
+    sc = wave_sum(sc);
+    su = wave_sum(su);
+    if (lane == 0) lq_out[row] = (lq_in ? lq_in[row] : 0.f) + (sc + su);
+}
+
+// its adjoints: gx (both halves, spline part), g_params [rows][n][3K+1], g_u the per-row
+// unconditional adjoints [rows][n][3K+1] (summed over rows by the caller)
+template <int K>
+__global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
+    CouplingArgs c, const float *__restrict__ x, const float *__restrict__ params, const float *__restrict__ uw,
+    const float *__restrict__ uh, const float *__restrict__ ud, const float *__restrict__ g_out,
+    const float *__restrict__ g_lq, float *gx, float *g_params, float *g_u) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= c.rows) return;
+    const float *xr = x + row * c.D;
+    const float gl = g_lq ? g_lq[row] : 0.f;
+    constexpr int P = 3 * K + 1;
+    for (int j = lane; j < c.n; j += 64) {
+        const int pi = (int)c.id[j], pt = (int)c.tr[j];
+        const float xi = xr[pi], xt = xr[pt];
+        const float got = g_out ? g_out[row * c.D + (pt + c.D - c.split) % c.D] : 0.f;
+        const float goi = g_out ? g_out[row * c.D + (pi + c.D - c.split) % c.D] : 0.f;
+        float *gp = g_params + (row * c.n + j) * P;
+        float *gu = g_u + (row * c.n + j) * P;
+        float gw[K], gh[K], gd[K + 1];
+        if (xt >= -c.bound && xt <= c.bound) {
+            const float *p = params + (row * c.n + j) * P;
+            float w[K], h[K];
+            cond_params<K>(p, c.sq, w, h);
+            float g;
+            rqs_point_bwd<K, false>(xt, w, h, p + 2 * K, c.bound, got, gl, g, gw, gh, gd);
+            gx[row * c.D + pt] = g;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                gp[k] = gw[k] / c.sq;
+                gp[K + k] = gh[k] / c.sq;
+            }
+#pragma unroll
+            for (int k = 0; k <= K; ++k) gp[2 * K + k] = gd[k];
+        } else {
+            gx[row * c.D + pt] = got;
+#pragma unroll
+            for (int k = 0; k < P; ++k) gp[k] = 0.f;
+        }
+        if (xi >= -c.bound && xi <= c.bound) {
+            float g;
+            rqs_point_bwd<K, false>(xi, uw + j * K, uh + j * K, ud + j * (K + 1), c.bound, goi, gl, g, gw, gh, gd);
+            gx[row * c.D + pi] = g;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                gu[k] = gw[k];
+                gu[K + k] = gh[k];
+            }
+#pragma unroll
+            for (int k = 0; k <= K; ++k) gu[2 * K + k] = gd[k];
+        } else {
+            gx[row * c.D + pi] = goi;
+#pragma unroll
+            for (int k = 0; k < P; ++k) gu[k] = 0.f;
+        }
+    }
+}
+
+// density direction, before the conditioner: t = [cos(s x_id), sin(s x_id)]
+__global__ __launch_bounds__(256) void coupling_features_fwd_kernel(CouplingArgs c, const float *__restrict__ x,
+                                                                    float *t) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= c.rows) return;
+    for (int j = lane; j < c.n; j += 64) {
+        const float v = c.scale * x[row * c.D + c.id[j]];
+        t[row * 2 * c.n + j] = cosf(v);
+        t[row * 2 * c.n + c.n + j] = sinf(v);
+    }
+}
+
+// adjoint of the periodic features t = [cos(s x_id), sin(s x_id)]: gx at the identity
+// positions, 0 at the transform positions
+__global__ __launch_bounds__(256) void coupling_features_bwd_kernel(CouplingArgs c, const float *__restrict__ x,
+                                                                    const float *__restrict__ g_t, float *gx) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= c.rows) return;
+    for (int j = lane; j < c.n; j += 64) {
+        const int pi = (int)c.id[j], pt = (int)c.tr[j];
+        const float v = c.scale * x[row * c.D + pi];
+        const float gc = g_t[row * 2 * c.n + j] * -sinf(v), gs = g_t[row * 2 * c.n + c.n + j] * cosf(v);
+        gx[row * c.D + pi] = gc * c.scale + gs * c.scale;
+        gx[row * c.D + pt] = 0.f;
+    }
+}
+
+// sampling direction (Coupling.inverse), forward only: roll, unconditional inverse spline
+// of the identity half, features of its output; out holds the new identity values and
+// the untouched transform half; lad_u[row] = its log-det sum
+template <int K>
+__global__ __launch_bounds__(256) void coupling_sample_pre_kernel(CouplingArgs c, const float *__restrict__ z,
+                                                                  const float *__restrict__ uw,
+                                                                  const float *__restrict__ uh,
+                                                                  const float *__restrict__ ud, float *t, float *out,
+                                                                  float *lad_u, int32_t *nan_flag) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= c.rows) return;
+    const float *zr = z + row * c.D;
+    float su = 0.f;
+    for (int j = lane; j < c.n; j += 64) {
+        const int pi = (int)c.id[j], pt = (int)c.tr[j];
+        const float xi = zr[(pi + c.split) % c.D];
+        float yi = xi, li = 0.f;
+        if (xi >= -c.bound && xi <= c.bound)
+            rqs_point<K, true>(xi, uw + j * K, uh + j * K, ud + j * (K + 1), c.bound, yi, li, nan_flag);
+        const float v = c.scale * yi;
+        t[row * 2 * c.n + j] = cosf(v);
+        t[row * 2 * c.n + c.n + j] = sinf(v);
+        out[row * c.D + pi] = yi;
+        out[row * c.D + pt] = zr[(pt + c.split) % c.D];
+        su += li;
+    }
+    su = wave_sum(su);
+    if (lane == 0) lad_u[row] = su;
+}
+
+// ... then the conditional inverse spline of the transform half in place;
+// lq_out = lq_in - (lad_u + sum lad_cond)
+template <int K>
+__global__ __launch_bounds__(256) void coupling_sample_post_kernel(CouplingArgs c, const float *__restrict__ params,
+                                                                   const float *__restrict__ lad_u,
+                                                                   const float *__restrict__ lq_in, float *out,
+                                                                   float *lq_out, int32_t *nan_flag) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= c.rows) return;
+    float sc = 0.f;
+    for (int j = lane; j < c.n; j += 64) {
+        const int pt = (int)c.tr[j];
+        const float xt = out[row * c.D + pt];
+        float yt = xt, lt = 0.f;
+        if (xt >= -c.bound && xt <= c.bound) {
+            const float *p = params + (row * c.n + j) * (3 * K + 1);
+            float w[K], h[K];
+            cond_params<K>(p, c.sq, w, h);
+            rqs_point<K, true>(xt, w, h, p + 2 * K, c.bound, yt, lt, nan_flag);
+        }
+        out[row * c.D + pt] = yt;
+        sc += lt;
+    }
+    sc = wave_sum(sc);
+    if (lane == 0) lq_out[row] = (lq_in ? lq_in[row] : 0.f) - (lad_u[row] + sc);
 }
 
 }  // namespace fs
@@ -317,4 +547,72 @@ hipError_t fs_rqs_backward_impl(int64_t M, int K, int inverse, const float *x, c
     FS_RQS_K(FS_B)
 #undef FS_B
     return hipErrorInvalidValue;
+}
+
+static fs::CouplingArgs coupling_args(const fs_coupling *c) {
+    fs::CouplingArgs a;
+    a.rows = c->rows;
+    a.D = c->D;
+    a.n = c->D / 2;
+    a.split = c->D / 2;
+    a.id = c->identity_features;
+    a.tr = c->transform_features;
+    a.bound = (float)c->tail_bound;
+    a.scale = (float)(M_PI / c->tail_bound);  // scale * ident with the Python-float scale (nn.py:133)
+    a.sq = (float)sqrt((double)c->hidden);     // np.sqrt(num_hidden_channels) (coupling.py:340)
+    return a;
+}
+
+#define FS_COUPLING_LAUNCH(KERNEL, ...)                                                         \
+    const fs::CouplingArgs a = coupling_args(cp);                                               \
+    if (a.rows <= 0) return hipSuccess;                                                         \
+    const dim3 grid((unsigned)((a.rows + 3) / 4)), block(256);                                  \
+    switch (cp->K) {                                                                            \
+    case 5: hipLaunchKernelGGL((KERNEL<5>), grid, block, 0, st, a, __VA_ARGS__); break;         \
+    case 8: hipLaunchKernelGGL((KERNEL<8>), grid, block, 0, st, a, __VA_ARGS__); break;         \
+    case 15: hipLaunchKernelGGL((KERNEL<15>), grid, block, 0, st, a, __VA_ARGS__); break;       \
+    case 32: hipLaunchKernelGGL((KERNEL<32>), grid, block, 0, st, a, __VA_ARGS__); break;       \
+    default: return hipErrorInvalidValue;                                                       \
+    }                                                                                           \
+    return hipGetLastError();
+
+hipError_t fs_coupling_density_fwd_impl(const fs_coupling *cp, const float *x, const float *params, const float *uw,
+                                        const float *uh, const float *ud, const float *lq_in, float *out, float *lq_out,
+                                        hipStream_t st) {
+    FS_COUPLING_LAUNCH(coupling_density_fwd_kernel, x, params, uw, uh, ud, lq_in, out, lq_out)
+}
+
+hipError_t fs_coupling_density_bwd_impl(const fs_coupling *cp, const float *x, const float *params, const float *uw,
+                                        const float *uh, const float *ud, const float *g_out, const float *g_lq,
+                                        float *gx, float *g_params, float *g_u, hipStream_t st) {
+    FS_COUPLING_LAUNCH(coupling_density_bwd_kernel, x, params, uw, uh, ud, g_out, g_lq, gx, g_params, g_u)
+}
+
+hipError_t fs_coupling_sample_pre_impl(const fs_coupling *cp, const float *z, const float *uw, const float *uh,
+                                       const float *ud, float *t, float *out, float *lad_u, int32_t *nan_flag,
+                                       hipStream_t st) {
+    FS_COUPLING_LAUNCH(coupling_sample_pre_kernel, z, uw, uh, ud, t, out, lad_u, nan_flag)
+}
+
+hipError_t fs_coupling_sample_post_impl(const fs_coupling *cp, const float *params, const float *lad_u,
+                                        const float *lq_in, float *out, float *lq_out, int32_t *nan_flag,
+                                        hipStream_t st) {
+    FS_COUPLING_LAUNCH(coupling_sample_post_kernel, params, lad_u, lq_in, out, lq_out, nan_flag)
+}
+#undef FS_COUPLING_LAUNCH
+
+hipError_t fs_coupling_features_fwd_impl(const fs_coupling *cp, const float *x, float *t, hipStream_t st) {
+    const fs::CouplingArgs a = coupling_args(cp);
+    if (a.rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(coupling_features_fwd_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, st, a, x, t);
+    return hipGetLastError();
+}
+
+hipError_t fs_coupling_features_bwd_impl(const fs_coupling *cp, const float *x, const float *g_t, float *gx,
+                                         hipStream_t st) {
+    const fs::CouplingArgs a = coupling_args(cp);
+    if (a.rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(coupling_features_bwd_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, st, a, x, g_t,
+                       gx);
+    return hipGetLastError();
 }

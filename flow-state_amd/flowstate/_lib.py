@@ -30,12 +30,20 @@ class Phys(ctypes.Structure):
                 ("beta", ctypes.c_double)]
 
 
+class Coupling(ctypes.Structure):
+    """fs_coupling (include/flowstate.h)."""
+    _fields_ = [("rows", ctypes.c_int64), ("D", ctypes.c_int32), ("K", ctypes.c_int32), ("hidden", ctypes.c_int32),
+                ("identity_features", ctypes.c_void_p), ("transform_features", ctypes.c_void_p),
+                ("tail_bound", ctypes.c_double)]
+
+
 class FlowStateError(RuntimeError):
     pass
 
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
+_CP = ctypes.POINTER(Coupling)
 _D = ctypes.POINTER(FlowDims)
 _PH = ctypes.POINTER(Phys)
 _SIGS = {
@@ -72,6 +80,12 @@ _SIGS = {
     "fs_bn_relu_train_fwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 6 + [ctypes.c_double, ctypes.c_double]
                              + [_P] * 4),
     "fs_bn_relu_train_bwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 10),
+    "fs_coupling_features_fwd": (ctypes.c_int, [_CP] + [_P] * 3),
+    "fs_coupling_density_fwd": (ctypes.c_int, [_CP] + [_P] * 9),
+    "fs_coupling_density_bwd": (ctypes.c_int, [_CP] + [_P] * 11),
+    "fs_coupling_features_bwd": (ctypes.c_int, [_CP] + [_P] * 4),
+    "fs_coupling_sample_pre": (ctypes.c_int, [_CP] + [_P] * 9),
+    "fs_coupling_sample_post": (ctypes.c_int, [_CP] + [_P] * 7),
     "fs_classify_wells": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
                                           _P, _P, _P, _P]),
     "fs_pair_hist": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, _P, ctypes.c_int32,

@@ -19,6 +19,8 @@ Reference math (paths relative to the reference root):
   ResidualNet / ResidualBlock         NF/normflows/nets/resnet.py:7-104 (dropout p = 0)
   PeriodicFeaturesElementwise         NF/normflows/utils/nn.py:120-137
 """
+import ctypes
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -358,3 +360,179 @@ def coupling_sample(layer, z):
     out = torch.empty_like(z)
     out = out.index_copy(1, p.identity_features, ident).index_copy(1, p.transform_features, trans)
     return out, lad
+
+
+# ---------------------------------------------------------------------------
+# Whole coupling layers on the device (csrc/spline_autograd.hip, fs_coupling_*): the
+# gather, periodic features, both splines, half-roll and log-det sums of one layer in one
+# launch on each side of the conditioner.
+
+
+def _coupling_desc(layer, rows):
+    from .. import _lib
+
+    p = layer.prqct
+    c = _lib.Coupling()
+    c.rows = rows
+    c.D = layer.num_input_channels
+    c.K = layer.num_bins
+    c.hidden = layer.num_hidden_channels
+    c.identity_features = p.identity_features.data_ptr()
+    c.transform_features = p.transform_features.data_ptr()
+    c.tail_bound = layer.tail_bound
+    return c
+
+
+def _check_shapes(layer, rows, params, uw, uh, ud):
+    """The kernels index params [rows][n][3K+1] and the unconditional [n][K], [n][K], [n][K+1]
+    from the layer's sizes: refuse anything else before launching."""
+    n, K = layer.num_input_channels // 2, layer.num_bins
+    want = [(params, (rows, n * (3 * K + 1))), (uw, (n, K)), (uh, (n, K)), (ud, (n, K + 1))]
+    for t, shp in want:
+        if tuple(t.shape) != shp or t.dtype != torch.float32:
+            raise ValueError(f"coupling operand of shape {tuple(t.shape)} / {t.dtype}, expected {shp} float32")
+
+
+def fused_coupling_ok(layer, x):
+    """Device f32 rows, an instantiated K, index buffers on the same device."""
+    p = layer.prqct
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] == layer.num_input_channels
+            and layer.num_bins in _HIP_K and p.identity_features.device == x.device
+            and p.identity_features.dtype == torch.int64 and p.transform_features.dtype == torch.int64)
+
+
+class _Features(torch.autograd.Function):
+    """t = [cos(s x_id), sin(s x_id)] (nn.py:120-137) and its adjoint."""
+
+    @staticmethod
+    def forward(ctx, x, layer):
+        from .. import _lib
+
+        x = x.contiguous()
+        t = torch.empty_like(x)
+        c = _coupling_desc(layer, x.shape[0])
+        _lib.require_device(x)
+        _lib.check(_lib.load().fs_coupling_features_fwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(t), _lib.stream_ptr()),
+                   "fs_coupling_features_fwd")
+        ctx.save_for_backward(x)
+        ctx.layer = layer
+        return t
+
+    @staticmethod
+    def backward(ctx, gt):
+        from .. import _lib
+
+        (x,) = ctx.saved_tensors
+        gt = gt.contiguous()
+        gx = torch.empty_like(x)
+        c = _coupling_desc(ctx.layer, x.shape[0])
+        _lib.check(_lib.load().fs_coupling_features_bwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(gt), _lib.ptr(gx),
+                                                        _lib.stream_ptr()), "fs_coupling_features_bwd")
+        return gx, None
+
+
+class _DensitySplines(torch.autograd.Function):
+    """Coupling.forward after the conditioner (coupling.py:71-102): conditional spline of the
+    transform half, unconditional spline of the identity half, half-roll, and
+    lq_out = lq_in + both log-det sums; backward through both splines."""
+
+    @staticmethod
+    def forward(ctx, x, params, uw, uh, ud, lq_in, layer):
+        from .. import _lib
+
+        x = x.contiguous()
+        params = params.contiguous()
+        uw, uh, ud = uw.contiguous(), uh.contiguous(), ud.contiguous()
+        _check_shapes(layer, x.shape[0], params, uw, uh, ud)
+        if lq_in is not None and tuple(lq_in.shape) != (x.shape[0],):
+            raise ValueError("log_q must be [rows]")
+        out = torch.empty_like(x)
+        lq = torch.empty((x.shape[0],), dtype=torch.float32, device=x.device)
+        c = _coupling_desc(layer, x.shape[0])
+        _lib.require_device(x, params, uw, lq_in)
+        _lib.check(_lib.load().fs_coupling_density_fwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(params), _lib.ptr(uw),
+                                                       _lib.ptr(uh), _lib.ptr(ud), _lib.ptr(lq_in), _lib.ptr(out),
+                                                       _lib.ptr(lq), _lib.stream_ptr()), "fs_coupling_density_fwd")
+        ctx.save_for_backward(x, params, uw, uh, ud)
+        ctx.layer = layer
+        ctx.has_lq = lq_in is not None
+        return out, lq
+
+    @staticmethod
+    def backward(ctx, g_out, g_lq):
+        from .. import _lib
+
+        x, params, uw, uh, ud = ctx.saved_tensors
+        layer = ctx.layer
+        K = layer.num_bins
+        g_out = g_out.contiguous() if g_out is not None else None
+        g_lq = g_lq.contiguous() if g_lq is not None else None
+        gx = torch.empty_like(x)
+        gp = torch.empty_like(params)
+        gu = torch.empty((x.shape[0], x.shape[1] // 2, 3 * K + 1), dtype=torch.float32, device=x.device)
+        c = _coupling_desc(layer, x.shape[0])
+        _lib.check(_lib.load().fs_coupling_density_bwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(params), _lib.ptr(uw),
+                                                       _lib.ptr(uh), _lib.ptr(ud), _lib.ptr(g_out), _lib.ptr(g_lq),
+                                                       _lib.ptr(gx), _lib.ptr(gp), _lib.ptr(gu), _lib.stream_ptr()),
+                   "fs_coupling_density_bwd")
+        gs = gu.sum(0)  # the unconditional parameters are shared by every row
+        return (gx, gp, gs[:, :K], gs[:, K:2 * K], gs[:, 2 * K:], g_lq if ctx.has_lq else None, None)
+
+
+def conditioner_from_features(net, t):
+    """ResidualNet.forward from the periodic features t (the rest of conditioner())."""
+    if _fused_ok(net, t):
+        return _conditioner_fused(net, t)
+    t = net.initial_layer(t)
+    for blk in net.blocks:
+        u = blk.batch_norm_layers[0](t)
+        u = F.relu(u)
+        u = blk.linear_layers[0](u)
+        u = blk.batch_norm_layers[1](u)
+        u = F.relu(u)
+        u = blk.linear_layers[1](u)
+        t = t + u
+    return net.final_layer(t)
+
+
+def density_step(layer, x, log_q):
+    """One layer of forward_kld on the device: (z, log_q + log_det), differentiable."""
+    p = layer.prqct
+    t = _Features.apply(x, layer)
+    params = conditioner_from_features(p.transform_net, t)
+    u = p.unconditional_transform
+    return _DensitySplines.apply(x, params, u.unnormalized_widths, u.unnormalized_heights,
+                                 u.unnormalized_derivatives, log_q, layer)
+
+
+@torch.no_grad()
+def sample_step(layer, z, log_q, nan_flag):
+    """One layer of reverse_kld's sampling direction on the device, without autograd:
+    (z, log_q - log_det); nan_flag (int32 [1]) |= 1 on a NaN discriminant."""
+    from .. import _lib
+
+    p = layer.prqct
+    z = z.contiguous()
+    rows = z.shape[0]
+    u = p.unconditional_transform
+    uw, uh, ud = (v.detach().contiguous() for v in (u.unnormalized_widths, u.unnormalized_heights,
+                                                      u.unnormalized_derivatives))
+    _check_shapes(layer, rows, torch.empty((rows, uw.shape[0] * (3 * layer.num_bins + 1))), uw, uh, ud)
+    t = torch.empty_like(z)
+    out = torch.empty_like(z)
+    lad_u = torch.empty((rows,), dtype=torch.float32, device=z.device)
+    c = _coupling_desc(layer, rows)
+    L = _lib.load()
+    _lib.require_device(z, uw, log_q, nan_flag)
+    _lib.check(L.fs_coupling_sample_pre(ctypes.byref(c), _lib.ptr(z), _lib.ptr(uw), _lib.ptr(uh), _lib.ptr(ud),
+                                        _lib.ptr(t), _lib.ptr(out), _lib.ptr(lad_u), _lib.ptr(nan_flag),
+                                        _lib.stream_ptr()), "fs_coupling_sample_pre")
+    params = conditioner_from_features(p.transform_net, t).contiguous()
+    _check_shapes(layer, rows, params, uw, uh, ud)
+    if log_q is not None and tuple(log_q.shape) != (rows,):
+        raise ValueError("log_q must be [rows]")
+    lq = torch.empty_like(lad_u)
+    _lib.check(L.fs_coupling_sample_post(ctypes.byref(c), _lib.ptr(params), _lib.ptr(lad_u), _lib.ptr(log_q),
+                                         _lib.ptr(out), _lib.ptr(lq), _lib.ptr(nan_flag), _lib.stream_ptr()),
+               "fs_coupling_sample_post")
+    return out, lq

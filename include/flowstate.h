@@ -250,6 +250,46 @@ int fs_bn_relu_train_fwd(int64_t Bn, int32_t H, const float *x, const float *gam
 int fs_bn_relu_train_bwd(int64_t Bn, int32_t H, const float *x, const float *y, const float *dy, const float *gamma,
                          const float *mean, const float *invstd, float *dx, float *dgamma, float *dbeta, void *stream);
 
+/* One circular-RQS coupling layer of the training path around its conditioner
+ * (Coupling.forward / inverse, NF/normflows/flows/neural_spline/coupling.py:71-134;
+ * periodic features nn.py:120-137; replaces the per-layer gather / cos / sin / cat /
+ * spline / index_copy / roll / sum kernels of autograd over torch ops).  x, z, out
+ * [rows][D] f32 row-major; identity_features / transform_features [D/2] int64 (the
+ * layer's buffers); params [rows][D/2][3K+1] = the conditioner output; uw, uh [D/2][K],
+ * ud [D/2][K+1] = the unconditional spline; t [rows][D] = [cos(s x_id), sin(s x_id)],
+ * s = pi / tail_bound; hidden = the conditioner width (params / sqrt(hidden)). */
+typedef struct fs_coupling {
+    int64_t rows;
+    int32_t D, K, hidden;
+    const int64_t *identity_features, *transform_features;
+    double tail_bound;
+} fs_coupling;
+
+/* Density direction, before the conditioner: t from x. */
+int fs_coupling_features_fwd(const fs_coupling *c, const float *x, float *t, void *stream);
+/* ... and after it: out = the half-rolled layer output, lq_out = lq_in (nullable = 0) +
+ * the two splines' log-det sums. */
+int fs_coupling_density_fwd(const fs_coupling *c, const float *x, const float *params, const float *uw,
+                            const float *uh, const float *ud, const float *lq_in, float *out, float *lq_out,
+                            void *stream);
+/* Its adjoints from g_out [rows][D] and g_lq [rows] (nullable = 0): gx [rows][D] through
+ * the splines, g_params [rows][D/2][3K+1], g_u [rows][D/2][3K+1] = per-row adjoints of
+ * (uw, uh, ud) (their sum over rows is the parameter gradient). */
+int fs_coupling_density_bwd(const fs_coupling *c, const float *x, const float *params, const float *uw,
+                            const float *uh, const float *ud, const float *g_out, const float *g_lq, float *gx,
+                            float *g_params, float *g_u, void *stream);
+/* Adjoint of t: gx [rows][D] (zero at the transform positions). */
+int fs_coupling_features_bwd(const fs_coupling *c, const float *x, const float *g_t, float *gx, void *stream);
+/* Sampling direction, forward only, in two launches around the conditioner:
+ * pre: t, out (identity half through the inverse unconditional spline, transform half
+ * copied), lad_u [rows]; post: the transform half through the inverse conditional spline
+ * (in place in out), lq_out = lq_in - (lad_u + its log-det sum).  nan_flag (nullable)
+ * |= 1 on a NaN discriminant (splines.py:176-183). */
+int fs_coupling_sample_pre(const fs_coupling *c, const float *z, const float *uw, const float *uh, const float *ud,
+                           float *t, float *out, float *lad_u, int32_t *nan_flag, void *stream);
+int fs_coupling_sample_post(const fs_coupling *c, const float *params, const float *lad_u, const float *lq_in,
+                            float *out, float *lq_out, int32_t *nan_flag, void *stream);
+
 /* ------------------------------------------------------------------ */
 /* Local moves (MCMC/monte_carlo.py)                                   */
 /* ------------------------------------------------------------------ */

@@ -118,3 +118,80 @@ def test_conditioner_falls_back_outside_train_mode():
     net.train()
     assert AF._fused_ok(net, t)
     assert not AF._fused_ok(net, t[:1])  # torch raises on a batch of one in train mode
+
+
+def a2_layer(seed, N=64, K=15, H=128):
+    from flowstate.models import build_flow, half_box
+
+    torch.manual_seed(seed)
+    m = build_flow(N, bound=half_box(N), device="cpu", L=1, H=H, nb=2, K=K)
+    layer = m.flows[0]
+    with torch.no_grad():  # leave the identity init: non-trivial splines and BatchNorm
+        for prm in layer.parameters():
+            prm.add_(0.05 * torch.randn_like(prm))
+    return layer.cuda()
+
+
+@pytest.mark.parametrize("K", [15, 8])
+def test_density_step_matches_torch_ops(K):
+    """density_step (fs_coupling_features_* + fs_coupling_density_*) against
+    coupling_density over torch ops: outputs, log q, input and parameter gradients,
+    running statistics; rows include coordinates outside [-B, B] (identity tails)."""
+    layer = a2_layer(5, K=K)
+    ref = copy.deepcopy(layer)
+    layer.train()
+    ref.train()
+    B = layer.tail_bound
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = (torch.rand(256, layer.num_input_channels, device="cuda", generator=g) * 2 - 1) * B
+    x[:8, :5] = B * 1.5  # outside the tails: identity, log-det 0
+    lq0 = torch.randn(256, device="cuda", generator=g)
+    x1 = x.clone().requires_grad_(True)
+    x2 = x.clone().requires_grad_(True)
+    assert AF.fused_coupling_ok(layer, x1)
+    z1, lq1 = AF.density_step(layer, x1, lq0)
+    z2, ld2 = AF.coupling_density(ref, x2)
+    lq2 = lq0 + ld2
+    close(z1, z2, 1e-5, "z")
+    close(lq1, lq2, 1e-5, "log q")
+    gz = torch.randn_like(z1)
+    gl = torch.randn_like(lq1)
+    ((z1 * gz).sum() + (lq1 * gl).sum()).backward()
+    ((z2 * gz).sum() + (lq2 * gl).sum()).backward()
+    close(x1.grad, x2.grad, 1e-4, "x grad")
+    for (n, p1), (_, p2) in zip(layer.named_parameters(), ref.named_parameters()):
+        if p2.grad is None:
+            assert p1.grad is None or not p1.grad.abs().max().item(), n
+            continue
+        close(p1.grad, p2.grad, 1e-4, n)
+    for (n, b1), (_, b2) in zip(layer.named_buffers(), ref.named_buffers()):
+        if b1.dtype == torch.int64:
+            assert torch.equal(b1, b2), n
+        else:
+            close(b1, b2, 1e-5, n)
+
+
+def test_sample_step_matches_torch_ops():
+    """sample_step (fs_coupling_sample_pre / _post) against coupling_sample, no autograd."""
+    layer = a2_layer(6)
+    ref = copy.deepcopy(layer)
+    layer.train()
+    ref.train()
+    B = layer.tail_bound
+    g = torch.Generator(device="cuda").manual_seed(2)
+    z = (torch.rand(256, layer.num_input_channels, device="cuda", generator=g) * 2 - 1) * B
+    z[3:6, 7:9] = -B * 1.2
+    lq0 = torch.randn(256, device="cuda", generator=g)
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    with torch.no_grad():
+        z1, lq1 = AF.sample_step(layer, z, lq0, flag)
+        z2, ld2 = AF.coupling_sample(ref, z)
+        AF._nan_flags.clear()
+    close(z1, z2, 1e-5, "z")
+    close(lq1, lq0 - ld2, 1e-5, "log q")
+    assert int(flag.item()) == 0
+    for (n, b1), (_, b2) in zip(layer.named_buffers(), ref.named_buffers()):
+        if b1.dtype == torch.int64:
+            assert torch.equal(b1, b2), n
+        else:
+            close(b1, b2, 1e-5, n)
