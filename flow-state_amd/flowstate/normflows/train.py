@@ -22,6 +22,8 @@ torch.cuda.graph (fused spline kernels and HIP GEMMs included) and replays it:
   * the spline's NaN-discriminant flags are reduced inside the graph and checked after
     the replay (the reference raises ValueError; here it is raised after the step).
 """
+import inspect
+
 import torch
 
 from . import autograd_flow as AF
@@ -90,8 +92,7 @@ class GraphedTrainStep:
         # the parameters, BatchNorm buffers and optimizer state back: capturing must not
         # change the model
         saved = [t.detach().clone() for t in list(model.parameters()) + list(model.buffers())]
-        saved_opt = [[v.detach().clone() if torch.is_tensor(v) else v for v in self.opt.state[p].values()]
-                     for p in self.params] if self.opt.state else None
+        saved_opt = [v.detach().clone() for v in self._opt_tensors()] if self.opt.state else None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -101,10 +102,8 @@ class GraphedTrainStep:
         with torch.no_grad():
             for t, v in zip(list(model.parameters()) + list(model.buffers()), saved):
                 t.copy_(v)
-            for i, p in enumerate(self.params):
-                for j, v in enumerate(self.opt.state[p].values()):
-                    if torch.is_tensor(v):
-                        v.copy_(saved_opt[i][j]) if saved_opt else v.zero_()
+            for j, v in enumerate(self._opt_tensors()):
+                v.copy_(saved_opt[j]) if saved_opt else v.zero_()
         # snapshots of everything the optimizer step mutates: parameters and Adam state
         # live in a few flat buffers, so the skip-on-non-finite snapshot / restore is 4
         # copies + 4 selects instead of ~4 per parameter tensor (~8k graph nodes at A2)
@@ -136,6 +135,9 @@ class GraphedTrainStep:
             AF._defer_nan = False
         return _Captured(graph, x, loss.detach(), nan_flag)  # keep no autograd graph alive
 
+    def _opt_tensors(self):
+        return [v for st in self.opt.state.values() for v in st.values() if torch.is_tensor(v)]
+
     def _bind_grads(self):
         """(Re)attach the flat gradient views (a zero_grad(set_to_none=True) elsewhere
         drops them; the captured graphs keep using the views regardless)."""
@@ -166,22 +168,26 @@ class GraphedTrainStep:
         self._flat_grad = torch.zeros_like(flat)
         self._grad_views = [self._flat_grad[o:o + n].view_as(p) for p, o, n in zip(ps, offs, sizes)]
         self._bind_grads()
-        bufs = [flat]
+        # Adam is elementwise, so one optimizer over the flat buffer is the same update as one
+        # per parameter, in a handful of launches instead of a per-tensor fallback of
+        # ~2 x (number of parameters) kernels: its state is the per-parameter state
+        # concatenated (every used parameter has taken the same number of steps)
+        state = {}
         for k, v0 in list(self.opt.state[ps[0]].items()):
             if not torch.is_tensor(v0):
-                continue
-            vals = [self.opt.state[p][k] for p in ps]
-            if v0.dim() == 0:  # capturable Adam's per-parameter step counts
-                buf = torch.stack(vals)
-                for i, p in enumerate(ps):
-                    self.opt.state[p][k] = buf[i]
+                state[k] = v0
+            elif v0.dim() == 0:  # capturable Adam's step count
+                state[k] = v0.detach().clone()
             else:
-                buf = torch.cat([v.reshape(-1) for v in vals])
-                for p, o, n in zip(ps, offs, sizes):
-                    self.opt.state[p][k] = buf[o:o + n].view_as(p)
-            bufs.append(buf)
+                state[k] = torch.cat([self.opt.state[p][k].reshape(-1) for p in ps])
+        self._flat_param = torch.nn.Parameter(flat)
+        self._flat_param.grad = self._flat_grad
+        known = inspect.signature(torch.optim.Adam.__init__).parameters
+        group = {k: v for k, v in self.opt.param_groups[0].items() if k != "params" and k in known}
+        self.opt = torch.optim.Adam([self._flat_param], **group)
+        self.opt.state[self._flat_param] = state
         self.model.invalidate_packed()
-        return bufs
+        return [flat] + [v for v in state.values() if torch.is_tensor(v)]
 
     def add_batch_size(self, bs, warmup=3):
         """Capture one more batch size (warm-up steps are undone, as at construction)."""
