@@ -58,24 +58,32 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     float rs = 0.f;
+    // PF k-blocks of loads in flight per wave (the operands come from L2 / the last
+    // kernel's output, so the loop is latency-bound without them)
+    constexpr int PF = 4;
     const int64_t step = 8 * SPLIT;
-    int64_t kb = 8 * w;
-    t4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
-    if (kb < g.K) {
-        a = load4<AK>(Ap, g.sak, kb + 4 * h, g.K, aok);
-        b = load4<BK>(Bp, g.sbk, kb + 4 * h, g.K, bok);
-    }
-    for (; kb < g.K; kb += step) {
-        t4 an = a, bn = b;
-        if (kb + step < g.K) {  // next k-block in flight under this one's MFMAs
-            an = load4<AK>(Ap, g.sak, kb + step + 4 * h, g.K, aok);
-            bn = load4<BK>(Bp, g.sbk, kb + step + 4 * h, g.K, bok);
-        }
+    const int64_t kb0 = 8 * w;
+    t4 a[PF], b[PF];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
-        if (rows) rs += ((a[0] + a[1]) + a[2]) + a[3];
-        a = an;
-        b = bn;
+    for (int s = 0; s < PF; ++s) {
+        const int64_t k = kb0 + s * step;
+        a[s] = load4<AK>(Ap, g.sak, k + 4 * h, g.K, aok && k < g.K);
+        b[s] = load4<BK>(Bp, g.sbk, k + 4 * h, g.K, bok && k < g.K);
+    }
+    for (int64_t kb = kb0; kb < g.K; kb += PF * step) {
+#pragma unroll
+        for (int s = 0; s < PF; ++s) {
+            const int64_t k = kb + s * step;
+            if (k < g.K) {  // wave-uniform
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][j], b[s][j], acc, 0, 0, 0);
+                if (rows) rs += ((a[s][0] + a[s][1]) + a[s][2]) + a[s][3];
+                const int64_t kn = k + PF * step;
+                a[s] = load4<AK>(Ap, g.sak, kn + 4 * h, g.K, aok && kn < g.K);
+                b[s] = load4<BK>(Bp, g.sbk, kn + 4 * h, g.K, bok && kn < g.K);
+            }
+        }
     }
     if (SPLIT > 1) {
         if (w > 0) part[w - 1][lane] = acc;
@@ -121,6 +129,9 @@ __device__ __forceinline__ float wg_colsum(float v, float (*red)[kBnCols], int c
     return s;
 }
 
+// R > 0: every thread holds its R rows (rows rg + q kBnRg) in registers, so each column is
+// read once and all of a thread's loads are in flight together; R = 0: any batch, re-read
+template <int R>
 __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_fwd_kernel(
     int64_t B, int H, const float *__restrict__ x, const float *__restrict__ gamma, const float *__restrict__ beta,
     float *running_mean, float *running_var, int64_t *num_batches, float momentum, float eps, float *__restrict__ y,
@@ -130,23 +141,51 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_fwd_kernel(
     const int col = blockIdx.x * kBnCols + c;
     const bool ok = col < H;
     const float *xc = x + (ok ? col : 0);
+    float v[R > 0 ? R : 1];
     float s = 0.f;
-    if (ok)
+    if (R > 0) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int64_t i = rg + (int64_t)q * kBnRg;
+            v[q] = (ok && i < B) ? xc[i * H] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < R; ++q) s += v[q];
+    } else if (ok) {
         for (int64_t i = rg; i < B; i += kBnRg) s += xc[i * H];
+    }
     const float mean = wg_colsum(s, red, c, rg) / (float)B;
-    float q = 0.f;
-    if (ok)
+    float sq = 0.f;
+    if (R > 0) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const float d = v[q] - mean;
+            if (rg + (int64_t)q * kBnRg < B) sq += d * d;
+        }
+    } else if (ok) {
         for (int64_t i = rg; i < B; i += kBnRg) {
             const float d = xc[i * H] - mean;
-            q += d * d;
+            sq += d * d;
         }
-    const float var = wg_colsum(q, red, c, rg) / (float)B;
+    }
+    const float var = wg_colsum(sq, red, c, rg) / (float)B;
     const float invstd = 1.f / sqrtf(var + eps);
     if (!ok) return;
     const float gm = gamma[col], bt = beta[col];
-    for (int64_t i = rg; i < B; i += kBnRg) {
-        const float v = gm * ((xc[i * H] - mean) * invstd) + bt;
-        y[i * H + col] = v > 0.f ? v : 0.f;
+    if (R > 0) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int64_t i = rg + (int64_t)q * kBnRg;
+            if (i < B) {
+                const float o = gm * ((v[q] - mean) * invstd) + bt;
+                y[i * H + col] = o > 0.f ? o : 0.f;
+            }
+        }
+    } else {
+        for (int64_t i = rg; i < B; i += kBnRg) {
+            const float o = gm * ((xc[i * H] - mean) * invstd) + bt;
+            y[i * H + col] = o > 0.f ? o : 0.f;
+        }
     }
     if (rg == 0) {
         mean_out[col] = mean;
@@ -161,6 +200,7 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_fwd_kernel(
 
 // dz = dy * (y > 0); dbeta = sum dz; dgamma = sum dz xhat;
 // dx = gamma invstd (dz - dbeta / B - xhat dgamma / B)   (torch's batch_norm_backward_elemt)
+template <int R>
 __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
     int64_t B, int H, const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ dy,
     const float *__restrict__ gamma, const float *__restrict__ mean, const float *__restrict__ invstd,
@@ -171,22 +211,46 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
     const bool ok = col < H;
     const int64_t o = ok ? col : 0;
     const float mu = mean[o], is = invstd[o];
+    float dzv[R > 0 ? R : 1], xhv[R > 0 ? R : 1];
     float sd = 0.f, sdx = 0.f;
-    if (ok)
+    if (R > 0) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int64_t i = rg + (int64_t)q * kBnRg;
+            const bool in = ok && i < B;
+            const float yv = in ? y[i * H + o] : 0.f, g = in ? dy[i * H + o] : 0.f, xv = in ? x[i * H + o] : mu;
+            dzv[q] = yv > 0.f ? g : 0.f;
+            xhv[q] = (xv - mu) * is;
+        }
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            sd += dzv[q];
+            sdx += dzv[q] * xhv[q];
+        }
+    } else if (ok) {
         for (int64_t i = rg; i < B; i += kBnRg) {
             const float dz = y[i * H + o] > 0.f ? dy[i * H + o] : 0.f;
             sd += dz;
             sdx += dz * ((x[i * H + o] - mu) * is);
         }
+    }
     const float db = wg_colsum(sd, red, c, rg);
     const float dg = wg_colsum(sdx, red, c, rg);
     if (!ok) return;
     const float gm = gamma[col];
     const float mdb = db / (float)B, mdg = dg / (float)B;
-    for (int64_t i = rg; i < B; i += kBnRg) {
-        const float dz = y[i * H + col] > 0.f ? dy[i * H + col] : 0.f;
-        const float xh = (x[i * H + col] - mu) * is;
-        dx[i * H + col] = (dz - mdb - xh * mdg) * (is * gm);
+    if (R > 0) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int64_t i = rg + (int64_t)q * kBnRg;
+            if (i < B) dx[i * H + col] = (dzv[q] - mdb - xhv[q] * mdg) * (is * gm);
+        }
+    } else {
+        for (int64_t i = rg; i < B; i += kBnRg) {
+            const float dz = y[i * H + col] > 0.f ? dy[i * H + col] : 0.f;
+            const float xh = (x[i * H + col] - mu) * is;
+            dx[i * H + col] = (dz - mdb - xh * mdg) * (is * gm);
+        }
     }
     if (rg == 0) {
         if (dgamma) dgamma[col] = dg;
@@ -221,9 +285,13 @@ hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const flo
                                      float *rm, float *rv, int64_t *nbt, float momentum, float eps, float *y,
                                      float *mean, float *invstd, hipStream_t st) {
     if (B <= 0 || H <= 0) return hipSuccess;
-    hipLaunchKernelGGL(bn_relu_train_fwd_kernel, dim3((unsigned)((H + kBnCols - 1) / kBnCols)),
-                       dim3(kBnCols * kBnRg), 0, st, B, H, x, gamma, beta, rm, rv, nbt, momentum, eps, y, mean,
-                       invstd);
+    const dim3 grid((unsigned)((H + kBnCols - 1) / kBnCols)), block(kBnCols * kBnRg);
+    if (B <= 16 * kBnRg)
+        hipLaunchKernelGGL(bn_relu_train_fwd_kernel<16>, grid, block, 0, st, B, H, x, gamma, beta, rm, rv, nbt,
+                           momentum, eps, y, mean, invstd);
+    else
+        hipLaunchKernelGGL(bn_relu_train_fwd_kernel<0>, grid, block, 0, st, B, H, x, gamma, beta, rm, rv, nbt,
+                           momentum, eps, y, mean, invstd);
     return hipGetLastError();
 }
 
@@ -231,7 +299,12 @@ hipError_t fs_bn_relu_train_bwd_impl(int64_t B, int H, const float *x, const flo
                                      const float *gamma, const float *mean, const float *invstd, float *dx,
                                      float *dgamma, float *dbeta, hipStream_t st) {
     if (B <= 0 || H <= 0) return hipSuccess;
-    hipLaunchKernelGGL(bn_relu_train_bwd_kernel, dim3((unsigned)((H + kBnCols - 1) / kBnCols)),
-                       dim3(kBnCols * kBnRg), 0, st, B, H, x, y, dy, gamma, mean, invstd, dx, dgamma, dbeta);
+    const dim3 grid((unsigned)((H + kBnCols - 1) / kBnCols)), block(kBnCols * kBnRg);
+    if (B <= 16 * kBnRg)
+        hipLaunchKernelGGL(bn_relu_train_bwd_kernel<16>, grid, block, 0, st, B, H, x, y, dy, gamma, mean, invstd, dx,
+                           dgamma, dbeta);
+    else
+        hipLaunchKernelGGL(bn_relu_train_bwd_kernel<0>, grid, block, 0, st, B, H, x, y, dy, gamma, mean, invstd, dx,
+                           dgamma, dbeta);
     return hipGetLastError();
 }

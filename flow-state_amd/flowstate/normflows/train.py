@@ -123,6 +123,7 @@ class GraphedTrainStep:
                 self._zero_grad()
                 loss = step_loss(model, x, self.batch_size, self.alpha)
                 loss.backward()
+                self._gather_grads()
                 finite = ~(torch.isnan(loss) | torch.isinf(loss))
                 for b, t in zip(self._backup, self._state_tensors):
                     b.copy_(t.detach())
@@ -138,18 +139,21 @@ class GraphedTrainStep:
     def _opt_tensors(self):
         return [v for st in self.opt.state.values() for v in st.values() if torch.is_tensor(v)]
 
-    def _bind_grads(self):
-        """(Re)attach the flat gradient views (a zero_grad(set_to_none=True) elsewhere
-        drops them; the captured graphs keep using the views regardless)."""
-        for p, g in zip(self.params, self._grad_views):
-            if p.grad is not g:
-                p.grad = g
-
     def _zero_grad(self):
         if getattr(self, "_flat_grad", None) is not None:
-            self._flat_grad.zero_()  # one fill for every parameter's gradient
+            for p in self.params:  # autograd hands each parameter its gradient buffer as is
+                p.grad = None
         else:
             self.opt.zero_grad(set_to_none=False)
+
+    def _gather_grads(self):
+        """The parameters' gradients into the flat buffer Adam reads: one concatenation
+        instead of one accumulate-add per parameter tensor."""
+        if getattr(self, "_flat_grad", None) is None:
+            return
+        gs = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=p.device)
+              for p in self.params]
+        torch.cat(gs, out=self._flat_grad)
 
     @torch.no_grad()
     def _flatten(self):
@@ -163,11 +167,8 @@ class GraphedTrainStep:
         flat = torch.cat([p.detach().reshape(-1) for p in ps])
         for p, o, n in zip(ps, offs, sizes):
             p.data = flat[o:o + n].view_as(p)
-        # gradients too: AccumulateGrad adds into an existing .grad in place, so the views
-        # stay the gradient storage and zeroing them is one fill
+        # gradients: gathered into one flat buffer after each backward (_gather_grads)
         self._flat_grad = torch.zeros_like(flat)
-        self._grad_views = [self._flat_grad[o:o + n].view_as(p) for p, o, n in zip(ps, offs, sizes)]
-        self._bind_grads()
         # Adam is elementwise, so one optimizer over the flat buffer is the same update as one
         # per parameter, in a handful of launches instead of a per-tensor fallback of
         # ~2 x (number of parameters) kernels: its state is the per-parameter state
@@ -205,8 +206,6 @@ class GraphedTrainStep:
     def eager_step(self, batch):
         """One step on a batch of another size (the epoch's last, partial batch) with the
         same optimizer state, outside the graph; returns the loss tensor."""
-        if getattr(self, "_flat_grad", None) is not None:
-            self._bind_grads()
         loss = self._eager_step(batch)
         self.model.invalidate_packed()
         return loss
@@ -216,6 +215,7 @@ class GraphedTrainStep:
         loss = step_loss(self.model, x, self.batch_size, self.alpha)
         if bool(~(torch.isnan(loss) | torch.isinf(loss))):
             loss.backward()
+            self._gather_grads()
             self.opt.step()
         return loss.detach()
 
