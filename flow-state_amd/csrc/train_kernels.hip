@@ -21,6 +21,16 @@
 
 #include "fs_internal.h"
 
+#ifndef FS_GEMM_PF
+#define FS_GEMM_PF 2  // k-blocks of operand loads in flight per wave
+#endif
+#ifndef FS_GEMM_SPLIT
+#define FS_GEMM_SPLIT 4  // waves sharing one 32 x 32 tile's reduction (short K)
+#endif
+#ifndef FS_GEMM_SPLIT_LONG
+#define FS_GEMM_SPLIT_LONG 16  // ... for K > 512
+#endif
+
 namespace fs {
 
 typedef float t4 __attribute__((ext_vector_type(4)));
@@ -60,7 +70,7 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_f32_kernel(GemmArgs g) {
     float rs = 0.f;
     // PF k-blocks of loads in flight per wave (the operands come from L2 / the last
     // kernel's output, so the loop is latency-bound without them)
-    constexpr int PF = 4;
+    constexpr int PF = FS_GEMM_PF;
     const int64_t step = 8 * SPLIT;
     const int64_t kb0 = 8 * w;
     t4 a[PF], b[PF];
@@ -269,14 +279,16 @@ hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st) {
     const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0;
     const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0;
     // enough waves per tile that each walks at most ~16 k-blocks
-    const int split = g.K > 8 * 4 * 16 ? 8 : 4;
+    const int split = g.K > 8 * 4 * 16 ? FS_GEMM_SPLIT_LONG : FS_GEMM_SPLIT;
 #define FS_G(S, A, B)                                                                           \
     if (split == S && ak == A && bk == B) {                                                     \
         hipLaunchKernelGGL((gemm_f32_kernel<S, A, B>), grid, dim3(64 * S), 0, st, g);           \
         return hipGetLastError();                                                               \
     }
-    FS_G(4, true, true) FS_G(4, true, false) FS_G(4, false, true) FS_G(4, false, false)
-    FS_G(8, true, true) FS_G(8, true, false) FS_G(8, false, true) FS_G(8, false, false)
+    FS_G(FS_GEMM_SPLIT, true, true) FS_G(FS_GEMM_SPLIT, true, false) FS_G(FS_GEMM_SPLIT, false, true)
+    FS_G(FS_GEMM_SPLIT, false, false)
+    FS_G(FS_GEMM_SPLIT_LONG, true, true) FS_G(FS_GEMM_SPLIT_LONG, true, false) FS_G(FS_GEMM_SPLIT_LONG, false, true)
+    FS_G(FS_GEMM_SPLIT_LONG, false, false)
 #undef FS_G
     return hipErrorInvalidValue;
 }

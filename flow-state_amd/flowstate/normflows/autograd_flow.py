@@ -176,6 +176,13 @@ def circular_rqs_torch(x, uw, uh, ud, B, inverse):
     return torch.where(inside, o, x), torch.where(inside, l, torch.zeros_like(l))
 
 
+# Output width from which the conditioner's final layer (n (3K+1) columns, 2944 at A2)
+# goes to hipBLASLt for its forward and input gradient: its macro tiles beat the
+# 32 x 32-tile kernel there (7.0 / 11.0 us against 8.7 / 27.9 us at 256 x 2944 x 128,
+# tools/train_gemm_probe.py), while the 128-wide layers run 3x faster on fs_linear_f32.
+_WIDE = 1024
+
+
 class _Linear(torch.autograd.Function):
     """nn.Linear (+ an optional residual added to the output) through fs_linear_f32
     (csrc/train_kernels.hip): y = x W^T + b (+ r); backward dx = dy W, dW = dy^T x and
@@ -188,13 +195,15 @@ class _Linear(torch.autograd.Function):
         x = x.contiguous()
         M, K = x.shape
         N = w.shape[0]
+        ctx.save_for_backward(x, w)
+        ctx.has_r = r is not None
+        if N >= _WIDE and r is None:
+            return torch.addmm(b, x, w.t())
         y = torch.empty((M, N), dtype=torch.float32, device=x.device)
         L = _lib.load()
         _lib.require_device(x, w, b, r)
         _lib.check(L.fs_linear_f32(M, N, K, _lib.ptr(x), K, 1, _lib.ptr(w), 1, K, _lib.ptr(b), _lib.ptr(r),
                                    N, _lib.ptr(y), N, None, _lib.stream_ptr()), "fs_linear_f32")
-        ctx.save_for_backward(x, w)
-        ctx.has_r = r is not None
         return y
 
     @staticmethod
@@ -207,7 +216,9 @@ class _Linear(torch.autograd.Function):
         N = w.shape[0]
         L = _lib.load()
         gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and N >= _WIDE:
+            gx = torch.mm(gy, w)
+        elif ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
             _lib.check(L.fs_linear_f32(M, K, N, _lib.ptr(gy), N, 1, _lib.ptr(w), K, 1, None, None, 0, _lib.ptr(gx),
                                        K, None, _lib.stream_ptr()), "fs_linear_f32")
