@@ -395,10 +395,13 @@ def _coupling_desc(layer, rows):
 
 
 def _check_shapes(layer, rows, params, uw, uh, ud):
-    """The kernels index params [rows][n][3K+1] and the unconditional [n][K], [n][K], [n][K+1]
-    from the layer's sizes: refuse anything else before launching."""
+    """The kernels index params [rows][n][3K+1] (None: not yet computed) and the
+    unconditional [n][K], [n][K], [n][K+1] from the layer's sizes: refuse anything else
+    before launching."""
     n, K = layer.num_input_channels // 2, layer.num_bins
-    want = [(params, (rows, n * (3 * K + 1))), (uw, (n, K)), (uh, (n, K)), (ud, (n, K + 1))]
+    want = [(uw, (n, K)), (uh, (n, K)), (ud, (n, K + 1))]
+    if params is not None:
+        want.append((params, (rows, n * (3 * K + 1))))
     for t, shp in want:
         if tuple(t.shape) != shp or t.dtype != torch.float32:
             raise ValueError(f"coupling operand of shape {tuple(t.shape)} / {t.dtype}, expected {shp} float32")
@@ -528,7 +531,7 @@ def sample_step(layer, z, log_q, nan_flag):
     u = p.unconditional_transform
     uw, uh, ud = (v.detach().contiguous() for v in (u.unnormalized_widths, u.unnormalized_heights,
                                                       u.unnormalized_derivatives))
-    _check_shapes(layer, rows, torch.empty((rows, uw.shape[0] * (3 * layer.num_bins + 1))), uw, uh, ud)
+    _check_shapes(layer, rows, None, uw, uh, ud)
     t = torch.empty_like(z)
     out = torch.empty_like(z)
     lad_u = torch.empty((rows,), dtype=torch.float32, device=z.device)
