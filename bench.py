@@ -164,6 +164,27 @@ def given_proposal(bmc, stepper, steps=3):
             "what": "energy + density pass + accept of supplied float32 proposals (proposal generation excluded)"}
 
 
+def config2(steps=5, C=4096, N=16):
+    """BASELINE config 2 (Algorithm 1, N=16, 4096 chains, A1 flow, f32) as a secondary
+    line: fused NF-MH steps/s with the same synthetic flow and states.  4096 chains are
+    64 workgroups of the flow kernel, a quarter of the CUs ("Next").  Reported
+    beside the headline, never as `value`."""
+    model = synthetic_model(N, torch.device("cuda"))
+    init, L = synthetic_states(N, C, 0)
+    phys = Physics(L, L, temperature=1.0, num_wells=2, V0_list=(-10.0, -10.5), r0=1.2, k=15)
+    bmc = BatchedMonteCarlo(model, init, phys, np.arange(42, 42 + C, dtype=np.uint64))
+    bmc.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        bmc.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"workload": "config 2: Algorithm 1, N=16, 4096 chains, A1 flow", "value": C * steps / dt,
+            "unit": "steps/s", "steps": steps, "ms_per_step": dt / steps * 1e3,
+            "acceptance_rate": int(bmc.n_accept.item()) / (C * (steps + 1))}
+
+
 class Stepper:
     """The fs_nf_mh_step kernel sequence, launched piecewise with HIP events."""
 
@@ -350,6 +371,8 @@ def main():
                     help="skip the secondary measurement of the split-bf16 modes")
     ap.add_argument("--no-given-proposal", action="store_true",
                     help="skip the secondary nf_big_move-equivalent measurement (supplied proposals)")
+    ap.add_argument("--no-config2", action="store_true",
+                    help="skip the secondary BASELINE config-2 line (N=16, 4096 chains)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -455,6 +478,8 @@ def main():
         out["alt_precision"] = alt_precisions(bmc, stepper)
     if world == 1 and not args.no_given_proposal:
         out["given_proposal"] = given_proposal(bmc, stepper)
+    if world == 1 and not args.no_config2:
+        out["config2"] = config2()
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
         # vs_baseline stays null: BASELINE.md has no published number for this metric
