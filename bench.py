@@ -164,25 +164,36 @@ def given_proposal(bmc, stepper, steps=3):
             "what": "energy + density pass + accept of supplied float32 proposals (proposal generation excluded)"}
 
 
-def config2(steps=5, C=4096, N=16):
+def config2(steps=16, C=4096, N=16):
     """BASELINE config 2 (Algorithm 1, N=16, 4096 chains, A1 flow, f32) as a secondary
     line: fused NF-MH steps/s with the same synthetic flow and states.  4096 chains are
-    64 workgroups of the flow kernel, a quarter of the CUs ("Next").  Reported
-    beside the headline, never as `value`."""
+    64 workgroups of the flow kernel, a quarter of the CUs, so BatchedMonteCarlo.step(n)
+    runs the proposal passes of several consecutive steps in one launch
+    (fs_nf_mh_steps: the same draws and results as one launch per step,
+    tests/test_gpu_mh.py::test_multi_step_launch_matches_single_steps); one step per
+    launch is reported beside it.  Never the headline `value`."""
     model = synthetic_model(N, torch.device("cuda"))
     init, L = synthetic_states(N, C, 0)
     phys = Physics(L, L, temperature=1.0, num_wells=2, V0_list=(-10.0, -10.5), r0=1.2, k=15)
     bmc = BatchedMonteCarlo(model, init, phys, np.arange(42, 42 + C, dtype=np.uint64))
-    bmc.step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        bmc.step()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    S = bmc.steps_per_launch()
+
+    def run(n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        bmc.step(n)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    run(S)  # warm-up
+    dt = run(steps)
+    bmc.MAX_STEPS_PER_LAUNCH = 1
+    run(1)
+    dt1 = run(4)
     return {"workload": "config 2: Algorithm 1, N=16, 4096 chains, A1 flow", "value": C * steps / dt,
-            "unit": "steps/s", "steps": steps, "ms_per_step": dt / steps * 1e3,
-            "acceptance_rate": int(bmc.n_accept.item()) / (C * (steps + 1))}
+            "unit": "steps/s", "steps": steps, "ms_per_step": dt / steps * 1e3, "steps_per_launch": S,
+            "one_step_per_launch": {"value": C * 4 / dt1, "ms_per_step": dt1 / 4 * 1e3},
+            "acceptance_rate": int(bmc.n_accept.item()) / int(bmc.attempts.sum().item())}
 
 
 class Stepper:

@@ -230,6 +230,56 @@ int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, i
     return hip_rc(e, "fs_nf_mh_step/accept");
 }
 
+int64_t fs_nf_mh_steps_ws_bytes(const fs_flow_dims *d, int64_t C, int64_t S) {
+    if (check_dims(d) != FS_OK || C < 0 || S < 1) return -1;
+    const int64_t D = 2 * d->N, R = C * S;
+    // config f32 [S C][D] | centered f32 [S C][D] | log_q f32 [S C] | E_new f64 [S C] | W_new f64 [S C]
+    return fs::rup(R * D * 4, 256) * 2 + fs::rup(R * 4, 256) + fs::rup(R * 8, 256) * 2;
+}
+
+int fs_nf_mh_steps(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C, int64_t S, uint64_t seed,
+                   uint64_t step0, int64_t chain_offset, double *E_old, double *W_old, double *nll_old, uint64_t *pcg,
+                   double *state, uint8_t *state_is_f32, uint8_t *accept, int64_t *attempts, int64_t *accepted,
+                   unsigned long long *n_accept, int32_t *err, int flags, void *ws, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    REQUIRE(p && C >= 0 && S >= 1 && (C == 0 || (packed && E_old && nll_old && pcg && accept && ws)),
+            "fs_nf_mh_steps: invalid arguments");
+    REQUIRE(!(flags & FS_MH_HYBRID), "fs_nf_mh_steps: FS_MH_HYBRID needs one step at a time (fs_nf_mh_step)");
+    REQUIRE(((uintptr_t)ws & 255) == 0, "fs_nf_mh_steps: workspace must be 256-byte aligned");
+    if (C == 0) return FS_OK;
+    const int64_t D = 2 * d->N, R = C * S;
+    char *w = (char *)ws;
+    float *config = (float *)w;
+    w += fs::rup(R * D * 4, 256);
+    float *centered = (float *)w;
+    w += fs::rup(R * D * 4, 256);
+    float *log_q = (float *)w;
+    w += fs::rup(R * 4, 256);
+    double *E_new = (double *)w;
+    w += fs::rup(R * 8, 256);
+    double *W_new = (double *)w;
+    hipStream_t st = (hipStream_t)stream;
+    const double half_width = p->Lx / 2.0;  // MonteCarlo.half_width (monte_carlo.py:66)
+    // the proposals of steps step0 .. step0+S-1 do not depend on the chain states: one
+    // launch of S*C rows per pass (rows s*C + c = step step0+s of chain c, the same Philox
+    // draws as S single steps), then the S accept/update launches in order
+    hipError_t e = fs_flow_pass_impl(d, packed, 2, nullptr, R, nullptr, nullptr, 0, config, centered, seed, step0,
+                                     chain_offset, half_width, err, st, C);
+    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_steps/propose");
+    e = fs_flow_pass_impl(d, packed, 0, centered, R, nullptr, log_q, 1, nullptr, nullptr, 0, 0, 0, 0.0, err, st);
+    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_steps/log_prob");
+    e = fs_energy_impl(p, config, 1, R, d->N, E_new, W_new, nullptr, nullptr, st);
+    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_steps/energy");
+    for (int64_t s = 0; s < S; ++s) {
+        e = fs_mh_accept_impl(p, C, d->N, E_old, W_old, nll_old, E_new + s * C, W_new + s * C, log_q + s * C, pcg,
+                              state, state_is_f32, state ? config + s * C * D : nullptr, accept, attempts, accepted,
+                              n_accept, flags, st);
+        if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_steps/accept");
+    }
+    return FS_OK;
+}
+
 int fs_local_moves(const fs_phys *p, int64_t C, int32_t N, double *state, const uint8_t *state_is_f32, double *E,
                    double *W, uint64_t *pcg, uint64_t *pcg_buf, double *max_disp, int64_t *attempts,
                    int64_t *accepted, int64_t *prev_counts, int64_t n_moves, int64_t step0, int32_t adjust_every,

@@ -34,6 +34,8 @@ struct FlowArgs {
     int64_t nrows;
     uint64_t seed, counter;
     int64_t row_offset;   // global index of row 0 (multi-GPU sharding of the proposal stream)
+    int64_t rows_per_counter;  // propose: > 0 = rows are (step, chain) = (row / rpc, row % rpc)
+                               // blocks of consecutive steps' proposals; 0 = one counter
     double half_width;
     int N, L, nb, K;
     int add_base;

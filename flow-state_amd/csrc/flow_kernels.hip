@@ -341,9 +341,13 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
         const int nq = (D + 3) / 4;
         for (int e = tid; e < kRows * nq; e += kThreads) {
             const int rr = e / nq, q = e - rr * nq;
-            const uint64_t gr = (uint64_t)(a.row_offset + row0 + rr);
-            uint4 c = make_uint4((uint32_t)gr, (uint32_t)(gr >> 32) ^ (uint32_t)(a.counter >> 32),
-                                 (uint32_t)a.counter, (uint32_t)q);
+            // Philox key (global chain, step): several steps' proposals in one launch
+            // (rows_per_counter > 0) draw exactly what one launch per step would
+            const int64_t lr = row0 + rr, rpc = a.rows_per_counter;
+            const uint64_t ctr = rpc > 0 ? a.counter + (uint64_t)(lr / rpc) : a.counter;
+            const uint64_t gr = (uint64_t)(a.row_offset + (rpc > 0 ? lr % rpc : lr));
+            uint4 c = make_uint4((uint32_t)gr, (uint32_t)(gr >> 32) ^ (uint32_t)(ctr >> 32), (uint32_t)ctr,
+                                 (uint32_t)q);
             uint4 o = philox4x32(c, make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32)));
             const uint32_t w[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
@@ -836,7 +840,7 @@ static void fill_args(FlowArgs &a, const fs_flow_dims *d, const void *packed, in
 hipError_t fs_flow_pass_impl(const fs_flow_dims *d, const void *packed, int mode, const float *in, int64_t B,
                              float *out, float *scalar, int add_base, float *config, float *centered,
                              uint64_t seed, uint64_t counter, int64_t row_offset, double half_width,
-                             int32_t *err, hipStream_t st) {
+                             int32_t *err, hipStream_t st, int64_t rows_per_counter) {
     if (B <= 0) return hipSuccess;
     FlowArgs a;
     fill_args(a, d, packed, B);
@@ -849,6 +853,7 @@ hipError_t fs_flow_pass_impl(const fs_flow_dims *d, const void *packed, int mode
     a.seed = seed;
     a.counter = counter;
     a.row_offset = row_offset;
+    a.rows_per_counter = rows_per_counter;
     a.half_width = half_width;
     a.err = err;
     if (d->precision != 0) return fs_flow_split_pass(a, mode, d->precision, d->N, d->H, d->K, st);

@@ -18,7 +18,7 @@ hipError_t fs_flow_pack_impl(const fs_flow_dims *d, const float *raw, float *pac
 hipError_t fs_flow_pass_impl(const fs_flow_dims *d, const void *packed, int mode, const float *in, int64_t B,
                              float *out, float *scalar, int add_base, float *config, float *centered,
                              uint64_t seed, uint64_t counter, int64_t row_offset, double half_width,
-                             int32_t *err, hipStream_t st);
+                             int32_t *err, hipStream_t st, int64_t rows_per_counter = 0);
 
 // split-bf16 flow image and pass (flow_split_kernels.hip; fs_flow_dims.precision 1 or 2)
 namespace fs { struct FlowArgs; }

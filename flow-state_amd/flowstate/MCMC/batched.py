@@ -191,19 +191,48 @@ class BatchedMonteCarlo:
         L = _lib.load()
         packed = self.model.packed()
         dims = self.model.dims()
-        ws = self._workspace()
         st = _lib.stream_ptr()
-        for _ in range(n):
-            _lib.check(L.fs_nf_mh_step(dims, _lib.ptr(packed), self.phys.c, self.C, self.proposal_seed,
-                                       self.step_count, self.chain_offset, _lib.ptr(self.E_old), _lib.ptr(self.W_old),
-                                       _lib.ptr(self.nll_old), _lib.ptr(self.pcg), _lib.ptr(self.state),
-                                       _lib.ptr(self.state_is_f32), _lib.ptr(self.accept),
-                                       _lib.ptr(self.attempts), _lib.ptr(self.accepted), _lib.ptr(self.n_accept),
-                                       _lib.ptr(self.err), self.flags | (_lib.FS_MH_HYBRID if self._moved else 0),
-                                       _lib.ptr(ws), st), "fs_nf_mh_step")
-            self.step_count += 1
+        done = 0
+        while done < n:
+            S = 1 if self._moved else min(n - done, self.steps_per_launch())
+            if S == 1:
+                _lib.check(L.fs_nf_mh_step(dims, _lib.ptr(packed), self.phys.c, self.C, self.proposal_seed,
+                                           self.step_count, self.chain_offset, _lib.ptr(self.E_old),
+                                           _lib.ptr(self.W_old), _lib.ptr(self.nll_old), _lib.ptr(self.pcg),
+                                           _lib.ptr(self.state), _lib.ptr(self.state_is_f32), _lib.ptr(self.accept),
+                                           _lib.ptr(self.attempts), _lib.ptr(self.accepted), _lib.ptr(self.n_accept),
+                                           _lib.ptr(self.err), self.flags | (_lib.FS_MH_HYBRID if self._moved else 0),
+                                           _lib.ptr(self._workspace()), st), "fs_nf_mh_step")
+            else:
+                _lib.check(L.fs_nf_mh_steps(dims, _lib.ptr(packed), self.phys.c, self.C, S, self.proposal_seed,
+                                            self.step_count, self.chain_offset, _lib.ptr(self.E_old),
+                                            _lib.ptr(self.W_old), _lib.ptr(self.nll_old), _lib.ptr(self.pcg),
+                                            _lib.ptr(self.state), _lib.ptr(self.state_is_f32), _lib.ptr(self.accept),
+                                            _lib.ptr(self.attempts), _lib.ptr(self.accepted),
+                                            _lib.ptr(self.n_accept), _lib.ptr(self.err), self.flags,
+                                            _lib.ptr(self._workspace_steps(S)), st), "fs_nf_mh_steps")
+            self.step_count += S
+            done += S
             self._moved = False
         return self.accept
+
+    # proposal rows per launch that fill the chip: 2 resident 64-chain workgroups on each
+    # of the 256 CUs (a batch that already fills it keeps one step per launch)
+    FILL_ROWS = 2 * 256 * 64
+    MAX_STEPS_PER_LAUNCH = 16
+
+    def steps_per_launch(self):
+        """Consecutive steps whose proposal passes share one launch (fs_nf_mh_steps)."""
+        return max(1, min(self.MAX_STEPS_PER_LAUNCH, self.FILL_ROWS // max(1, self.C)))
+
+    def _workspace_steps(self, S):
+        """Workspace of fs_nf_mh_steps for S steps (grown on demand, kept)."""
+        n = _lib.load().fs_nf_mh_steps_ws_bytes(self.model.dims(), self.C, S)
+        _lib.check(0 if n >= 0 else -1, "fs_nf_mh_steps_ws_bytes")
+        ws = getattr(self, "_ws_steps", None)
+        if ws is None or ws.numel() * 8 < n:
+            self._ws_steps = torch.empty((n + 7) // 8, dtype=torch.float64, device=self.device)
+        return self._ws_steps
 
     @_on_own_device
     def local_moves(self, n, adjust_every=0, sample_every=0, step0=0, log_accepts=False):

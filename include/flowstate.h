@@ -207,6 +207,19 @@ int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, i
                   int64_t *attempts, int64_t *accepted, unsigned long long *n_accept,
                   int32_t *err, int flags, void *ws, void *stream);
 
+/* S consecutive fs_nf_mh_step calls (steps step0 .. step0+S-1) with the same results:
+ * the proposals, their log q and energies do not depend on the chain states, so each
+ * pass runs once over S*C rows (a small C then fills the chip), followed by the S
+ * accept/update launches in order.  Not with FS_MH_HYBRID.  Workspace: config f32
+ * [S C][2N] | centered f32 [S C][2N] | log_q f32 [S C] | E_new f64 [S C] | W_new f64 [S C],
+ * 256-byte padded sections. */
+int64_t fs_nf_mh_steps_ws_bytes(const fs_flow_dims *d, int64_t C, int64_t S);
+int fs_nf_mh_steps(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C, int64_t S,
+                   uint64_t seed, uint64_t step0, int64_t chain_offset, double *E_old, double *W_old, double *nll_old,
+                   uint64_t *pcg, double *state, uint8_t *state_is_f32, uint8_t *accept,
+                   int64_t *attempts, int64_t *accepted, unsigned long long *n_accept,
+                   int32_t *err, int flags, void *ws, void *stream);
+
 /* ------------------------------------------------------------------ */
 /* Training (Algorithm 2): the circular RQS element-wise, with backward */
 /* ------------------------------------------------------------------ */

@@ -223,3 +223,33 @@ def test_nf_big_move_float64_proposals():
     ok = mc.nf_big_move(cfg[0])
     assert ok == bool(acc_o[0])
     assert mc.particles.dtype == np.float64
+
+
+@pytest.mark.parametrize("local_first", [False, True])
+def test_multi_step_launch_matches_single_steps(local_first):
+    """fs_nf_mh_steps (several steps' proposal passes in one launch of S*C rows, then the
+    accepts in order) leaves every chain exactly where S fs_nf_mh_step calls do: states,
+    energies, NLLs, PCG64 streams, accept masks and counters, bit for bit; after local
+    moves the first step stays a single hybrid step."""
+    N, C = 16, 512
+    dims_kw = dict(L=3, H=64, nb=2, K=8)
+    dims = OF.FlowDims(N=N, B=half_box(N), **dims_kw)
+    sd = OF.random_state_dict(dims, seed=6)
+    model = flow_from_state_dict(sd, N, bound=dims.B, **dims_kw)
+    L = float(np.sqrt(N / 0.03))
+    rng = np.random.default_rng(4)
+    init = np.mod(OP.fcc_lattice(N)[None] + rng.normal(0, 0.05, (C, N, 2)), L)
+    seeds = np.arange(42, 42 + C, dtype=np.uint64)
+    multi = BatchedMonteCarlo(model, init, Physics(L, L), seeds, chain_offset=1000)
+    single = BatchedMonteCarlo(model, init, Physics(L, L), seeds, chain_offset=1000)
+    single.MAX_STEPS_PER_LAUNCH = 1
+    assert multi.steps_per_launch() > 1 and single.steps_per_launch() == 1
+    for m in (multi, single):
+        if local_first:
+            m.local_moves(20)
+        m.step(9)
+    for name in ("state", "E_old", "W_old", "nll_old", "pcg", "accept", "attempts", "accepted", "n_accept"):
+        a, b = getattr(multi, name), getattr(single, name)
+        assert torch.equal(a, b), name
+    assert multi.step_count == single.step_count == 9
+    assert int(multi.accepted.sum().item()) > 0
