@@ -171,9 +171,9 @@ int fs_metropolis_judge(double beta, int64_t C, int64_t M, const double *E_ref, 
 int64_t fs_nf_mh_step_ws_bytes(const fs_flow_dims *d, int64_t C) {
     if (check_dims(d) != FS_OK || C < 0) return -1;
     const int64_t D = 2 * d->N;
-    // config f32 [C][D] | centered f32 [C][D] | log_q f32 [C] | E_new f64 [C] | W_new f64 [C]
-    // | (FS_MH_HYBRID) centered_old f32 [C][D] | log_q_old f32 [C] | E_cur f64 [C] | W_cur f64 [C]
-    return (fs::rup(C * D * 4, 256) * 2 + fs::rup(C * 4, 256) + fs::rup(C * 8, 256) * 2) * 2;
+    // config f32 [C][D] | centered f32 [C][D] + centered_old f32 [C][D] | log_q f32 [C] +
+    // log_q_old f32 [C] | E_new f64 [C] | W_new f64 [C] | E_cur f64 [C] | W_cur f64 [C]
+    return fs::rup(C * D * 4, 256) + fs::rup(2 * C * D * 4, 256) + fs::rup(2 * C * 4, 256) + fs::rup(C * 8, 256) * 4;
 }
 
 int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C, uint64_t seed,
@@ -189,18 +189,16 @@ int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, i
     char *w = (char *)ws;
     float *config = (float *)w;
     w += fs::rup(C * D * 4, 256);
-    float *centered = (float *)w;
-    w += fs::rup(C * D * 4, 256);
-    float *log_q = (float *)w;
-    w += fs::rup(C * 4, 256);
+    float *centered = (float *)w;  // [C][D], then centered_old [C][D] right behind it
+    float *centered_old = centered + C * D;
+    w += fs::rup(2 * C * D * 4, 256);
+    float *log_q = (float *)w;  // [C], then log_q_old [C]
+    float *log_q_old = log_q + C;
+    w += fs::rup(2 * C * 4, 256);
     double *E_new = (double *)w;
     w += fs::rup(C * 8, 256);
     double *W_new = (double *)w;
     w += fs::rup(C * 8, 256);
-    float *centered_old = (float *)w;
-    w += fs::rup(C * D * 4, 256);
-    float *log_q_old = (float *)w;
-    w += fs::rup(C * 4, 256);
     double *E_cur = (double *)w;
     w += fs::rup(C * 8, 256);
     double *W_cur = (double *)w;
@@ -211,16 +209,18 @@ int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, i
     hipError_t e = fs_flow_pass_impl(d, packed, 2, nullptr, C, nullptr, nullptr, 0, config, centered, seed, step,
                                      chain_offset, half_width, err, st);
     if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/propose");
-    e = fs_flow_pass_impl(d, packed, 0, centered, C, nullptr, log_q, 1, nullptr, nullptr, 0, 0, 0, 0.0, err, st);
-    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/log_prob");
-    e = fs_energy_impl(p, config, 1, C, d->N, E_new, W_new, nullptr, nullptr, st);
-    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/energy");
     if (hybrid) {  // the state moved since nll_old / E_old were exact: re-derive both
         e = fs_center_impl(state, C * D, half_width, centered_old, st);
         if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/center");
-        e = fs_flow_pass_impl(d, packed, 0, centered_old, C, nullptr, log_q_old, 1, nullptr, nullptr, 0, 0, 0, 0.0,
-                              err, st);
-        if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/log_prob_old");
+    }
+    // log q of the proposals and (hybrid) of the current states: one density launch over
+    // C or 2C rows (the rows are independent, so a small C gets twice the workgroups)
+    e = fs_flow_pass_impl(d, packed, 0, centered, hybrid ? 2 * C : C, nullptr, log_q, 1, nullptr, nullptr, 0, 0, 0,
+                          0.0, err, st);
+    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/log_prob");
+    e = fs_energy_impl(p, config, 1, C, d->N, E_new, W_new, nullptr, nullptr, st);
+    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/energy");
+    if (hybrid) {
         e = fs_energy_impl(p, state, 0, C, d->N, E_cur, W_cur, nullptr, nullptr, st, state_is_f32);
         if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/energy_old");
     }

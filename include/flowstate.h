@@ -196,10 +196,11 @@ int fs_metropolis_judge(double beta, int64_t C, int64_t M, const double *E_ref, 
  * fs_mh_accept.  chain_offset: global index of chain 0 (proposal stream row), so a
  * chain's trajectory does not depend on how chains are sharded over GPUs.
  * ws: caller workspace of fs_nf_mh_step_ws_bytes() bytes (256-byte aligned):
- * config f32 [C][2N] | centered f32 [C][2N] | log_q f32 [C] | E_new f64 [C] |
- * W_new f64 [C] | centered_old f32 [C][2N] | log_q_old f32 [C] | E_cur f64 [C] |
- * W_cur f64 [C] (the last four used with FS_MH_HYBRID), each section padded to
- * 256 bytes. */
+ * config f32 [C][2N] | centered f32 [C][2N] directly followed by centered_old f32
+ * [C][2N] | log_q f32 [C] directly followed by log_q_old f32 [C] | E_new f64 [C] |
+ * W_new f64 [C] | E_cur f64 [C] | W_cur f64 [C] (the *_old / *_cur parts used with
+ * FS_MH_HYBRID, whose two density passes run as one launch over 2C rows), each
+ * section padded to 256 bytes. */
 int64_t fs_nf_mh_step_ws_bytes(const fs_flow_dims *d, int64_t C);
 int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C,
                   uint64_t seed, uint64_t step, int64_t chain_offset, double *E_old, double *W_old, double *nll_old,
