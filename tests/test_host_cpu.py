@@ -104,6 +104,27 @@ def test_abi_rejects_invalid_arguments_before_touching_the_device():
     rc = L.fs_nf_mh_step(_lib.FlowDims(N=16, L=2, H=64, nb=1, K=8, precision=0, tail_bound=5.0), one, ph, 4, 0, 0, 0,
                          None, None, None, None, None, None, None, None, None, None, None, 0, one, None)
     assert rc == -1
+    d64 = _lib.FlowDims(N=16, L=2, H=64, nb=1, K=8, precision=0, tail_bound=5.0)
+    rc = L.fs_nf_mh_steps(d64, one, ph, 4, 2, 0, 0, 0, one, one, one, one, one, None, one, None, None, None, None,
+                          _lib.FS_MH_HYBRID, one, None)
+    assert rc == -1 and b"FS_MH_HYBRID" in L.fs_last_error()
+    assert L.fs_nf_mh_steps_ws_bytes(d64, 4, 0) == -1
+    # training kernels
+    rc = L.fs_linear_f32(-1, 4, 4, one, 4, 1, one, 1, 4, None, None, 0, one, 4, None, None)
+    assert rc == -1 and b"fs_linear_f32" in L.fs_last_error()
+    rc = L.fs_linear_f32(4, 8, 4, one, 4, 1, one, 1, 4, None, None, 0, one, 4, None, None)  # ldc < N
+    assert rc == -1
+    rc = L.fs_bn_relu_train_fwd(1, 8, one, one, one, None, None, None, 0.1, 1e-3, one, one, one, None)
+    assert rc == -1  # a batch of one has no batch statistics (torch raises)
+    c = _lib.Coupling(rows=4, D=16, K=7, hidden=64, identity_features=1, transform_features=1, tail_bound=3.0)
+    rc = L.fs_coupling_features_fwd(ctypes.byref(c), one, one, None)
+    assert rc == -1 and b"K=7" in L.fs_last_error()
+    c = _lib.Coupling(rows=4, D=15, K=8, hidden=64, identity_features=1, transform_features=1, tail_bound=3.0)
+    rc = L.fs_coupling_density_fwd(ctypes.byref(c), one, one, one, one, one, None, one, one, None)
+    assert rc == -1 and b"coupling description" in L.fs_last_error()
+    c = _lib.Coupling(rows=4, D=16, K=8, hidden=64, identity_features=1, transform_features=1, tail_bound=3.0)
+    rc = L.fs_coupling_sample_pre(ctypes.byref(c), one, one, one, one, one, one, one, None, None)  # out aliases z
+    assert rc == -1 and b"alias" in L.fs_last_error()
 
 
 class _FakeDeviceTensor:
