@@ -168,6 +168,24 @@ __device__ __forceinline__ void final_tile(const float *__restrict__ X, __amdgpu
     lanes_to_chains(t[0][0], t[1][0]);
 }
 
+// The same for K <= 16 with two transform features per tile: feature 2p in columns
+// 0..15, feature 2p+1 in 16..31 (ba, bb: their bias rows), so the widths / heights GEMMs
+// of a pair cost one tile each instead of two half-empty ones.
+template <int XS>
+__device__ __forceinline__ void final_tile_pair(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec,
+                                                int kg, int tile, const float *__restrict__ ba,
+                                                const float *__restrict__ bb, f32x16 (&t)[2][1]) {
+    const int h = (threadIdx.x >> 5) & 1;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *(const f32x4 *)((g < 2 ? ba + 8 * g : bb + 8 * (g - 2)) + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[0][0][4 * g + j] = t[1][0][4 * g + j] = v[j];
+    }
+    gemm64<XS, 2, 1, 4, true, true>(X, W, sec, kg, 0, tile, t);
+    lanes_to_chains(t[0][0], t[1][0]);
+}
+
 #pragma clang fp contract(off)
 
 // Derivative-row gathers of cond_spline: QB quads (16-byte pieces of rows bin and
@@ -294,6 +312,81 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
 #else
     drows_dot<QB>(g0, xr, 0, ud0, ud1);
 #endif
+    pf.mark(PH_FINAL_GEMM);
+    const float icw = INV ? o0 : s0, cw1 = INV ? o1 : s1;
+    const float ich = INV ? s0 : o0, ch1 = INV ? s1 : o1;
+    const float d0 = kMinD + softplus_t(ud0.x + ud0.y);
+    const float d1 = kMinD + softplus_t(ud1.x + ud1.y);
+    float y, l;
+    bool nd;
+    rqs_eval<INV>(x, icw, cw1 - icw, ich, ch1 - ich, d0, d1, y, l, nd);
+    pf.mark(PH_SPLINE);
+    if (inside) {
+        CO[lane * cs + p] = y;
+        nan_any |= nd;
+        return l;
+    }
+    return 0.f;
+}
+
+// cond_spline for a feature pair (K <= 16): both tiles of the pair first, then each
+// feature's spline from its 16 columns (c0 = 0 or 16) of the lane-per-chain tiles.
+template <int XS, int H, int K, bool INV>
+__device__ __forceinline__ float spline_from_tiles(const f32x16 (&tS)[2][1], const f32x16 (&tO)[2][1], int c0,
+                                                   const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int dsec,
+                                                   const float *__restrict__ bd, float *CO, int cs, int p,
+                                                   const FlowArgs &a, bool &nan_any, Prof &pf) {
+    constexpr int NQ = H / 4;
+    constexpr int QB = NQ >= 8 ? 4 : NQ / 2;
+    const int lane = threadIdx.x & 63;
+    const float x = CO[lane * cs + p];
+    const bool inside = (x >= a.negB) && (x <= a.B);
+    float ks[K + 1];
+    {
+        float u[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) u[k] = tile_row(tS[0][0], tS[1][0], c0 + k);
+        knots_from_logits<K>(u, ks, INV ? kMinHd : kMinWd, a);
+    }
+    int bin = 0;
+    float s0 = ks[0], s1 = ks[1];
+#pragma unroll
+    for (int k = 1; k < K; ++k) {
+        if (x >= ks[k]) {
+            bin = k;
+            s0 = ks[k];
+            s1 = ks[k + 1];
+        }
+    }
+    const int voff = bin * 16;
+    DRows<QB> g0, g1;
+    drows_issue<QB, K>(g0, W, voff, dsec, 0);
+    f32x2 ud0 = {bd[bin], 0.f}, ud1 = {bd[bin + 1], 0.f};
+    float o0, o1;
+    {
+        float u[K], ko[K + 1];
+#pragma unroll
+        for (int k = 0; k < K; ++k) u[k] = tile_row(tO[0][0], tO[1][0], c0 + k);
+        knots_from_logits<K>(u, ko, INV ? kMinWd : kMinHd, a);
+        o0 = ko[0];
+        o1 = ko[1];
+#pragma unroll
+        for (int k = 1; k < K; ++k) {
+            if (k == bin) {
+                o0 = ko[k];
+                o1 = ko[k + 1];
+            }
+        }
+    }
+    pf.mark(PH_SPLINE);
+    const float *xr = X + lane * XS;
+#pragma unroll 1
+    for (int q0 = 0; q0 < NQ; q0 += 2 * QB) {
+        drows_issue<QB, K>(g1, W, voff, dsec, q0 + QB);
+        drows_dot<QB>(g0, xr, q0, ud0, ud1);
+        if (q0 + 2 * QB < NQ) drows_issue<QB, K>(g0, W, voff, dsec, q0 + 2 * QB);
+        drows_dot<QB>(g1, xr, q0 + QB, ud0, ud1);
+    }
     pf.mark(PH_FINAL_GEMM);
     const float icw = INV ? o0 : s0, cw1 = INV ? o1 : s1;
     const float ich = INV ? s0 : o0, ch1 = INV ? s1 : o1;
@@ -509,6 +602,29 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
             for (int z = 0; z < FS_STAGGER; ++z) __builtin_amdgcn_s_sleep(127);
 #endif
         // final layer + conditional spline, feature by feature
+        if constexpr (K <= 16) {  // feature pairs share the widths / heights tiles
+            constexpr bool INV = MODE != MODE_DENSITY;
+            constexpr int TS = INV ? 1 : 0;
+            for (int pp = wid; pp < (N + 1) / 2; pp += kWaves) {
+                const int ja = 2 * pp, jb = 2 * pp + 1;
+                const bool hb = jb < N;
+                const float *ba = V + PL.v_bf + 96 * ja;
+                const float *bb = hb ? V + PL.v_bf + 96 * jb : ba + 16;  // zeros beyond K
+                f32x16 tS[2][1], tO[2][1];
+                final_tile_pair<XS>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + TS, ba + 32 * TS, bb + 32 * TS, tS);
+                final_tile_pair<XS>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + 1 - TS, ba + 32 * (1 - TS),
+                                    bb + 32 * (1 - TS), tO);
+                pf.mark(PH_FINAL_GEMM);
+                ld += spline_from_tiles<XS, H, K, INV>(tS, tO, 0, X, W, (int)((PL.wd + (int64_t)ja * H * (K + 1)) * 4),
+                                                       V + PL.v_bd + ja * (K + 1), CO, cs, (2 * ja + 1 + off) % D, a,
+                                                       nan_any, pf);
+                if (hb)
+                    ld += spline_from_tiles<XS, H, K, INV>(tS, tO, 16, X, W,
+                                                           (int)((PL.wd + (int64_t)jb * H * (K + 1)) * 4),
+                                                           V + PL.v_bd + jb * (K + 1), CO, cs, (2 * jb + 1 + off) % D,
+                                                           a, nan_any, pf);
+            }
+        } else {
 #ifdef FS_TIMING_NO_FINAL  // timing-only A/B build (wrong results): no final layer / conditional spline
         for (int j = wid; j < 0; j += kWaves) {
 #else
@@ -518,6 +634,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
             ld += cond_spline<XS, H, K, MODE != MODE_DENSITY>(
                 X, W, (int)(PL.wf * 4), PL.kg_h, V + PL.v_bf + 96 * j, (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
                 V + PL.v_bd + j * (K + 1), CO, cs, p, j, a, nan_any, pf);
+        }
         }
         if (MODE == MODE_DENSITY) {
 #ifndef FS_TIMING_NO_UNC
@@ -586,10 +703,14 @@ __global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restr
         if (kind == 0) {
             const int col = 32 * tile + c;
             row = col < nout ? col : -1;
-        } else {
+        } else if (kind == 1) {
             const int feat = tile / 2, t = tile % 2;
             if (c < K) row = (int64_t)feat * P + t * K + c;
             sc = wh_scale;  // / sqrt(H) (coupling.py:340-342) and * log2(e) folded in
+        } else {  // K <= 16: one tile per feature pair, feature 2p in columns 0..15, 2p+1 in 16..31
+            const int pair = tile / 2, t = tile % 2, feat = 2 * pair + (c >> 4), cc = c & 15;
+            if (feat < nout && cc < K) row = (int64_t)feat * P + t * K + cc;
+            sc = wh_scale;
         }
         dst[idx] = (row >= 0 && k < kin) ? src[row * kin + k] * sc : 0.f;
     }
@@ -804,7 +925,10 @@ hipError_t fs_flow_pack_impl(const fs_flow_dims *d, const float *raw, float *pac
             lin(o, B + RawLayout::w0(H), H, PL.kg_h, H / 32, H, 0);
             lin(o + PL.block_stride / 2, B + RawLayout::w1(H), H, PL.kg_h, H / 32, H, 0);
         }
-        lin(dst + PL.wf, src + R.wf, H, PL.kg_h, 2 * N, 0, 1);
+        if (K <= 16)
+            lin(dst + PL.wf, src + R.wf, H, PL.kg_h, 2 * ((N + 1) / 2), N, 2);  // feature pairs
+        else
+            lin(dst + PL.wf, src + R.wf, H, PL.kg_h, 2 * N, 0, 1);
         {
             const int64_t tot = (int64_t)N * H * (K + 1);
             int blocks = (int)((tot + 255) / 256);

@@ -67,6 +67,26 @@ def test_a1_log_prob_matches_oracle(N):
     close(got, want)
 
 
+@pytest.mark.parametrize("N", [15, 64])
+def test_a2_log_prob_and_sample_match_oracle(N):
+    """Algorithm-2 hyper-parameters (L=23, H=128, 2 blocks, K=15): the K <= 16 kernels
+    compute two transform features per widths / heights tile (columns 0-15, 16-31).  Odd
+    N=15 leaves the last pair with one feature.  log_prob and the sampling direction
+    against the oracle."""
+    from flowstate.models import A2
+
+    dims = OF.FlowDims(N=N, B=half_box(N), **A2)
+    sd = OF.random_state_dict(dims, seed=11)
+    m = flow_from_state_dict(sd, N, bound=dims.B, **A2)
+    g = torch.Generator().manual_seed(4)
+    x = (torch.rand((96, dims.D), generator=g) * 2 - 1) * dims.B
+    close(m.log_prob(x.cuda()).cpu().numpy(), OF.log_prob(sd, x.clone(), dims).numpy())
+    z = (torch.rand((96, dims.D), generator=g) * 2 - 1) * dims.B
+    xs = m.forward(z.cuda()).cpu().numpy()
+    want = OF.sample_from(sd, z.clone(), dims).numpy()
+    np.testing.assert_allclose(xs, want, rtol=0, atol=5e-4 * dims.B)
+
+
 def test_a1_log_prob_on_flow_samples_within_reference_f32_envelope():
     """The bench's inputs: proposals drawn by the flow itself (sampling pass), A1, N=64.
     There the reference's own float32 log_prob is up to ~2e-5 relative from the exact
