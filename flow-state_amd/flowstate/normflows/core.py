@@ -241,14 +241,15 @@ class NormalizingFlow(nn.Module):
 
         log_q = None  # zeros (core.py:96); the first fused layer starts from 0
         z = x
-        for i in range(len(self.flows) - 1, -1, -1):
-            if AF.fused_coupling_ok(self.flows[i], z):
-                z, log_q = AF.density_step(self.flows[i], z, log_q)
-            else:
-                if log_q is None:
-                    log_q = torch.zeros(len(x), device=x.device)
-                z, log_det = AF.coupling_density(self.flows[i], z)
-                log_q = log_q + log_det
+        with _lib.on_device(x):  # the HIP kernels launch on the current device's stream
+            for i in range(len(self.flows) - 1, -1, -1):
+                if AF.fused_coupling_ok(self.flows[i], z):
+                    z, log_q = AF.density_step(self.flows[i], z, log_q)
+                else:
+                    if log_q is None:
+                        log_q = torch.zeros(len(x), device=x.device)
+                    z, log_det = AF.coupling_density(self.flows[i], z)
+                    log_q = log_q + log_det
         AF.check_nan_flags()
         if log_q is None:
             log_q = torch.zeros(len(x), device=x.device)
@@ -266,16 +267,17 @@ class NormalizingFlow(nn.Module):
         log_q = None  # zeros (core.py:118); the first fused layer starts from 0
         grads = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         nan_flag = None
-        for flow in self.flows:
-            if not grads and AF.fused_coupling_ok(flow, z):
-                if nan_flag is None:
-                    nan_flag = torch.zeros(1, dtype=torch.int32, device=z.device)
-                z, log_q = AF.sample_step(flow, z, log_q, nan_flag)
-            else:
-                if log_q is None:
-                    log_q = torch.zeros(len(z), device=z.device)
-                z, log_det = AF.coupling_sample(flow, z)
-                log_q = log_q - log_det
+        with _lib.on_device(z):
+            for flow in self.flows:
+                if not grads and AF.fused_coupling_ok(flow, z):
+                    if nan_flag is None:
+                        nan_flag = torch.zeros(1, dtype=torch.int32, device=z.device)
+                    z, log_q = AF.sample_step(flow, z, log_q, nan_flag)
+                else:
+                    if log_q is None:
+                        log_q = torch.zeros(len(z), device=z.device)
+                    z, log_det = AF.coupling_sample(flow, z)
+                    log_q = log_q - log_det
         if nan_flag is not None:
             AF._nan_flags.append(nan_flag[0] != 0)
         if log_q is None:
