@@ -63,6 +63,21 @@ __device__ __forceinline__ float softplus_grad(float v) {
     return z / (z + 1.f);
 }
 
+// knots c[b], c[b+1] of bin b by a register scan (a dynamically indexed array would live
+// in scratch memory)
+template <int K>
+__device__ __forceinline__ void pick_bin(const float *c, int b, float &lo, float &hi) {
+    lo = c[0];
+    hi = c[1];
+#pragma unroll
+    for (int k = 1; k < K; ++k) {
+        if (k == b) {
+            lo = c[k];
+            hi = c[k + 1];
+        }
+    }
+}
+
 // values of the bin that contains x (searchsorted over `knots`, eps on the last one)
 template <int K>
 __device__ __forceinline__ int find_bin(float x, const float *knots) {
@@ -84,8 +99,10 @@ __device__ __forceinline__ void rqs_point(float xv, const float *uw, const float
     build_knots<K>(uh, B, Hh);
     const int b = find_bin<K>(xv, INV ? Hh.c : W.c);
     const float d0 = kMin + softplus(dd[b]), d1 = kMin + softplus(dd[b + 1]);
-    const float icw = W.c[b], ibw = W.c[b + 1] - W.c[b];
-    const float ich = Hh.c[b], ih = Hh.c[b + 1] - Hh.c[b];
+    float icw, cw1, ich, ch1;
+    pick_bin<K>(W.c, b, icw, cw1);
+    pick_bin<K>(Hh.c, b, ich, ch1);
+    const float ibw = cw1 - icw, ih = ch1 - ich;
     const float s = ih / ibw;
     float th;
     if (INV) {
@@ -113,7 +130,7 @@ __device__ __forceinline__ void rqs_point(float xv, const float *uw, const float
 }
 
 template <int K, bool INV>
-__global__ void rqs_forward_kernel(int64_t M, const float *__restrict__ x, const float *__restrict__ uw,
+__global__ __launch_bounds__(256) void rqs_forward_kernel(int64_t M, const float *__restrict__ x, const float *__restrict__ uw,
                                    const float *__restrict__ uh, const float *__restrict__ ud, float B,
                                    float *__restrict__ out, float *__restrict__ lad, int32_t *__restrict__ nan_flag) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -156,8 +173,10 @@ __device__ __forceinline__ void rqs_point_bwd(float xv, const float *uw, const f
     const int b = find_bin<K>(xv, INV ? Hh.c : W.c);
     const float e0 = dd[b], e1 = dd[b + 1];
     const float d0 = kMin + softplus(e0), d1 = kMin + softplus(e1);
-    const float icw = W.c[b], ibw = W.c[b + 1] - W.c[b];
-    const float ich = Hh.c[b], ih = Hh.c[b + 1] - Hh.c[b];
+    float icw, cw1, ich, ch1;
+    pick_bin<K>(W.c, b, icw, cw1);
+    pick_bin<K>(Hh.c, b, ich, ch1);
+    const float ibw = cw1 - icw, ih = ch1 - ich;
     const float s = ih / ibw;
     float th;
     if (INV) {
@@ -258,7 +277,7 @@ __device__ __forceinline__ void rqs_point_bwd(float xv, const float *uw, const f
 
 
 template <int K, bool INV>
-__global__ void rqs_backward_kernel(int64_t M, const float *__restrict__ x, const float *__restrict__ uw,
+__global__ __launch_bounds__(256) void rqs_backward_kernel(int64_t M, const float *__restrict__ x, const float *__restrict__ uw,
                                     const float *__restrict__ uh, const float *__restrict__ ud, float B,
                                     const float *__restrict__ g_out, const float *__restrict__ g_lad,
                                     float *__restrict__ gx, float *__restrict__ guw, float *__restrict__ guh,
