@@ -394,7 +394,10 @@ __global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
         const float got = g_out ? g_out[row * c.D + (pt + c.D - c.split) % c.D] : 0.f;
         const float goi = g_out ? g_out[row * c.D + (pi + c.D - c.split) % c.D] : 0.f;
         float *gp = g_params + (row * c.n + j) * P;
-        float *gu = g_u + (row * c.n + j) * P;
+        // g_u row: [uw n*K | uh n*K | ud n*(K+1)], the parameters' own layouts back to back
+        float *guw = g_u + row * c.n * P + j * K;
+        float *guh = guw + c.n * K;
+        float *gud = g_u + row * c.n * P + 2 * c.n * K + j * (K + 1);
         float gw[K], gh[K], gd[K + 1];
         if (xt >= -c.bound && xt <= c.bound) {
             const float *p = params + (row * c.n + j) * P;
@@ -421,15 +424,20 @@ __global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
             gx[row * c.D + pi] = g;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                gu[k] = gw[k];
-                gu[K + k] = gh[k];
+                guw[k] = gw[k];
+                guh[k] = gh[k];
             }
 #pragma unroll
-            for (int k = 0; k <= K; ++k) gu[2 * K + k] = gd[k];
+            for (int k = 0; k <= K; ++k) gud[k] = gd[k];
         } else {
             gx[row * c.D + pi] = goi;
 #pragma unroll
-            for (int k = 0; k < P; ++k) gu[k] = 0.f;
+            for (int k = 0; k < K; ++k) {
+                guw[k] = 0.f;
+                guh[k] = 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k <= K; ++k) gud[k] = 0.f;
         }
     }
 }

@@ -483,14 +483,19 @@ class _DensitySplines(torch.autograd.Function):
         g_lq = g_lq.contiguous() if g_lq is not None else None
         gx = torch.empty_like(x)
         gp = torch.empty_like(params)
-        gu = torch.empty((x.shape[0], x.shape[1] // 2, 3 * K + 1), dtype=torch.float32, device=x.device)
+        n = x.shape[1] // 2
+        gu = torch.empty((x.shape[0], n * (3 * K + 1)), dtype=torch.float32, device=x.device)
         c = _coupling_desc(layer, x.shape[0])
         _lib.check(_lib.load().fs_coupling_density_bwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(params), _lib.ptr(uw),
                                                        _lib.ptr(uh), _lib.ptr(ud), _lib.ptr(g_out), _lib.ptr(g_lq),
                                                        _lib.ptr(gx), _lib.ptr(gp), _lib.ptr(gu), _lib.stream_ptr()),
                    "fs_coupling_density_bwd")
         gs = gu.sum(0)  # the unconditional parameters are shared by every row
-        return (gx, gp, gs[:, :K], gs[:, K:2 * K], gs[:, 2 * K:], g_lq if ctx.has_lq else None, None)
+        # [uw | uh | ud] back to back: contiguous views, no copies when the gradients are gathered
+        guw = gs[:n * K].view(n, K)
+        guh = gs[n * K:2 * n * K].view(n, K)
+        gud = gs[2 * n * K:].view(n, K + 1)
+        return (gx, gp, guw, guh, gud, g_lq if ctx.has_lq else None, None)
 
 
 def conditioner_from_features(net, t):

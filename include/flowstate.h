@@ -287,8 +287,9 @@ int fs_coupling_density_fwd(const fs_coupling *c, const float *x, const float *p
                             const float *uh, const float *ud, const float *lq_in, float *out, float *lq_out,
                             void *stream);
 /* Its adjoints from g_out [rows][D] and g_lq [rows] (nullable = 0): gx [rows][D] through
- * the splines, g_params [rows][D/2][3K+1], g_u [rows][D/2][3K+1] = per-row adjoints of
- * (uw, uh, ud) (their sum over rows is the parameter gradient). */
+ * the splines, g_params [rows][D/2][3K+1], g_u [rows][(D/2)(3K+1)] = per-row adjoints
+ * of uw [D/2][K], uh [D/2][K], ud [D/2][K+1], back to back in each row (their sum over rows
+ * is the parameter gradient). */
 int fs_coupling_density_bwd(const fs_coupling *c, const float *x, const float *params, const float *uw,
                             const float *uh, const float *ud, const float *g_out, const float *g_lq, float *gx,
                             float *g_params, float *g_u, void *stream);
