@@ -237,6 +237,44 @@ int64_t fs_nf_mh_steps_ws_bytes(const fs_flow_dims *d, int64_t C, int64_t S) {
     return fs::rup(R * D * 4, 256) * 2 + fs::rup(R * 4, 256) + fs::rup(R * 8, 256) * 2;
 }
 
+namespace {
+// sections of an S-step proposal bank (the fs_nf_mh_steps workspace): rows s*C + c hold
+// step step0+s of chain c
+struct Bank {
+    float *config, *centered, *log_q;
+    double *E_new, *W_new;
+};
+Bank bank_sections(void *ws, int64_t R, int64_t D) {
+    char *w = (char *)ws;
+    Bank b;
+    b.config = (float *)w;
+    w += fs::rup(R * D * 4, 256);
+    b.centered = (float *)w;
+    w += fs::rup(R * D * 4, 256);
+    b.log_q = (float *)w;
+    w += fs::rup(R * 4, 256);
+    b.E_new = (double *)w;
+    w += fs::rup(R * 8, 256);
+    b.W_new = (double *)w;
+    return b;
+}
+
+// the proposals of steps step0 .. step0+S-1 do not depend on the chain states: one launch
+// of S*C rows per pass (the same Philox draws as S single steps), then their energies
+int fill_bank(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C, int64_t S, uint64_t seed,
+              uint64_t step0, int64_t chain_offset, int32_t *err, const Bank &b, hipStream_t st, const char *who) {
+    const int64_t R = C * S;
+    const double half_width = p->Lx / 2.0;  // MonteCarlo.half_width (monte_carlo.py:66)
+    hipError_t e = fs_flow_pass_impl(d, packed, 2, nullptr, R, nullptr, nullptr, 0, b.config, b.centered, seed,
+                                     step0, chain_offset, half_width, err, st, C);
+    if (e != hipSuccess) return hip_rc(e, who);
+    e = fs_flow_pass_impl(d, packed, 0, b.centered, R, nullptr, b.log_q, 1, nullptr, nullptr, 0, 0, 0, 0.0, err, st);
+    if (e != hipSuccess) return hip_rc(e, who);
+    e = fs_energy_impl(p, b.config, 1, R, d->N, b.E_new, b.W_new, nullptr, nullptr, st);
+    return hip_rc(e, who);
+}
+}  // namespace
+
 int fs_nf_mh_steps(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C, int64_t S, uint64_t seed,
                    uint64_t step0, int64_t chain_offset, double *E_old, double *W_old, double *nll_old, uint64_t *pcg,
                    double *state, uint8_t *state_is_f32, uint8_t *accept, int64_t *attempts, int64_t *accepted,
@@ -248,36 +286,77 @@ int fs_nf_mh_steps(const fs_flow_dims *d, const void *packed, const fs_phys *p, 
     REQUIRE(!(flags & FS_MH_HYBRID), "fs_nf_mh_steps: FS_MH_HYBRID needs one step at a time (fs_nf_mh_step)");
     REQUIRE(((uintptr_t)ws & 255) == 0, "fs_nf_mh_steps: workspace must be 256-byte aligned");
     if (C == 0) return FS_OK;
-    const int64_t D = 2 * d->N, R = C * S;
-    char *w = (char *)ws;
-    float *config = (float *)w;
-    w += fs::rup(R * D * 4, 256);
-    float *centered = (float *)w;
-    w += fs::rup(R * D * 4, 256);
-    float *log_q = (float *)w;
-    w += fs::rup(R * 4, 256);
-    double *E_new = (double *)w;
-    w += fs::rup(R * 8, 256);
-    double *W_new = (double *)w;
+    const int64_t D = 2 * d->N;
+    const Bank b = bank_sections(ws, C * S, D);
     hipStream_t st = (hipStream_t)stream;
-    const double half_width = p->Lx / 2.0;  // MonteCarlo.half_width (monte_carlo.py:66)
-    // the proposals of steps step0 .. step0+S-1 do not depend on the chain states: one
-    // launch of S*C rows per pass (rows s*C + c = step step0+s of chain c, the same Philox
-    // draws as S single steps), then the S accept/update launches in order
-    hipError_t e = fs_flow_pass_impl(d, packed, 2, nullptr, R, nullptr, nullptr, 0, config, centered, seed, step0,
-                                     chain_offset, half_width, err, st, C);
-    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_steps/propose");
-    e = fs_flow_pass_impl(d, packed, 0, centered, R, nullptr, log_q, 1, nullptr, nullptr, 0, 0, 0, 0.0, err, st);
-    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_steps/log_prob");
-    e = fs_energy_impl(p, config, 1, R, d->N, E_new, W_new, nullptr, nullptr, st);
-    if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_steps/energy");
+    rc = fill_bank(d, packed, p, C, S, seed, step0, chain_offset, err, b, st, "fs_nf_mh_steps/bank");
+    if (rc) return rc;
     for (int64_t s = 0; s < S; ++s) {
-        e = fs_mh_accept_impl(p, C, d->N, E_old, W_old, nll_old, E_new + s * C, W_new + s * C, log_q + s * C, pcg,
-                              state, state_is_f32, state ? config + s * C * D : nullptr, accept, attempts, accepted,
-                              n_accept, flags, st);
+        hipError_t e = fs_mh_accept_impl(p, C, d->N, E_old, W_old, nll_old, b.E_new + s * C, b.W_new + s * C,
+                                         b.log_q + s * C, pcg, state, state_is_f32,
+                                         state ? b.config + s * C * D : nullptr, accept, attempts, accepted, n_accept,
+                                         flags, st);
         if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_steps/accept");
     }
     return FS_OK;
+}
+
+int fs_nf_mh_bank(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C, int64_t S, uint64_t seed,
+                  uint64_t step0, int64_t chain_offset, int32_t *err, void *bank, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    REQUIRE(p && C >= 0 && S >= 1 && (C == 0 || (packed && bank)), "fs_nf_mh_bank: invalid arguments");
+    REQUIRE(((uintptr_t)bank & 255) == 0, "fs_nf_mh_bank: bank must be 256-byte aligned");
+    if (C == 0) return FS_OK;
+    return fill_bank(d, packed, p, C, S, seed, step0, chain_offset, err, bank_sections(bank, C * S, 2 * d->N),
+                     (hipStream_t)stream, "fs_nf_mh_bank");
+}
+
+int64_t fs_nf_mh_banked_ws_bytes(const fs_flow_dims *d, int64_t C) {
+    if (check_dims(d) != FS_OK || C < 0) return -1;
+    // centered_old f32 [C][D] | log_q_old f32 [C] | E_cur f64 [C] | W_cur f64 [C]
+    return fs::rup(C * 2 * d->N * 4, 256) + fs::rup(C * 4, 256) + fs::rup(C * 8, 256) * 2;
+}
+
+int fs_nf_mh_step_banked(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C, int64_t S, int64_t s,
+                         const void *bank, double *E_old, double *W_old, double *nll_old, uint64_t *pcg, double *state,
+                         uint8_t *state_is_f32, uint8_t *accept, int64_t *attempts, int64_t *accepted,
+                         unsigned long long *n_accept, int32_t *err, int flags, void *hws, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    const bool hybrid = (flags & FS_MH_HYBRID) != 0;
+    REQUIRE(p && C >= 0 && S >= 1 && s >= 0 && s < S &&
+                (C == 0 || (packed && bank && E_old && nll_old && pcg && accept && (!hybrid || (state && hws)))),
+            "fs_nf_mh_step_banked: invalid arguments");
+    REQUIRE(((uintptr_t)bank & 255) == 0 && ((uintptr_t)hws & 255) == 0,
+            "fs_nf_mh_step_banked: bank and workspace must be 256-byte aligned");
+    if (C == 0) return FS_OK;
+    const int64_t D = 2 * d->N;
+    const Bank b = bank_sections(const_cast<void *>(bank), C * S, D);
+    hipStream_t st = (hipStream_t)stream;
+    float *centered_old = nullptr, *log_q_old = nullptr;
+    double *E_cur = nullptr, *W_cur = nullptr;
+    if (hybrid) {  // monte_carlo.py:251-261 (old NLL of the moved state) and :299-301 (its energy)
+        char *w = (char *)hws;
+        centered_old = (float *)w;
+        w += fs::rup(C * D * 4, 256);
+        log_q_old = (float *)w;
+        w += fs::rup(C * 4, 256);
+        E_cur = (double *)w;
+        w += fs::rup(C * 8, 256);
+        W_cur = (double *)w;
+        hipError_t e = fs_center_impl(state, C * D, p->Lx / 2.0, centered_old, st);
+        if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step_banked/center");
+        e = fs_flow_pass_impl(d, packed, 0, centered_old, C, nullptr, log_q_old, 1, nullptr, nullptr, 0, 0, 0, 0.0,
+                              err, st);
+        if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step_banked/log_prob_old");
+        e = fs_energy_impl(p, state, 0, C, d->N, E_cur, W_cur, nullptr, nullptr, st, state_is_f32);
+        if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step_banked/energy_old");
+    }
+    hipError_t e = fs_mh_accept_impl(p, C, d->N, E_old, W_old, nll_old, b.E_new + s * C, b.W_new + s * C,
+                                     b.log_q + s * C, pcg, state, state_is_f32, state ? b.config + s * C * D : nullptr,
+                                     accept, attempts, accepted, n_accept, flags, st, log_q_old, E_cur, W_cur);
+    return hip_rc(e, "fs_nf_mh_step_banked/accept");
 }
 
 int fs_local_moves(const fs_phys *p, int64_t C, int32_t N, double *state, const uint8_t *state_is_f32, double *E,

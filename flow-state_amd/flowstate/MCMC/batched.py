@@ -29,6 +29,7 @@ values are exactly those numbers.  The flow model is optional until the first
 big move (the reference equilibrates before set_nf_model).
 """
 import functools
+import weakref
 
 import numpy as np
 import torch
@@ -194,7 +195,28 @@ class BatchedMonteCarlo:
         st = _lib.stream_ptr()
         done = 0
         while done < n:
-            S = 1 if self._moved else min(n - done, self.steps_per_launch())
+            fill = self.steps_per_launch()
+            if fill > 1 and (self._bank_covers(packed) or (self._moved and self._last_packed is not None
+                                                         and self._last_packed() is packed)):
+                # a small batch after local moves with the flow unchanged since the last
+                # step (Algorithm 1's cycle): this step's proposal, log q and energy come
+                # from a bank of `fill` steps made in one launch per pass; only the current
+                # states' density pass and energy run per step.  A step after new weights
+                # (Algorithm 2's refeed) stays one fused step: its bank would not be reused.
+                bank, s = self._bank_for(packed, dims, fill)
+                _lib.check(L.fs_nf_mh_step_banked(dims, _lib.ptr(packed), self.phys.c, self.C, self._bank["S"], s,
+                                                  _lib.ptr(bank), _lib.ptr(self.E_old), _lib.ptr(self.W_old),
+                                                  _lib.ptr(self.nll_old), _lib.ptr(self.pcg), _lib.ptr(self.state),
+                                                  _lib.ptr(self.state_is_f32), _lib.ptr(self.accept),
+                                                  _lib.ptr(self.attempts), _lib.ptr(self.accepted),
+                                                  _lib.ptr(self.n_accept), _lib.ptr(self.err),
+                                                  self.flags | (_lib.FS_MH_HYBRID if self._moved else 0),
+                                                  _lib.ptr(self._workspace_banked()), st), "fs_nf_mh_step_banked")
+                self.step_count += 1
+                done += 1
+                self._moved = False
+                continue
+            S = 1 if self._moved else min(n - done, fill)
             if S == 1:
                 _lib.check(L.fs_nf_mh_step(dims, _lib.ptr(packed), self.phys.c, self.C, self.proposal_seed,
                                            self.step_count, self.chain_offset, _lib.ptr(self.E_old),
@@ -214,6 +236,7 @@ class BatchedMonteCarlo:
             self.step_count += S
             done += S
             self._moved = False
+        self._last_packed = weakref.ref(packed)  # not kept alive past a repack
         return self.accept
 
     # proposal rows per launch that fill the chip: 2 resident 64-chain workgroups on each
@@ -233,6 +256,44 @@ class BatchedMonteCarlo:
         if ws is None or ws.numel() * 8 < n:
             self._ws_steps = torch.empty((n + 7) // 8, dtype=torch.float64, device=self.device)
         return self._ws_steps
+
+    _bank = None
+    _last_packed = None
+
+    def _bank_key(self, packed):
+        # what a bank's rows depend on: the flow image (a new tensor on every repack),
+        # the proposal stream and the chains' global indices
+        return (id(packed), self.proposal_seed, self.chain_offset, self.C)
+
+    def _bank_covers(self, packed):
+        b = self._bank
+        return (b is not None and b["packed"]() is packed and b["key"] == self._bank_key(packed)
+                and b["step0"] <= self.step_count < b["step0"] + b["S"])
+
+    def _bank_for(self, packed, dims, S):
+        """(bank buffer, row block) of step step_count: the open bank when it covers the
+        step, else a new bank of steps step_count .. step_count+S-1 (fs_nf_mh_bank)."""
+        if not self._bank_covers(packed):
+            n = _lib.load().fs_nf_mh_steps_ws_bytes(dims, self.C, S)
+            _lib.check(0 if n >= 0 else -1, "fs_nf_mh_steps_ws_bytes")
+            buf = self._bank["buf"] if self._bank is not None else None
+            if buf is None or buf.numel() * 8 < n:
+                buf = torch.empty((n + 7) // 8, dtype=torch.float64, device=self.device)
+            self._bank = None  # a failed fill leaves no bank behind
+            _lib.check(_lib.load().fs_nf_mh_bank(dims, _lib.ptr(packed), self.phys.c, self.C, S, self.proposal_seed,
+                                                 self.step_count, self.chain_offset, _lib.ptr(self.err),
+                                                 _lib.ptr(buf), _lib.stream_ptr()), "fs_nf_mh_bank")
+            self._bank = {"packed": weakref.ref(packed), "key": self._bank_key(packed), "step0": self.step_count, "S": S,
+                          "buf": buf}
+        return self._bank["buf"], self.step_count - self._bank["step0"]
+
+    def _workspace_banked(self):
+        ws = getattr(self, "_ws_banked", None)
+        if ws is None:
+            n = _lib.load().fs_nf_mh_banked_ws_bytes(self.model.dims(), self.C)
+            _lib.check(0 if n >= 0 else -1, "fs_nf_mh_banked_ws_bytes")
+            ws = self._ws_banked = torch.empty((n + 7) // 8, dtype=torch.float64, device=self.device)
+        return ws
 
     @_on_own_device
     def local_moves(self, n, adjust_every=0, sample_every=0, step0=0, log_accepts=False):
@@ -345,13 +406,33 @@ class BatchedMonteCarlo:
         return acc.sum(dim=1, dtype=torch.int64), M
 
     @_on_own_device
-    def nf_big_move(self, configs):
+    def proposal_terms(self, configs):
+        """(E_new, W_new, log_q) of R supplied proposals (R, N, 2) box coords, each exactly
+        as nf_big_move derives it (monte_carlo.py:247, 251-262): energy and virial in the
+        config's dtype, log q of fl32(config - half_width).  They do not depend on the chain
+        states, so the proposals of many attempts (the drivers pre-generate them,
+        main_algorithm_1.py:340-343) share one launch per pass; pass each attempt's rows to
+        nf_big_move(configs, terms=...).  The kernels are row-independent: the values are
+        bit-identical to nf_big_move's own."""
+        cfg = torch.as_tensor(configs, device=self.device)
+        if cfg.dtype not in (torch.float32, torch.float64):
+            raise ValueError(f"proposals must be float32 or float64, got {cfg.dtype}")
+        cfg = cfg.reshape(-1, self.N, 2).contiguous()
+        self._need_model()
+        E, W, _ = total_energy(cfg, self.phys.c)
+        lq = self.model.log_prob(self._centered_f32(cfg.to(torch.float64)))
+        return E, W, lq
+
+    @_on_own_device
+    def nf_big_move(self, configs, terms=None):
         """Batched nf_big_move with supplied proposals (C, N, 2) box coords.
 
         The proposals keep their dtype, as in the reference (monte_carlo.py:245-296):
         float32 (the drivers' proposals, main_algorithm_1.py:340-343) or float64.  The
         energy is computed in that dtype, the flow sees fl32(config - half_width)
-        either way (:251-258), and an accepted chain's state takes the config's dtype."""
+        either way (:251-258), and an accepted chain's state takes the config's dtype.
+        terms: optional (E_new, W_new, log_q), each (C,), of these configs from
+        proposal_terms()."""
         cfg = torch.as_tensor(configs, device=self.device)
         if cfg.dtype not in (torch.float32, torch.float64):
             raise ValueError(f"proposals must be float32 or float64, got {cfg.dtype}")
@@ -364,8 +445,15 @@ class BatchedMonteCarlo:
         if stale:  # old NLL of the current state (monte_carlo.py:251-261); energy for a reject (:299-301)
             self.nll_old = -(self.model.log_prob(self._centered_f32(self.state)).to(torch.float64))
             E_cur, W_cur = self._energy_of_state()
-        E_new, W_new, _ = total_energy(cfg if cfg64 is None else cfg64, self.phys.c)
-        lq = self.model.log_prob(self._centered_f32(cfg.to(torch.float64) if cfg64 is None else cfg64))
+        if terms is None:
+            E_new, W_new, _ = total_energy(cfg if cfg64 is None else cfg64, self.phys.c)
+            lq = self.model.log_prob(self._centered_f32(cfg.to(torch.float64) if cfg64 is None else cfg64))
+        else:
+            E_new, W_new, lq = terms
+            for t, dt in ((E_new, torch.float64), (W_new, torch.float64), (lq, torch.float32)):
+                if not torch.is_tensor(t) or t.dtype != dt or t.shape != (self.C,) or t.device != self.device:
+                    raise ValueError(f"terms must be proposal_terms() rows for {self.C} chains on {self.device}")
+            E_new, W_new, lq = E_new.contiguous(), W_new.contiguous(), lq.contiguous()
         L = _lib.load()
         _lib.check(L.fs_mh_accept(self.phys.c, self.C, self.N, _lib.ptr(self.E_old), _lib.ptr(self.W_old),
                                   _lib.ptr(self.nll_old), _lib.ptr(E_new), _lib.ptr(W_new), _lib.ptr(lq),

@@ -70,6 +70,9 @@ _SIGS = {
     "fs_nf_mh_steps_ws_bytes": (_I64, [_D, _I64, _I64]),
     "fs_nf_mh_steps": (ctypes.c_int, [_D, _P, _PH, _I64, _I64, ctypes.c_uint64, ctypes.c_uint64, _I64] + [_P] * 11
                        + [ctypes.c_int, _P, _P]),
+    "fs_nf_mh_bank": (ctypes.c_int, [_D, _P, _PH, _I64, _I64, ctypes.c_uint64, ctypes.c_uint64, _I64, _P, _P, _P]),
+    "fs_nf_mh_banked_ws_bytes": (_I64, [_D, _I64]),
+    "fs_nf_mh_step_banked": (ctypes.c_int, [_D, _P, _PH, _I64, _I64, _I64] + [_P] * 12 + [ctypes.c_int, _P, _P]),
     "fs_local_moves": (ctypes.c_int, [_PH, _I64, ctypes.c_int32] + [_P] * 10
                        + [_I64, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_int32] + [_P] * 5),
     "fs_local_samples_per_chain": (_I64, [_I64, _I64, ctypes.c_int32]),

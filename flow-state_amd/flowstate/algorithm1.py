@@ -146,9 +146,19 @@ def testing_phase(bmc: BatchedMonteCarlo, test_configs, attempts, interval, samp
         raise IndexError(f"index {attempts * C - 1} is out of bounds for axis 0 with size {cfg.shape[0]}")
     cfg = cfg.to(bmc.device)
     snaps, acc = [], []
+    # the test configurations' energies and log q do not depend on the chain states: one
+    # launch per pass over a block of attempts (bit-identical rows), so each attempt's big
+    # move runs only the current states' density pass and energy
+    block = max(1, BatchedMonteCarlo.FILL_ROWS // max(1, C))
+    terms, a0 = None, 0
     for a in range(int(attempts)):
         snaps.append(_local(bmc, int(interval), 0, int(sampling_frequency)))
-        acc.append(bmc.nf_big_move(cfg[a * C:(a + 1) * C]).clone())
+        if bmc.model is not None and a % block == 0:
+            a0, a1 = a, min(int(attempts), a + block)
+            terms = bmc.proposal_terms(cfg[a0 * C:a1 * C])
+        o = (a - a0) * C
+        t = tuple(x[o:o + C] for x in terms) if bmc.model is not None else None
+        acc.append(bmc.nf_big_move(cfg[a * C:(a + 1) * C], terms=t).clone())
     accepts = torch.stack(acc, 1) if acc else torch.zeros((C, 0), dtype=torch.uint8, device=bmc.device)
     p, s, tot, att, nacc = acceptance_history(accepts, int(interval), total_mcmc_steps, big_move_attempts,
                                               big_move_accepts)

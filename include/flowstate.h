@@ -221,6 +221,25 @@ int fs_nf_mh_steps(const fs_flow_dims *d, const void *packed, const fs_phys *p, 
                    int64_t *attempts, int64_t *accepted, unsigned long long *n_accept,
                    int32_t *err, int flags, void *ws, void *stream);
 
+/* Proposal bank for steps interleaved with local moves (Algorithm 1's cycle,
+ * main_algorithm_1.py:384-395, which pre-generates its proposals in batches,
+ * :340-343 / utils.py:422-450).  fs_nf_mh_bank fills `bank` (the fs_nf_mh_steps
+ * workspace layout, fs_nf_mh_steps_ws_bytes(d, C, S) bytes) with the proposals of steps
+ * step0 .. step0+S-1, their log q and their energies: one launch of S*C rows per pass.
+ * fs_nf_mh_step_banked then runs step step0+s (0 <= s < S) of that bank exactly as
+ * fs_nf_mh_step would, FS_MH_HYBRID included: the hybrid's density pass over the current
+ * states (C rows) and their energy are its only flow / energy work.  hws: caller
+ * workspace of fs_nf_mh_banked_ws_bytes() bytes (256-byte aligned), used with
+ * FS_MH_HYBRID: centered_old f32 [C][2N] | log_q_old f32 [C] | E_cur f64 [C] | W_cur f64 [C]. */
+int fs_nf_mh_bank(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C, int64_t S,
+                  uint64_t seed, uint64_t step0, int64_t chain_offset, int32_t *err, void *bank, void *stream);
+int64_t fs_nf_mh_banked_ws_bytes(const fs_flow_dims *d, int64_t C);
+int fs_nf_mh_step_banked(const fs_flow_dims *d, const void *packed, const fs_phys *p, int64_t C, int64_t S,
+                         int64_t s, const void *bank, double *E_old, double *W_old, double *nll_old, uint64_t *pcg,
+                         double *state, uint8_t *state_is_f32, uint8_t *accept, int64_t *attempts,
+                         int64_t *accepted, unsigned long long *n_accept, int32_t *err, int flags, void *hws,
+                         void *stream);
+
 /* ------------------------------------------------------------------ */
 /* Training (Algorithm 2): the circular RQS element-wise, with backward */
 /* ------------------------------------------------------------------ */

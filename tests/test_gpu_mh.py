@@ -253,3 +253,70 @@ def test_multi_step_launch_matches_single_steps(local_first):
         assert torch.equal(a, b), name
     assert multi.step_count == single.step_count == 9
     assert int(multi.accepted.sum().item()) > 0
+
+
+def test_banked_hybrid_steps_match_single_steps():
+    """Algorithm 1's cycle on a small batch (local moves, then one big move, repeated with
+    the flow unchanged): from the second cycle on, each step's proposal, log q and energy
+    come from a bank of several steps made in one launch per pass (fs_nf_mh_bank), and the
+    step runs only the current states' density pass and energy (fs_nf_mh_step_banked).
+    Every chain ends exactly where single fused steps leave it, bit for bit, also across
+    pure steps inside the bank and a weight change (which drops the bank)."""
+    N, C = 16, 512
+    dims_kw = dict(L=3, H=64, nb=2, K=8)
+    dims = OF.FlowDims(N=N, B=half_box(N), **dims_kw)
+    sd = OF.random_state_dict(dims, seed=8)
+    model = flow_from_state_dict(sd, N, bound=dims.B, **dims_kw)
+    L = float(np.sqrt(N / 0.03))
+    rng = np.random.default_rng(5)
+    init = np.mod(OP.fcc_lattice(N)[None] + rng.normal(0, 0.05, (C, N, 2)), L)
+    seeds = np.arange(42, 42 + C, dtype=np.uint64)
+    banked = BatchedMonteCarlo(model, init, Physics(L, L), seeds, chain_offset=7)
+    single = BatchedMonteCarlo(model, init, Physics(L, L), seeds, chain_offset=7)
+    single.MAX_STEPS_PER_LAUNCH = 1
+    names = ("state", "E_old", "W_old", "nll_old", "pcg", "accept", "attempts", "accepted", "n_accept")
+    used = 0
+    for cycle in range(8):
+        if cycle == 5:  # new weights: the open bank is stale
+            with torch.no_grad():
+                model.flows[1].prqct.transform_net.final_layer.weight.mul_(1.5)
+        for m in (banked, single):
+            m.local_moves(25)
+            m.step(2 if cycle == 3 else 1)  # cycle 3: a pure step follows the hybrid one
+        used += banked._bank is not None and banked._bank["step0"] <= banked.step_count - 1
+        for name in names:
+            assert torch.equal(getattr(banked, name), getattr(single, name)), (cycle, name)
+    assert used >= 4 and banked._bank is not None and banked._bank["S"] > 1
+    assert banked.step_count == single.step_count == 9
+    assert int(banked.accepted.sum().item()) > 0
+
+
+def test_nf_big_move_with_precomputed_terms():
+    """proposal_terms() over several attempts' configurations in one launch per pass gives
+    each attempt's energies and log q bit for bit, so nf_big_move(cfg, terms=...) leaves the
+    chains exactly where nf_big_move(cfg) does (the testing phase's path)."""
+    N, C, A = 16, 128, 3
+    dims_kw = dict(L=2, H=32, nb=1, K=8)
+    dims = OF.FlowDims(N=N, B=half_box(N), **dims_kw)
+    sd = OF.random_state_dict(dims, seed=5)
+    model = flow_from_state_dict(sd, N, bound=dims.B, **dims_kw)
+    L = float(np.sqrt(N / 0.03))
+    rng = np.random.default_rng(12)
+    init = np.mod(OP.fcc_lattice(N)[None] + rng.normal(0, 0.05, (C, N, 2)), L)
+    cfg = torch.from_numpy(np.mod(OP.fcc_lattice(N)[None] + rng.normal(0, 0.3, (A * C, N, 2)), L)
+                           .astype(np.float32)).cuda()
+    seeds = np.arange(42, 42 + C, dtype=np.uint64)
+    a = BatchedMonteCarlo(model, init, Physics(L, L), seeds)
+    b = BatchedMonteCarlo(model, init, Physics(L, L), seeds)
+    E, W, lq = b.proposal_terms(cfg)
+    for k in range(A):
+        for m in (a, b):
+            m.local_moves(10)
+        a.nf_big_move(cfg[k * C:(k + 1) * C])
+        b.nf_big_move(cfg[k * C:(k + 1) * C], terms=(E[k * C:(k + 1) * C], W[k * C:(k + 1) * C],
+                                                      lq[k * C:(k + 1) * C]))
+        for name in ("state", "state_is_f32", "E_old", "W_old", "nll_old", "pcg", "accept", "accepted"):
+            assert torch.equal(getattr(a, name), getattr(b, name)), (k, name)
+    assert int(a.accepted.sum().item()) > 0
+    with pytest.raises(ValueError):
+        b.nf_big_move(cfg[:C], terms=(E[:C], W[:C], lq[:C].double()))

@@ -109,6 +109,20 @@ def test_abi_rejects_invalid_arguments_before_touching_the_device():
                           _lib.FS_MH_HYBRID, one, None)
     assert rc == -1 and b"FS_MH_HYBRID" in L.fs_last_error()
     assert L.fs_nf_mh_steps_ws_bytes(d64, 4, 0) == -1
+    # proposal bank: S >= 1, step index inside the bank, aligned buffers, hybrid needs state
+    rc = L.fs_nf_mh_bank(d64, one, ph, 4, 0, 0, 0, 0, None, one, None)
+    assert rc == -1 and b"fs_nf_mh_bank" in L.fs_last_error()
+    aligned = ctypes.c_void_p(256)
+    rc = L.fs_nf_mh_step_banked(d64, one, ph, 4, 2, 2, aligned, one, one, one, one, one, None, one, None, None, None,
+                                None, 0, aligned, None)
+    assert rc == -1 and b"fs_nf_mh_step_banked" in L.fs_last_error()
+    rc = L.fs_nf_mh_step_banked(d64, one, ph, 4, 2, 1, aligned, one, one, one, one, None, None, one, None, None, None,
+                                None, _lib.FS_MH_HYBRID, aligned, None)
+    assert rc == -1
+    rc = L.fs_nf_mh_step_banked(d64, one, ph, 4, 2, 1, one, one, one, one, one, one, None, one, None, None, None,
+                                None, 0, aligned, None)
+    assert rc == -1 and b"aligned" in L.fs_last_error()
+    assert L.fs_nf_mh_banked_ws_bytes(d64, 4) > 0 and L.fs_nf_mh_banked_ws_bytes(d64, -1) == -1
     # training kernels
     rc = L.fs_linear_f32(-1, 4, 4, one, 4, 1, one, 1, 4, None, None, 0, one, 4, None, None)
     assert rc == -1 and b"fs_linear_f32" in L.fs_last_error()

@@ -3,7 +3,10 @@ per cycle, BIG_MOVE_INTERVAL = 1000 local moves of every chain (fs_local_moves) 
 NF-proposed big move (fs_nf_mh_step with FS_MH_HYBRID: proposal pass, density pass
 of the proposal, density pass of the moved state, energies, accept).  65536 chains,
 N=64, A1 flow.  Prints one JSON line: big-move attempts/s, local moves/s and the
-per-cycle split."""
+per-cycle split.  Options: --N, --C, --cycles, --interval; --single runs every big move as
+one fused step (no proposal bank: BatchedMonteCarlo.MAX_STEPS_PER_LAUNCH = 1), the
+comparison for small batches, where the bank is used from the second cycle on."""
+import argparse
 import json
 import os
 import sys
@@ -21,12 +24,14 @@ from flowstate import parallel  # noqa: E402
 from flowstate.MCMC import BatchedMonteCarlo, Physics  # noqa: E402
 
 
-def main(cycles=3, warmup=1, interval=1000, N=64, C=65536):
+def main(cycles=3, warmup=1, interval=1000, N=64, C=65536, single=False):
     dev = torch.device("cuda")
     model = synthetic_model(N, dev)
     init, L = synthetic_states(N, C, 0)
     _, seeds = parallel.shard(C, 0)
     b = BatchedMonteCarlo(model, init, Physics(L, L), seeds, device=dev, initial_max_displacement=0.65)
+    if single:
+        b.MAX_STEPS_PER_LAUNCH = 1
     ev = lambda: torch.cuda.Event(enable_timing=True)
     for _ in range(warmup):
         b.local_moves(interval)
@@ -47,14 +52,23 @@ def main(cycles=3, warmup=1, interval=1000, N=64, C=65536):
         t_big += e1.elapsed_time(e2)
     dt = time.perf_counter() - t0
     print(json.dumps({
-        "metric": "Algorithm-1 cycles (1000 local moves + 1 NF big move per chain), N=64, 65536 chains",
+        "metric": f"Algorithm-1 cycles ({interval} local moves + 1 NF big move per chain), N={N}, {C} chains",
         "value": C * cycles / dt, "unit": "big-move attempts/s", "local_moves_per_s": C * cycles * interval / dt,
         "ms_per_cycle": dt / cycles * 1e3, "local_ms_per_cycle": t_local / cycles,
         "big_move_ms_per_cycle": t_big / cycles, "n_gpus": 1, "steps": cycles, "warmup": warmup,
         "big_move_acceptance": (b.n_accept.item() - a0) / (C * cycles),
+        "proposal_bank_steps": 1 if single else b.steps_per_launch(),
         "dtype": "f64 local / f32 flow", "data": "synthetic (FCC + jitter, random-init A1 flow)",
         "config": {"workload": f"{C} chains x ({interval} local moves + 1 hybrid NF-MH step), N={N}, A1 flow"}}))
 
 
 if __name__ == "__main__":
-    main()
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--N", type=int, default=64)
+    ap.add_argument("--C", type=int, default=65536)
+    ap.add_argument("--cycles", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--interval", type=int, default=1000)
+    ap.add_argument("--single", action="store_true")
+    a = ap.parse_args()
+    main(a.cycles, a.warmup, a.interval, a.N, a.C, a.single)
