@@ -198,11 +198,20 @@ def config2(steps=16, C=4096, N=16):
     a0 = int(bmc.n_accept.item())
     dt = run(steps)
     rate = (int(bmc.n_accept.item()) - a0) / (C * steps)
+    # a loop of step(1) calls (the per-call pattern of the reference's driver loop): the
+    # proposal bank serves them from S-step launches (fs_nf_mh_bank / fs_nf_mh_step_banked)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        bmc.step(1)
+    torch.cuda.synchronize()
+    dt_call = time.perf_counter() - t0
     bmc.MAX_STEPS_PER_LAUNCH = 1
     run(1)
     dt1 = run(4)
     return {"workload": "config 2: Algorithm 1, N=16, 4096 chains, A1 flow", "value": C * steps / dt,
             "unit": "steps/s", "steps": steps, "ms_per_step": dt / steps * 1e3, "steps_per_launch": S,
+            "step1_calls": {"value": C * steps / dt_call, "ms_per_step": dt_call / steps * 1e3},
             "one_step_per_launch": {"value": C * 4 / dt1, "ms_per_step": dt1 / 4 * 1e3},
             "acceptance_rate": rate}
 

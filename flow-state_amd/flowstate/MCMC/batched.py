@@ -196,13 +196,15 @@ class BatchedMonteCarlo:
         done = 0
         while done < n:
             fill = self.steps_per_launch()
-            if fill > 1 and (self._bank_covers(packed) or (self._moved and self._last_packed is not None
-                                                         and self._last_packed() is packed)):
-                # a small batch after local moves with the flow unchanged since the last
-                # step (Algorithm 1's cycle): this step's proposal, log q and energy come
-                # from a bank of `fill` steps made in one launch per pass; only the current
-                # states' density pass and energy run per step.  A step after new weights
-                # (Algorithm 2's refeed) stays one fused step: its bank would not be reused.
+            same_flow = self._last_packed is not None and self._last_packed() is packed
+            if fill > 1 and (self._bank_covers(packed) or (same_flow and (self._moved or n - done == 1))):
+                # a small batch stepped one step at a time with the flow unchanged since
+                # the last step (Algorithm 1's cycle: local moves between big moves, or a
+                # loop of step(1) calls): this step's proposal, log q and energy come from
+                # a bank of `fill` steps made in one launch per pass; after local moves
+                # only the current states' density pass and energy run per step.  A step
+                # after new weights (Algorithm 2's refeed) stays one fused step: its bank
+                # would not be reused.
                 bank, s = self._bank_for(packed, dims, fill)
                 _lib.check(L.fs_nf_mh_step_banked(dims, _lib.ptr(packed), self.phys.c, self.C, self._bank["S"], s,
                                                   _lib.ptr(bank), _lib.ptr(self.E_old), _lib.ptr(self.W_old),
@@ -212,6 +214,7 @@ class BatchedMonteCarlo:
                                                   _lib.ptr(self.n_accept), _lib.ptr(self.err),
                                                   self.flags | (_lib.FS_MH_HYBRID if self._moved else 0),
                                                   _lib.ptr(self._workspace_banked()), st), "fs_nf_mh_step_banked")
+                self._last_src = (bank, self._bank["S"] * self.C, s)
                 self.step_count += 1
                 done += 1
                 self._moved = False
@@ -225,6 +228,7 @@ class BatchedMonteCarlo:
                                            _lib.ptr(self.attempts), _lib.ptr(self.accepted), _lib.ptr(self.n_accept),
                                            _lib.ptr(self.err), self.flags | (_lib.FS_MH_HYBRID if self._moved else 0),
                                            _lib.ptr(self._workspace()), st), "fs_nf_mh_step")
+                self._last_src = (self._ws, self.C, 0)
             else:
                 _lib.check(L.fs_nf_mh_steps(dims, _lib.ptr(packed), self.phys.c, self.C, S, self.proposal_seed,
                                             self.step_count, self.chain_offset, _lib.ptr(self.E_old),
@@ -233,6 +237,7 @@ class BatchedMonteCarlo:
                                             _lib.ptr(self.attempts), _lib.ptr(self.accepted),
                                             _lib.ptr(self.n_accept), _lib.ptr(self.err), self.flags,
                                             _lib.ptr(self._workspace_steps(S)), st), "fs_nf_mh_steps")
+                self._last_src = (self._ws_steps, S * self.C, S - 1)
             self.step_count += S
             done += S
             self._moved = False
@@ -259,6 +264,20 @@ class BatchedMonteCarlo:
 
     _bank = None
     _last_packed = None
+    _last_src = None
+
+    def last_proposals(self, centered=False):
+        """The float32 proposals (C, N, 2) box coordinates of the last step() (or, with
+        centered, the flow's input fl32(config - half_width), (C, 2N)), read from the
+        buffer that step used: the fused step's workspace, the multi-step launch's or the
+        proposal bank's rows of that step.  Valid until the next step()."""
+        if self._last_src is None:
+            raise RuntimeError("no step() has run")
+        buf, R, s = self._last_src
+        D = 2 * self.N
+        off = ((R * D * 4 + 255) // 256 * 256 if centered else 0) + s * self.C * D * 4
+        rows = buf.view(torch.uint8)[off:off + self.C * D * 4].view(torch.float32)
+        return rows.reshape(self.C, D) if centered else rows.reshape(self.C, self.N, 2)
 
     def _bank_key(self, packed):
         # what a bank's rows depend on: the flow image (a new tensor on every repack),

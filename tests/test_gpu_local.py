@@ -262,9 +262,8 @@ def test_hybrid_big_moves_after_local_moves():
         for ch in chains:
             ch.local_moves(200)
         b.step()
-        ws = b._ws
         D = 2 * N
-        cfg = ws.view(torch.uint8)[: C * D * 4].view(torch.float32).reshape(C, N, 2).cpu().numpy()
+        cfg = b.last_proposals().cpu().numpy()
         acc = b.accept.cpu().numpy().astype(bool)
         x_old = torch.from_numpy(np.stack([(ch.particles - L / 2).reshape(-1) for ch in chains]).astype(np.float32))
         x_new = torch.from_numpy((cfg.astype(np.float64) - L / 2).astype(np.float32).reshape(C, -1))

@@ -69,11 +69,9 @@ def _fused_vs_oracle(N, dims_kw, C, steps, seed_w=11, precision="f32"):
     total_acc = 0
     for s in range(steps):
         bmc.step()
-        ws = bmc._ws
         D = 2 * N
-        nbytes = C * D * 4
-        cfg = ws.view(torch.uint8)[:nbytes].view(torch.float32).reshape(C, N, 2).cpu().numpy()
-        cen = ws.view(torch.uint8)[(nbytes + 255) // 256 * 256:][:nbytes].view(torch.float32).reshape(C, D).cpu()
+        cfg = bmc.last_proposals().cpu().numpy()
+        cen = bmc.last_proposals(centered=True).cpu()
         np.testing.assert_array_equal(cen.numpy(), (cfg.astype(np.float64) - L / 2).astype(np.float32).reshape(C, D))
         assert np.all(cfg >= 0) and np.all(cfg <= L + 1e-3)
         E_new = OP.total_energy_batch(cfg, OP.make_phys(N))[0]
@@ -143,10 +141,8 @@ def test_fused_step_config3_full_batch_subset():
         state0 = bmc.state.cpu().numpy()
         pcg0 = bmc.pcg.cpu().numpy().view(np.uint64)[sub].copy()
         bmc.step()
-        ws = bmc._ws
-        nbytes = C * 2 * N * 4
-        cfg = ws.view(torch.uint8)[:nbytes].view(torch.float32).reshape(C, N, 2).cpu().numpy()
-        cen = ws.view(torch.uint8)[(nbytes + 255) // 256 * 256:][:nbytes].view(torch.float32).reshape(C, 2 * N)
+        cfg = bmc.last_proposals().cpu().numpy()
+        cen = bmc.last_proposals(centered=True)
         acc = bmc.accept.cpu().numpy().astype(bool)
         tot += int(acc.sum())
         # whole batch: accepted chains hold their proposal, rejected ones their old state
@@ -261,7 +257,8 @@ def test_banked_hybrid_steps_match_single_steps():
     come from a bank of several steps made in one launch per pass (fs_nf_mh_bank), and the
     step runs only the current states' density pass and energy (fs_nf_mh_step_banked).
     Every chain ends exactly where single fused steps leave it, bit for bit, also across
-    pure steps inside the bank and a weight change (which drops the bank)."""
+    pure steps inside the bank (step(2), a loop of step(1) calls) and a weight change
+    (which drops the bank)."""
     N, C = 16, 512
     dims_kw = dict(L=3, H=64, nb=2, K=8)
     dims = OF.FlowDims(N=N, B=half_box(N), **dims_kw)
@@ -281,13 +278,20 @@ def test_banked_hybrid_steps_match_single_steps():
             with torch.no_grad():
                 model.flows[1].prqct.transform_net.final_layer.weight.mul_(1.5)
         for m in (banked, single):
-            m.local_moves(25)
+            if cycle != 7:  # cycle 7: a pure step(1) right after a hybrid one
+                m.local_moves(25)
             m.step(2 if cycle == 3 else 1)  # cycle 3: a pure step follows the hybrid one
         used += banked._bank is not None and banked._bank["step0"] <= banked.step_count - 1
         for name in names:
             assert torch.equal(getattr(banked, name), getattr(single, name)), (cycle, name)
+    for _ in range(3):  # a loop of pure step(1) calls draws from the open bank
+        for m in (banked, single):
+            m.step(1)
+    for name in names:
+        assert torch.equal(getattr(banked, name), getattr(single, name)), name
     assert used >= 4 and banked._bank is not None and banked._bank["S"] > 1
-    assert banked.step_count == single.step_count == 9
+    assert banked._bank["step0"] < banked.step_count - 3
+    assert banked.step_count == single.step_count == 12
     assert int(banked.accepted.sum().item()) > 0
 
 
