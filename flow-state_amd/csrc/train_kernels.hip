@@ -21,11 +21,19 @@
 
 #include "fs_internal.h"
 
+// Defaults from A/B builds of the A2 training step (tools/gpu_gemm_ab.sh, batch 256,
+// profiles/r02/train/gemm_split_ab.log): 8 waves per tile, one k-block of loads in flight
+// per wave: 113 steps/s against 106 for (4, 4, 2) and 109-112 for the other mixes.
+// These GEMMs are latency-bound (2 to 4 k-blocks per wave): more waves each walking
+// fewer k-blocks shorten the dependent chain more than deeper prefetch does.
 #ifndef FS_GEMM_PF
-#define FS_GEMM_PF 2  // k-blocks of operand loads in flight per wave
+#define FS_GEMM_PF 1  // k-blocks of operand loads in flight per wave
 #endif
 #ifndef FS_GEMM_SPLIT
-#define FS_GEMM_SPLIT 4  // waves sharing one 32 x 32 tile's reduction (short K)
+#define FS_GEMM_SPLIT 8  // waves sharing one 32 x 32 tile's reduction (short K)
+#endif
+#ifndef FS_GEMM_SPLIT_MID
+#define FS_GEMM_SPLIT_MID 8  // ... for 256 <= K <= 512 (the weight gradients at batch 256)
 #endif
 #ifndef FS_GEMM_SPLIT_LONG
 #define FS_GEMM_SPLIT_LONG 16  // ... for K > 512
@@ -279,7 +287,7 @@ hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st) {
     const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0;
     const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0;
     // enough waves per tile that each walks at most ~16 k-blocks
-    const int split = g.K > 8 * 4 * 16 ? FS_GEMM_SPLIT_LONG : FS_GEMM_SPLIT;
+    const int split = g.K > 8 * 4 * 16 ? FS_GEMM_SPLIT_LONG : g.K >= 256 ? FS_GEMM_SPLIT_MID : FS_GEMM_SPLIT;
 #define FS_G(S, A, B)                                                                           \
     if (split == S && ak == A && bk == B) {                                                     \
         hipLaunchKernelGGL((gemm_f32_kernel<S, A, B>), grid, dim3(64 * S), 0, st, g);           \
@@ -287,6 +295,8 @@ hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st) {
     }
     FS_G(FS_GEMM_SPLIT, true, true) FS_G(FS_GEMM_SPLIT, true, false) FS_G(FS_GEMM_SPLIT, false, true)
     FS_G(FS_GEMM_SPLIT, false, false)
+    FS_G(FS_GEMM_SPLIT_MID, true, true) FS_G(FS_GEMM_SPLIT_MID, true, false) FS_G(FS_GEMM_SPLIT_MID, false, true)
+    FS_G(FS_GEMM_SPLIT_MID, false, false)
     FS_G(FS_GEMM_SPLIT_LONG, true, true) FS_G(FS_GEMM_SPLIT_LONG, true, false) FS_G(FS_GEMM_SPLIT_LONG, false, true)
     FS_G(FS_GEMM_SPLIT_LONG, false, false)
 #undef FS_G
