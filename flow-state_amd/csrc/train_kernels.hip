@@ -12,7 +12,7 @@
 //
 // bn_relu_train_*: BatchNorm1d in train mode followed by ReLU (resnet.py:35-51, the
 // block's batch_norm_layers[i] then the activation), forward and backward.  A workgroup
-// owns 16 feature columns over the whole batch, so the batch statistics are workgroup
+// owns 4 feature columns (64 row groups) over the whole batch, so the batch statistics are workgroup
 // reductions in a fixed order: two-pass mean / biased variance, running statistics
 // updated as torch does (momentum, unbiased variance), num_batches_tracked += 1.
 #include <hip/hip_runtime.h>
@@ -134,8 +134,18 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_f32_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------
-// BatchNorm1d (train) + ReLU.  Workgroup = 16 columns x 16 row groups.
-constexpr int kBnCols = 16, kBnRg = 16;
+// BatchNorm1d (train) + ReLU.  Workgroup = kBnCols columns x kBnRg row groups.
+// 4 columns x 64 row groups (32 workgroups at H = 128, 4 register-cached rows per thread):
+// A/B builds of the A2 step (profiles/r02/train/bn_tiling_ab.log) gave 122-124 steps/s
+// against 113 for 16 x 16 (8 workgroups, 16 rows per thread) at batch 256
+#ifndef FS_BN_COLS
+#define FS_BN_COLS 4
+#endif
+#ifndef FS_BN_RG
+#define FS_BN_RG 64
+#endif
+constexpr int kBnCols = FS_BN_COLS, kBnRg = FS_BN_RG;
+constexpr int kBnR = (256 + kBnRg - 1) / kBnRg;  // register-cached rows per thread (batch <= 256)
 
 __device__ __forceinline__ float wg_colsum(float v, float (*red)[kBnCols], int c, int rg) {
     red[rg][c] = v;
@@ -308,8 +318,8 @@ hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const flo
                                      float *mean, float *invstd, hipStream_t st) {
     if (B <= 0 || H <= 0) return hipSuccess;
     const dim3 grid((unsigned)((H + kBnCols - 1) / kBnCols)), block(kBnCols * kBnRg);
-    if (B <= 16 * kBnRg)
-        hipLaunchKernelGGL(bn_relu_train_fwd_kernel<16>, grid, block, 0, st, B, H, x, gamma, beta, rm, rv, nbt,
+    if (B <= kBnR * kBnRg)
+        hipLaunchKernelGGL(bn_relu_train_fwd_kernel<kBnR>, grid, block, 0, st, B, H, x, gamma, beta, rm, rv, nbt,
                            momentum, eps, y, mean, invstd);
     else
         hipLaunchKernelGGL(bn_relu_train_fwd_kernel<0>, grid, block, 0, st, B, H, x, gamma, beta, rm, rv, nbt,
@@ -322,8 +332,8 @@ hipError_t fs_bn_relu_train_bwd_impl(int64_t B, int H, const float *x, const flo
                                      float *dgamma, float *dbeta, hipStream_t st) {
     if (B <= 0 || H <= 0) return hipSuccess;
     const dim3 grid((unsigned)((H + kBnCols - 1) / kBnCols)), block(kBnCols * kBnRg);
-    if (B <= 16 * kBnRg)
-        hipLaunchKernelGGL(bn_relu_train_bwd_kernel<16>, grid, block, 0, st, B, H, x, y, dy, gamma, mean, invstd, dx,
+    if (B <= kBnR * kBnRg)
+        hipLaunchKernelGGL(bn_relu_train_bwd_kernel<kBnR>, grid, block, 0, st, B, H, x, y, dy, gamma, mean, invstd, dx,
                            dgamma, dbeta);
     else
         hipLaunchKernelGGL(bn_relu_train_bwd_kernel<0>, grid, block, 0, st, B, H, x, y, dy, gamma, mean, invstd, dx,
