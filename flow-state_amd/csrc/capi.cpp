@@ -465,10 +465,11 @@ int fs_bn_relu_train_fwd(int64_t Bn, int32_t H, const float *x, const float *gam
 }
 
 int fs_bn_relu_train_bwd(int64_t Bn, int32_t H, const float *x, const float *y, const float *dy, const float *gamma,
-                         const float *mean, const float *invstd, float *dx, float *dgamma, float *dbeta, void *stream) {
+                         const float *mean, const float *invstd, float *dx, const float *dx_add, float *dgamma,
+                         float *dbeta, void *stream) {
     REQUIRE(Bn >= 2 && H >= 1 && x && y && dy && gamma && mean && invstd && dx,
             "fs_bn_relu_train_bwd: invalid arguments");
-    return hip_rc(fs_bn_relu_train_bwd_impl(Bn, H, x, y, dy, gamma, mean, invstd, dx, dgamma, dbeta,
+    return hip_rc(fs_bn_relu_train_bwd_impl(Bn, H, x, y, dy, gamma, mean, invstd, dx, dx_add, dgamma, dbeta,
                                             (hipStream_t)stream),
                   "fs_bn_relu_train_bwd");
 }

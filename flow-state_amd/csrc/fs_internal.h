@@ -103,7 +103,7 @@ hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const flo
                                      float *mean, float *invstd, hipStream_t st);
 hipError_t fs_bn_relu_train_bwd_impl(int64_t B, int H, const float *x, const float *y, const float *dy,
                                      const float *gamma, const float *mean, const float *invstd, float *dx,
-                                     float *dgamma, float *dbeta, hipStream_t st);
+                                     const float *dx_add, float *dgamma, float *dbeta, hipStream_t st);
 hipError_t fs_coupling_density_fwd_impl(const fs_coupling *cp, const float *x, const float *params, const float *uw,
                                         const float *uh, const float *ud, const float *lq_in, float *out, float *lq_out,
                                         hipStream_t st);

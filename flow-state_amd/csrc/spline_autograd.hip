@@ -337,6 +337,12 @@ __device__ __forceinline__ void cond_params(const float *p, float sq, float *w, 
     }
 }
 
+#ifndef FS_CPL_ROWS
+#define FS_CPL_ROWS 1  // A/B at batch 256 (profiles/r02/train/cpl_rows_ab.log): 1 row ~1 % ahead of 2 or 4
+#endif
+// sample rows (one wave each) per workgroup of the coupling kernels
+constexpr int kCplRows = FS_CPL_ROWS;
+
 // density direction forward (Coupling.forward), after the conditioner: both splines,
 // rolled output, lq_out = lq_in + (sum lad_cond + sum lad_uncond)
 template <int K>
@@ -348,7 +354,7 @@ __global__ __launch_bounds__(256) void coupling_density_fwd_kernel(CouplingArgs 
                                                                    const float *__restrict__ lq_in, float *out,
                                                                    float *lq_out) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
     if (row >= c.rows) return;
     const float *xr = x + row * c.D;
     float sc = 0.f, su = 0.f;
@@ -383,7 +389,7 @@ __global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
     const float *__restrict__ uh, const float *__restrict__ ud, const float *__restrict__ g_out,
     const float *__restrict__ g_lq, float *gx, float *g_params, float *g_u) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
     if (row >= c.rows) return;
     const float *xr = x + row * c.D;
     const float gl = g_lq ? g_lq[row] : 0.f;
@@ -446,7 +452,7 @@ __global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
 __global__ __launch_bounds__(256) void coupling_features_fwd_kernel(CouplingArgs c, const float *__restrict__ x,
                                                                     float *t) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
     if (row >= c.rows) return;
     for (int j = lane; j < c.n; j += 64) {
         const float v = c.scale * x[row * c.D + c.id[j]];
@@ -460,7 +466,7 @@ __global__ __launch_bounds__(256) void coupling_features_fwd_kernel(CouplingArgs
 __global__ __launch_bounds__(256) void coupling_features_bwd_kernel(CouplingArgs c, const float *__restrict__ x,
                                                                     const float *__restrict__ g_t, float *gx) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
     if (row >= c.rows) return;
     for (int j = lane; j < c.n; j += 64) {
         const int pi = (int)c.id[j], pt = (int)c.tr[j];
@@ -481,7 +487,7 @@ __global__ __launch_bounds__(256) void coupling_sample_pre_kernel(CouplingArgs c
                                                                   const float *__restrict__ ud, float *t, float *out,
                                                                   float *lad_u, int32_t *nan_flag) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
     if (row >= c.rows) return;
     const float *zr = z + row * c.D;
     float su = 0.f;
@@ -510,7 +516,7 @@ __global__ __launch_bounds__(256) void coupling_sample_post_kernel(CouplingArgs 
                                                                    const float *__restrict__ lq_in, float *out,
                                                                    float *lq_out, int32_t *nan_flag) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
     if (row >= c.rows) return;
     float sc = 0.f;
     for (int j = lane; j < c.n; j += 64) {
@@ -593,7 +599,7 @@ static fs::CouplingArgs coupling_args(const fs_coupling *c) {
 #define FS_COUPLING_LAUNCH(KERNEL, ...)                                                         \
     const fs::CouplingArgs a = coupling_args(cp);                                               \
     if (a.rows <= 0) return hipSuccess;                                                         \
-    const dim3 grid((unsigned)((a.rows + 3) / 4)), block(256);                                  \
+    const dim3 grid((unsigned)((a.rows + kCplRows - 1) / kCplRows)), block(64 * kCplRows);                                  \
     switch (cp->K) {                                                                            \
     case 5: hipLaunchKernelGGL((KERNEL<5>), grid, block, 0, st, a, __VA_ARGS__); break;         \
     case 8: hipLaunchKernelGGL((KERNEL<8>), grid, block, 0, st, a, __VA_ARGS__); break;         \
@@ -631,7 +637,7 @@ hipError_t fs_coupling_sample_post_impl(const fs_coupling *cp, const float *para
 hipError_t fs_coupling_features_fwd_impl(const fs_coupling *cp, const float *x, float *t, hipStream_t st) {
     const fs::CouplingArgs a = coupling_args(cp);
     if (a.rows <= 0) return hipSuccess;
-    hipLaunchKernelGGL(coupling_features_fwd_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, st, a, x, t);
+    hipLaunchKernelGGL(coupling_features_fwd_kernel, dim3((unsigned)((a.rows + kCplRows - 1) / kCplRows)), dim3(64 * kCplRows), 0, st, a, x, t);
     return hipGetLastError();
 }
 
@@ -639,7 +645,7 @@ hipError_t fs_coupling_features_bwd_impl(const fs_coupling *cp, const float *x, 
                                          hipStream_t st) {
     const fs::CouplingArgs a = coupling_args(cp);
     if (a.rows <= 0) return hipSuccess;
-    hipLaunchKernelGGL(coupling_features_bwd_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, st, a, x, g_t,
+    hipLaunchKernelGGL(coupling_features_bwd_kernel, dim3((unsigned)((a.rows + kCplRows - 1) / kCplRows)), dim3(64 * kCplRows), 0, st, a, x, g_t,
                        gx);
     return hipGetLastError();
 }

@@ -232,7 +232,7 @@ template <int R>
 __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
     int64_t B, int H, const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ dy,
     const float *__restrict__ gamma, const float *__restrict__ mean, const float *__restrict__ invstd,
-    float *__restrict__ dx, float *__restrict__ dgamma, float *__restrict__ dbeta) {
+    float *__restrict__ dx, const float *__restrict__ dx_add, float *__restrict__ dgamma, float *__restrict__ dbeta) {
     __shared__ float red[kBnRg][kBnCols];
     const int c = threadIdx.x % kBnCols, rg = threadIdx.x / kBnCols;
     const int col = blockIdx.x * kBnCols + c;
@@ -271,13 +271,13 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int64_t i = rg + (int64_t)q * kBnRg;
-            if (i < B) dx[i * H + col] = (dzv[q] - mdb - xhv[q] * mdg) * (is * gm);
+            if (i < B) dx[i * H + col] = (dzv[q] - mdb - xhv[q] * mdg) * (is * gm) + (dx_add ? dx_add[i * H + col] : 0.f);
         }
     } else {
         for (int64_t i = rg; i < B; i += kBnRg) {
             const float dz = y[i * H + col] > 0.f ? dy[i * H + col] : 0.f;
             const float xh = (x[i * H + col] - mu) * is;
-            dx[i * H + col] = (dz - mdb - xh * mdg) * (is * gm);
+            dx[i * H + col] = (dz - mdb - xh * mdg) * (is * gm) + (dx_add ? dx_add[i * H + col] : 0.f);
         }
     }
     if (rg == 0) {
@@ -329,14 +329,14 @@ hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const flo
 
 hipError_t fs_bn_relu_train_bwd_impl(int64_t B, int H, const float *x, const float *y, const float *dy,
                                      const float *gamma, const float *mean, const float *invstd, float *dx,
-                                     float *dgamma, float *dbeta, hipStream_t st) {
+                                     const float *dx_add, float *dgamma, float *dbeta, hipStream_t st) {
     if (B <= 0 || H <= 0) return hipSuccess;
     const dim3 grid((unsigned)((H + kBnCols - 1) / kBnCols)), block(kBnCols * kBnRg);
     if (B <= kBnR * kBnRg)
         hipLaunchKernelGGL(bn_relu_train_bwd_kernel<kBnR>, grid, block, 0, st, B, H, x, y, dy, gamma, mean, invstd, dx,
-                           dgamma, dbeta);
+                           dx_add, dgamma, dbeta);
     else
         hipLaunchKernelGGL(bn_relu_train_bwd_kernel<0>, grid, block, 0, st, B, H, x, y, dy, gamma, mean, invstd, dx,
-                           dgamma, dbeta);
+                           dx_add, dgamma, dbeta);
     return hipGetLastError();
 }

@@ -85,7 +85,7 @@ _SIGS = {
                                      _P, _P]),
     "fs_bn_relu_train_fwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 6 + [ctypes.c_double, ctypes.c_double]
                              + [_P] * 4),
-    "fs_bn_relu_train_bwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 10),
+    "fs_bn_relu_train_bwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 11),
     "fs_coupling_features_fwd": (ctypes.c_int, [_CP] + [_P] * 3),
     "fs_coupling_density_fwd": (ctypes.c_int, [_CP] + [_P] * 9),
     "fs_coupling_density_bwd": (ctypes.c_int, [_CP] + [_P] * 11),

@@ -189,7 +189,7 @@ class _Linear(torch.autograd.Function):
     db = column sums of dy (from the same launch)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, r):
+    def forward(ctx, x, w, b, r, res=None):
         from .. import _lib
 
         x = x.contiguous()
@@ -197,6 +197,7 @@ class _Linear(torch.autograd.Function):
         N = w.shape[0]
         ctx.save_for_backward(x, w)
         ctx.has_r = r is not None
+        ctx.res = res
         if N >= _WIDE and r is None:
             return torch.addmm(b, x, w.t())
         y = torch.empty((M, N), dtype=torch.float32, device=x.device)
@@ -227,7 +228,12 @@ class _Linear(torch.autograd.Function):
             gb = torch.empty((N,), dtype=torch.float32, device=x.device)
             _lib.check(L.fs_linear_f32(N, K, M, _lib.ptr(gy), 1, N, _lib.ptr(x), K, 1, None, None, 0, _lib.ptr(gw),
                                        K, _lib.ptr(gb), _lib.stream_ptr()), "fs_linear_f32")
-        return gx, gw, gb, (gy if ctx.has_r and ctx.needs_input_grad[3] else None)
+        if ctx.res is not None and ctx.needs_input_grad[3]:
+            # the residual's gradient goes to the block's first BatchNorm backward, which
+            # adds it in its own launch (no autograd accumulation kernel)
+            ctx.res.g = gy
+            return gx, gw, gb, None, None
+        return gx, gw, gb, (gy if ctx.has_r and ctx.needs_input_grad[3] else None), None
 
 
 class _BnRelu(torch.autograd.Function):
@@ -236,7 +242,7 @@ class _BnRelu(torch.autograd.Function):
     same launch (torch.nn.BatchNorm1d.forward, momentum form)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, bn):
+    def forward(ctx, x, gamma, beta, bn, res=None):
         from .. import _lib
 
         x = x.contiguous()
@@ -252,6 +258,7 @@ class _BnRelu(torch.autograd.Function):
                                           _lib.ptr(y), _lib.ptr(mean), _lib.ptr(invstd), _lib.stream_ptr()),
                    "fs_bn_relu_train_fwd")
         ctx.save_for_backward(x, y, gamma, mean, invstd)
+        ctx.res = res
         return y
 
     @staticmethod
@@ -264,10 +271,16 @@ class _BnRelu(torch.autograd.Function):
         gx = torch.empty_like(x)
         gg = torch.empty_like(gamma)
         gb = torch.empty_like(gamma)
+        add = None
+        if ctx.res is not None and ctx.res.g is not None:
+            add, ctx.res.g = ctx.res.g, None
+            if add.shape != x.shape:
+                raise RuntimeError("residual gradient does not match the block input")
         _lib.check(_lib.load().fs_bn_relu_train_bwd(M, H, _lib.ptr(x), _lib.ptr(y), _lib.ptr(gy), _lib.ptr(gamma),
-                                                    _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(gx), _lib.ptr(gg),
-                                                    _lib.ptr(gb), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
-        return gx, gg, gb, None
+                                                    _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(gx), _lib.ptr(add),
+                                                    _lib.ptr(gg), _lib.ptr(gb), _lib.stream_ptr()),
+                   "fs_bn_relu_train_bwd")
+        return gx, gg, gb, None, None
 
 
 def _fused_ok(net, t):
@@ -284,19 +297,33 @@ def _fused_ok(net, t):
     return True
 
 
+class _ResidualGrad:
+    """Carries a block input's residual-branch gradient from the block's second Linear
+    (whose backward runs first: the chain l1 -> bn1 -> l0 -> bn0 orders them) to its first
+    BatchNorm's backward, which adds it in its own launch (fs_bn_relu_train_bwd dx_add)
+    instead of autograd summing the two branches in a separate kernel."""
+
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+
 def _conditioner_fused(net, t):
     """ResidualNet.forward (resnet.py:82-104, blocks :35-51) in train mode: every Linear
     on fs_linear_f32 (the block's residual add fused into its second Linear), every
-    BatchNorm + ReLU pair on fs_bn_relu_train_fwd."""
+    BatchNorm + ReLU pair on fs_bn_relu_train_fwd; backward: the residual gradient added
+    by the block's first BatchNorm backward."""
     li = net.initial_layer
     t = _Linear.apply(t, li.weight, li.bias, None)
     for blk in net.blocks:
         bn0, bn1 = blk.batch_norm_layers
         l0, l1 = blk.linear_layers
-        u = _BnRelu.apply(t, bn0.weight, bn0.bias, bn0)
+        res = _ResidualGrad()
+        u = _BnRelu.apply(t, bn0.weight, bn0.bias, bn0, res)
         u = _Linear.apply(u, l0.weight, l0.bias, None)
         u = _BnRelu.apply(u, bn1.weight, bn1.bias, bn1)
-        t = _Linear.apply(u, l1.weight, l1.bias, t)
+        t = _Linear.apply(u, l1.weight, l1.bias, t, res)
     lf = net.final_layer
     return _Linear.apply(t, lf.weight, lf.bias, None)
 
@@ -490,7 +517,13 @@ class _DensitySplines(torch.autograd.Function):
                                                        _lib.ptr(uh), _lib.ptr(ud), _lib.ptr(g_out), _lib.ptr(g_lq),
                                                        _lib.ptr(gx), _lib.ptr(gp), _lib.ptr(gu), _lib.stream_ptr()),
                    "fs_coupling_density_bwd")
-        gs = gu.sum(0)  # the unconditional parameters are shared by every row
+        # the unconditional parameters are shared by every row: their gradient is the column
+        # sum of gu, taken as fs_linear_f32's row sum of gu^T (N = 0: no product), which
+        # spreads it over (n(3K+1))/32 workgroups (torch's reduction took 16 us at batch 256)
+        P = n * (3 * K + 1)
+        gs = torch.empty((P,), dtype=torch.float32, device=x.device)
+        _lib.check(_lib.load().fs_linear_f32(P, 0, x.shape[0], _lib.ptr(gu), 1, P, None, 0, 0, None, None, 0, None, 0,
+                                             _lib.ptr(gs), _lib.stream_ptr()), "fs_linear_f32")
         # [uw | uh | ud] back to back: contiguous views, no copies when the gradients are gathered
         guw = gs[:n * K].view(n, K)
         guh = gs[n * K:2 * n * K].view(n, K)

@@ -280,8 +280,12 @@ int fs_bn_relu_train_fwd(int64_t Bn, int32_t H, const float *x, const float *gam
 
 /* Gradients of the above: dx [Bn][H], dgamma, dbeta [H] (nullable) from dy = dL/dy and
  * the forward's x, y, mean, invstd. */
+/* fs_bn_relu_train_bwd: dx = the input gradient (+ dx_add [Bn][H], nullable: the block
+ * input's residual-branch gradient, resnet.py:51, added in the same launch instead of by
+ * autograd); dgamma, dbeta nullable. */
 int fs_bn_relu_train_bwd(int64_t Bn, int32_t H, const float *x, const float *y, const float *dy, const float *gamma,
-                         const float *mean, const float *invstd, float *dx, float *dgamma, float *dbeta, void *stream);
+                         const float *mean, const float *invstd, float *dx, const float *dx_add, float *dgamma,
+                         float *dbeta, void *stream);
 
 /* One circular-RQS coupling layer of the training path around its conditioner
  * (Coupling.forward / inverse, NF/normflows/flows/neural_spline/coupling.py:71-134;
