@@ -514,11 +514,12 @@ int fs_coupling_density_bwd(const fs_coupling *c, const float *x, const float *p
                   "fs_coupling_density_bwd");
 }
 
-int fs_coupling_features_bwd(const fs_coupling *c, const float *x, const float *g_t, float *gx, void *stream) {
+int fs_coupling_features_bwd(const fs_coupling *c, const float *x, const float *g_t, float *gx, const float *gx_add,
+                             void *stream) {
     int rc = check_coupling(c, "fs_coupling_features_bwd");
     if (rc) return rc;
     REQUIRE(c->rows == 0 || (x && g_t && gx), "fs_coupling_features_bwd: invalid arguments");
-    return hip_rc(fs_coupling_features_bwd_impl(c, x, g_t, gx, (hipStream_t)stream), "fs_coupling_features_bwd");
+    return hip_rc(fs_coupling_features_bwd_impl(c, x, g_t, gx, gx_add, (hipStream_t)stream), "fs_coupling_features_bwd");
 }
 
 int fs_coupling_sample_pre(const fs_coupling *c, const float *z, const float *uw, const float *uh, const float *ud,

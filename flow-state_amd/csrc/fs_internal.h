@@ -118,4 +118,4 @@ hipError_t fs_coupling_sample_post_impl(const fs_coupling *cp, const float *para
                                         const float *lq_in, float *out, float *lq_out, int32_t *nan_flag,
                                         hipStream_t st);
 hipError_t fs_coupling_features_bwd_impl(const fs_coupling *cp, const float *x, const float *g_t, float *gx,
-                                         hipStream_t st);
+                                         const float *gx_add, hipStream_t st);

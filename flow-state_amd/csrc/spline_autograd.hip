@@ -462,9 +462,10 @@ __global__ __launch_bounds__(256) void coupling_features_fwd_kernel(CouplingArgs
 }
 
 // adjoint of the periodic features t = [cos(s x_id), sin(s x_id)]: gx at the identity
-// positions, 0 at the transform positions
+// positions, 0 at the transform positions (+ gx_add, the splines' gradient of the same x)
 __global__ __launch_bounds__(256) void coupling_features_bwd_kernel(CouplingArgs c, const float *__restrict__ x,
-                                                                    const float *__restrict__ g_t, float *gx) {
+                                                                    const float *__restrict__ g_t, float *gx,
+                                                                    const float *__restrict__ gx_add) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
     if (row >= c.rows) return;
@@ -472,8 +473,9 @@ __global__ __launch_bounds__(256) void coupling_features_bwd_kernel(CouplingArgs
         const int pi = (int)c.id[j], pt = (int)c.tr[j];
         const float v = c.scale * x[row * c.D + pi];
         const float gc = g_t[row * 2 * c.n + j] * -sinf(v), gs = g_t[row * 2 * c.n + c.n + j] * cosf(v);
-        gx[row * c.D + pi] = gc * c.scale + gs * c.scale;
-        gx[row * c.D + pt] = 0.f;
+        const float ai = gx_add ? gx_add[row * c.D + pi] : 0.f, at = gx_add ? gx_add[row * c.D + pt] : 0.f;
+        gx[row * c.D + pi] = (gc * c.scale + gs * c.scale) + ai;
+        gx[row * c.D + pt] = at;
     }
 }
 
@@ -642,10 +644,10 @@ hipError_t fs_coupling_features_fwd_impl(const fs_coupling *cp, const float *x, 
 }
 
 hipError_t fs_coupling_features_bwd_impl(const fs_coupling *cp, const float *x, const float *g_t, float *gx,
-                                         hipStream_t st) {
+                                         const float *gx_add, hipStream_t st) {
     const fs::CouplingArgs a = coupling_args(cp);
     if (a.rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(coupling_features_bwd_kernel, dim3((unsigned)((a.rows + kCplRows - 1) / kCplRows)), dim3(64 * kCplRows), 0, st, a, x, g_t,
-                       gx);
+                       gx, gx_add);
     return hipGetLastError();
 }

@@ -89,7 +89,7 @@ _SIGS = {
     "fs_coupling_features_fwd": (ctypes.c_int, [_CP] + [_P] * 3),
     "fs_coupling_density_fwd": (ctypes.c_int, [_CP] + [_P] * 9),
     "fs_coupling_density_bwd": (ctypes.c_int, [_CP] + [_P] * 11),
-    "fs_coupling_features_bwd": (ctypes.c_int, [_CP] + [_P] * 4),
+    "fs_coupling_features_bwd": (ctypes.c_int, [_CP] + [_P] * 5),
     "fs_coupling_sample_pre": (ctypes.c_int, [_CP] + [_P] * 9),
     "fs_coupling_sample_post": (ctypes.c_int, [_CP] + [_P] * 7),
     "fs_classify_wells": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double,

@@ -446,7 +446,7 @@ class _Features(torch.autograd.Function):
     """t = [cos(s x_id), sin(s x_id)] (nn.py:120-137) and its adjoint."""
 
     @staticmethod
-    def forward(ctx, x, layer):
+    def forward(ctx, x, layer, res=None):
         from .. import _lib
 
         x = x.contiguous()
@@ -457,6 +457,7 @@ class _Features(torch.autograd.Function):
                    "fs_coupling_features_fwd")
         ctx.save_for_backward(x)
         ctx.layer = layer
+        ctx.res = res
         return t
 
     @staticmethod
@@ -466,10 +467,15 @@ class _Features(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         gt = gt.contiguous()
         gx = torch.empty_like(x)
+        add = None
+        if ctx.res is not None and ctx.res.g is not None:
+            add, ctx.res.g = ctx.res.g, None
+            if add.shape != x.shape:
+                raise RuntimeError("spline gradient does not match the layer input")
         c = _coupling_desc(ctx.layer, x.shape[0])
         _lib.check(_lib.load().fs_coupling_features_bwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(gt), _lib.ptr(gx),
-                                                        _lib.stream_ptr()), "fs_coupling_features_bwd")
-        return gx, None
+                                                        _lib.ptr(add), _lib.stream_ptr()), "fs_coupling_features_bwd")
+        return gx, None, None
 
 
 class _DensitySplines(torch.autograd.Function):
@@ -478,7 +484,7 @@ class _DensitySplines(torch.autograd.Function):
     lq_out = lq_in + both log-det sums; backward through both splines."""
 
     @staticmethod
-    def forward(ctx, x, params, uw, uh, ud, lq_in, layer):
+    def forward(ctx, x, params, uw, uh, ud, lq_in, layer, res=None):
         from .. import _lib
 
         x = x.contiguous()
@@ -497,6 +503,7 @@ class _DensitySplines(torch.autograd.Function):
         ctx.save_for_backward(x, params, uw, uh, ud)
         ctx.layer = layer
         ctx.has_lq = lq_in is not None
+        ctx.res = res
         return out, lq
 
     @staticmethod
@@ -528,7 +535,12 @@ class _DensitySplines(torch.autograd.Function):
         guw = gs[:n * K].view(n, K)
         guh = gs[n * K:2 * n * K].view(n, K)
         gud = gs[2 * n * K:].view(n, K + 1)
-        return (gx, gp, guw, guh, gud, g_lq if ctx.has_lq else None, None)
+        if ctx.res is not None and ctx.needs_input_grad[0]:
+            # x's spline gradient is added by the features backward of the same layer, which
+            # runs after this one (it needs the conditioner's adjoint, which needs gp)
+            ctx.res.g = gx
+            gx = None
+        return (gx, gp, guw, guh, gud, g_lq if ctx.has_lq else None, None, None)
 
 
 def conditioner_from_features(net, t):
@@ -550,11 +562,14 @@ def conditioner_from_features(net, t):
 def density_step(layer, x, log_q):
     """One layer of forward_kld on the device: (z, log_q + log_det), differentiable."""
     p = layer.prqct
-    t = _Features.apply(x, layer)
+    # x feeds the features and the splines: the features backward adds the splines' x
+    # gradient in its own launch (no autograd accumulation kernel)
+    res = _ResidualGrad() if x.requires_grad and torch.is_grad_enabled() else None
+    t = _Features.apply(x, layer, res)
     params = conditioner_from_features(p.transform_net, t)
     u = p.unconditional_transform
     return _DensitySplines.apply(x, params, u.unnormalized_widths, u.unnormalized_heights,
-                                 u.unnormalized_derivatives, log_q, layer)
+                                 u.unnormalized_derivatives, log_q, layer, res)
 
 
 @torch.no_grad()

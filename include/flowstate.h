@@ -317,7 +317,11 @@ int fs_coupling_density_bwd(const fs_coupling *c, const float *x, const float *p
                             const float *uh, const float *ud, const float *g_out, const float *g_lq, float *gx,
                             float *g_params, float *g_u, void *stream);
 /* Adjoint of t: gx [rows][D] (zero at the transform positions). */
-int fs_coupling_features_bwd(const fs_coupling *c, const float *x, const float *g_t, float *gx, void *stream);
+/* fs_coupling_features_bwd: gx = the features' adjoint (identity positions, 0 elsewhere)
+ * + gx_add [rows][D] (nullable: the splines' gradient of the same x, added in this launch
+ * instead of by autograd). */
+int fs_coupling_features_bwd(const fs_coupling *c, const float *x, const float *g_t, float *gx,
+                             const float *gx_add, void *stream);
 /* Sampling direction, forward only, in two launches around the conditioner:
  * pre: t, out (identity half through the inverse unconditional spline, transform half
  * copied), lad_u [rows]; post: the transform half through the inverse conditional spline
