@@ -216,6 +216,80 @@ def config2(steps=16, C=4096, N=16):
             "acceptance_rate": rate}
 
 
+def config5(cycles=3, train_steps=20):
+    """BASELINE config 5 (Algorithm 2 on-the-fly retrain + sample, N=64, A2 flow) on one
+    GPU as a secondary line, at the reference's sizes (main_algorithm_2.py:33-52): 100
+    runs, UPDATE_NUM_SAMPLES=1000 (100 local moves per run, sample() every 10), one
+    epoch of batch 256 (graph-captured forward_kld + reverse_kld + Adam, ALPHA=1), then
+    the refeed (one fused NF-MH step per run).  Reports cycles/s with the phase split,
+    graphed training steps/s on a full batch, and the training step's achieved
+    TFLOP/s: 4 A2 passes per sample (forward_kld forward + its backward at 2x, and
+    reverse_kld's sampling pass) x 256 samples x SURVEY §8(d)'s F_pass, against the
+    dense f32 peak.  Never the headline `value`."""
+    from flowstate.algorithm2 import Algorithm2
+    from flowstate.models import A2
+    from flowstate.normflows.Energy import DoubleWellLJ
+
+    N, runs, bs = 64, 100, 256
+    dev = torch.device("cuda", torch.cuda.current_device())
+    torch.manual_seed(0)
+    B = half_box(N)
+    m = build_flow(N, bound=B, device="cpu", **A2)
+    m.p = DoubleWellLJ(2 * N, N, 1.0, B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+    m = m.to(dev)
+    m.q0.device = dev
+    base, box = initialise_fcc(num_particles=N, rho=0.03, aspect_ratio=1.0)
+    bmc = BatchedMonteCarlo(None, np.repeat(base[None], runs, 0), Physics(box.box_size_x, box.box_size_y),
+                            [42 + i for i in range(runs)], device=dev, initial_max_displacement=0.65)
+    bmc.local_moves(10 * N, adjust_every=5 * N)
+    algo = Algorithm2(bmc, m, batch_size=bs, alpha=1.0, sampling_frequency=10, update_num_samples=1000)
+    t = np.zeros(3)
+
+    def cycle(timed):
+        ts = [time.perf_counter()]
+        algo.production()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter())
+        algo.train()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter())
+        algo.refeed()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter())
+        if timed:
+            t[:] += np.diff(ts)
+
+    cycle(False)
+    t0 = time.perf_counter()
+    for _ in range(cycles):
+        cycle(True)
+    dt = time.perf_counter() - t0
+    bmc.check_errors()
+    # graphed training steps on one full batch of the last training set
+    step = algo._step
+    x = algo.training_data[:bs].to(dev)
+    step.step(x)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(train_steps):
+        step.step(x)
+    torch.cuda.synchronize()
+    sps = train_steps / (time.perf_counter() - t1)
+    fpp = flops_per_pass(N, **A2)
+    ach = 4 * fpp * bs * sps / 1e12
+    return {"workload": "config 5: Algorithm 2 cycle, A2 flow (L=23 H=128 blocks=2 K=15), N=64, 100 runs, "
+                        "UPDATE_NUM_SAMPLES=1000, batch 256, 1 GPU",
+            "value": cycles / dt, "unit": "cycles/s", "cycles": cycles, "ms_per_cycle": dt / cycles * 1e3,
+            "phase_ms": {"production": t[0] / cycles * 1e3, "training": t[1] / cycles * 1e3,
+                         "refeed": t[2] / cycles * 1e3},
+            "train_steps_per_s": sps,
+            "train_roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                               "frac": ach / PEAK_F32_TFLOPS,
+                               "flop_per_step": 4 * fpp * bs,
+                               "what": "4 A2 passes per sample (forward_kld fwd + bwd, reverse_kld sampling) x 256"},
+            "last_loss": algo.loss_history[-1], "last_p_acc": algo.p_acc_history[-1]}
+
+
 class Stepper:
     """The fs_nf_mh_step kernel sequence, launched piecewise with HIP events."""
 
@@ -271,39 +345,71 @@ class Stepper:
 
 
 def final_reduction(bmc):
-    """End-of-run reduction: density histogram + well occupancy of the
-    current states, all-reduced over the ranks; per-chain counters gathered to rank 0."""
-    hist = bmc.histogram2d(100)
-    per_chain = bmc.well_counts()
-    wells = per_chain.sum(dim=0)
-    parallel.all_reduce_stats(hist, wells)
-    table = parallel.gather_chain_counters(torch.cat([per_chain, bmc.accepted[:, None], bmc.attempts[:, None]], 1))
-    return hist, wells, table
+    """End-of-run reduction: flowstate.parallel.final_reduction."""
+    return parallel.final_reduction(bmc)
 
 
-def _pmc_traffic():
-    """HBM bytes per flow-pass launch from the committed rocprofv3 PMC passes
-    (FETCH_SIZE x2 per the gfx950 calibration + WRITE_SIZE, tools/pmc_traffic.py);
-    None if no profile of the current build has been recorded."""
+def _pmc_traffic(C):
+    """HBM bytes per flow-pass launch of THIS bench's shape (C rows: grid C/64*512) from
+    the committed rocprofv3 PMC passes (profiles/traffic.json, tools/pmc_traffic.py:
+    FETCH_SIZE x2 per the gfx950 calibration + WRITE_SIZE): the mean of the propose
+    (<256,32,2>) and density (<256,32,0>) launches at that grid.  (None, None) if no
+    profile of that shape was recorded."""
     path = os.path.join(REPO, "profiles", "traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
-        return t.get("flow_pass_bytes_per_launch")
     except (OSError, ValueError):
-        return None
+        return None, None
+    grid = str((C + 63) // 64 * 512)
+    vals = [v[grid][0] for k, v in t.get("kernels", {}).items()
+            if k.startswith(("void fs::flow_pass_kernel<256, 32, 0>", "void fs::flow_pass_kernel<256, 32, 2>"))
+            and isinstance(v, dict) and grid in v]
+    if not vals:
+        return None, None
+    return sum(vals) / len(vals), {"profile": "profiles/traffic.json", "head": t.get("head"), "grid": int(grid),
+                                   "launch_kinds": len(vals)}
+
+
+def flow_algorithmic_bytes(model, C, N):
+    """Algorithmic HBM bytes of one flow-pass launch (mean of the propose and density
+    launches): the flow's parameters read once, plus the launch's own rows: propose
+    writes config + centered (2 x C x 2N float32), density reads C x 2N float32 and
+    writes C float32 log q."""
+    w = sum(p.numel() * p.element_size() for p in model.parameters())
+    D = 2 * N
+    return w + (2 * C * D * 4 + (C * D * 4 + C * 4)) / 2
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(N, budget_s=15.0):
-    """The oracle's restatement of the reference CPU path, per chain, on the host
-    cores: proposals generated in a batch (as main_algorithm_1.py:340-343 does)
-    then, per chain, nf_big_move semantics (monte_carlo.py:235-303): total energy
-    of the proposal (reference pair loop order), batch-1 log_prob of old AND new,
-    PCG64 accept, energy recompute on reject."""
+    """The reference CPU path restated (oracle/, test infrastructure), per chain, on the
+    host cores: proposals generated in a batch (as main_algorithm_1.py:340-343 does),
+    then per chain nf_big_move semantics (monte_carlo.py:235-303): the proposal's total
+    energy by the reference's numpy pair loop (oracle.physics.total_energy_pairloop,
+    bit-identical to energy_calculator.py:121-203), batch-1 float32 log_prob of old AND
+    new in torch-CPU (the reference's op sequence), the PCG64 accept, and the energy
+    recomputed on reject.  Threads: every CPU this process may run on, capped by
+    OMP_NUM_THREADS when the host sets it (the GPU box allots a 16-CPU share of its
+    256 visible CPUs that way); both numbers and the CPU model are reported."""
     from oracle import flow as OF
     from oracle import physics as OP
 
-    threads = torch.get_num_threads()  # honours OMP_NUM_THREADS (the box's CPU share)
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    threads = min(avail, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else avail
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
     dims = OF.FlowDims(N=N, B=half_box(N), **A1)
     sd = {k: v.detach().cpu() for k, v in synthetic_model(N, "cpu").state_dict().items()}
     init, L = synthetic_states(N, 4, 0)
@@ -311,7 +417,7 @@ def cpu_baseline(N, budget_s=15.0):
     hw = L / 2
     chains = [dict(state=init[c].copy(), pcg=OP.pcg64_seed(42 + c)[None].copy()) for c in range(4)]
     for ch in chains:
-        ch["E"] = OP.total_energy(ch["state"], phys)[0]
+        ch["E"] = OP.total_energy_pairloop(ch["state"], phys)[0]
     t0 = time.perf_counter()
     g = torch.Generator().manual_seed(1234)
     z = (torch.rand((16, dims.D), generator=g) * 2 - 1) * dims.B
@@ -322,7 +428,7 @@ def cpu_baseline(N, budget_s=15.0):
         ch = chains[steps % len(chains)]
         cfg = props[k % len(props)].reshape(N, 2)
         k += 1
-        E_new = OP.total_energy(cfg, phys)[0]
+        E_new = OP.total_energy_pairloop(cfg, phys)[0]
         old = torch.tensor((ch["state"] - np.array([hw, hw])).reshape(1, -1), dtype=torch.float)
         new = torch.tensor((cfg - np.array([hw, hw])).reshape(1, -1), dtype=torch.float)
         nll_o = -OF.log_prob(sd, old, dims).item()
@@ -331,46 +437,75 @@ def cpu_baseline(N, budget_s=15.0):
         if acc[0]:
             ch["state"], ch["E"] = cfg, E_new
         else:
-            ch["E"] = OP.total_energy(ch["state"], phys)[0]
+            ch["E"] = OP.total_energy_pairloop(ch["state"], phys)[0]
         steps += 1
     dt = time.perf_counter() - t0
+    torch.set_num_threads(prev)
     return {"value": steps / dt, "unit": "steps/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "cpus_available": avail, "omp_num_threads": cap, "cpu_model": _cpu_model(),
             "sample": f"{steps} nf_big_move steps (A1 flow, N={N}) over 4 chains incl. batched generation of "
-                      f"16 proposals, {dt:.1f} s wall on {threads} host threads ({os.cpu_count()} visible CPUs)"}
+                      f"16 proposals, {dt:.1f} s wall on {threads} host threads ({avail} CPUs available to the "
+                      f"process, {os.cpu_count()} visible, OMP_NUM_THREADS={cap}); energy by the reference's numpy "
+                      f"pair loop, log_prob by its torch-CPU float32 op sequence at batch 1"}
 
 
-def acceptance_match(bmc, stepper, n_chains=2048):
-    """Checker of the cpu_baseline leg (the metric's "acceptance-rate match"): one more
-    fused step of all chains, untimed, then the oracle's restatement of the reference
-    (oracle/, test infrastructure) re-derives the first n_chains decisions from the same
-    inputs: the old state (its NLL recomputed by the oracle), the cached old energy
-    (monte_carlo.py:243), the proposals the kernel made, and each chain's PCG64 state
-    before the step.  Reports both acceptance counts and the decisions that differ."""
+def acceptance_match(bmc, stepper, n_chains=2048, steps=10):
+    """Checker of the metric's "acceptance-rate match" (oracle/, test infrastructure):
+    `steps` more fused steps of all chains, untimed, then the oracle's restatement of
+    the reference replays the first n_chains chains through the same steps on its own:
+    the old state's energy and NLL recomputed from the state (monte_carlo.py:243-262),
+    then per step the kernel's proposals (both sides see the same float32 configs),
+    their energy and log q by the reference's float32 arithmetic, and each chain's own
+    PCG64 stream (draw only when ratio < 1, :284-287).  Reported: both acceptance
+    counts per step, the decisions that differ (a flip makes that chain's later inputs
+    differ: `chains_diverged`), and log q against the reference-order float32 value
+    (max, median, fraction beyond the north star's 1e-5) and, on a subset, both
+    float32 evaluations against the exact (float64) value."""
     from oracle import flow as OF
     from oracle import physics as OP
 
     N, S = bmc.N, min(n_chains, bmc.C)
     dims = OF.FlowDims(N=N, B=half_box(N), **A1)
     hw = bmc.phys.half_width
-    E0 = bmc.E_old[:S].cpu().numpy()
-    state0 = bmc.state[:S].cpu().numpy()
-    pcg0 = bmc.pcg[:S].cpu().numpy().view(np.uint64).copy()
-    stepper.step(timed=False)
+    phys = OP.make_phys(N)
     torch.cuda.synchronize()
-    cfg = stepper.config[:S].cpu().numpy().reshape(S, N, 2)
-    cen = stepper.centered[:S].cpu()
-    lq_gpu = stepper.log_q[:S].cpu().numpy().astype(np.float64)
-    acc = bmc.accept[:S].cpu().numpy().astype(bool)
+    state0 = bmc.state[:S].cpu().numpy()
+    f32 = bmc.state_is_f32[:S].cpu().numpy().astype(bool)
+    pcg = bmc.pcg[:S].cpu().numpy().view(np.uint64).copy()
+    rec = []
+    for _ in range(steps):
+        stepper.step(timed=False)
+        torch.cuda.synchronize()
+        rec.append((stepper.config[:S].cpu().numpy().reshape(S, N, 2), stepper.centered[:S].cpu().clone(),
+                    stepper.log_q[:S].cpu().numpy().astype(np.float64), bmc.accept[:S].cpu().numpy().astype(bool)))
     t0 = time.perf_counter()
     sd = {k: v.detach().cpu() for k, v in bmc.model.state_dict().items()}
-    E_new = OP.total_energy_batch(cfg, OP.make_phys(N))[0]
-    lq = OF.log_prob(sd, cen.clone(), dims).numpy().astype(np.float64)
-    x_old = torch.from_numpy((state0 - hw).astype(np.float32).reshape(S, -1))
-    nll_old = -OF.log_prob(sd, x_old, dims).numpy().astype(np.float64)
-    acc_o, _ = OP.mh_accept(E0, E_new, nll_old, -lq, pcg0)
-    acc_o = acc_o.astype(bool)
+    # the chain's running energy / NLL as the reference holds them: E of the state in its
+    # dtype (float32 after an accepted big move), -log q of fl32(state - half_width)
+    E = np.where(f32, OP.total_energy_batch(state0.astype(np.float32), phys)[0],
+                 OP.total_energy_batch(state0, phys)[0])
+    nll = -OF.log_prob(sd, torch.from_numpy((state0 - hw).astype(np.float32).reshape(S, -1)), dims).numpy() \
+        .astype(np.float64)
+    diverged = np.zeros(S, bool)
+    per_step, rels = [], []
+    for cfg, cen, lq_gpu, acc in rec:
+        E_new = OP.total_energy_batch(cfg, phys)[0]
+        lq = OF.log_prob(sd, cen.clone(), dims).numpy().astype(np.float64)
+        acc_o, _ = OP.mh_accept(E, E_new, nll, -lq, pcg)
+        acc_o = acc_o.astype(bool)
+        flips = acc != acc_o
+        per_step.append({"gpu_accepts": int(acc.sum()), "oracle_accepts": int(acc_o.sum()),
+                         "mismatched": int(flips.sum()), "mismatched_on_identical_inputs": int((flips & ~diverged).sum())})
+        diverged |= flips
+        E = np.where(acc_o, E_new, E)
+        nll = np.where(acc_o, -lq, nll)
+        fin = np.isfinite(lq)
+        rels.append(np.abs(lq_gpu[fin] - lq[fin]) / np.abs(lq[fin]))
+    rel = np.concatenate(rels)
     # both float32 evaluations against the exact value (the oracle in float64) on a subset
     S64 = min(256, S)
+    cen, lq_gpu = rec[-1][1], rec[-1][2]
+    lq = OF.log_prob(sd, cen[:S64].clone(), dims).numpy().astype(np.float64)
     sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
     lq64 = OF.log_prob(sd64, cen[:S64].double(), dims).numpy()
 
@@ -378,12 +513,36 @@ def acceptance_match(bmc, stepper, n_chains=2048):
         fin = np.isfinite(b)
         return float((np.abs(a[fin] - b[fin]) / np.abs(b[fin])).max()) if fin.any() else 0.0
 
-    return {"chains": S, "steps": 1, "gpu_accepts": int(acc.sum()), "oracle_accepts": int(acc_o.sum()),
-            "mismatched_decisions": int((acc != acc_o).sum()),
-            "max_rel_log_q_gpu_vs_oracle_f32": max_rel(lq_gpu, lq),
+    n = S * steps
+    ga = sum(p["gpu_accepts"] for p in per_step)
+    oa = sum(p["oracle_accepts"] for p in per_step)
+    return {"chains": S, "steps": steps, "decisions": n,
+            "gpu_acceptance_rate": ga / n, "oracle_acceptance_rate": oa / n,
+            "gpu_accepts": ga, "oracle_accepts": oa,
+            "mismatched_decisions": sum(p["mismatched"] for p in per_step),
+            "mismatched_on_identical_inputs": sum(p["mismatched_on_identical_inputs"] for p in per_step),
+            "chains_diverged": int(diverged.sum()), "per_step": per_step,
+            "log_q_vs_oracle_f32": {"rows": int(rel.size), "max_rel": float(rel.max()) if rel.size else 0.0,
+                                    "median_rel": float(np.median(rel)) if rel.size else 0.0,
+                                    "frac_beyond_1e-5": float((rel > 1e-5).mean()) if rel.size else 0.0},
+            "max_rel_log_q_gpu_vs_oracle_f32": float(rel.max()) if rel.size else 0.0,
             "max_rel_log_q_vs_f64": {"chains": S64, "gpu_f32": max_rel(lq_gpu[:S64], lq64),
-                                     "oracle_f32": max_rel(lq[:S64], lq64)},
+                                     "oracle_f32": max_rel(lq, lq64)},
             "oracle_s": time.perf_counter() - t0}
+
+
+def _launch_ranks(n):
+    """python -m torch.distributed.run --nproc-per-node n bench.py <same args>, on
+    127.0.0.1 and a free port; returns its exit code (rank 0 prints the JSON line)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -404,12 +563,24 @@ def main():
                     help="skip the secondary nf_big_move-equivalent measurement (supplied proposals)")
     ap.add_argument("--no-config2", action="store_true",
                     help="skip the secondary BASELINE config-2 line (N=16, 4096 chains)")
+    ap.add_argument("--no-config5", action="store_true",
+                    help="skip the secondary BASELINE config-5 line (Algorithm 2 cycle, A2 flow, N=64)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` outside a launcher: start the N rank processes here, as fresh
+        # children (nothing in this process has touched the GPU), and exit with their code
+        sys.exit(_launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = torch.cuda.device_count()
+    ndev = torch.cuda.device_count()  # counts devices without initialising them
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if args.backend == "nccl" and world > ndev:
+        print(f"bench.py: {world} ranks need {world} GPUs, {ndev} visible", file=sys.stderr)
+        sys.exit(2)
     local = local % max(1, ndev)  # rehearsal with more ranks than GPUs (gloo) shares devices
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -465,6 +636,8 @@ def main():
     mfpp = mfma_flops_per_pass(N, **A1)
     mfma_ach = 2 * mfpp * C / ((t_prop + t_lp) * 1e-3) / 1e12
     peak = PEAK_F32_TFLOPS if args.precision == "f32" else PEAK_BF16_TFLOPS / SPLIT_PRODUCTS[args.precision]
+    traffic, traffic_src = _pmc_traffic(C) if args.precision == "f32" else (None, None)
+    alg_bytes = flow_algorithmic_bytes(model, C, N)
     out = {
         "metric": "NF-proposed MH steps/sec, N=64 2D LJ, 65536 chains; acceptance-rate match",
         "value": value,
@@ -488,7 +661,9 @@ def main():
                         "deltaF_mean_sem": parallel.free_energy_stats(table)[:2]},
         "kernel_ms": {"flow_propose": t_prop, "flow_log_prob": t_lp, "energy": t_en, "mh_accept": t_acc},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                     "frac": achieved / peak, "traffic": _pmc_traffic() if args.precision == "f32" else None,
+                     "frac": achieved / peak, "traffic": traffic,
+                     "traffic_source": traffic_src, "algorithmic_bytes_per_launch": alg_bytes,
+                     "traffic_over_algorithmic": traffic / alg_bytes if traffic else None,
                      "kernel": "flow_pass_kernel<256,32,*> (propose + log_prob)",
                      "algorithmic_flop_per_launch": fpp * C,
                      # what the matrix cores actually execute (the derivative logits are
@@ -512,6 +687,8 @@ def main():
         out["given_proposal"] = given_proposal(bmc, stepper)
     if world == 1 and not args.no_config2:
         out["config2"] = config2()
+    if world == 1 and not args.no_config5:
+        out["config5"] = config5()
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
         # vs_baseline stays null: BASELINE.md has no published number for this metric

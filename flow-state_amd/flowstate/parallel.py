@@ -50,6 +50,21 @@ def all_reduce_stats(hist, well_totals, group=None):
     return hist, well_totals
 
 
+def final_reduction(bmc, group=None, bins=100):
+    """End-of-run reduction of a sharded run: the density histogram of
+    the current states (utils.py:488-495) and the well-occupancy totals (utils.py:61-101)
+    all-reduced over the group, and the per-chain counters (all-in-A, all-in-B, samples,
+    accepted, attempts) all-gathered in rank order.  Returns (hist (bins-1, bins-1),
+    wells (3,), table (world*C, 5)), all int64 on the engine's device."""
+    hist = bmc.histogram2d(bins)
+    per_chain = bmc.well_counts()
+    wells = per_chain.sum(dim=0)
+    all_reduce_stats(hist, wells, group=group)
+    table = gather_chain_counters(torch.cat([per_chain, bmc.accepted[:, None], bmc.attempts[:, None]], 1),
+                                  group=group)
+    return hist, wells, table
+
+
 def allreduce_gradients(model, group=None, bucket_bytes=64 << 20):
     """Average the gradients of `model` over the group (Algorithm 2 data-parallel
     training): gradients are flattened into buckets of at most

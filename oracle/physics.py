@@ -131,6 +131,59 @@ def total_energy_batch(pos, phys):
     return E, W, ov
 
 
+def total_energy_pairloop(pos, phys):
+    """calculate_total_energy_virial exactly as the reference runs it on the CPU
+    (energy_calculator.py:121-203): for each row i a Python loop over the pairs j > i
+    (SimulationBox.compute_distances, simulation_box.py:31-65: per-pair minimum_image
+    with np.round and np.linalg.norm), the hard-core early return (:150-153),
+    lennard_jones_energy_virial on the row (potential.py:3-29) summed into Python
+    floats, then the double well over all particles (potential.py:55-116).  Numpy
+    scalar code, one chain per call: the timed CPU baseline of bench.py (the C
+    restatement above is the parity checker)."""
+    pos = np.asarray(pos)
+    # the box sizes are numpy float64 in the reference (np.sqrt in initialise_fcc), so a
+    # float32 state's wrap runs in float64 (numpy 2 promotion)
+    Lx, Ly = np.float64(phys.Lx), np.float64(phys.Ly)
+    N = pos.shape[0]
+    rc = phys.r_cut
+    e_cut = 4.0 * ((1.0 / rc) ** 6 * (1.0 / rc) ** 6 - (1.0 / rc) ** 6)
+    E = 0.0
+    W = 0.0
+    for i in range(N - 1):
+        others = pos[i + 1:]
+        r = np.zeros(len(others))
+        for j, q in enumerate(others):
+            d = pos[i] - q
+            d[0] -= Lx * np.round(d[0] / Lx)
+            d[1] -= Ly * np.round(d[1] / Ly)
+            r[j] = np.linalg.norm(d)
+        if np.any(r < phys.r_core):
+            return float("inf"), float("inf")
+        e = np.zeros_like(r)
+        w = np.zeros_like(r)
+        m = r <= rc
+        sr6 = (1.0 / r[m]) ** 6
+        sr12 = sr6 * sr6
+        e[m] = 4.0 * (sr12 - sr6)
+        w[m] = 48.0 * (sr12 - 0.5 * sr6)
+        e[m] -= e_cut
+        E += np.sum(e)
+        W += np.sum(w)
+    if phys.num_wells > 0:
+        x, y = pos[:, 0], pos[:, 1]
+        centres = [[Lx / 4, Ly / 2]] + ([[3 * Lx / 4, Ly / 2]] if phys.num_wells == 2 else [])
+        V = np.zeros_like(x, dtype=np.float64)
+        for i, c in enumerate(np.array(centres)):
+            dx = x - c[0]
+            dy = y - c[1]
+            dx -= Lx * np.round(dx / Lx)
+            dy -= Ly * np.round(dy / Ly)
+            rr = np.sqrt(dx ** 2 + dy ** 2)
+            V += phys.V0[i] * (1 - 0.5 * (1 + np.tanh(phys.k * (rr - phys.r0))))
+        E += V.sum()
+    return E, W
+
+
 def min_image_dist(pos, i, j, phys):
     pos = np.ascontiguousarray(pos)
     return lib().oracle_min_image_dist(_ptr(pos), int(pos.dtype == np.float32), i, j,

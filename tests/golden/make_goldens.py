@@ -21,6 +21,9 @@ Fixtures:
   judge_trace.npz   reference judge_normalizing_flow / bulk_judge_normalizing_flow /
                     metropolis_acceptance_particle_move on a scripted op sequence
                     (with nf_big_move after a bulk judge), results + energies + PCG64
+  flow_a1.npz       reference log_prob (float32, and the same model in float64) at the
+                    headline flow A1, N=64, with bench.synthetic_model's weights (checksum
+                    only), on uniform rows and flow samples prepared as nf_big_move does
   box_trace.npz     reference SimulationBox.minimum_image / compute_distance(s) and
                     EnergyCalculator.calculate_particle_energy_virial outputs
 """
@@ -251,6 +254,51 @@ def mh_trace_case(NF, MC, SimulationBox):
         out[f"N{N}_checksum"] = np.frombuffer(bytes.fromhex(sd_checksum(sd)), dtype=np.uint8)
         out[f"N{N}_chains"] = np.int64(chains)
     np.savez_compressed(os.path.join(HERE, "mh_trace.npz"), **out)
+
+
+def a1_case(NF, nrows=32):
+    """The headline flow (A1: L=15, H=256, 32 blocks, K=32; main_algorithm_1.py:59-67,
+    281-283) at N=64, with the bench's own synthetic weights (bench.synthetic_model:
+    reference init order under torch.manual_seed(0), perturbed final layers and
+    unconditional splines), loaded into the REFERENCE NormalizingFlow.  353 MB of
+    weights are not committed: the fixture holds their checksum, and the test rebuilds
+    them with the same recipe.  Rows: half uniform in the box, half flow samples (the
+    class the bench's proposals belong to), the latter prepared as the MH step feeds
+    them to the flow: config = fl32(x + HALF_BOX) (main_algorithm_1.py:340-343), then
+    fl32(config - half_width) (monte_carlo.py:251-258).  Outputs: the reference's
+    float32 log_prob, and the same reference model in float64 (the exact value the two
+    float32 evaluations are measured against)."""
+    import bench
+    N = 64
+    B = bench.half_box(N)
+    sd = bench.synthetic_model(N, "cpu").state_dict()
+    from oracle import flow as OF
+    dims = OF.FlowDims(N=N, B=B, **bench.A1)
+    model = build_ref_model(NF, dims)
+    model.load_state_dict(sd, strict=True)
+    model.eval()
+    g = torch.Generator().manual_seed(2024)
+    half = nrows // 2
+    hw = float(np.sqrt(N / 0.03)) / 2  # MonteCarlo.half_width = box_x / 2 (monte_carlo.py:66)
+    with torch.no_grad():
+        xu = (torch.rand((half, dims.D), generator=g) * 2 - 1) * B
+        z = (torch.rand((half, dims.D), generator=g) * 2 - 1) * B
+        xs = z.clone()
+        for f in model.flows:
+            xs, _ = f(xs)
+        cfg = xs.numpy() + B                              # float32 array + Python float -> float32
+        cen = (cfg.astype(np.float64) - np.float64(hw)).astype(np.float32)
+        x = torch.cat([xu, torch.from_numpy(cen)])
+        lp = model.log_prob(x.clone())
+        m64 = build_ref_model(NF, dims)
+        m64.load_state_dict(sd, strict=True)
+        m64 = m64.double().eval()
+        lp64 = m64.log_prob(x.clone().double())
+    out = dict(N=N, B=B, checksum=np.frombuffer(bytes.fromhex(sd_checksum(sd)), dtype=np.uint8),
+               x=x.numpy(), n_uniform=half, log_prob=lp.numpy(), log_prob_f64=lp64.numpy())
+    np.savez_compressed(os.path.join(HERE, "flow_a1.npz"), **out)
+    rel = (lp.double() - lp64).abs() / lp64.abs()
+    print(f"flow_a1: log_prob[:2]={lp[:2].tolist()} ref f32 vs f64 max rel {float(rel.max()):.3g}")
 
 
 def init_case(NF):
@@ -871,6 +919,10 @@ def main(only=None):
     if only == "box":
         box_case(MC)
         return
+    if only == "a1":
+        torch.set_num_threads(8)
+        a1_case(NF)
+        return
     flow_case(NF, "tiny", OF.FlowDims(N=4, L=2, H=32, nb=1, K=5, B=OF.half_box(4)), 1, 64, True)
     flow_case(NF, "n16", OF.FlowDims(N=16, L=3, H=64, nb=2, K=8, B=OF.half_box(16)), 2, 48, False)
     flow_case(NF, "n64", OF.FlowDims(N=64, L=2, H=128, nb=2, K=32, B=OF.half_box(64)), 3, 16, False)
@@ -886,6 +938,8 @@ def main(only=None):
     train_cycle_case(NF)
     judge_case(NF, MC)
     box_case(MC)
+    torch.set_num_threads(8)
+    a1_case(NF)
 
 
 if __name__ == "__main__":

@@ -77,3 +77,105 @@ def test_update_cycle_refeeds_with_trained_weights():
     fresh.eval()
     x = (bmc.state - phys.half_width).to(torch.float32).reshape(runs, -1)
     torch.testing.assert_close(bmc.nll_old, -fresh.log_prob(x).double(), rtol=0, atol=0)
+
+
+def test_config5_cycle_at_reference_sizes():
+    """BASELINE config 5's cycle at the reference's sizes (main_algorithm_2.py:33-52,
+    393-577): A2 flow (L=23, H=128, 2 blocks, K=15), N=64, NUM_MC_RUNS=100,
+    UPDATE_NUM_SAMPLES=1000 (100 local moves per run, sample() every 10), one epoch of
+    batch 256 (3 full batches + 1 of 232), ALPHA=1, then the refeed.
+    Checked: the epoch's invariants (every BatchNorm counted 2 forwards per step, as the
+    reference's forward_kld + reverse_kld in train mode; 4 Adam steps; parameters moved
+    and finite) and the graphed epoch against the eager one from the same start; then
+    all 100 refeed decisions against the oracle's restatement of nf_big_move with the
+    trained weights (old NLL re-derived from the moved states, the running energy of the
+    local moves in the ratio, the kernel's own proposals, each run's PCG64 stream), the
+    energies a reject writes back, and the cached NLL."""
+    from flowstate.MCMC import initialise_fcc
+    from flowstate.models import A2, build_flow, half_box
+    from oracle import physics as OP
+
+    N, runs = 64, 100
+    torch.manual_seed(0)
+    B = half_box(N)
+    m = build_flow(N, bound=B, device="cpu", **A2)
+    m.p = DoubleWellLJ(2 * N, N, 1.0, B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+    m = m.cuda()
+    m.q0.device = torch.device("cuda", torch.cuda.current_device())
+    base, box = initialise_fcc(num_particles=N, rho=0.03, aspect_ratio=1.0)
+    phys = Physics(box.box_size_x, box.box_size_y)
+    bmc = BatchedMonteCarlo(None, np.repeat(base[None], runs, 0), phys, [42 + i for i in range(runs)],
+                            device="cuda", initial_max_displacement=0.65)
+    bmc.local_moves(10 * N, adjust_every=5 * N)
+    a = Algorithm2(bmc, m, batch_size=256, alpha=1.0, sampling_frequency=10, update_num_samples=1000)
+    assert a.production_runs == 100
+    a.production()
+    assert a.training_data.shape == (1000, 2 * N)
+
+    # --- training epoch: invariants + graphed vs eager from the same start
+    twin = build_flow(N, bound=B, device="cpu", **A2)
+    twin.p = DoubleWellLJ(2 * N, N, 1.0, B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+    twin = twin.cuda()
+    twin.load_state_dict(m.state_dict())
+    twin.q0.device = m.q0.device
+    before = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    torch.manual_seed(5)
+    loss = a.train()
+    assert np.isfinite(loss)
+    assert int(a._step.opt.state[a._step._flat_param]["step"].item()) == 4
+    sd = m.state_dict()
+    for k, v in sd.items():
+        if k.endswith("num_batches_tracked"):
+            assert int(v) - int(before[k]) == 2 * 4, k
+        elif v.is_floating_point():
+            assert torch.isfinite(v).all(), k
+    moved = [k for k in sd if "final_layer.weight" in k and not torch.equal(sd[k], before[k])]
+    assert len(moved) == len(m.flows)
+    b2 = Algorithm2(type("E", (), {"C": runs})(), twin, batch_size=256, alpha=1.0, graphed=False)
+    b2.training_data = a.training_data
+    torch.manual_seed(5)
+    loss2 = b2.train()
+    np.testing.assert_allclose(loss, loss2, rtol=1e-4)
+    for k, v in twin.state_dict().items():
+        if "running" in k or not v.is_floating_point():
+            continue
+        step = (sd[k] - before[k]).norm().item()
+        assert (v - sd[k]).norm().item() <= 3e-2 * step + 1e-6, k
+
+    # --- refeed against the oracle
+    hw = phys.half_width
+    state0 = bmc.state.cpu().numpy()
+    f32 = bmc.state_is_f32.cpu().numpy().astype(bool)
+    E_run = bmc.E_old.cpu().numpy().copy()
+    pcg = bmc.pcg.cpu().numpy().view(np.uint64).copy()
+    acc, p = a.refeed()
+    torch.cuda.synchronize()
+    bmc.check_errors()
+    cfg = bmc.last_proposals().cpu().numpy()
+    acc = acc.cpu().numpy().astype(bool)
+    E_after = bmc.E_old.cpu().numpy()
+    nll_after = bmc.nll_old.cpu().numpy()
+    sd_cpu = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    dims = OF.FlowDims(N=N, B=B, **A2)
+    ophys = OP.make_phys(N)
+    nll_old = -OF.log_prob(sd_cpu, torch.from_numpy((state0 - hw).astype(np.float32).reshape(runs, -1)),
+                           dims).numpy().astype(np.float64)
+    lq = OF.log_prob(sd_cpu, torch.from_numpy((cfg.astype(np.float64) - hw).astype(np.float32).reshape(runs, -1)),
+                     dims).numpy().astype(np.float64)
+    E_new = OP.total_energy_batch(cfg, ophys)[0]
+    acc_o, u = OP.mh_accept(E_run, E_new, nll_old, -lq, pcg.copy())
+    acc_o = acc_o.astype(bool)
+    with np.errstate(over="ignore", invalid="ignore", divide="ignore"):
+        log_ratio = -(E_new - E_run) - (-lq - nll_old)
+        border = (log_ratio < 0) & (np.abs(np.log(u) - log_ratio) < 1e-2)
+    assert ((acc == acc_o) | border).all(), (np.flatnonzero(acc != acc_o), border.sum())
+    assert border.sum() <= 2
+    E_state = np.where(f32, OP.total_energy_batch(state0.astype(np.float32), ophys)[0],
+                       OP.total_energy_batch(state0, ophys)[0])
+    want_E = np.where(acc, E_new, E_state)
+    fin = np.isfinite(want_E)
+    assert np.array_equal(np.isfinite(E_after), fin)
+    np.testing.assert_allclose(E_after[fin], want_E[fin], rtol=1e-12)
+    want_nll = np.where(acc, -lq, nll_old)
+    np.testing.assert_allclose(nll_after, want_nll, rtol=1e-5, atol=1e-4)
+    assert p == acc.mean()
