@@ -164,6 +164,69 @@ def given_proposal(bmc, stepper, steps=3):
             "what": "energy + density pass + accept of supplied float32 proposals (proposal generation excluded)"}
 
 
+def single_pass(bmc, stepper, steps=3, n_chains=2048):
+    """SURVEY §7 option (i), opt-in (FS_MH_SINGLE_PASS), never the headline: the
+    proposals' log q taken from the sampling pass's own log-dets (log q0(z) - sum of
+    log|dx/dz|, core.py:178-196 with the log-dets kept) instead of the reference's
+    second, density-direction pass over fl32(config - half_width) (monte_carlo.py:
+    251-262), so one flow pass per step.  Reports: the deviation from the density-pass
+    value on one full batch of proposals (all chains), fused single-pass steps/s on the
+    same chains, and one step's decisions on the first n_chains chains against the
+    oracle's restatement of the reference (which evaluates log q with the second pass)."""
+    from oracle import flow as OF
+    from oracle import physics as OP
+
+    L, p, st = _lib.load(), _lib.ptr, _lib.stream_ptr()
+    C, N, hw = bmc.C, bmc.N, bmc.phys.half_width
+    lq1 = torch.empty(C, dtype=torch.float32, device=bmc.device)
+    _lib.check(L.fs_flow_propose_lq(stepper.dims, p(stepper.packed), C, bmc.proposal_seed, bmc.step_count + 10 ** 6,
+                                    bmc.chain_offset, hw, p(stepper.config), p(stepper.centered), None, p(lq1),
+                                    p(bmc.err), st))
+    _lib.check(L.fs_flow_log_prob(stepper.dims, p(stepper.packed), p(stepper.centered), C, p(stepper.log_q), None,
+                                  p(bmc.err), st))
+    a, b = lq1.double(), stepper.log_q.double()
+    fin = torch.isfinite(b) & torch.isfinite(a)
+    rel = ((a - b).abs() / b.abs())[fin]
+    acc_rel = {"rows": int(fin.sum().item()), "max_rel": float(rel.max().item()),
+               "median_rel": float(rel.median().item()), "frac_beyond_1e-5": float((rel > 1e-5).double().mean().item())}
+    bmc.single_pass_log_q = True
+    try:
+        bmc.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            bmc.step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        S = min(n_chains, C)
+        state0 = bmc.state[:S].cpu().numpy()
+        f32 = bmc.state_is_f32[:S].cpu().numpy().astype(bool)
+        pcg = bmc.pcg[:S].cpu().numpy().view(np.uint64).copy()
+        bmc.step()
+        torch.cuda.synchronize()
+        cfg = bmc.last_proposals()[:S].cpu().numpy()
+        acc = bmc.accept[:S].cpu().numpy().astype(bool)
+    finally:
+        bmc.single_pass_log_q = False
+    bmc.check_errors()
+    sd = {k: v.detach().cpu() for k, v in bmc.model.state_dict().items()}
+    dims = OF.FlowDims(N=N, B=half_box(N), **A1)
+    phys = OP.make_phys(N)
+    E = np.where(f32, OP.total_energy_batch(state0.astype(np.float32), phys)[0], OP.total_energy_batch(state0, phys)[0])
+    nll = -OF.log_prob(sd, torch.from_numpy((state0 - hw).astype(np.float32).reshape(S, -1)), dims).numpy() \
+        .astype(np.float64)
+    lq = OF.log_prob(sd, torch.from_numpy((cfg.astype(np.float64) - hw).astype(np.float32).reshape(S, -1)),
+                     dims).numpy().astype(np.float64)
+    acc_o, _ = OP.mh_accept(E, OP.total_energy_batch(cfg, phys)[0], nll, -lq, pcg)
+    acc_o = acc_o.astype(bool)
+    return {"value": C * steps / dt, "unit": "steps/s", "steps": steps, "ms_per_step": dt / steps * 1e3,
+            "log_q_vs_density_pass": acc_rel,
+            "decisions_vs_oracle": {"chains": S, "gpu_accepts": int(acc.sum()), "oracle_accepts": int(acc_o.sum()),
+                                    "mismatched": int((acc != acc_o).sum())},
+            "what": "opt-in FS_MH_SINGLE_PASS: log q(x') from the sampling pass (one flow pass per step); "
+                    "not the reference's semantics"}
+
+
 def decorrelate(bmc):
     """SURVEY §8(d) synthetic states: 10 N local moves per chain on its PCG64 stream
     (default_rng(42 + i)) away from the lattice, then one big move, which re-derives the
@@ -563,6 +626,8 @@ def main():
                     help="skip the secondary nf_big_move-equivalent measurement (supplied proposals)")
     ap.add_argument("--no-config2", action="store_true",
                     help="skip the secondary BASELINE config-2 line (N=16, 4096 chains)")
+    ap.add_argument("--no-single-pass", action="store_true",
+                    help="skip the secondary measurement of the opt-in single-pass log q mode")
     ap.add_argument("--no-config5", action="store_true",
                     help="skip the secondary BASELINE config-5 line (Algorithm 2 cycle, A2 flow, N=64)")
     args = ap.parse_args()
@@ -683,6 +748,8 @@ def main():
         out["acceptance_match"] = acceptance_match(bmc, stepper)
     if world == 1 and not args.no_alt_precision and args.precision == "f32":
         out["alt_precision"] = alt_precisions(bmc, stepper)
+    if world == 1 and not args.no_single_pass and args.precision == "f32":
+        out["single_pass"] = single_pass(bmc, stepper)
     if world == 1 and not args.no_given_proposal:
         out["given_proposal"] = given_proposal(bmc, stepper)
     if world == 1 and not args.no_config2:

@@ -111,6 +111,17 @@ int fs_flow_propose(const fs_flow_dims *d, const void *packed, int64_t B, uint64
                   "fs_flow_propose");
 }
 
+int fs_flow_propose_lq(const fs_flow_dims *d, const void *packed, int64_t B, uint64_t seed, uint64_t counter,
+                       int64_t row_offset, double half_width, float *config, float *centered, float *x_out,
+                       float *log_q, int32_t *err, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    REQUIRE(B >= 0 && (B == 0 || (packed && log_q)), "fs_flow_propose_lq: invalid arguments");
+    return hip_rc(fs_flow_pass_impl(d, packed, 2, nullptr, B, x_out, log_q, 1, config, centered, seed, counter,
+                                    row_offset, half_width, err, (hipStream_t)stream),
+                  "fs_flow_propose_lq");
+}
+
 int fs_energy_lj_dw(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int32_t N, double *E, double *W,
                     uint8_t *overlap, uint64_t *nbr, void *stream) {
     REQUIRE(p && C >= 0 && (C == 0 || (pos && E)), "fs_energy_lj_dw: invalid arguments");
@@ -205,18 +216,24 @@ int fs_nf_mh_step(const fs_flow_dims *d, const void *packed, const fs_phys *p, i
     hipStream_t st = (hipStream_t)stream;
     const double half_width = p->Lx / 2.0;  // MonteCarlo.half_width (monte_carlo.py:66)
     const bool hybrid = (flags & FS_MH_HYBRID) != 0;
+    const bool single = (flags & FS_MH_SINGLE_PASS) != 0;
     REQUIRE(!hybrid || state, "fs_nf_mh_step: FS_MH_HYBRID needs the state");
-    hipError_t e = fs_flow_pass_impl(d, packed, 2, nullptr, C, nullptr, nullptr, 0, config, centered, seed, step,
-                                     chain_offset, half_width, err, st);
+    hipError_t e = fs_flow_pass_impl(d, packed, 2, nullptr, C, nullptr, single ? log_q : nullptr, single ? 1 : 0,
+                                     config, centered, seed, step, chain_offset, half_width, err, st);
     if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/propose");
     if (hybrid) {  // the state moved since nll_old / E_old were exact: re-derive both
         e = fs_center_impl(state, C * D, half_width, centered_old, st);
         if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/center");
     }
     // log q of the proposals and (hybrid) of the current states: one density launch over
-    // C or 2C rows (the rows are independent, so a small C gets twice the workgroups)
-    e = fs_flow_pass_impl(d, packed, 0, centered, hybrid ? 2 * C : C, nullptr, log_q, 1, nullptr, nullptr, 0, 0, 0,
-                          0.0, err, st);
+    // C or 2C rows (the rows are independent, so a small C gets twice the workgroups);
+    // with FS_MH_SINGLE_PASS the proposals' log q came from the propose launch
+    if (!single)
+        e = fs_flow_pass_impl(d, packed, 0, centered, hybrid ? 2 * C : C, nullptr, log_q, 1, nullptr, nullptr, 0, 0,
+                              0, 0.0, err, st);
+    else if (hybrid)
+        e = fs_flow_pass_impl(d, packed, 0, centered_old, C, nullptr, log_q_old, 1, nullptr, nullptr, 0, 0, 0, 0.0,
+                              err, st);
     if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/log_prob");
     e = fs_energy_impl(p, config, 1, C, d->N, E_new, W_new, nullptr, nullptr, st);
     if (e != hipSuccess) return hip_rc(e, "fs_nf_mh_step/energy");
@@ -284,6 +301,7 @@ int fs_nf_mh_steps(const fs_flow_dims *d, const void *packed, const fs_phys *p, 
     REQUIRE(p && C >= 0 && S >= 1 && (C == 0 || (packed && E_old && nll_old && pcg && accept && ws)),
             "fs_nf_mh_steps: invalid arguments");
     REQUIRE(!(flags & FS_MH_HYBRID), "fs_nf_mh_steps: FS_MH_HYBRID needs one step at a time (fs_nf_mh_step)");
+    REQUIRE(!(flags & FS_MH_SINGLE_PASS), "fs_nf_mh_steps: FS_MH_SINGLE_PASS is a flag of fs_nf_mh_step");
     REQUIRE(((uintptr_t)ws & 255) == 0, "fs_nf_mh_steps: workspace must be 256-byte aligned");
     if (C == 0) return FS_OK;
     const int64_t D = 2 * d->N;
@@ -418,6 +436,16 @@ int fs_rqs_backward(int64_t M, int32_t K, int32_t inverse, const float *x, const
     return hip_rc(fs_rqs_backward_impl(M, K, inverse, x, uw, uh, ud, (float)tail_bound, g_out, g_lad, gx, guw, guh,
                                        gud, (hipStream_t)stream),
                   "fs_rqs_backward");
+}
+
+int fs_target_energy(const float *x, int64_t B, int32_t N, double bound, double temperature, int32_t num_wells,
+                     double V0_0, double V0_1, double r0, double k, float *E, float *grad_x, void *stream) {
+    REQUIRE(B >= 0 && N >= 1 && N <= 1024 && bound > 0.0 && temperature > 0.0 && num_wells >= 0 && num_wells <= 2 &&
+                (B == 0 || (x && E)),
+            "fs_target_energy: invalid arguments");
+    return hip_rc(fs_target_energy_impl(x, B, N, bound, temperature, num_wells, V0_0, V0_1, r0, k, E, grad_x,
+                                        (hipStream_t)stream),
+                  "fs_target_energy");
 }
 
 int fs_classify_wells(const void *pos, int pos_is_f32, int64_t M, int32_t N, double half_box, double r0,

@@ -665,6 +665,9 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
             }
             outv = tot + (inb ? a.base_lp : -INFINITY);
         }
+        // single-pass log q (FS_MH_SINGLE_PASS): log q(x') = log q0(z) - sum of the sampling
+        // direction's log|dx/dz| (base draws are inside the bound by construction)
+        if (MODE == MODE_PROPOSE && a.add_base) outv = a.base_lp - tot;
         if (row_valid && a.scalar_out) a.scalar_out[row0 + lane] = outv;
     }
     for (int e = tid; e < kRows * D; e += kThreads) {

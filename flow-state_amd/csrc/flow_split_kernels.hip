@@ -533,6 +533,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_split_kernel(FlowArgs a) {
             }
             outv = tot + (inb ? a.base_lp : -INFINITY);
         }
+        if (MODE == MODE_PROPOSE && a.add_base) outv = a.base_lp - tot;  // FS_MH_SINGLE_PASS
         if (row_valid && a.scalar_out) a.scalar_out[row0 + lane] = outv;
     }
     for (int e = tid; e < kRows * D; e += kThreads) {

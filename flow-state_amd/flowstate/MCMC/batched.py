@@ -91,8 +91,13 @@ def default_proposal_seed(seeds, chain_offset=0):
 class BatchedMonteCarlo:
     def __init__(self, model, particles, physics, seeds, device=None, proposal_seed=None,
                  correct_sign=False, state_is_f32=None, chain_offset=0, initial_max_displacement=0.5,
-                 target_acceptance=0.5):
+                 target_acceptance=0.5, single_pass_log_q=False):
+        """single_pass_log_q: opt-in, not the reference's semantics (FS_MH_SINGLE_PASS):
+        step() takes the proposals' log q from the sampling pass's own log-dets instead of
+        the reference's second (density) pass over fl32(config - half_width), one flow
+        pass per step instead of two, always one fused step per launch."""
         self.model = None
+        self.single_pass_log_q = bool(single_pass_log_q)
         self.phys = physics
         if device is None:
             device = next(model.parameters()).device if model is not None else "cuda"
@@ -195,7 +200,7 @@ class BatchedMonteCarlo:
         st = _lib.stream_ptr()
         done = 0
         while done < n:
-            fill = self.steps_per_launch()
+            fill = 1 if self.single_pass_log_q else self.steps_per_launch()
             same_flow = self._last_packed is not None and self._last_packed() is packed
             if fill > 1 and (self._bank_covers(packed) or (same_flow and (self._moved or n - done == 1))):
                 # a small batch stepped one step at a time with the flow unchanged since
@@ -226,7 +231,8 @@ class BatchedMonteCarlo:
                                            _lib.ptr(self.W_old), _lib.ptr(self.nll_old), _lib.ptr(self.pcg),
                                            _lib.ptr(self.state), _lib.ptr(self.state_is_f32), _lib.ptr(self.accept),
                                            _lib.ptr(self.attempts), _lib.ptr(self.accepted), _lib.ptr(self.n_accept),
-                                           _lib.ptr(self.err), self.flags | (_lib.FS_MH_HYBRID if self._moved else 0),
+                                           _lib.ptr(self.err), self.flags | (_lib.FS_MH_HYBRID if self._moved else 0)
+                                           | (_lib.FS_MH_SINGLE_PASS if self.single_pass_log_q else 0),
                                            _lib.ptr(self._workspace()), st), "fs_nf_mh_step")
                 self._last_src = (self._ws, self.C, 0)
             else:

@@ -16,6 +16,7 @@ _lib = None
 
 FS_MH_CORRECT_SIGN = 1
 FS_MH_HYBRID = 2
+FS_MH_SINGLE_PASS = 4
 
 
 class FlowDims(ctypes.Structure):
@@ -57,6 +58,8 @@ _SIGS = {
     "fs_flow_forward": (ctypes.c_int, [_D, _P, _P, _I64, _P, _P, _P, _P]),
     "fs_flow_propose": (ctypes.c_int, [_D, _P, _I64, ctypes.c_uint64, ctypes.c_uint64, _I64, ctypes.c_double,
                                        _P, _P, _P, _P, _P]),
+    "fs_flow_propose_lq": (ctypes.c_int, [_D, _P, _I64, ctypes.c_uint64, ctypes.c_uint64, _I64, ctypes.c_double]
+                           + [_P] * 5 + [_P]),
     "fs_energy_lj_dw": (ctypes.c_int, [_PH, _P, ctypes.c_int, _I64, ctypes.c_int32, _P, _P, _P, _P, _P]),
     "fs_pcg64_seed": (ctypes.c_int, [_P, _I64, _P, _P]),
     "fs_pcg64_random": (ctypes.c_int, [_P, _I64, _P, _P]),
@@ -92,6 +95,8 @@ _SIGS = {
     "fs_coupling_features_bwd": (ctypes.c_int, [_CP] + [_P] * 5),
     "fs_coupling_sample_pre": (ctypes.c_int, [_CP] + [_P] * 9),
     "fs_coupling_sample_post": (ctypes.c_int, [_CP] + [_P] * 7),
+    "fs_target_energy": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_int32]
+                         + [ctypes.c_double] * 4 + [_P, _P, _P]),
     "fs_classify_wells": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
                                           _P, _P, _P, _P]),
     "fs_pair_hist": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, _P, ctypes.c_int32,

@@ -64,6 +64,37 @@ class SimpleLJ(nn.Module):
         return en.sum(dim=1) / self.temperature
 
 
+class _TargetEnergy(torch.autograd.Function):
+    """DoubleWellLJ._energy on the device: fs_target_energy (csrc/target_kernels.hip), one
+    launch for the energy and, when x needs a gradient, dE/dx (saved for the backward,
+    which is one multiply).  Replaces the ~40 torch kernels of the restatement below
+    (pairwise distance matrix, triu gather, where, pow, Python-looped wells)."""
+
+    @staticmethod
+    def forward(ctx, x, mod):
+        from .. import _lib
+
+        x = x.contiguous()
+        B, D = x.shape
+        N = mod._n_particles
+        E = torch.empty(B, dtype=torch.float32, device=x.device)
+        g = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        V0 = [float(v) for v in mod.V0_list.tolist()]
+        with _lib.on_device(x):
+            _lib.require_device(x)
+            _lib.check(_lib.load().fs_target_energy(_lib.ptr(x), B, N, float(mod.bound), float(mod.temperature), 2,
+                                                   V0[0], V0[1], float(mod.r0), float(mod.k), _lib.ptr(E),
+                                                   _lib.ptr(g), _lib.stream_ptr()), "fs_target_energy")
+        if g is not None:
+            ctx.save_for_backward(g)
+        return E
+
+    @staticmethod
+    def backward(ctx, gE):
+        (g,) = ctx.saved_tensors
+        return gE[:, None].to(g.dtype) * g, None
+
+
 class DoubleWellLJ(SimpleLJ):
     """SimpleLJ + the two-well external potential (reference: Energy/SimpleLJ.py:44-130),
     wells at (-bound/2, 0) and (bound/2, 0) in the centred frame."""
@@ -106,5 +137,13 @@ class DoubleWellLJ(SimpleLJ):
         return Vp.sum(dim=1)
 
     def _energy(self, x):
+        """Device float32 samples of the flow's dimension: the HIP kernel (energy and
+        gradient); anything else (CPU tensors, other dtypes): the torch restatement."""
+        if x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] == self._dim \
+                and self._dim == 2 * self._n_particles and len(self.V0_list) == 2:
+            return _TargetEnergy.apply(x, self)
+        return self._energy_torch(x)
+
+    def _energy_torch(self, x):
         lj = super()._energy(x)
         return lj + self.double_well_potential(x.view(x.shape[0], self._n_particles, self._n_dimensions))

@@ -121,6 +121,14 @@ int fs_flow_propose(const fs_flow_dims *d, const void *packed, int64_t B, uint64
                     uint64_t counter, int64_t row_offset, double half_width, float *config,
                     float *centered, float *x_out, int32_t *err, void *stream);
 
+/* fs_flow_propose that also writes log_q [B] = log q(x') from the sampling pass itself
+ * (log q0(z) minus the sampling direction's summed log|dx/dz|, NormalizingFlow.sample
+ * with its log-dets kept, core.py:178-196): the single-pass value of FS_MH_SINGLE_PASS.
+ * The reference instead evaluates log_prob on `centered` with a second pass. */
+int fs_flow_propose_lq(const fs_flow_dims *d, const void *packed, int64_t B, uint64_t seed,
+                       uint64_t counter, int64_t row_offset, double half_width, float *config,
+                       float *centered, float *x_out, float *log_q, int32_t *err, void *stream);
+
 /* ------------------------------------------------------------------ */
 /* Physics (MCMC/)                                                     */
 /* ------------------------------------------------------------------ */
@@ -173,6 +181,14 @@ int fs_pcg64_random(uint64_t *state, int64_t C, double *out, void *stream);
  * still uses the running E_old, :243), and on reject the total energy recomputed
  * from the current state (:299-301). */
 #define FS_MH_HYBRID 2
+/* flags bit2 (fs_nf_mh_step only; opt-in, never the reference's semantics): take the
+ * proposals' log q from the sampling pass itself, log q(x') = log q0(z) - sum of the
+ * sampling direction's log|dx/dz| (core.py:178-196 run with its log-dets kept), instead
+ * of the reference's second, density-direction pass over fl32(config - half_width)
+ * (monte_carlo.py:251-262).  One flow pass per step instead of two; the value differs
+ * from the reference's by the two passes' float32 noise and the box-coordinate
+ * rounding of x' (bench.py `single_pass` reports the deviation and the decision flips). */
+#define FS_MH_SINGLE_PASS 4
 int fs_mh_accept(const fs_phys *p, int64_t C, int32_t N, double *E_old, double *W_old,
                  double *nll_old, const double *E_new, const double *W_new, const float *log_q_new,
                  uint64_t *pcg, double *state, uint8_t *state_is_f32, const float *config,
@@ -243,6 +259,16 @@ int fs_nf_mh_step_banked(const fs_flow_dims *d, const void *packed, const fs_phy
 /* ------------------------------------------------------------------ */
 /* Training (Algorithm 2): the circular RQS element-wise, with backward */
 /* ------------------------------------------------------------------ */
+
+/* Algorithm 2's target energy, DoubleWellLJ._energy (NF/normflows/Energy/SimpleLJ.py:
+ * 15-39, 63-128; used by NormalizingFlow.reverse_kld, core.py:105-142), for B sample rows
+ * x [B][2N] float32 in the flow's centred frame: LJ over all pairs plus an extra particle
+ * at the origin (each particle wrapped into [-bound, bound), no minimum image between
+ * particles, linear core -80 (r - 0.82) + 30 for r <= 0.82), divided by temperature, plus
+ * the double well (num_wells <= 2, centres (-+bound/2, 0), depths V0_0 / V0_1, r0, k) on
+ * the raw coordinates.  E [B] float32; grad_x (nullable) [B][2N] = dE/dx. */
+int fs_target_energy(const float *x, int64_t B, int32_t N, double bound, double temperature, int32_t num_wells,
+                     double V0_0, double V0_1, double r0, double k, float *E, float *grad_x, void *stream);
 
 /* unconstrained_rational_quadratic_spline, circular tails (NF/normflows/utils/
  * splines.py:16-222) for M independent elements: x [M], unnormalised widths /

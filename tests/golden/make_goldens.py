@@ -21,6 +21,8 @@ Fixtures:
   judge_trace.npz   reference judge_normalizing_flow / bulk_judge_normalizing_flow /
                     metropolis_acceptance_particle_move on a scripted op sequence
                     (with nf_big_move after a bulk judge), results + energies + PCG64
+  target_energy.npz reference DoubleWellLJ._energy and its gradient wrt the samples
+                    (N = 4, 16, 64; uniform, lattice, linear-core and near-origin rows)
   flow_a1.npz       reference log_prob (float32, and the same model in float64) at the
                     headline flow A1, N=64, with bench.synthetic_model's weights (checksum
                     only), on uniform rows and flow samples prepared as nf_big_move does
@@ -299,6 +301,49 @@ def a1_case(NF, nrows=32):
     np.savez_compressed(os.path.join(HERE, "flow_a1.npz"), **out)
     rel = (lp.double() - lp64).abs() / lp64.abs()
     print(f"flow_a1: log_prob[:2]={lp[:2].tolist()} ref f32 vs f64 max rel {float(rel.max()):.3g}")
+
+
+def target_energy_case(NF):
+    """DoubleWellLJ._energy (NF/normflows/Energy/SimpleLJ.py:15-39, 63-128) and its
+    gradient with respect to the samples (torch.autograd.grad of the energy sum), by the
+    reference module on CPU (its hard-coded device='cuda' zero row routed to the CPU).
+    N = 4, 16, 64 with the drivers' constants (bound = HALF_BOX, T = 1, V0 = -10, -10.5,
+    r0 = 1.2, k = 15): uniform rows (some outside the box, so the wrap acts), lattice rows,
+    rows with a pair inside the linear core, one particle near the origin particle."""
+    from oracle import flow as OF
+    from oracle.physics import fcc_lattice
+    real_zeros = torch.zeros
+
+    def zeros_cpu(*a, **k):
+        if k.get("device") == "cuda":
+            k["device"] = "cpu"
+        return real_zeros(*a, **k)
+
+    out = {}
+    g = torch.Generator().manual_seed(99)
+    torch.zeros = zeros_cpu
+    try:
+        for N in (4, 16, 64):
+            B = OF.half_box(N)
+            mod = NF.Energy.DoubleWellLJ(2 * N, N, 1.0, B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+            rows = [(torch.rand((6, 2 * N), generator=g) * 2 - 1) * B * 1.1]
+            lat = torch.from_numpy(fcc_lattice(N) - B).float().reshape(1, -1)
+            rows.append(lat + torch.randn((4, 2 * N), generator=g) * 0.05)
+            core = lat.repeat(3, 1)
+            core[0, 2:4] = core[0, 0:2] + torch.tensor([0.5, 0.1])     # pair at r ~ 0.51
+            core[1, 2:4] = core[1, 0:2] + torch.tensor([0.0, 0.8])     # just inside 0.82
+            core[2, 0:2] = torch.tensor([0.3, -0.2])                   # near the origin particle
+            rows.append(core)
+            x = torch.cat(rows).contiguous()
+            xr = x.clone().requires_grad_(True)
+            E = mod._energy(xr)
+            (gx,) = torch.autograd.grad(E.sum(), xr)
+            out[f"N{N}_x"], out[f"N{N}_E"], out[f"N{N}_grad"] = x.numpy(), E.detach().numpy(), gx.numpy()
+            out[f"N{N}_B"] = np.float64(B)
+    finally:
+        torch.zeros = real_zeros
+    np.savez_compressed(os.path.join(HERE, "target_energy.npz"), **out)
+    print("target_energy: ok", out["N64_E"][:3])
 
 
 def init_case(NF):
@@ -919,6 +964,9 @@ def main(only=None):
     if only == "box":
         box_case(MC)
         return
+    if only == "target":
+        target_energy_case(NF)
+        return
     if only == "a1":
         torch.set_num_threads(8)
         a1_case(NF)
@@ -938,6 +986,7 @@ def main(only=None):
     train_cycle_case(NF)
     judge_case(NF, MC)
     box_case(MC)
+    target_energy_case(NF)
     torch.set_num_threads(8)
     a1_case(NF)
 

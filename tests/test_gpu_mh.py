@@ -324,3 +324,41 @@ def test_nf_big_move_with_precomputed_terms():
     assert int(a.accepted.sum().item()) > 0
     with pytest.raises(ValueError):
         b.nf_big_move(cfg[:C], terms=(E[:C], W[:C], lq[:C].double()))
+
+
+def test_single_pass_log_q_flag():
+    """Opt-in FS_MH_SINGLE_PASS (SURVEY §7 option (i)): the step draws the same proposals
+    as the reference-semantics step, and the log q it uses is the sampling pass's own
+    (fs_flow_propose_lq), close to the density pass's value on fl32(config - half_width).
+    Decisions may differ only where that float32 difference straddles the draw."""
+    from flowstate import _lib
+
+    N, C = 16, 2048
+    kw = dict(L=3, H=64, nb=2, K=8)
+    dims = OF.FlowDims(N=N, B=half_box(N), **kw)
+    model = flow_from_state_dict(OF.random_state_dict(dims, seed=13), N, bound=dims.B, **kw)
+    L = float(np.sqrt(N / 0.03))
+    init = np.mod(OP.fcc_lattice(N)[None] + np.random.default_rng(2).normal(0, 0.05, (C, N, 2)), L)
+    seeds = np.arange(42, 42 + C, dtype=np.uint64)
+    one = BatchedMonteCarlo(model, init, Physics(L, L), seeds, single_pass_log_q=True)
+    two = BatchedMonteCarlo(model, init, Physics(L, L), seeds)
+    one.step()
+    two.step()
+    torch.cuda.synchronize()
+    assert torch.equal(one.last_proposals(), two.last_proposals())
+    # the single-pass value, recomputed through the ABI on the same stream rows
+    lib, p = _lib.load(), _lib.ptr
+    cfg = torch.empty((C, 2 * N), device="cuda")
+    cen = torch.empty_like(cfg)
+    lq1 = torch.empty(C, device="cuda")
+    _lib.check(lib.fs_flow_propose_lq(model.dims(), p(model.packed()), C, one.proposal_seed, 0, 0, L / 2, p(cfg),
+                                      p(cen), None, p(lq1), p(one.err), _lib.stream_ptr()))
+    torch.testing.assert_close(cfg.view(C, N, 2), one.last_proposals(), rtol=0, atol=0)
+    lq2 = model.log_prob(cen)
+    rel = ((lq1.double() - lq2.double()).abs() / lq2.double().abs()).cpu().numpy()
+    assert np.median(rel) < 1e-5 and rel.max() < 1e-3, (np.median(rel), rel.max())
+    acc = one.accept.cpu().numpy().astype(bool)
+    nll = one.nll_old.cpu().numpy()
+    np.testing.assert_array_equal(nll[acc], -lq1.double().cpu().numpy()[acc])  # the accepted chains cache it
+    flips = int((one.accept != two.accept).sum().item())
+    assert flips <= max(2, C // 500), flips

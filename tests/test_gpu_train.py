@@ -38,3 +38,20 @@ def test_inference_kernels_see_trained_parameters():
             lq += ld
         lq += m.q0.log_prob(z)
     np.testing.assert_allclose(after.cpu().numpy(), lq.cpu().numpy(), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("N", [4, 16, 64])
+def test_target_energy_kernel_matches_reference(N):
+    """DoubleWellLJ._energy on the device runs fs_target_energy (csrc/target_kernels.hip):
+    energies and dE/dx against the reference's (tests/golden/target_energy.npz)."""
+    from test_train_cpu import _target_case, check_target_energy
+
+    f, mod = _target_case(N)
+    x = torch.from_numpy(f[f"N{N}_x"]).cuda().requires_grad_(True)
+    E = mod._energy(x)
+    assert "TargetEnergy" in type(E.grad_fn).__name__  # the HIP kernel, not the torch restatement
+    (gx,) = torch.autograd.grad(E.sum(), x)
+    check_target_energy(mod, f, N, x, E, gx)
+    with torch.no_grad():
+        E2 = mod._energy(x.detach())
+    torch.testing.assert_close(E2, E.detach(), rtol=0, atol=0)  # energy-only launch, same values

@@ -91,3 +91,36 @@ def test_torch_spline_forward_inverse_consistent():
     x2, ld2 = circular_rqs_torch(y, uw, uh, ud, B, True)
     torch.testing.assert_close(x2, x, atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(ld + ld2, torch.zeros_like(ld), atol=1e-3, rtol=1e-3)
+
+
+def _target_case(N):
+    from flowstate.normflows.Energy import DoubleWellLJ
+
+    f = np.load(os.path.join(G, "target_energy.npz"))
+    mod = DoubleWellLJ(2 * N, N, 1.0, float(f[f"N{N}_B"]), V0_list=[-10.0, -10.5], r0=1.2, k=15)
+    return f, mod
+
+
+def check_target_energy(mod, f, N, x, E, gx):
+    ref_E, ref_g = f[f"N{N}_E"], f[f"N{N}_grad"]
+    E = E.detach().double().cpu().numpy()
+    assert np.all(np.abs(E - ref_E) <= 1e-5 * np.abs(ref_E) + 1e-4), np.abs(E - ref_E).max()
+    gx = gx.double().cpu().numpy()
+    # the reference's NaN gradients (coinciding particles: torch.where's pow branch) kept
+    np.testing.assert_array_equal(np.isnan(gx), np.isnan(ref_g))
+    ok = ~np.isnan(ref_g).any(axis=1)
+    assert ok.sum() >= len(ok) - 3
+    g, r = gx[ok], ref_g[ok]
+    scale = np.abs(r).max(axis=1, keepdims=True)
+    assert np.all(np.abs(g - r) <= 1e-5 * scale + 1e-4 * np.abs(r)), np.abs(g - r).max()
+
+
+@pytest.mark.parametrize("N", [4, 16, 64])
+def test_target_energy_restatement_matches_reference(N):
+    """The torch restatement of DoubleWellLJ._energy (CPU tensors) against the
+    reference's values and gradients (tests/golden/target_energy.npz)."""
+    f, mod = _target_case(N)
+    x = torch.from_numpy(f[f"N{N}_x"]).requires_grad_(True)
+    E = mod._energy(x)
+    (gx,) = torch.autograd.grad(E.sum(), x)
+    check_target_energy(mod, f, N, x, E, gx)
