@@ -438,6 +438,8 @@ int fs_rqs_backward(int64_t M, int32_t K, int32_t inverse, const float *x, const
                   "fs_rqs_backward");
 }
 
+int64_t fs_set_wide_rows(int64_t rows) { return fs_set_wide_rows_impl(rows); }
+
 int fs_target_energy(const float *x, int64_t B, int32_t N, double bound, double temperature, int32_t num_wells,
                      double V0_0, double V0_1, double r0, double k, float *E, float *grad_x, void *stream) {
     REQUIRE(B >= 0 && N >= 1 && N <= 1024 && bound > 0.0 && temperature > 0.0 && num_wells >= 0 && num_wells <= 2 &&

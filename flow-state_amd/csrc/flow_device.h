@@ -199,11 +199,12 @@ __device__ __forceinline__ void rqs_eval(float x, float icw, float ibw, float ic
     }
 }
 
-// Unconditional spline over this wave's identity features (lane = chain).
+// Unconditional spline over the identity features f = wid, wid + 8, ... (lane = chain);
+// wid is the wave's index in the fused kernel and the virtual wave of the wide path.
 template <int K, bool INV>
-__device__ __forceinline__ float uncond_spline(const float *__restrict__ U, float *CO, int cs, int N,
-                                               int D, int off, const FlowArgs &a, bool &nan_any) {
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+__device__ __forceinline__ float uncond_spline_w(const float *__restrict__ U, float *CO, int cs, int N,
+                                                 int D, int off, const FlowArgs &a, bool &nan_any, int wid) {
+    const int lane = threadIdx.x & 63;
     constexpr int K1 = K + 1;
     float ld = 0.f;
     for (int f = wid; f < N; f += kWaves) {
@@ -229,6 +230,12 @@ __device__ __forceinline__ float uncond_spline(const float *__restrict__ U, floa
         }
     }
     return ld;
+}
+
+template <int K, bool INV>
+__device__ __forceinline__ float uncond_spline(const float *__restrict__ U, float *CO, int cs, int N,
+                                               int D, int off, const FlowArgs &a, bool &nan_any) {
+    return uncond_spline_w<K, INV>(U, CO, cs, N, D, off, a, nan_any, (int)(threadIdx.x >> 6));
 }
 
 #pragma clang fp contract(on)

@@ -26,6 +26,11 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <atomic>
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "flow_device.h"
 #include "flow_layout.h"
 #include "fs_internal.h"
@@ -685,6 +690,270 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Wide path for small batches.  flow_pass_kernel carries 64 rows through every layer
+// in one workgroup, so a batch of R rows occupies R/64 CUs: 4096 chains are a quarter
+// of the chip, the Algorithm-2 refeed's 100 runs two CUs.  The wide path runs the same
+// pass phase by phase over the whole batch, each phase one launch spread over as many
+// workgroups as it has independent tiles:
+//   input   rows -> CO (coordinates, [R][2N] physical order), log-det partials zeroed
+//   start   per layer: (sampling) roll + unconditional spline, periodic features -> XA
+//   GEMMs   initial layer, then per residual block GEMM0 / GEMM1: one wave per 32x32
+//           output tile, its 32 activation rows staged in LDS; epilogues as the fused
+//           kernel's (BatchNorm folded, ReLU, residual stream HR without deferred biases)
+//   final   per (64-row block, virtual wave w): the final layer + conditional spline of
+//           the transform features the fused kernel's wave w owns, then (density) its
+//           unconditional features; w's running log-det lives in LDW[row][w]
+//   output  the 8 partials summed in wave order, base density, outputs.
+// Every value is computed by the fused kernel's own device code (gemm_run, FS_EPI,
+// cond_spline, uncond_spline_w, the Philox draws) with the same operands in the same
+// order, so the results are bit-identical to flow_pass_kernel's
+// (tests/test_gpu_wide.py); only the schedule differs.  The state between phases (a few
+// MB at these sizes) stays in the L2 / MALL.
+// ---------------------------------------------------------------------------
+struct WideArgs {
+    FlowArgs a;
+    float *CO;     // [R][D]
+    float *XA;     // [R][XS] periodic features, GEMM1 / initial-layer epilogue output (final-layer input)
+    float *XB;     // [R][XS] GEMM0 epilogue output
+    float *HR;     // [R][H] residual stream without its deferred biases
+    float *LDW;    // [R][8] log-det partial of virtual wave w
+    int64_t R;     // rows padded to 64
+    int off;       // physical index of logical coordinate 0 in this phase
+    int layer;
+    int jb;
+};
+
+template <int MODE>
+__global__ void __launch_bounds__(256) wide_input_kernel(WideArgs w) {
+    const FlowArgs &a = w.a;
+    const int N = a.N, D = 2 * N;
+    const int64_t row0 = (int64_t)blockIdx.x * kRows;
+    float *CO = w.CO + row0 * D;
+    if (MODE == MODE_PROPOSE) {
+        const int nq = (D + 3) / 4;
+        for (int e = threadIdx.x; e < kRows * nq; e += blockDim.x) {
+            const int rr = e / nq, q = e - rr * nq;
+            const int64_t lr = row0 + rr, rpc = a.rows_per_counter;
+            const uint64_t ctr = rpc > 0 ? a.counter + (uint64_t)(lr / rpc) : a.counter;
+            const uint64_t gr = (uint64_t)(a.row_offset + (rpc > 0 ? lr % rpc : lr));
+            uint4 c = make_uint4((uint32_t)gr, (uint32_t)(gr >> 32) ^ (uint32_t)(ctr >> 32), (uint32_t)ctr,
+                                 (uint32_t)q);
+            uint4 o = philox4x32(c, make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32)));
+            const uint32_t v[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int i = 4 * q + t;
+                if (i < D) {
+                    const float u = (float)(v[t] >> 8) * 5.9604644775390625e-08f;  // [0,1)
+                    CO[rr * D + i] = u * a.twoB + a.negB;
+                }
+            }
+        }
+    } else {
+        for (int e = threadIdx.x; e < kRows * D; e += blockDim.x) {
+            const int rr = e / D, i = e - rr * D;
+            const int64_t gr = row0 + rr;
+            CO[rr * D + i] = (gr < a.nrows) ? a.in[gr * D + i] : 0.f;
+        }
+    }
+    for (int e = threadIdx.x; e < kRows * kWaves; e += blockDim.x) w.LDW[row0 * kWaves + e] = 0.f;
+}
+
+// (sampling modes) the unconditional spline of virtual wave wid's identity features,
+// then the periodic features of the layer -> XA.  One workgroup of 8 waves per 64 rows.
+template <int H, int K, int MODE>
+__global__ void __launch_bounds__(kThreads) wide_start_kernel(WideArgs w) {
+    constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
+    const FlowArgs &a = w.a;
+    const int N = a.N, D = 2 * N;
+    const PackLayout PL = pack_layout(N, H, a.nb, a.K);
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t row0 = (int64_t)blockIdx.x * kRows;
+    float *CO = w.CO + row0 * D;
+    float *X = w.XA + row0 * XS;
+    const float *P = a.packed + (int64_t)w.layer * PL.stride;
+    if (MODE != MODE_DENSITY) {
+        bool nan_any = false;
+        float ld = w.LDW[(row0 + lane) * kWaves + wid];
+        ld += uncond_spline_w<K, true>(P + PL.unc, CO, D, N, D, w.off, a, nan_any, wid);
+        w.LDW[(row0 + lane) * kWaves + wid] = ld;
+        if (nan_any && row0 + lane < a.nrows && a.err) atomicOr(a.err, 1);
+    }
+    for (int f = wid; f < N; f += kWaves) {
+        const float v = CO[lane * D + (2 * f + w.off) % D];
+        const float sv = a.scale_pf * v;
+        X[lane * XS + f] = cosf(sv);
+        X[lane * XS + N + f] = sinf(sv);
+    }
+    for (int c = D + wid; c < 8 * PL.kg_in; c += kWaves) X[lane * XS + c] = 0.f;
+}
+
+// One residual-net GEMM of a layer.  KIND 0: initial layer (XA -> HR, XB = block 0's
+// first epilogue, or h + s_h without blocks); 1: block jb's GEMM0 (XB -> XA); 2: block
+// jb's GEMM1 (HR += XA . W1 -> HR, XB = block jb+1's first epilogue or h + s_h).
+// Workgroup = 32 rows x 4 column tiles (one wave each).
+template <int H, int KIND>
+__global__ void __launch_bounds__(256) wide_gemm_kernel(WideArgs w) {
+    constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
+    constexpr int NT = H / 32;
+    __shared__ __attribute__((aligned(16))) float Xs[32 * XS];
+    const FlowArgs &a = w.a;
+    const int N = a.N;
+    const PackLayout PL = pack_layout(N, H, a.nb, a.K);
+    const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t rowt = (int64_t)blockIdx.x * 32;
+    const int tile = (int)blockIdx.y * 4 + wid;
+    const int kg = KIND == 0 ? PL.kg_in : PL.kg_h;
+    const float *Xin = (KIND == 1 ? w.XB : w.XA) + rowt * XS;
+    for (int e = threadIdx.x; e < 32 * (8 * kg / 4); e += blockDim.x) {  // the 32 rows' used columns
+        const int rr = e / (2 * kg), q = e - rr * (2 * kg);
+        *(f32x4 *)(Xs + rr * XS + 4 * q) = *(const f32x4 *)(Xin + rr * XS + 4 * q);
+    }
+    __syncthreads();
+    if (tile >= NT) return;
+    const float *P = a.packed + (int64_t)w.layer * PL.stride;
+    const float *V = P + PL.vec;
+    const __amdgpu_buffer_rsrc_t W =
+        __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
+    const int col = 32 * tile + r;
+    f32x16 acc[1][1];
+    if (KIND == 0) {
+        gemm64<XS, 1, 1, FS_RPD>(Xs, W, (int)(PL.win * 4), kg, 0, tile, acc);
+    } else {
+        const int w0 = (int)((PL.blocks + w.jb * PL.block_stride) * 4);
+        if (KIND == 1) {
+            gemm64<XS, 1, 1, FS_RPD>(Xs, W, w0, kg, 0, tile, acc);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[0][0][i] = w.HR[(rowt + acc_row(0, i, h)) * H + col];
+            gemm64<XS, 1, 1, FS_RPD, true>(Xs, W, w0 + (int)(PL.block_stride * 2), kg, 0, tile, acc);
+        }
+    }
+    if (KIND == 1) {
+        const float *VB = V + PL.v_blocks + (int64_t)4 * H * w.jb;
+        const float e2 = VB[2 * H + col], e3 = VB[3 * H + col];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w.XA[(rowt + acc_row(0, i, h)) * XS + col] = FS_EPI(acc[0][0][i], e2, e3);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w.HR[(rowt + acc_row(0, i, h)) * H + col] = acc[0][0][i];
+    const int jn = KIND == 0 ? 0 : w.jb + 1;  // the block whose first epilogue follows
+    if (jn < a.nb) {
+        const float *VB = V + PL.v_blocks + (int64_t)4 * H * jn;
+        const float e0 = VB[col], e1 = VB[H + col];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w.XB[(rowt + acc_row(0, i, h)) * XS + col] = FS_EPI(acc[0][0][i], e0, e1);
+    } else {
+        const float sh = V[col];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w.XB[(rowt + acc_row(0, i, h)) * XS + col] = acc[0][0][i] + sh;
+    }
+}
+
+// Final layer + conditional spline (+ density: unconditional spline) of the features
+// virtual wave vw owns, for one 64-row block; WPW virtual waves per workgroup share the
+// block's final-layer input staged in LDS.
+template <int H, int K, int MODE, int WPW>
+__global__ void __launch_bounds__(64 * WPW) wide_final_kernel(WideArgs w) {
+    constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float *X = (float *)smem;
+    const FlowArgs &a = w.a;
+    const int N = a.N, D = 2 * N;
+    const PackLayout PL = pack_layout(N, H, a.nb, a.K);
+    const int lane = threadIdx.x & 63;
+    const int vw = __builtin_amdgcn_readfirstlane((int)blockIdx.y * WPW + (int)(threadIdx.x >> 6));
+    const int64_t row0 = (int64_t)blockIdx.x * kRows;
+    const float *Xg = w.XB + row0 * XS;
+    for (int e = threadIdx.x; e < kRows * (H / 4); e += blockDim.x) {
+        const int rr = e / (H / 4), q = e - rr * (H / 4);
+        *(f32x4 *)(X + rr * XS + 4 * q) = *(const f32x4 *)(Xg + rr * XS + 4 * q);
+    }
+    __syncthreads();
+    float *CO = w.CO + row0 * D;
+    const int cs = D, off = w.off;
+    const float *P = a.packed + (int64_t)w.layer * PL.stride;
+    const float *V = P + PL.vec;
+    const __amdgpu_buffer_rsrc_t W =
+        __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
+    bool nan_any = false;
+    Prof pf;
+    float ld = w.LDW[(row0 + lane) * kWaves + vw];
+    if constexpr (K <= 16) {
+        constexpr bool INV = MODE != MODE_DENSITY;
+        constexpr int TS = INV ? 1 : 0;
+        for (int pp = vw; pp < (N + 1) / 2; pp += kWaves) {
+            const int ja = 2 * pp, jb = 2 * pp + 1;
+            const bool hb = jb < N;
+            const float *ba = V + PL.v_bf + 96 * ja;
+            const float *bb = hb ? V + PL.v_bf + 96 * jb : ba + 16;
+            f32x16 tS[2][1], tO[2][1];
+            final_tile_pair<XS>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + TS, ba + 32 * TS, bb + 32 * TS, tS);
+            final_tile_pair<XS>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + 1 - TS, ba + 32 * (1 - TS),
+                                bb + 32 * (1 - TS), tO);
+            ld += spline_from_tiles<XS, H, K, INV>(tS, tO, 0, X, W, (int)((PL.wd + (int64_t)ja * H * (K + 1)) * 4),
+                                                   V + PL.v_bd + ja * (K + 1), CO, cs, (2 * ja + 1 + off) % D, a,
+                                                   nan_any, pf);
+            if (hb)
+                ld += spline_from_tiles<XS, H, K, INV>(tS, tO, 16, X, W, (int)((PL.wd + (int64_t)jb * H * (K + 1)) * 4),
+                                                       V + PL.v_bd + jb * (K + 1), CO, cs, (2 * jb + 1 + off) % D, a,
+                                                       nan_any, pf);
+        }
+    } else {
+        for (int j = vw; j < N; j += kWaves) {
+            const int p = (2 * j + 1 + off) % D;
+            ld += cond_spline<XS, H, K, MODE != MODE_DENSITY>(
+                X, W, (int)(PL.wf * 4), PL.kg_h, V + PL.v_bf + 96 * j, (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
+                V + PL.v_bd + j * (K + 1), CO, cs, p, j, a, nan_any, pf);
+        }
+    }
+    if (MODE == MODE_DENSITY) ld += uncond_spline_w<K, false>(P + PL.unc, CO, cs, N, D, off, a, nan_any, vw);
+    w.LDW[(row0 + lane) * kWaves + vw] = ld;
+    if (nan_any && row0 + lane < a.nrows && a.err) atomicOr(a.err, 1);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) wide_output_kernel(WideArgs w) {
+    const FlowArgs &a = w.a;
+    const int N = a.N, D = 2 * N;
+    const int64_t row0 = (int64_t)blockIdx.x * kRows;
+    const float *CO = w.CO + row0 * D;
+    const int off = w.off;
+    if (threadIdx.x < kRows) {
+        const int lane = threadIdx.x;
+        float tot = 0.f;
+#pragma unroll
+        for (int v = 0; v < kWaves; ++v) tot += w.LDW[(row0 + lane) * kWaves + v];
+        float outv = tot;
+        if (MODE == MODE_DENSITY && a.add_base) {
+            bool inb = true;
+            for (int i = 0; i < D; ++i) {
+                const float z = CO[lane * D + i];
+                inb = inb && (z >= a.negB) && (z <= a.B);
+            }
+            outv = tot + (inb ? a.base_lp : -INFINITY);
+        }
+        if (MODE == MODE_PROPOSE && a.add_base) outv = a.base_lp - tot;
+        if (row0 + lane < a.nrows && a.scalar_out) a.scalar_out[row0 + lane] = outv;
+    }
+    for (int e = threadIdx.x; e < kRows * D; e += blockDim.x) {
+        const int rr = e / D, i = e - rr * D;
+        const int64_t gr = row0 + rr;
+        if (gr >= a.nrows) continue;
+        const float v = CO[rr * D + (i + off) % D];
+        if (a.out) a.out[gr * D + i] = v;
+        if (MODE == MODE_PROPOSE) {
+            const float cfg = v + a.B;
+            if (a.config) a.config[gr * D + i] = cfg;
+            if (a.centered) a.centered[gr * D + i] = (float)((double)cfg - a.half_width);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Packing kernels
 // ---------------------------------------------------------------------------
 // kind 0: plain linear W[nout][kin];  kind 1: final layer widths / heights (2 tiles per feature)
@@ -841,9 +1110,133 @@ static hipError_t launch_pass_mode(const FlowArgs &a, int N, int H, int K, hipSt
     return hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------------------
+// wide path: host side
+// ---------------------------------------------------------------------------
+// Largest batch that takes the wide path (FS_WIDE_ROWS, or fs_set_wide_rows(); 0 disables
+// it).  Above it the fused kernel has enough 64-row workgroups to occupy the chip.
+static std::atomic<int64_t> g_wide_rows{-1};
+static int64_t wide_rows_limit() {
+    int64_t lim = g_wide_rows.load(std::memory_order_relaxed);
+    if (lim < 0) {
+        const char *e = getenv("FS_WIDE_ROWS");
+        lim = e ? atoll(e) : 8192;
+        if (lim < 0) lim = 0;
+        int64_t expect = -1;
+        g_wide_rows.compare_exchange_strong(expect, lim);
+        lim = g_wide_rows.load(std::memory_order_relaxed);
+    }
+    return lim;
+}
+
+// Internal workspace of the wide path, one per (device, stream), allocated once at the
+// size of the largest supported shape (never freed or moved: a captured graph may hold
+// its address).  nullptr when it would have to be allocated during stream capture.
+static void *wide_workspace(size_t bytes, hipStream_t st) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> ws;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    auto &e = ws[{dev, st}];
+    if (e.first && e.second >= bytes) return e.first;
+    if (e.first) return nullptr;  // a larger shape than the first one sized for: fused kernel
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    e = {p, bytes};
+    return p;
+}
+
+constexpr int64_t kWideMaxRows = 65536;  // the workspace never grows beyond this many rows
+
+static size_t wide_bytes(int64_t R, int N, int H) {
+    const int64_t XS = flow_xw(H) + 4;
+    return (size_t)(rup(R * 2 * N * 4, 256) + 2 * rup(R * XS * 4, 256) + rup(R * H * 4, 256) +
+                    rup(R * kWaves * 4, 256));
+}
+
+template <int H, int K, int MODE>
+static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &used) {
+    used = false;
+    const int64_t R = rup(a.nrows, kRows);
+    // size the one allocation for the limit's rows at the widest supported shape
+    // one allocation per (device, stream), sized for at least 16384 rows at the widest
+    // supported shape (~60 MB) or the current limit if larger
+    const int64_t lim = wide_rows_limit() < 16384 ? 16384 : wide_rows_limit();
+    const size_t cap = wide_bytes(rup(lim, kRows), kMaxN, 256);
+    if (wide_bytes(R, N, H) > cap) return hipSuccess;
+    char *p = (char *)wide_workspace(cap, st);
+    if (!p) return hipSuccess;
+    constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
+    const int D = 2 * N;
+    WideArgs w;
+    w.a = a;
+    w.R = R;
+    w.CO = (float *)p;
+    p += rup(R * D * 4, 256);
+    w.XA = (float *)p;
+    p += rup(R * XS * 4, 256);
+    w.XB = (float *)p;
+    p += rup(R * XS * 4, 256);
+    w.HR = (float *)p;
+    p += rup(R * H * 4, 256);
+    w.LDW = (float *)p;
+    w.off = 0;
+    w.layer = 0;
+    w.jb = 0;
+    const unsigned nblk = (unsigned)(R / kRows);
+    constexpr int WPW = 2;
+    const size_t fin_lds = (size_t)kRows * XS * 4;
+    {
+        auto kf = wide_final_kernel<H, K, MODE, WPW>;
+        static std::atomic<unsigned long long> attr_set{0};
+        if (hipError_t e = fs_set_max_lds_once((const void *)kf, attr_set); e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(wide_input_kernel<MODE>, dim3(nblk), dim3(256), 0, st, w);
+    const dim3 ggrid((unsigned)(R / 32), (unsigned)((H / 32 + 3) / 4));
+    for (int s = 0; s < a.L; ++s) {
+        w.layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
+        if (MODE != MODE_DENSITY) w.off = (w.off + N) % D;
+        hipLaunchKernelGGL((wide_start_kernel<H, K, MODE>), dim3(nblk), dim3(kThreads), 0, st, w);
+        hipLaunchKernelGGL((wide_gemm_kernel<H, 0>), ggrid, dim3(256), 0, st, w);
+        for (int jb = 0; jb < a.nb; ++jb) {
+            w.jb = jb;
+            hipLaunchKernelGGL((wide_gemm_kernel<H, 1>), ggrid, dim3(256), 0, st, w);
+            hipLaunchKernelGGL((wide_gemm_kernel<H, 2>), ggrid, dim3(256), 0, st, w);
+        }
+        hipLaunchKernelGGL((wide_final_kernel<H, K, MODE, WPW>), dim3(nblk, kWaves / WPW), dim3(64 * WPW), fin_lds,
+                           st, w);
+        if (MODE == MODE_DENSITY) w.off = (w.off + N) % D;
+    }
+    hipLaunchKernelGGL(wide_output_kernel<MODE>, dim3(nblk), dim3(256), 0, st, w);
+    used = true;
+    return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t wide_pass_mode(const FlowArgs &a, int N, int H, int K, hipStream_t st, bool &used) {
+    used = false;
+#define FS_CASE(HH, KK) \
+    if (H == HH && K == KK) return wide_pass_t<HH, KK, MODE>(a, N, st, used);
+    FS_FLOW_INSTANCES
+#undef FS_CASE
+    return hipSuccess;
+}
+
 }  // namespace fs
 
 using namespace fs;
+
+int64_t fs_set_wide_rows_impl(int64_t rows) {
+    const int64_t prev = wide_rows_limit();
+    g_wide_rows.store(rows < 0 ? 0 : (rows > kWideMaxRows ? kWideMaxRows : rows), std::memory_order_relaxed);
+    return prev;
+}
 
 #ifdef FS_PROF
 extern "C" int fs_prof_read(unsigned long long *out, int reset) {
@@ -984,6 +1377,14 @@ hipError_t fs_flow_pass_impl(const fs_flow_dims *d, const void *packed, int mode
     a.half_width = half_width;
     a.err = err;
     if (d->precision != 0) return fs_flow_split_pass(a, mode, d->precision, d->N, d->H, d->K, st);
+    if (B <= wide_rows_limit() && (B + kRows - 1) / kRows < 2 * 256) {
+        // small batch: the wide path (bit-identical results), when its workspace is available
+        bool used = false;
+        hipError_t e = mode == MODE_DENSITY  ? wide_pass_mode<MODE_DENSITY>(a, d->N, d->H, d->K, st, used)
+                       : mode == MODE_SAMPLE ? wide_pass_mode<MODE_SAMPLE>(a, d->N, d->H, d->K, st, used)
+                                             : wide_pass_mode<MODE_PROPOSE>(a, d->N, d->H, d->K, st, used);
+        if (e != hipSuccess || used) return e;
+    }
     if (mode == MODE_DENSITY) return launch_pass_mode<MODE_DENSITY>(a, d->N, d->H, d->K, st);
     if (mode == MODE_SAMPLE) return launch_pass_mode<MODE_SAMPLE>(a, d->N, d->H, d->K, st);
     return launch_pass_mode<MODE_PROPOSE>(a, d->N, d->H, d->K, st);

@@ -95,6 +95,7 @@ _SIGS = {
     "fs_coupling_features_bwd": (ctypes.c_int, [_CP] + [_P] * 5),
     "fs_coupling_sample_pre": (ctypes.c_int, [_CP] + [_P] * 9),
     "fs_coupling_sample_post": (ctypes.c_int, [_CP] + [_P] * 7),
+    "fs_set_wide_rows": (_I64, [_I64]),
     "fs_target_energy": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_int32]
                          + [ctypes.c_double] * 4 + [_P, _P, _P]),
     "fs_classify_wells": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double,

@@ -256,6 +256,13 @@ int fs_nf_mh_step_banked(const fs_flow_dims *d, const void *packed, const fs_phy
                          int64_t *accepted, unsigned long long *n_accept, int32_t *err, int flags, void *hws,
                          void *stream);
 
+/* Largest batch (rows) the flow passes run on the wide path: phase-by-phase launches
+ * spread over the whole chip instead of one 64-row workgroup carrying its rows through
+ * every layer, bit-identical results (f32 image only).  Default 8192 or the
+ * FS_WIDE_ROWS environment variable; 0 disables it; capped at 65536.  Returns the
+ * previous limit.  Process-wide. */
+int64_t fs_set_wide_rows(int64_t rows);
+
 /* ------------------------------------------------------------------ */
 /* Training (Algorithm 2): the circular RQS element-wise, with backward */
 /* ------------------------------------------------------------------ */

@@ -1,0 +1,116 @@
+"""The wide path of the flow passes (small batches, csrc/flow_kernels.hip "Wide path"):
+the same pass phase by phase over the whole chip.  It must be bit-identical to the
+fused kernel (flow_pass_kernel) in every mode: density (log_prob / inverse), sampling
+(forward) and propose (in-kernel base draws -> config / centered), including ragged
+batch sizes, the K <= 16 feature-pair kernels (A2), the K = 32 kernels (A1), and the
+fused NF-MH step built on them."""
+import numpy as np
+import pytest
+import torch
+
+from flowstate import _lib
+from flowstate.MCMC import BatchedMonteCarlo, Physics
+from flowstate.models import A1, A2, flow_from_state_dict, half_box
+from oracle import flow as OF
+from oracle import physics as OP
+
+pytestmark = pytest.mark.gpu
+
+
+class wide_rows:
+    """Set the wide-path row limit for a block (0 = always the fused kernel)."""
+
+    def __init__(self, rows):
+        self.rows = rows
+
+    def __enter__(self):
+        self.prev = _lib.load().fs_set_wide_rows(self.rows)
+
+    def __exit__(self, *exc):
+        _lib.load().fs_set_wide_rows(self.prev)
+
+
+def _model(N, kw, seed=21):
+    dims = OF.FlowDims(N=N, B=half_box(N), **kw)
+    sd = OF.random_state_dict(dims, seed=seed)
+    return dims, sd, flow_from_state_dict(sd, N, bound=dims.B, **kw)
+
+
+def _both(fn):
+    with wide_rows(0):
+        a = fn()
+        torch.cuda.synchronize()
+    with wide_rows(16384):
+        b = fn()
+        torch.cuda.synchronize()
+    return a, b
+
+
+CASES = [(16, dict(L=3, H=64, nb=2, K=8)), (64, A2), (16, A1), (3, dict(L=2, H=32, nb=2, K=5))]
+
+
+@pytest.mark.parametrize("N,kw", CASES, ids=["n16-h64", "a2-n64", "a1-n16", "n3-h32"])
+@pytest.mark.parametrize("B", [1, 63, 100, 257])
+def test_density_and_sampling_bit_identical(N, kw, B):
+    dims, sd, m = _model(N, kw)
+    g = torch.Generator().manual_seed(B)
+    x = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B * 1.001).cuda()  # a few rows outside the bound
+    (lq_f, z_f), (lq_w, z_w) = _both(lambda: (m.log_prob(x).clone(), m.inverse(x).clone()))
+    assert torch.equal(lq_f, lq_w) and torch.equal(z_f, z_w)
+    zb = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
+    (xf, lf), (xw, lw) = _both(lambda: tuple(t.clone() for t in m.forward_and_log_det(zb)))
+    assert torch.equal(xf, xw) and torch.equal(lf, lw)
+
+
+@pytest.mark.parametrize("N,kw", CASES[:3], ids=["n16-h64", "a2-n64", "a1-n16"])
+def test_propose_bit_identical(N, kw):
+    dims, sd, m = _model(N, kw)
+    L = _lib.load()
+    C = 300
+
+    def run():
+        cfg = torch.empty((C, dims.D), device="cuda")
+        cen = torch.empty_like(cfg)
+        lq = torch.empty(C, device="cuda")
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        _lib.check(L.fs_flow_propose_lq(m.dims(), _lib.ptr(m.packed()), C, 99, 7, 1000, 2 * dims.B / 2, _lib.ptr(cfg),
+                                        _lib.ptr(cen), None, _lib.ptr(lq), _lib.ptr(err), _lib.stream_ptr()))
+        return cfg, cen, lq
+
+    (a, b, c), (d, e, f) = _both(run)
+    assert torch.equal(a, d) and torch.equal(b, e) and torch.equal(c, f)
+
+
+def test_a1_oracle_parity_on_wide_path():
+    """The wide path against the oracle at A1 (N=16, 96 rows), as the fused kernel's test."""
+    dims, sd, m = _model(16, A1, seed=7)
+    g = torch.Generator().manual_seed(3)
+    x = (torch.rand((96, dims.D), generator=g) * 2 - 1) * dims.B
+    with wide_rows(16384):
+        got = m.log_prob(x.cuda()).cpu().numpy()
+    want = OF.log_prob(sd, x.clone(), dims).numpy()
+    assert np.all(np.abs(got - want) <= 1e-5 * np.abs(want) + 1e-4)
+
+
+@pytest.mark.parametrize("N,kw,C", [(16, A1, 512), (64, A2, 100)], ids=["a1-n16", "a2-n64-refeed"])
+def test_fused_steps_bit_identical(N, kw, C):
+    """Whole NF-MH steps (pure, then hybrid after local moves) on the two paths: states,
+    energies, NLLs, PCG64 states and counters identical."""
+    dims, sd, m = _model(N, kw, seed=5)
+    Lb = float(np.sqrt(N / 0.03))
+    init = np.mod(OP.fcc_lattice(N)[None] + np.random.default_rng(1).normal(0, 0.05, (C, N, 2)), Lb)
+    seeds = np.arange(42, 42 + C, dtype=np.uint64)
+
+    def run():
+        bmc = BatchedMonteCarlo(m, init, Physics(Lb), seeds)
+        bmc.MAX_STEPS_PER_LAUNCH = 1
+        bmc.step()
+        bmc.step()
+        bmc.local_moves(20)
+        bmc.step()
+        torch.cuda.synchronize()
+        return [t.clone() for t in (bmc.state, bmc.E_old, bmc.nll_old, bmc.pcg, bmc.accepted, bmc.attempts)]
+
+    a, b = _both(run)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
