@@ -30,6 +30,7 @@
 #include <map>
 #include <mutex>
 #include <utility>
+#include <vector>
 
 #include "flow_device.h"
 #include "flow_layout.h"
@@ -1160,11 +1161,129 @@ static size_t wide_bytes(int64_t R, int N, int H) {
                     rup(R * kWaves * 4, 256));
 }
 
+struct WideLaunch {
+    const void *func;
+    dim3 grid, block;
+    unsigned lds;
+    WideArgs w;
+};
+
+// Replaying a pass: ~67 launches per A1 layer, each a few microseconds of GPU work, so
+// launch overhead would dominate.  Outside stream capture the sequence is instantiated
+// once as a HIP graph per (shape, image, workspace) and replayed; only the input and
+// output launches see the call's own pointers and Philox keys, so they are the only
+// nodes updated per call.  Inside a caller's capture the launches go straight into it.
+struct WideGraph {
+    std::vector<char> key;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    hipGraphNode_t first = nullptr, last = nullptr;
+};
+
+static std::vector<char> wide_key(const WideArgs &w, const void *kfn0, int H, int K, int mode) {
+    WideArgs k = w;
+    FlowArgs &a = k.a;  // the call-specific fields only the input / output launches read
+    a.in = nullptr;
+    a.out = a.scalar_out = a.config = a.centered = nullptr;
+    a.seed = a.counter = 0;
+    a.row_offset = a.rows_per_counter = 0;
+    a.half_width = 0.0;
+    a.add_base = 0;
+    k.off = k.layer = k.jb = 0;
+    std::vector<char> key(sizeof(WideArgs) + sizeof(void *) + 3 * sizeof(int));
+    char *p = key.data();
+    memset(p, 0, key.size());
+    memcpy(p, &k, sizeof(WideArgs));
+    memcpy(p + sizeof(WideArgs), &kfn0, sizeof(void *));
+    const int hk[3] = {H, K, mode};
+    memcpy(p + sizeof(WideArgs) + sizeof(void *), hk, sizeof(hk));
+    return key;
+}
+
+static hipError_t wide_run(const std::vector<WideLaunch> &seq, std::vector<char> key, hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipError_t e = hipStreamIsCapturing(st, &cs); e != hipSuccess) return e;
+    if (cs != hipStreamCaptureStatusNone) {
+        for (const WideLaunch &l : seq) {
+            WideArgs w = l.w;
+            void *args[] = {&w};
+            if (hipError_t e = hipLaunchKernel(l.func, l.grid, l.block, args, l.lds, st); e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, std::vector<WideGraph>> cache;  // most recent last
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+    std::lock_guard<std::mutex> g(mu);
+    std::vector<WideGraph> &lst = cache[{dev, st}];
+    int hit = -1;
+    for (int i = 0; i < (int)lst.size(); ++i)
+        if (lst[i].key == key) hit = i;
+    auto params = [](const WideLaunch &l, WideArgs *w, void **args) {
+        *w = l.w;
+        args[0] = w;
+        hipKernelNodeParams p;
+        memset(&p, 0, sizeof(p));
+        p.func = (void *)l.func;
+        p.gridDim = l.grid;
+        p.blockDim = l.block;
+        p.sharedMemBytes = l.lds;
+        p.kernelParams = args;
+        p.extra = nullptr;
+        return p;
+    };
+    if (hit < 0) {
+        WideGraph wg;
+        wg.key = std::move(key);
+        if (hipError_t e = hipGraphCreate(&wg.graph, 0); e != hipSuccess) return e;
+        hipGraphNode_t prev = nullptr;
+        for (size_t i = 0; i < seq.size(); ++i) {
+            WideArgs w;
+            void *args[1];
+            hipKernelNodeParams p = params(seq[i], &w, args);
+            hipGraphNode_t node;
+            hipError_t e = hipGraphAddKernelNode(&node, wg.graph, prev ? &prev : nullptr, prev ? 1 : 0, &p);
+            if (e != hipSuccess) {
+                (void)hipGraphDestroy(wg.graph);
+                return e;
+            }
+            if (i == 0) wg.first = node;
+            prev = node;
+        }
+        wg.last = prev;
+        if (hipError_t e = hipGraphInstantiate(&wg.exec, wg.graph, nullptr, nullptr, 0); e != hipSuccess) {
+            (void)hipGraphDestroy(wg.graph);
+            return e;
+        }
+        if (lst.size() >= 8) {  // evict the least recently used (after the stream's work drains)
+            (void)hipStreamSynchronize(st);
+            (void)hipGraphExecDestroy(lst.front().exec);
+            (void)hipGraphDestroy(lst.front().graph);
+            lst.erase(lst.begin());
+        }
+        lst.push_back(std::move(wg));
+    } else {
+        WideGraph wg = std::move(lst[hit]);
+        lst.erase(lst.begin() + hit);
+        lst.push_back(std::move(wg));
+        // this call's pointers / Philox keys: the input and output launches
+        WideArgs w0, w1;
+        void *a0[1], *a1[1];
+        hipKernelNodeParams p0 = params(seq.front(), &w0, a0);
+        hipKernelNodeParams p1 = params(seq.back(), &w1, a1);
+        if (hipError_t e = hipGraphExecKernelNodeSetParams(lst.back().exec, lst.back().first, &p0); e != hipSuccess)
+            return e;
+        if (hipError_t e = hipGraphExecKernelNodeSetParams(lst.back().exec, lst.back().last, &p1); e != hipSuccess)
+            return e;
+    }
+    return hipGraphLaunch(lst.back().exec, st);
+}
+
 template <int H, int K, int MODE>
 static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &used) {
     used = false;
     const int64_t R = rup(a.nrows, kRows);
-    // size the one allocation for the limit's rows at the widest supported shape
     // one allocation per (device, stream), sized for at least 16384 rows at the widest
     // supported shape (~60 MB) or the current limit if larger
     const int64_t lim = wide_rows_limit() < 16384 ? 16384 : wide_rows_limit();
@@ -1175,6 +1294,7 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
     const int D = 2 * N;
     WideArgs w;
+    memset(&w, 0, sizeof(w));
     w.a = a;
     w.R = R;
     w.CO = (float *)p;
@@ -1186,36 +1306,37 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     w.HR = (float *)p;
     p += rup(R * H * 4, 256);
     w.LDW = (float *)p;
-    w.off = 0;
-    w.layer = 0;
-    w.jb = 0;
     const unsigned nblk = (unsigned)(R / kRows);
     constexpr int WPW = 2;
-    const size_t fin_lds = (size_t)kRows * XS * 4;
+    const unsigned fin_lds = (unsigned)(kRows * XS * 4);
     {
         auto kf = wide_final_kernel<H, K, MODE, WPW>;
         static std::atomic<unsigned long long> attr_set{0};
         if (hipError_t e = fs_set_max_lds_once((const void *)kf, attr_set); e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(wide_input_kernel<MODE>, dim3(nblk), dim3(256), 0, st, w);
+    std::vector<WideLaunch> seq;
+    seq.reserve(4 + (size_t)a.L * (3 + 2 * a.nb));
+    auto add = [&](const void *f, dim3 g, dim3 b, unsigned lds) { seq.push_back({f, g, b, lds, w}); };
+    add((const void *)wide_input_kernel<MODE>, dim3(nblk), dim3(256), 0);
     const dim3 ggrid((unsigned)(R / 32), (unsigned)((H / 32 + 3) / 4));
     for (int s = 0; s < a.L; ++s) {
         w.layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
         if (MODE != MODE_DENSITY) w.off = (w.off + N) % D;
-        hipLaunchKernelGGL((wide_start_kernel<H, K, MODE>), dim3(nblk), dim3(kThreads), 0, st, w);
-        hipLaunchKernelGGL((wide_gemm_kernel<H, 0>), ggrid, dim3(256), 0, st, w);
+        add((const void *)wide_start_kernel<H, K, MODE>, dim3(nblk), dim3(kThreads), 0);
+        add((const void *)wide_gemm_kernel<H, 0>, ggrid, dim3(256), 0);
         for (int jb = 0; jb < a.nb; ++jb) {
             w.jb = jb;
-            hipLaunchKernelGGL((wide_gemm_kernel<H, 1>), ggrid, dim3(256), 0, st, w);
-            hipLaunchKernelGGL((wide_gemm_kernel<H, 2>), ggrid, dim3(256), 0, st, w);
+            add((const void *)wide_gemm_kernel<H, 1>, ggrid, dim3(256), 0);
+            add((const void *)wide_gemm_kernel<H, 2>, ggrid, dim3(256), 0);
         }
-        hipLaunchKernelGGL((wide_final_kernel<H, K, MODE, WPW>), dim3(nblk, kWaves / WPW), dim3(64 * WPW), fin_lds,
-                           st, w);
+        add((const void *)wide_final_kernel<H, K, MODE, WPW>, dim3(nblk, kWaves / WPW), dim3(64 * WPW), fin_lds);
         if (MODE == MODE_DENSITY) w.off = (w.off + N) % D;
     }
-    hipLaunchKernelGGL(wide_output_kernel<MODE>, dim3(nblk), dim3(256), 0, st, w);
-    used = true;
-    return hipGetLastError();
+    add((const void *)wide_output_kernel<MODE>, dim3(nblk), dim3(256), 0);
+    w.off = w.layer = w.jb = 0;
+    hipError_t e = wide_run(seq, wide_key(w, seq.front().func, H, K, MODE), st);
+    if (e == hipSuccess) used = true;
+    return e;
 }
 
 template <int MODE>

@@ -60,6 +60,15 @@ def test_density_and_sampling_bit_identical(N, kw, B):
     zb = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
     (xf, lf), (xw, lw) = _both(lambda: tuple(t.clone() for t in m.forward_and_log_det(zb)))
     assert torch.equal(xf, xw) and torch.equal(lf, lw)
+    # the wide pass replays a cached graph: a second call with new inputs of the same
+    # shape must see them (input / output launches updated per call)
+    x2 = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
+    with wide_rows(16384):
+        a1 = m.log_prob(x).clone()
+        a2 = m.log_prob(x2).clone()
+    with wide_rows(0):
+        b2 = m.log_prob(x2).clone()
+    assert torch.equal(a1, lq_w) and torch.equal(a2, b2)
 
 
 @pytest.mark.parametrize("N,kw", CASES[:3], ids=["n16-h64", "a2-n64", "a1-n16"])
@@ -79,6 +88,7 @@ def test_propose_bit_identical(N, kw):
 
     (a, b, c), (d, e, f) = _both(run)
     assert torch.equal(a, d) and torch.equal(b, e) and torch.equal(c, f)
+    assert not torch.equal(a[0], a[1])  # rows draw different proposals
 
 
 def test_a1_oracle_parity_on_wide_path():
