@@ -701,9 +701,11 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
 //   GEMMs   initial layer, then per residual block GEMM0 / GEMM1: one wave per 32x32
 //           output tile, its 32 activation rows staged in LDS; epilogues as the fused
 //           kernel's (BatchNorm folded, ReLU, residual stream HR without deferred biases)
-//   final   per (64-row block, virtual wave w): the final layer + conditional spline of
-//           the transform features the fused kernel's wave w owns, then (density) its
-//           unconditional features; w's running log-det lives in LDW[row][w]
+//   final   per (64-row block, feature unit): the final layer + conditional spline of one
+//           transform feature (a pair for K <= 16), (density) the unconditional spline of
+//           the same-index identity feature; log-dets per feature to LDC / LDU
+//   fold    (in the next start / output launch) each row's per-feature log-dets added to
+//           LDW[row][w] in the order the fused kernel's wave w adds them
 //   output  the 8 partials summed in wave order, base density, outputs.
 // Every value is computed by the fused kernel's own device code (gemm_run, FS_EPI,
 // cond_spline, uncond_spline_w, the Philox draws) with the same operands in the same
@@ -717,7 +719,10 @@ struct WideArgs {
     float *XA;     // [R][XS] periodic features, GEMM1 / initial-layer epilogue output (final-layer input)
     float *XB;     // [R][XS] GEMM0 epilogue output
     float *HR;     // [R][H] residual stream without its deferred biases
-    float *LDW;    // [R][8] log-det partial of virtual wave w
+    float *LDW;    // [R][8] log-det partial of virtual wave w (the fused kernel's wave w)
+    float *LDC;    // [R][N] the last final phase's conditional log-det of transform feature j
+    float *LDU;    // [R][N] (density) its unconditional log-det of identity feature f
+    int pending;   // the start / output launch first folds the previous final phase into LDW
     int64_t R;     // rows padded to 64
     int off;       // physical index of logical coordinate 0 in this phase
     int layer;
@@ -760,6 +765,31 @@ __global__ void __launch_bounds__(256) wide_input_kernel(WideArgs w) {
     for (int e = threadIdx.x; e < kRows * kWaves; e += blockDim.x) w.LDW[row0 * kWaves + e] = 0.f;
 }
 
+
+// LDW[row][w] += the previous final phase's per-feature log-dets, in the order wave w of
+// the fused kernel added them: its transform features (pairs 2pp, 2pp+1 for K <= 16) in
+// ascending order, then (density) the sum over its identity features, added as one term.
+template <int K, int MODE>
+__device__ __forceinline__ float wide_fold(const WideArgs &w, int64_t row, int vw, float ld) {
+    const int N = w.a.N;
+    const float *lc = w.LDC + row * N;
+    if constexpr (K <= 16) {
+        for (int pp = vw; pp < (N + 1) / 2; pp += kWaves) {
+            ld += lc[2 * pp];
+            if (2 * pp + 1 < N) ld += lc[2 * pp + 1];
+        }
+    } else {
+        for (int j = vw; j < N; j += kWaves) ld += lc[j];
+    }
+    if (MODE == MODE_DENSITY) {
+        const float *lu = w.LDU + row * N;
+        float su = 0.f;
+        for (int f = vw; f < N; f += kWaves) su += lu[f];
+        ld += su;
+    }
+    return ld;
+}
+
 // (sampling modes) the unconditional spline of virtual wave wid's identity features,
 // then the periodic features of the layer -> XA.  One workgroup of 8 waves per 64 rows.
 template <int H, int K, int MODE>
@@ -774,10 +804,11 @@ __global__ void __launch_bounds__(kThreads) wide_start_kernel(WideArgs w) {
     float *CO = w.CO + row0 * D;
     float *X = w.XA + row0 * XS;
     const float *P = a.packed + (int64_t)w.layer * PL.stride;
-    if (MODE != MODE_DENSITY) {
+    if (w.pending || MODE != MODE_DENSITY) {
         bool nan_any = false;
         float ld = w.LDW[(row0 + lane) * kWaves + wid];
-        ld += uncond_spline_w<K, true>(P + PL.unc, CO, D, N, D, w.off, a, nan_any, wid);
+        if (w.pending) ld = wide_fold<K, MODE>(w, row0 + lane, wid, ld);
+        if (MODE != MODE_DENSITY) ld += uncond_spline_w<K, true>(P + PL.unc, CO, D, N, D, w.off, a, nan_any, wid);
         w.LDW[(row0 + lane) * kWaves + wid] = ld;
         if (nan_any && row0 + lane < a.nrows && a.err) atomicOr(a.err, 1);
     }
@@ -854,11 +885,42 @@ __global__ void __launch_bounds__(256) wide_gemm_kernel(WideArgs w) {
     }
 }
 
-// Final layer + conditional spline (+ density: unconditional spline) of the features
-// virtual wave vw owns, for one 64-row block; WPW virtual waves per workgroup share the
-// block's final-layer input staged in LDS.
-template <int H, int K, int MODE, int WPW>
-__global__ void __launch_bounds__(64 * WPW) wide_final_kernel(WideArgs w) {
+// One feature of uncond_spline_w: the same arithmetic, its log-det returned (0 outside).
+template <int K, bool INV>
+__device__ __forceinline__ float uncond_one(const float *__restrict__ U, float *CO, int cs, int D, int off,
+                                            const FlowArgs &a, bool &nan_any, int f) {
+    const int lane = threadIdx.x & 63;
+    constexpr int K1 = K + 1;
+    const float *T = U + (size_t)f * 3 * K1;
+    const int p = (2 * f + off) % D;
+    const float x = CO[lane * cs + p];
+    const bool inside = (x >= a.negB) && (x <= a.B);
+    const float *kn = INV ? T + K1 : T;
+    int bin = -1;
+#pragma unroll
+    for (int k = 0; k < K; ++k) bin += (x >= kn[k]) ? 1 : 0;
+    bin = bin < 0 ? 0 : (bin > K - 1 ? K - 1 : bin);
+    const float icw = T[bin], cw1 = T[bin + 1];
+    const float ich = T[K1 + bin], ch1 = T[K1 + bin + 1];
+    const float d0 = T[2 * K1 + bin], d1 = T[2 * K1 + bin + 1];
+    float y, l;
+    bool nd;
+    rqs_eval<INV>(x, icw, cw1 - icw, ich, ch1 - ich, d0, d1, y, l, nd);
+    if (inside) {
+        CO[lane * cs + p] = y;
+        nan_any |= nd;
+        return l;
+    }
+    return 0.f;
+}
+
+// Final layer + conditional spline of one feature unit (a transform feature, or a pair of
+// them for K <= 16) per wave, for one 64-row block; (density) also the unconditional
+// spline of the same-index identity feature(s).  WPB waves per workgroup share the
+// block's final-layer input staged in LDS.  Log-dets go to LDC / LDU per feature; the
+// next start / output launch adds them in the fused kernel's order (wide_fold).
+template <int H, int K, int MODE, int WPB>
+__global__ void __launch_bounds__(64 * WPB) wide_final_kernel(WideArgs w) {
     constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float *X = (float *)smem;
@@ -866,7 +928,7 @@ __global__ void __launch_bounds__(64 * WPW) wide_final_kernel(WideArgs w) {
     const int N = a.N, D = 2 * N;
     const PackLayout PL = pack_layout(N, H, a.nb, a.K);
     const int lane = threadIdx.x & 63;
-    const int vw = __builtin_amdgcn_readfirstlane((int)blockIdx.y * WPW + (int)(threadIdx.x >> 6));
+    const int u = __builtin_amdgcn_readfirstlane((int)blockIdx.y * WPB + (int)(threadIdx.x >> 6));
     const int64_t row0 = (int64_t)blockIdx.x * kRows;
     const float *Xg = w.XB + row0 * XS;
     for (int e = threadIdx.x; e < kRows * (H / 4); e += blockDim.x) {
@@ -874,6 +936,8 @@ __global__ void __launch_bounds__(64 * WPW) wide_final_kernel(WideArgs w) {
         *(f32x4 *)(X + rr * XS + 4 * q) = *(const f32x4 *)(Xg + rr * XS + 4 * q);
     }
     __syncthreads();
+    constexpr int UPF = K <= 16 ? 2 : 1;  // features per unit
+    if (u * UPF >= N) return;
     float *CO = w.CO + row0 * D;
     const int cs = D, off = w.off;
     const float *P = a.packed + (int64_t)w.layer * PL.stride;
@@ -882,47 +946,52 @@ __global__ void __launch_bounds__(64 * WPW) wide_final_kernel(WideArgs w) {
         __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
     bool nan_any = false;
     Prof pf;
-    float ld = w.LDW[(row0 + lane) * kWaves + vw];
+    float *lc = w.LDC + (row0 + lane) * N;
     if constexpr (K <= 16) {
         constexpr bool INV = MODE != MODE_DENSITY;
         constexpr int TS = INV ? 1 : 0;
-        for (int pp = vw; pp < (N + 1) / 2; pp += kWaves) {
-            const int ja = 2 * pp, jb = 2 * pp + 1;
-            const bool hb = jb < N;
-            const float *ba = V + PL.v_bf + 96 * ja;
-            const float *bb = hb ? V + PL.v_bf + 96 * jb : ba + 16;
-            f32x16 tS[2][1], tO[2][1];
-            final_tile_pair<XS>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + TS, ba + 32 * TS, bb + 32 * TS, tS);
-            final_tile_pair<XS>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + 1 - TS, ba + 32 * (1 - TS),
-                                bb + 32 * (1 - TS), tO);
-            ld += spline_from_tiles<XS, H, K, INV>(tS, tO, 0, X, W, (int)((PL.wd + (int64_t)ja * H * (K + 1)) * 4),
-                                                   V + PL.v_bd + ja * (K + 1), CO, cs, (2 * ja + 1 + off) % D, a,
-                                                   nan_any, pf);
-            if (hb)
-                ld += spline_from_tiles<XS, H, K, INV>(tS, tO, 16, X, W, (int)((PL.wd + (int64_t)jb * H * (K + 1)) * 4),
-                                                       V + PL.v_bd + jb * (K + 1), CO, cs, (2 * jb + 1 + off) % D, a,
-                                                       nan_any, pf);
-        }
+        const int pp = u, ja = 2 * pp, jb = 2 * pp + 1;
+        const bool hb = jb < N;
+        const float *ba = V + PL.v_bf + 96 * ja;
+        const float *bb = hb ? V + PL.v_bf + 96 * jb : ba + 16;
+        f32x16 tS[2][1], tO[2][1];
+        final_tile_pair<XS>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + TS, ba + 32 * TS, bb + 32 * TS, tS);
+        final_tile_pair<XS>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + 1 - TS, ba + 32 * (1 - TS), bb + 32 * (1 - TS),
+                            tO);
+        lc[ja] = spline_from_tiles<XS, H, K, INV>(tS, tO, 0, X, W, (int)((PL.wd + (int64_t)ja * H * (K + 1)) * 4),
+                                                  V + PL.v_bd + ja * (K + 1), CO, cs, (2 * ja + 1 + off) % D, a,
+                                                  nan_any, pf);
+        if (hb)
+            lc[jb] = spline_from_tiles<XS, H, K, INV>(tS, tO, 16, X, W, (int)((PL.wd + (int64_t)jb * H * (K + 1)) * 4),
+                                                      V + PL.v_bd + jb * (K + 1), CO, cs, (2 * jb + 1 + off) % D, a,
+                                                      nan_any, pf);
     } else {
-        for (int j = vw; j < N; j += kWaves) {
-            const int p = (2 * j + 1 + off) % D;
-            ld += cond_spline<XS, H, K, MODE != MODE_DENSITY>(
-                X, W, (int)(PL.wf * 4), PL.kg_h, V + PL.v_bf + 96 * j, (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
-                V + PL.v_bd + j * (K + 1), CO, cs, p, j, a, nan_any, pf);
-        }
+        const int j = u;
+        lc[j] = cond_spline<XS, H, K, MODE != MODE_DENSITY>(
+            X, W, (int)(PL.wf * 4), PL.kg_h, V + PL.v_bf + 96 * j, (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
+            V + PL.v_bd + j * (K + 1), CO, cs, (2 * j + 1 + off) % D, j, a, nan_any, pf);
     }
-    if (MODE == MODE_DENSITY) ld += uncond_spline_w<K, false>(P + PL.unc, CO, cs, N, D, off, a, nan_any, vw);
-    w.LDW[(row0 + lane) * kWaves + vw] = ld;
+    if (MODE == MODE_DENSITY) {
+        float *lu = w.LDU + (row0 + lane) * N;
+        for (int f = u * UPF; f < (u + 1) * UPF && f < N; ++f)
+            lu[f] = uncond_one<K, false>(P + PL.unc, CO, cs, D, off, a, nan_any, f);
+    }
     if (nan_any && row0 + lane < a.nrows && a.err) atomicOr(a.err, 1);
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(256) wide_output_kernel(WideArgs w) {
+template <int K, int MODE>
+__global__ void __launch_bounds__(kThreads) wide_output_kernel(WideArgs w) {
     const FlowArgs &a = w.a;
     const int N = a.N, D = 2 * N;
     const int64_t row0 = (int64_t)blockIdx.x * kRows;
     const float *CO = w.CO + row0 * D;
     const int off = w.off;
+    {
+        const int vw = threadIdx.x >> 6;
+        const int64_t row = row0 + (threadIdx.x & 63);
+        w.LDW[row * kWaves + vw] = wide_fold<K, MODE>(w, row, vw, w.LDW[row * kWaves + vw]);
+    }
+    __syncthreads();
     if (threadIdx.x < kRows) {
         const int lane = threadIdx.x;
         float tot = 0.f;
@@ -1158,7 +1227,7 @@ constexpr int64_t kWideMaxRows = 65536;  // the workspace never grows beyond thi
 static size_t wide_bytes(int64_t R, int N, int H) {
     const int64_t XS = flow_xw(H) + 4;
     return (size_t)(rup(R * 2 * N * 4, 256) + 2 * rup(R * XS * 4, 256) + rup(R * H * 4, 256) +
-                    rup(R * kWaves * 4, 256));
+                    rup(R * kWaves * 4, 256) + 2 * rup(R * N * 4, 256));
 }
 
 struct WideLaunch {
@@ -1306,8 +1375,14 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     w.HR = (float *)p;
     p += rup(R * H * 4, 256);
     w.LDW = (float *)p;
+    p += rup(R * kWaves * 4, 256);
+    w.LDC = (float *)p;
+    p += rup(R * N * 4, 256);
+    w.LDU = (float *)p;
+    w.pending = 0;
     const unsigned nblk = (unsigned)(R / kRows);
-    constexpr int WPW = 2;
+    constexpr int WPW = 4;  // feature units (waves) per final-phase workgroup
+    const int units = K <= 16 ? (N + 1) / 2 : N;
     const unsigned fin_lds = (unsigned)(kRows * XS * 4);
     {
         auto kf = wide_final_kernel<H, K, MODE, WPW>;
@@ -1322,6 +1397,7 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     for (int s = 0; s < a.L; ++s) {
         w.layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
         if (MODE != MODE_DENSITY) w.off = (w.off + N) % D;
+        w.pending = s > 0;
         add((const void *)wide_start_kernel<H, K, MODE>, dim3(nblk), dim3(kThreads), 0);
         add((const void *)wide_gemm_kernel<H, 0>, ggrid, dim3(256), 0);
         for (int jb = 0; jb < a.nb; ++jb) {
@@ -1329,11 +1405,13 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
             add((const void *)wide_gemm_kernel<H, 1>, ggrid, dim3(256), 0);
             add((const void *)wide_gemm_kernel<H, 2>, ggrid, dim3(256), 0);
         }
-        add((const void *)wide_final_kernel<H, K, MODE, WPW>, dim3(nblk, kWaves / WPW), dim3(64 * WPW), fin_lds);
+        add((const void *)wide_final_kernel<H, K, MODE, WPW>, dim3(nblk, (units + WPW - 1) / WPW), dim3(64 * WPW),
+            fin_lds);
         if (MODE == MODE_DENSITY) w.off = (w.off + N) % D;
     }
-    add((const void *)wide_output_kernel<MODE>, dim3(nblk), dim3(256), 0);
-    w.off = w.layer = w.jb = 0;
+    w.pending = 1;
+    add((const void *)wide_output_kernel<K, MODE>, dim3(nblk), dim3(kThreads), 0);
+    w.off = w.layer = w.jb = w.pending = 0;
     hipError_t e = wide_run(seq, wide_key(w, seq.front().func, H, K, MODE), st);
     if (e == hipSuccess) used = true;
     return e;
