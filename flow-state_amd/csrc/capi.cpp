@@ -483,6 +483,22 @@ int fs_linear_f32(int64_t M, int64_t N, int64_t K, const float *A, int64_t sam, 
     return hip_rc(fs_linear_f32_impl(g, (hipStream_t)stream), "fs_linear_f32");
 }
 
+int fs_linear_f32_pair(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, void *stream) {
+    REQUIRE(g0 && g1, "fs_linear_f32_pair: NULL descriptor");
+    fs::GemmArgs a[2];
+    const fs_gemm_f32 *gs[2] = {g0, g1};
+    for (int i = 0; i < 2; ++i) {
+        const fs_gemm_f32 &g = *gs[i];
+        REQUIRE(g.M >= 0 && g.N >= 0 && g.K >= 0 && (g.M == 0 || g.N == 0 || (g.C && (g.K == 0 || (g.A && g.B)))) &&
+                    g.ldc >= g.N && (!g.R || g.ldr >= g.N),
+                "fs_linear_f32_pair: invalid arguments (product %d)", i);
+        REQUIRE(g.M <= 32LL * 65535 && g.N <= 32LL * 65535, "fs_linear_f32_pair: M, N at most %lld", 32LL * 65535);
+        a[i] = fs::GemmArgs{g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C, g.ldc,
+                            g.rowsum_a};
+    }
+    return hip_rc(fs_linear_f32_pair_impl(a[0], a[1], (hipStream_t)stream), "fs_linear_f32_pair");
+}
+
 int fs_bn_relu_train_fwd(int64_t Bn, int32_t H, const float *x, const float *gamma, const float *beta,
                          float *running_mean, float *running_var, int64_t *num_batches, double momentum, double eps,
                          float *y, float *mean, float *invstd, void *stream) {

@@ -61,17 +61,24 @@ __device__ __forceinline__ t4 load4(const float *p, int64_t stride, int64_t k0, 
     return v;
 }
 
+template <int SPLIT>
+struct GemmLds {
+    t16 part[SPLIT > 1 ? SPLIT - 1 : 1][64];
+    float rs_part[SPLIT][64];
+};
+
+// One 32 x 32 output tile (bx, by) of g by the workgroup's SPLIT waves.
 template <int SPLIT, bool AK, bool BK>
-__global__ __launch_bounds__(64 * SPLIT) void gemm_f32_kernel(GemmArgs g) {
-    __shared__ t16 part[SPLIT > 1 ? SPLIT - 1 : 1][64];
-    __shared__ float rs_part[SPLIT][64];
+__device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t by, GemmLds<SPLIT> &L) {
+    auto &part = L.part;
+    auto &rs_part = L.rs_part;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int64_t m0 = (int64_t)blockIdx.x * 32, n0 = (int64_t)blockIdx.y * 32;
+    const int64_t m0 = bx * 32, n0 = by * 32;
     const bool aok = m0 + r < g.M, bok = n0 + r < g.N;
     const float *Ap = aok ? g.A + (m0 + r) * g.sam : g.A;
     const float *Bp = bok ? g.B + (n0 + r) * g.sbn : g.B;
-    const bool rows = g.rowsum_a != nullptr && blockIdx.y == 0;
+    const bool rows = g.rowsum_a != nullptr && by == 0;
     t16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
@@ -131,6 +138,26 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_f32_kernel(GemmArgs g) {
             g.C[row * g.ldc + col] = v;
         }
     }
+}
+
+template <int SPLIT, bool AK, bool BK>
+__global__ __launch_bounds__(64 * SPLIT) void gemm_f32_kernel(GemmArgs g) {
+    __shared__ GemmLds<SPLIT> L;
+    gemm_tile<SPLIT, AK, BK>(g, blockIdx.x, blockIdx.y, L);
+}
+
+// Two independent products in one launch (nn.Linear's backward: input gradient and weight
+// gradient): workgroups [0, t0) take the tiles of g0 (column-major over its mt0 row
+// tiles), the rest those of g1.  Each tile is computed exactly as gemm_f32_kernel does.
+template <int SPLIT, bool A0K, bool B0K, bool A1K, bool B1K>
+__global__ __launch_bounds__(64 * SPLIT) void gemm2_f32_kernel(GemmArgs g0, GemmArgs g1, unsigned t0, unsigned mt0,
+                                                              unsigned mt1) {
+    __shared__ GemmLds<SPLIT> L;
+    const unsigned b = blockIdx.x;
+    if (b < t0)
+        gemm_tile<SPLIT, A0K, B0K>(g0, b % mt0, b / mt0, L);
+    else
+        gemm_tile<SPLIT, A1K, B1K>(g1, (b - t0) % mt1, (b - t0) / mt1, L);
 }
 
 // ---------------------------------------------------------------------------
@@ -290,6 +317,10 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
 
 using namespace fs;
 
+static int gemm_split(const GemmArgs &g) {
+    return g.K > 8 * 4 * 16 ? FS_GEMM_SPLIT_LONG : g.K >= 256 ? FS_GEMM_SPLIT_MID : FS_GEMM_SPLIT;
+}
+
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st) {
     if (g.M <= 0 || (g.N <= 0 && !g.rowsum_a)) return hipSuccess;
     // one column tile even when N = 0, so that rowsum_a is still written
@@ -297,7 +328,7 @@ hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st) {
     const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0;
     const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0;
     // enough waves per tile that each walks at most ~16 k-blocks
-    const int split = g.K > 8 * 4 * 16 ? FS_GEMM_SPLIT_LONG : g.K >= 256 ? FS_GEMM_SPLIT_MID : FS_GEMM_SPLIT;
+    const int split = gemm_split(g);
 #define FS_G(S, A, B)                                                                           \
     if (split == S && ak == A && bk == B) {                                                     \
         hipLaunchKernelGGL((gemm_f32_kernel<S, A, B>), grid, dim3(64 * S), 0, st, g);           \
@@ -311,6 +342,25 @@ hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st) {
     FS_G(FS_GEMM_SPLIT_LONG, false, false)
 #undef FS_G
     return hipErrorInvalidValue;
+}
+
+hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, hipStream_t st) {
+    const bool a0 = g0.sak == 1 && ((uintptr_t)g0.A & 15) == 0 && g0.sam % 4 == 0;
+    const bool b0 = g0.sbk == 1 && ((uintptr_t)g0.B & 15) == 0 && g0.sbn % 4 == 0;
+    const bool a1 = g1.sak == 1 && ((uintptr_t)g1.A & 15) == 0 && g1.sam % 4 == 0;
+    const bool b1 = g1.sbk == 1 && ((uintptr_t)g1.B & 15) == 0 && g1.sbn % 4 == 0;
+    const bool live0 = g0.M > 0 && g0.N > 0, live1 = g1.M > 0 && g1.N > 0;
+    // the instantiated pair: nn.Linear's input gradient (dY W) and weight gradient (dY^T X)
+    if (live0 && live1 && gemm_split(g0) == FS_GEMM_SPLIT && gemm_split(g1) == FS_GEMM_SPLIT && a0 && !b0 && !a1 &&
+        !b1) {
+        const unsigned mt0 = (unsigned)((g0.M + 31) / 32), mt1 = (unsigned)((g1.M + 31) / 32);
+        const unsigned t0 = mt0 * (unsigned)((g0.N + 31) / 32), t1 = mt1 * (unsigned)((g1.N + 31) / 32);
+        hipLaunchKernelGGL((gemm2_f32_kernel<FS_GEMM_SPLIT, true, false, false, false>), dim3(t0 + t1),
+                           dim3(64 * FS_GEMM_SPLIT), 0, st, g0, g1, t0, mt0, mt1);
+        return hipGetLastError();
+    }
+    if (hipError_t e = fs_linear_f32_impl(g0, st); e != hipSuccess) return e;
+    return fs_linear_f32_impl(g1, st);
 }
 
 hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,

@@ -29,6 +29,7 @@ values are exactly those numbers.  The flow model is optional until the first
 big move (the reference equilibrates before set_nf_model).
 """
 import functools
+import warnings
 import weakref
 
 import numpy as np
@@ -128,6 +129,13 @@ class BatchedMonteCarlo:
         seeds_np = np.asarray(seeds, dtype=np.uint64).reshape(-1)
         if seeds_np.size != self.C:
             raise ValueError("one seed per chain")
+        if proposal_seed is None and self.chain_offset > 0 and self.C > 1 and not np.array_equal(
+                seeds_np, seeds_np[0] + np.arange(self.C, dtype=np.uint64)):
+            # the default stream assumes seed = MASTER_SEED + global chain index on every rank
+            # (main_algorithm_1.py:139); with other seeds each rank would derive its own stream
+            warnings.warn("BatchedMonteCarlo: chain_offset > 0 with seeds that are not seeds[0] + arange(C): the "
+                          "default proposal stream is then not one global stream across ranks; pass proposal_seed",
+                          stacklevel=3)
         self.proposal_seed = default_proposal_seed(seeds_np, self.chain_offset) if proposal_seed is None \
             else int(proposal_seed)
         seeds = torch.as_tensor(seeds_np.view(np.int64), device=dev)
@@ -362,6 +370,12 @@ class BatchedMonteCarlo:
                    "fs_adjust_displacement")
 
     def check_errors(self):
+        """Raise the reference's ValueError if any flow pass since construction met a NaN
+        discriminant (splines.py:176-183).  Passes that make several steps' proposals at once
+        (step(n), the proposal bank) report a NaN in any of those proposals when they are
+        made, as the reference raises when it pre-generates its proposals in batches
+        (main_algorithm_1.py:340-343, utils.py:422-450), even if a later weight change
+        retires the bank before those steps run."""
         if int(self.err.item()) & 1:
             raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
 

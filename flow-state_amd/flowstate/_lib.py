@@ -38,6 +38,14 @@ class Coupling(ctypes.Structure):
                 ("tail_bound", ctypes.c_double)]
 
 
+class GemmF32(ctypes.Structure):
+    """fs_gemm_f32 (include/flowstate.h): one fs_linear_f32 product."""
+    _fields_ = [("M", ctypes.c_int64), ("N", ctypes.c_int64), ("K", ctypes.c_int64), ("A", ctypes.c_void_p),
+                ("sam", ctypes.c_int64), ("sak", ctypes.c_int64), ("B", ctypes.c_void_p), ("sbk", ctypes.c_int64),
+                ("sbn", ctypes.c_int64), ("bias", ctypes.c_void_p), ("R", ctypes.c_void_p), ("ldr", ctypes.c_int64),
+                ("C", ctypes.c_void_p), ("ldc", ctypes.c_int64), ("rowsum_a", ctypes.c_void_p)]
+
+
 class FlowStateError(RuntimeError):
     pass
 
@@ -86,6 +94,7 @@ _SIGS = {
                         + [_P] * 7),
     "fs_linear_f32": (ctypes.c_int, [_I64, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _P, _I64, _P, _I64,
                                      _P, _P]),
+    "fs_linear_f32_pair": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(GemmF32), _P]),
     "fs_bn_relu_train_fwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 6 + [ctypes.c_double, ctypes.c_double]
                              + [_P] * 4),
     "fs_bn_relu_train_bwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 11),

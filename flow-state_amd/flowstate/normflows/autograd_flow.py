@@ -217,13 +217,22 @@ class _Linear(torch.autograd.Function):
         N = w.shape[0]
         L = _lib.load()
         gx = gw = gb = None
-        if ctx.needs_input_grad[0] and N >= _WIDE:
+        if ctx.needs_input_grad[0] and N < _WIDE and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]):
+            # input gradient dY W and weight / bias gradients dY^T X in one launch
+            gx = torch.empty_like(x)
+            gw = torch.empty_like(w)
+            gb = torch.empty((N,), dtype=torch.float32, device=x.device)
+            p = _lib.ptr
+            g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
+            g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
+            _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
+        elif ctx.needs_input_grad[0] and N >= _WIDE:
             gx = torch.mm(gy, w)
         elif ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
             _lib.check(L.fs_linear_f32(M, K, N, _lib.ptr(gy), N, 1, _lib.ptr(w), K, 1, None, None, 0, _lib.ptr(gx),
                                        K, None, _lib.stream_ptr()), "fs_linear_f32")
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+        if (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]) and gw is None:
             gw = torch.empty_like(w)
             gb = torch.empty((N,), dtype=torch.float32, device=x.device)
             _lib.check(L.fs_linear_f32(N, K, M, _lib.ptr(gy), 1, N, _lib.ptr(x), K, 1, None, None, 0, _lib.ptr(gw),
@@ -231,6 +240,8 @@ class _Linear(torch.autograd.Function):
         if ctx.res is not None and ctx.needs_input_grad[3]:
             # the residual's gradient goes to the block's first BatchNorm backward, which
             # adds it in its own launch (no autograd accumulation kernel)
+            if ctx.res.g is not None:
+                raise RuntimeError("residual gradient stash was never consumed by its BatchNorm backward")
             ctx.res.g = gy
             return gx, gw, gb, None, None
         return gx, gw, gb, (gy if ctx.has_r and ctx.needs_input_grad[3] else None), None
@@ -301,7 +312,14 @@ class _ResidualGrad:
     """Carries a block input's residual-branch gradient from the block's second Linear
     (whose backward runs first: the chain l1 -> bn1 -> l0 -> bn0 orders them) to its first
     BatchNorm's backward, which adds it in its own launch (fs_bn_relu_train_bwd dx_add)
-    instead of autograd summing the two branches in a separate kernel."""
+    instead of autograd summing the two branches in a separate kernel.
+
+    A side channel: autograd sees None for that gradient, so it is correct only when the
+    gradient reaches the consuming BatchNorm's backward, as in loss.backward() through
+    the whole conditioner (_conditioner_fused).  Checking these Functions in isolation
+    (gradcheck, or autograd.grad on an intermediate that skips the block's first BatchNorm)
+    must construct them with res=None, which returns the residual gradient normally.
+    A stash still unconsumed when the next one is written raises."""
 
     __slots__ = ("g",)
 

@@ -302,6 +302,25 @@ int fs_linear_f32(int64_t M, int64_t N, int64_t K, const float *A, int64_t sam, 
                   int64_t sbk, int64_t sbn, const float *bias, const float *R, int64_t ldr, float *C, int64_t ldc,
                   float *rowsum_a, void *stream);
 
+/* Two independent fs_linear_f32 products in one launch (nn.Linear's backward: the input
+ * gradient dY W and the weight / bias gradients dY^T X, which torch's autograd runs as two
+ * GEMMs), each with exactly fs_linear_f32's arithmetic and results.  The arguments of
+ * each are those of fs_linear_f32, in this POD. */
+typedef struct fs_gemm_f32 {
+    int64_t M, N, K;
+    const float *A;
+    int64_t sam, sak;
+    const float *B;
+    int64_t sbk, sbn;
+    const float *bias;
+    const float *R;
+    int64_t ldr;
+    float *C;
+    int64_t ldc;
+    float *rowsum_a;
+} fs_gemm_f32;
+int fs_linear_f32_pair(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, void *stream);
+
 /* BatchNorm1d (training mode) followed by ReLU over x [Bn][H] (row-major):
  * batch mean / biased variance, y = relu(gamma (x - mean) invstd + beta),
  * running_mean / running_var updated with `momentum` (unbiased variance) and

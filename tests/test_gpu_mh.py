@@ -292,6 +292,28 @@ def test_banked_hybrid_steps_match_single_steps():
     assert used >= 4 and banked._bank is not None and banked._bank["S"] > 1
     assert banked._bank["step0"] < banked.step_count - 3
     assert banked.step_count == single.step_count == 12
+    # no NaN discriminant in either path (a bank reports its proposals' errors when it is
+    # made, as the reference's batch pre-generation does)
+    assert int(banked.err.item()) == int(single.err.item()) == 0
+
+
+def test_sharded_seeds_warning():
+    """The default proposal stream is one global stream across ranks only for seeds
+    MASTER_SEED + global index; other seeds on a shard with chain_offset > 0 warn."""
+    import warnings
+
+    N, C = 16, 8
+    kw = dict(L=2, H=32, nb=1, K=8)
+    dims = OF.FlowDims(N=N, B=half_box(N), **kw)
+    model = flow_from_state_dict(OF.random_state_dict(dims, seed=2), N, bound=dims.B, **kw)
+    L = float(np.sqrt(N / 0.03))
+    init = np.repeat(OP.fcc_lattice(N)[None], C, 0)
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        BatchedMonteCarlo(model, init, Physics(L, L), np.arange(50, 50 + C, dtype=np.uint64), chain_offset=8)
+    assert not [w for w in rec if "proposal_seed" in str(w.message)]
+    with pytest.warns(UserWarning, match="proposal_seed"):
+        BatchedMonteCarlo(model, init, Physics(L, L), np.arange(C, dtype=np.uint64)[::-1].copy() + 50, chain_offset=8)
     assert int(banked.accepted.sum().item()) > 0
 
 

@@ -55,3 +55,50 @@ def test_target_energy_kernel_matches_reference(N):
     with torch.no_grad():
         E2 = mod._energy(x.detach())
     torch.testing.assert_close(E2, E.detach(), rtol=0, atol=0)  # energy-only launch, same values
+
+
+def test_linear_residual_path_gradcheck():
+    """_Linear's residual input r with res=None (no side channel) returns its gradient to
+    autograd: numerical gradcheck in float32 with float32-sized steps."""
+    from flowstate.normflows.autograd_flow import _Linear
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn((40, 24), generator=g).cuda().requires_grad_(True)
+    w = (torch.randn((16, 24), generator=g) * 0.3).cuda().requires_grad_(True)
+    b = torch.randn(16, generator=g).cuda().requires_grad_(True)
+    r = torch.randn((40, 16), generator=g).cuda().requires_grad_(True)
+    assert torch.autograd.gradcheck(lambda *t: _Linear.apply(*t, None), (x, w, b, r), eps=1e-2, atol=2e-2,
+                                    rtol=1e-2, nondet_tol=1e-5)
+    y = _Linear.apply(x, w, b, r, None)
+    (gr,) = torch.autograd.grad(y.sum() * 2.0, r)
+    torch.testing.assert_close(gr, torch.full_like(r, 2.0))
+
+
+def test_linear_pair_launch_matches_two_launches():
+    """fs_linear_f32_pair (nn.Linear's backward in one launch) gives exactly what the two
+    fs_linear_f32 calls give, at the A2 training shapes and a ragged one."""
+    from flowstate import _lib
+
+    L, p = _lib.load(), _lib.ptr
+    g = torch.Generator().manual_seed(1)
+    for M, K, N in ((256, 128, 128), (232, 128, 128), (256, 128, 96), (37, 40, 24)):
+        x = torch.randn((M, K), generator=g).cuda()
+        w = torch.randn((N, K), generator=g).cuda()
+        gy = torch.randn((M, N), generator=g).cuda()
+        outs = []
+        for pair in (True, False):
+            gx, gw, gb = torch.empty_like(x), torch.empty_like(w), torch.empty(N, device="cuda")
+            g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
+            g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
+            if pair:
+                _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()))
+            else:
+                for gg in (g0, g1):
+                    _lib.check(L.fs_linear_f32(gg.M, gg.N, gg.K, gg.A, gg.sam, gg.sak, gg.B, gg.sbk, gg.sbn, None,
+                                               None, 0, gg.C, gg.ldc, gg.rowsum_a, _lib.stream_ptr()))
+            outs.append((gx, gw, gb))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b)
+        torch.testing.assert_close(outs[0][0], gy @ w, rtol=1e-5, atol=1e-4)
+        torch.testing.assert_close(outs[0][1], gy.t() @ x, rtol=1e-5, atol=1e-4)
+        torch.testing.assert_close(outs[0][2], gy.sum(0), rtol=1e-5, atol=1e-4)
