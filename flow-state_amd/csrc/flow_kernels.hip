@@ -160,7 +160,7 @@ __device__ __forceinline__ void gemm64(const float *__restrict__ X, __amdgpu_buf
 // Transposed final-layer tile of both chain halves with the column biases preset in the
 // accumulators (register i of lane half h = column 8 (i >> 2) + 4 h + (i & 3)), turned
 // lane-per-chain by 16 v_permlane32_swap: row k of the result is tile_row(t[0][0], t[1][0], k).
-template <int XS>
+template <int XS, int FPD = 4>
 __device__ __forceinline__ void final_tile(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
                                            int tile, const float *__restrict__ b, f32x16 (&t)[2][1]) {
     const int h = (threadIdx.x >> 5) & 1;
@@ -170,14 +170,14 @@ __device__ __forceinline__ void final_tile(const float *__restrict__ X, __amdgpu
 #pragma unroll
         for (int j = 0; j < 4; ++j) t[0][0][4 * g + j] = t[1][0][4 * g + j] = v[j];
     }
-    gemm64<XS, 2, 1, 4, true, true>(X, W, sec, kg, 0, tile, t);
+    gemm64<XS, 2, 1, FPD, true, true>(X, W, sec, kg, 0, tile, t);
     lanes_to_chains(t[0][0], t[1][0]);
 }
 
 // The same for K <= 16 with two transform features per tile: feature 2p in columns
 // 0..15, feature 2p+1 in 16..31 (ba, bb: their bias rows), so the widths / heights GEMMs
 // of a pair cost one tile each instead of two half-empty ones.
-template <int XS>
+template <int XS, int FPD = 4>
 __device__ __forceinline__ void final_tile_pair(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec,
                                                 int kg, int tile, const float *__restrict__ ba,
                                                 const float *__restrict__ bb, f32x16 (&t)[2][1]) {
@@ -188,7 +188,7 @@ __device__ __forceinline__ void final_tile_pair(const float *__restrict__ X, __a
 #pragma unroll
         for (int j = 0; j < 4; ++j) t[0][0][4 * g + j] = t[1][0][4 * g + j] = v[j];
     }
-    gemm64<XS, 2, 1, 4, true, true>(X, W, sec, kg, 0, tile, t);
+    gemm64<XS, 2, 1, FPD, true, true>(X, W, sec, kg, 0, tile, t);
     lanes_to_chains(t[0][0], t[1][0]);
 }
 
@@ -234,7 +234,7 @@ __device__ __forceinline__ void drows_dot(const DRows<QB> &g, const float *xr, i
 // d_K tail GEMM: 9 % of the pass's MFMA work.  The bin comes from the knots of the
 // searched tile (cumwidths in the density direction, cumheights when inverting), so
 // that tile runs first and the first gathers are in flight during the other tile's GEMM.
-template <int XS, int H, int K, bool INV>
+template <int XS, int H, int K, bool INV, int FPD = 4>
 __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec,
                                              int kg, const float *__restrict__ bf, int dsec,
                                              const float *__restrict__ bd, float *CO, int cs, int p, int j,
@@ -248,7 +248,7 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
     float ks[K + 1];
     {
         f32x16 acc[2][1];
-        final_tile<XS>(X, W, sec, kg, 2 * j + TS, bf + 32 * TS, acc);
+        final_tile<XS, FPD>(X, W, sec, kg, 2 * j + TS, bf + 32 * TS, acc);
         pf.mark(PH_FINAL_GEMM);
         float u[K];
 #pragma unroll
@@ -283,7 +283,7 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
     float o0, o1;
     {
         f32x16 acc[2][1];
-        final_tile<XS>(X, W, sec, kg, 2 * j + 1 - TS, bf + 32 * (1 - TS), acc);
+        final_tile<XS, FPD>(X, W, sec, kg, 2 * j + 1 - TS, bf + 32 * (1 - TS), acc);
         pf.mark(PH_FINAL_GEMM);
         float u[K], ko[K + 1];
 #pragma unroll
@@ -713,6 +713,18 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
 // (tests/test_gpu_wide.py); only the schedule differs.  The state between phases (a few
 // MB at these sizes) stays in the L2 / MALL.
 // ---------------------------------------------------------------------------
+// Weight-fragment ring depths of the wide path: its launches start with the weights in
+// no L2 (every phase streams them from the MALL / HBM), so more k-groups are in flight
+// than in the fused kernel, whose weights stay L2-resident.  Latency only: the operand
+// order and the results are the fused kernel's.
+#ifndef FS_WIDE_PD
+#define FS_WIDE_PD 16
+#endif
+#ifndef FS_WIDE_FPD
+#define FS_WIDE_FPD 8
+#endif
+constexpr int kWidePD = FS_WIDE_PD, kWideFPD = FS_WIDE_FPD;
+
 struct WideArgs {
     FlowArgs a;
     float *CO;     // [R][D]
@@ -852,15 +864,15 @@ __global__ void __launch_bounds__(256) wide_gemm_kernel(WideArgs w) {
     const int col = 32 * tile + r;
     f32x16 acc[1][1];
     if (KIND == 0) {
-        gemm64<XS, 1, 1, FS_RPD>(Xs, W, (int)(PL.win * 4), kg, 0, tile, acc);
+        gemm64<XS, 1, 1, kWidePD>(Xs, W, (int)(PL.win * 4), kg, 0, tile, acc);
     } else {
         const int w0 = (int)((PL.blocks + w.jb * PL.block_stride) * 4);
         if (KIND == 1) {
-            gemm64<XS, 1, 1, FS_RPD>(Xs, W, w0, kg, 0, tile, acc);
+            gemm64<XS, 1, 1, kWidePD>(Xs, W, w0, kg, 0, tile, acc);
         } else {
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[0][0][i] = w.HR[(rowt + acc_row(0, i, h)) * H + col];
-            gemm64<XS, 1, 1, FS_RPD, true>(Xs, W, w0 + (int)(PL.block_stride * 2), kg, 0, tile, acc);
+            gemm64<XS, 1, 1, kWidePD, true>(Xs, W, w0 + (int)(PL.block_stride * 2), kg, 0, tile, acc);
         }
     }
     if (KIND == 1) {
@@ -955,8 +967,8 @@ __global__ void __launch_bounds__(64 * WPB) wide_final_kernel(WideArgs w) {
         const float *ba = V + PL.v_bf + 96 * ja;
         const float *bb = hb ? V + PL.v_bf + 96 * jb : ba + 16;
         f32x16 tS[2][1], tO[2][1];
-        final_tile_pair<XS>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + TS, ba + 32 * TS, bb + 32 * TS, tS);
-        final_tile_pair<XS>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + 1 - TS, ba + 32 * (1 - TS), bb + 32 * (1 - TS),
+        final_tile_pair<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + TS, ba + 32 * TS, bb + 32 * TS, tS);
+        final_tile_pair<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + 1 - TS, ba + 32 * (1 - TS), bb + 32 * (1 - TS),
                             tO);
         lc[ja] = spline_from_tiles<XS, H, K, INV>(tS, tO, 0, X, W, (int)((PL.wd + (int64_t)ja * H * (K + 1)) * 4),
                                                   V + PL.v_bd + ja * (K + 1), CO, cs, (2 * ja + 1 + off) % D, a,
@@ -967,7 +979,7 @@ __global__ void __launch_bounds__(64 * WPB) wide_final_kernel(WideArgs w) {
                                                       nan_any, pf);
     } else {
         const int j = u;
-        lc[j] = cond_spline<XS, H, K, MODE != MODE_DENSITY>(
+        lc[j] = cond_spline<XS, H, K, MODE != MODE_DENSITY, kWideFPD>(
             X, W, (int)(PL.wf * 4), PL.kg_h, V + PL.v_bf + 96 * j, (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
             V + PL.v_bd + j * (K + 1), CO, cs, (2 * j + 1 + off) % D, j, a, nan_any, pf);
     }
