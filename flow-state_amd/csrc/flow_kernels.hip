@@ -698,9 +698,9 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
 // workgroups as it has independent tiles:
 //   input   rows -> CO (coordinates, [R][2N] physical order), log-det partials zeroed
 //   start   per layer: (sampling) roll + unconditional spline, periodic features -> XA
-//   GEMMs   initial layer, then per residual block GEMM0 / GEMM1: one wave per 32x32
-//           output tile, its 32 activation rows staged in LDS; epilogues as the fused
-//           kernel's (BatchNorm folded, ReLU, residual stream HR without deferred biases)
+//   trunk   the layer's ResidualNet per 32-row tile (the fused kernel's trunk for one row
+//           group): one wave per 32-column tile, activations in LDS between the GEMMs
+//           (BatchNorm folded, ReLU, residual stream in the accumulators)
 //   final   per (64-row block, feature unit): the final layer + conditional spline of one
 //           transform feature (a pair for K <= 16), (density) the unconditional spline of
 //           the same-index identity feature; log-dets per feature to LDC / LDU
@@ -728,9 +728,8 @@ constexpr int kWidePD = FS_WIDE_PD, kWideFPD = FS_WIDE_FPD;
 struct WideArgs {
     FlowArgs a;
     float *CO;     // [R][D]
-    float *XA;     // [R][XS] periodic features, GEMM1 / initial-layer epilogue output (final-layer input)
-    float *XB;     // [R][XS] GEMM0 epilogue output
-    float *HR;     // [R][H] residual stream without its deferred biases
+    float *XA;     // [R][XS] periodic features (the trunk's input)
+    float *XB;     // [R][XS] the final layer's input (the trunk's output)
     float *LDW;    // [R][8] log-det partial of virtual wave w (the fused kernel's wave w)
     float *LDC;    // [R][N] the last final phase's conditional log-det of transform feature j
     float *LDU;    // [R][N] (density) its unconditional log-det of identity feature f
@@ -833,68 +832,52 @@ __global__ void __launch_bounds__(kThreads) wide_start_kernel(WideArgs w) {
     for (int c = D + wid; c < 8 * PL.kg_in; c += kWaves) X[lane * XS + c] = 0.f;
 }
 
-// One residual-net GEMM of a layer.  KIND 0: initial layer (XA -> HR, XB = block 0's
-// first epilogue, or h + s_h without blocks); 1: block jb's GEMM0 (XB -> XA); 2: block
-// jb's GEMM1 (HR += XA . W1 -> HR, XB = block jb+1's first epilogue or h + s_h).
-// Workgroup = 32 rows x 4 column tiles (one wave each).
-template <int H, int KIND>
-__global__ void __launch_bounds__(256) wide_gemm_kernel(WideArgs w) {
+// The layer's whole ResidualNet for one 32-row tile: the initial layer and every residual
+// block, one wave per 32-column tile (H/32 waves), the activations in LDS between GEMMs
+// (the fused kernel's trunk for one row group: same GEMMs, epilogues, deferred biases and
+// residual stream in the accumulators), reading the periodic features from XA and
+// writing the final layer's input h + s_h to XB.
+template <int H>
+__global__ void __launch_bounds__(64 * (H / 32)) wide_trunk_kernel(WideArgs w) {
     constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
-    constexpr int NT = H / 32;
-    __shared__ __attribute__((aligned(16))) float Xs[32 * XS];
+    __shared__ __attribute__((aligned(16))) float X[32 * XS];
     const FlowArgs &a = w.a;
     const int N = a.N;
     const PackLayout PL = pack_layout(N, H, a.nb, a.K);
     const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tile = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t rowt = (int64_t)blockIdx.x * 32;
-    const int tile = (int)blockIdx.y * 4 + wid;
-    const int kg = KIND == 0 ? PL.kg_in : PL.kg_h;
-    const float *Xin = (KIND == 1 ? w.XB : w.XA) + rowt * XS;
-    for (int e = threadIdx.x; e < 32 * (8 * kg / 4); e += blockDim.x) {  // the 32 rows' used columns
-        const int rr = e / (2 * kg), q = e - rr * (2 * kg);
-        *(f32x4 *)(Xs + rr * XS + 4 * q) = *(const f32x4 *)(Xin + rr * XS + 4 * q);
+    const int nq = 2 * PL.kg_in;  // 16-byte quads of the used feature columns
+    for (int e = threadIdx.x; e < 32 * nq; e += blockDim.x) {
+        const int rr = e / nq, q = e - rr * nq;
+        *(f32x4 *)(X + rr * XS + 4 * q) = *(const f32x4 *)(w.XA + (rowt + rr) * XS + 4 * q);
     }
     __syncthreads();
-    if (tile >= NT) return;
     const float *P = a.packed + (int64_t)w.layer * PL.stride;
     const float *V = P + PL.vec;
     const __amdgpu_buffer_rsrc_t W =
         __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
     const int col = 32 * tile + r;
-    f32x16 acc[1][1];
-    if (KIND == 0) {
-        gemm64<XS, 1, 1, kWidePD>(Xs, W, (int)(PL.win * 4), kg, 0, tile, acc);
-    } else {
-        const int w0 = (int)((PL.blocks + w.jb * PL.block_stride) * 4);
-        if (KIND == 1) {
-            gemm64<XS, 1, 1, kWidePD>(Xs, W, w0, kg, 0, tile, acc);
-        } else {
+    f32x16 hr[1][1], acc[1][1];
+    gemm64<XS, 1, 1, kWidePD>(X, W, (int)(PL.win * 4), PL.kg_in, 0, tile, hr);  // initial_layer
+    for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
+        const float *VB = V + PL.v_blocks + (int64_t)4 * H * jb;
+        const float e0 = VB[col], e1 = VB[H + col], e2 = VB[2 * H + col], e3 = VB[3 * H + col];
+        const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4);
+        __syncthreads();
 #pragma unroll
-            for (int i = 0; i < 16; ++i) acc[0][0][i] = w.HR[(rowt + acc_row(0, i, h)) * H + col];
-            gemm64<XS, 1, 1, kWidePD, true>(Xs, W, w0 + (int)(PL.block_stride * 2), kg, 0, tile, acc);
-        }
+        for (int i = 0; i < 16; ++i) X[acc_row(0, i, h) * XS + col] = FS_EPI(hr[0][0][i], e0, e1);
+        __syncthreads();
+        gemm64<XS, 1, 1, kWidePD>(X, W, w0, PL.kg_h, 0, tile, acc);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) X[acc_row(0, i, h) * XS + col] = FS_EPI(acc[0][0][i], e2, e3);
+        __syncthreads();
+        gemm64<XS, 1, 1, kWidePD, true>(X, W, w0 + (int)(PL.block_stride * 2), PL.kg_h, 0, tile, hr);  // h += Lin1(t)
     }
-    if (KIND == 1) {
-        const float *VB = V + PL.v_blocks + (int64_t)4 * H * w.jb;
-        const float e2 = VB[2 * H + col], e3 = VB[3 * H + col];
+    const float sh = V[col];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) w.XA[(rowt + acc_row(0, i, h)) * XS + col] = FS_EPI(acc[0][0][i], e2, e3);
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) w.HR[(rowt + acc_row(0, i, h)) * H + col] = acc[0][0][i];
-    const int jn = KIND == 0 ? 0 : w.jb + 1;  // the block whose first epilogue follows
-    if (jn < a.nb) {
-        const float *VB = V + PL.v_blocks + (int64_t)4 * H * jn;
-        const float e0 = VB[col], e1 = VB[H + col];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w.XB[(rowt + acc_row(0, i, h)) * XS + col] = FS_EPI(acc[0][0][i], e0, e1);
-    } else {
-        const float sh = V[col];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w.XB[(rowt + acc_row(0, i, h)) * XS + col] = acc[0][0][i] + sh;
-    }
+    for (int i = 0; i < 16; ++i) w.XB[(rowt + acc_row(0, i, h)) * XS + col] = hr[0][0][i] + sh;
 }
 
 // One feature of uncond_spline_w: the same arithmetic, its log-det returned (0 outside).
@@ -1238,8 +1221,8 @@ constexpr int64_t kWideMaxRows = 65536;  // the workspace never grows beyond thi
 
 static size_t wide_bytes(int64_t R, int N, int H) {
     const int64_t XS = flow_xw(H) + 4;
-    return (size_t)(rup(R * 2 * N * 4, 256) + 2 * rup(R * XS * 4, 256) + rup(R * H * 4, 256) +
-                    rup(R * kWaves * 4, 256) + 2 * rup(R * N * 4, 256));
+    return (size_t)(rup(R * 2 * N * 4, 256) + 2 * rup(R * XS * 4, 256) + rup(R * kWaves * 4, 256) +
+                    2 * rup(R * N * 4, 256));
 }
 
 struct WideLaunch {
@@ -1384,8 +1367,6 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     p += rup(R * XS * 4, 256);
     w.XB = (float *)p;
     p += rup(R * XS * 4, 256);
-    w.HR = (float *)p;
-    p += rup(R * H * 4, 256);
     w.LDW = (float *)p;
     p += rup(R * kWaves * 4, 256);
     w.LDC = (float *)p;
@@ -1402,21 +1383,15 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
         if (hipError_t e = fs_set_max_lds_once((const void *)kf, attr_set); e != hipSuccess) return e;
     }
     std::vector<WideLaunch> seq;
-    seq.reserve(4 + (size_t)a.L * (3 + 2 * a.nb));
+    seq.reserve(4 + (size_t)a.L * 3);
     auto add = [&](const void *f, dim3 g, dim3 b, unsigned lds) { seq.push_back({f, g, b, lds, w}); };
     add((const void *)wide_input_kernel<MODE>, dim3(nblk), dim3(256), 0);
-    const dim3 ggrid((unsigned)(R / 32), (unsigned)((H / 32 + 3) / 4));
     for (int s = 0; s < a.L; ++s) {
         w.layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
         if (MODE != MODE_DENSITY) w.off = (w.off + N) % D;
         w.pending = s > 0;
         add((const void *)wide_start_kernel<H, K, MODE>, dim3(nblk), dim3(kThreads), 0);
-        add((const void *)wide_gemm_kernel<H, 0>, ggrid, dim3(256), 0);
-        for (int jb = 0; jb < a.nb; ++jb) {
-            w.jb = jb;
-            add((const void *)wide_gemm_kernel<H, 1>, ggrid, dim3(256), 0);
-            add((const void *)wide_gemm_kernel<H, 2>, ggrid, dim3(256), 0);
-        }
+        add((const void *)wide_trunk_kernel<H>, dim3((unsigned)(R / 32)), dim3(64 * (H / 32)), 0);
         add((const void *)wide_final_kernel<H, K, MODE, WPW>, dim3(nblk, (units + WPW - 1) / WPW), dim3(64 * WPW),
             fin_lds);
         if (MODE == MODE_DENSITY) w.off = (w.off + N) % D;
