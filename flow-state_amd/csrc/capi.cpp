@@ -499,6 +499,24 @@ int fs_linear_f32_pair(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, void *strea
     return hip_rc(fs_linear_f32_pair_impl(a[0], a[1], (hipStream_t)stream), "fs_linear_f32_pair");
 }
 
+int fs_linear_f32_ex(const fs_gemm_f32 *d, const fs_bn_in *bn, float *stats_out, void *stream) {
+    REQUIRE(d, "fs_linear_f32_ex: NULL descriptor");
+    const fs_gemm_f32 &g = *d;
+    REQUIRE(g.M >= 0 && g.N >= 0 && g.K >= 0 && (g.M == 0 || g.N == 0 || (g.C && (g.K == 0 || (g.A && g.B)))) &&
+                g.ldc >= g.N && (!g.R || g.ldr >= g.N),
+            "fs_linear_f32_ex: invalid arguments");
+    REQUIRE(g.M <= 32LL * 65535 && g.N <= 32LL * 65535, "fs_linear_f32_ex: M, N at most %lld", 32LL * 65535);
+    fs::GemmArgs a{g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C, g.ldc, g.rowsum_a};
+    a.stats = stats_out;
+    if (!bn) return hip_rc(fs_linear_f32_impl(a, (hipStream_t)stream), "fs_linear_f32_ex");
+    REQUIRE(bn->stats && bn->gamma && bn->beta && bn->rows >= 2 && bn->tiles == (bn->rows + 31) / 32 &&
+                bn->rows == g.M && g.K <= 256 && bn->eps > 0.f && (!bn->running_mean) == (!bn->running_var),
+            "fs_linear_f32_ex: invalid BatchNorm arguments");
+    fs::BnIn b{bn->stats, bn->tiles, bn->rows, bn->gamma, bn->beta, bn->eps, bn->momentum, bn->running_mean,
+               bn->running_var, bn->num_batches, bn->mean_out, bn->invstd_out, bn->a_out};
+    return hip_rc(fs_linear_bn_f32_impl(a, &b, (hipStream_t)stream), "fs_linear_f32_ex");
+}
+
 int fs_bn_relu_train_fwd(int64_t Bn, int32_t H, const float *x, const float *gamma, const float *beta,
                          float *running_mean, float *running_var, int64_t *num_batches, double momentum, double eps,
                          float *y, float *mean, float *invstd, void *stream) {

@@ -1185,7 +1185,7 @@ static int64_t wide_rows_limit() {
     int64_t lim = g_wide_rows.load(std::memory_order_relaxed);
     if (lim < 0) {
         const char *e = getenv("FS_WIDE_ROWS");
-        lim = e ? atoll(e) : 8192;
+        lim = e ? atoll(e) : 12288;
         if (lim < 0) lim = 0;
         int64_t expect = -1;
         g_wide_rows.compare_exchange_strong(expect, lim);

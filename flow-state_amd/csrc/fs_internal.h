@@ -98,10 +98,27 @@ struct GemmArgs {
     float *C;
     int64_t ldc;
     float *rowsum_a;
+    float *stats = nullptr;  // [ceil(M/32)][N][2] per 32-row tile: column mean, sum of squared deviations
+};
+// BatchNorm1d (train) + ReLU applied to the A operand as it is loaded (A = the raw
+// pre-BatchNorm activations x [rows][K], row-major): batch statistics combined from the
+// producer's per-tile column statistics (Chan's formula, tiles in order), u = relu(gamma
+// (x - mean) invstd + beta).  Workgroup (0, 0) writes mean / invstd and updates the
+// running statistics; the workgroups of column tile 0 write u (a_out, nullable).
+struct BnIn {
+    const float *stats;  // [tiles][K][2] from the producer's epilogue
+    int64_t tiles, rows;
+    const float *gamma, *beta;
+    float eps, momentum;
+    float *running_mean, *running_var;
+    int64_t *num_batches;
+    float *mean_out, *invstd_out;
+    float *a_out;
 };
 }  // namespace fs
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st);
 hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, hipStream_t st);
+hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipStream_t st);
 hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,
                                      float *rm, float *rv, int64_t *nbt, float momentum, float eps, float *y,
                                      float *mean, float *invstd, hipStream_t st);

@@ -67,9 +67,19 @@ struct GemmLds {
     float rs_part[SPLIT][64];
 };
 
+constexpr int kBnMaxK = 256;  // BatchNorm-in-load: widest A (the conditioner's hidden width)
+
+// A operand with BatchNorm + ReLU applied on load (bn_relu_train_fwd's arithmetic).
+struct BnLoad {
+    const float *mu, *is, *gm, *bt;  // LDS, per k
+    float *a_out;                    // nullable: u written back (column tile 0 only)
+    int64_t lda;
+};
+
 // One 32 x 32 output tile (bx, by) of g by the workgroup's SPLIT waves.
-template <int SPLIT, bool AK, bool BK>
-__device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t by, GemmLds<SPLIT> &L) {
+template <int SPLIT, bool AK, bool BK, bool BNA = false>
+__device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t by, GemmLds<SPLIT> &L,
+                                          const BnLoad *bnl = nullptr) {
     auto &part = L.part;
     auto &rs_part = L.rs_part;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -89,10 +99,26 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
     const int64_t step = 8 * SPLIT;
     const int64_t kb0 = 8 * w;
     t4 a[PF], b[PF];
+    // BNA: u = relu(gamma (x - mean) invstd + beta) of the loaded A elements (k < K only)
+    auto bn = [&](t4 v, int64_t k0, bool ok) {
+        if constexpr (BNA) {
+            if (!ok) return v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t k = k0 + j;
+                if (k < g.K) {
+                    const float o = bnl->gm[k] * ((v[j] - bnl->mu[k]) * bnl->is[k]) + bnl->bt[k];
+                    v[j] = o > 0.f ? o : 0.f;
+                    if (bnl->a_out) bnl->a_out[(m0 + r) * bnl->lda + k] = v[j];
+                }
+            }
+        }
+        return v;
+    };
 #pragma unroll
     for (int s = 0; s < PF; ++s) {
         const int64_t k = kb0 + s * step;
-        a[s] = load4<AK>(Ap, g.sak, k + 4 * h, g.K, aok && k < g.K);
+        a[s] = bn(load4<AK>(Ap, g.sak, k + 4 * h, g.K, aok && k < g.K), k + 4 * h, aok && k < g.K);
         b[s] = load4<BK>(Bp, g.sbk, k + 4 * h, g.K, bok && k < g.K);
     }
     for (int64_t kb = kb0; kb < g.K; kb += PF * step) {
@@ -105,7 +131,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][j], b[s][j], acc, 0, 0, 0);
                 if (rows) rs += ((a[s][0] + a[s][1]) + a[s][2]) + a[s][3];
                 const int64_t kn = k + PF * step;
-                a[s] = load4<AK>(Ap, g.sak, kn + 4 * h, g.K, aok && kn < g.K);
+                a[s] = bn(load4<AK>(Ap, g.sak, kn + 4 * h, g.K, aok && kn < g.K), kn + 4 * h, aok && kn < g.K);
                 b[s] = load4<BK>(Bp, g.sbk, kn + 4 * h, g.K, bok && kn < g.K);
             }
         }
@@ -127,15 +153,33 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
         if (h == 0 && aok) g.rowsum_a[m0 + r] = rs;
     }
     const int64_t col = n0 + r;
-    if (!bok) return;
-    const float bias = g.bias ? g.bias[col] : 0.f;
+    const float bias = (g.bias && bok) ? g.bias[col] : 0.f;
+    float sv = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
-        if (row < g.M) {
-            float v = acc[i] + bias;
+        float v = acc[i] + bias;
+        if (row < g.M && bok) {
             if (g.R) v = v + g.R[row * g.ldr + col];
             g.C[row * g.ldc + col] = v;
+        }
+        acc[i] = v;
+        if (row < g.M) sv += v;
+    }
+    if (g.stats) {  // this tile's column mean and sum of squared deviations (the consumer's BatchNorm)
+        const int64_t nr = g.M - m0 < 32 ? g.M - m0 : 32;
+        const float mean = (sv + __shfl_xor(sv, 32)) / (float)nr;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
+            const float d = acc[i] - mean;
+            if (row < g.M) q += d * d;
+        }
+        q += __shfl_xor(q, 32);
+        if (h == 0 && bok) {
+            g.stats[(bx * g.N + col) * 2] = mean;
+            g.stats[(bx * g.N + col) * 2 + 1] = q;
         }
     }
 }
@@ -144,6 +188,46 @@ template <int SPLIT, bool AK, bool BK>
 __global__ __launch_bounds__(64 * SPLIT) void gemm_f32_kernel(GemmArgs g) {
     __shared__ GemmLds<SPLIT> L;
     gemm_tile<SPLIT, AK, BK>(g, blockIdx.x, blockIdx.y, L);
+}
+
+// nn.Linear of relu(BatchNorm1d_train(x)): every workgroup combines the producer's tile
+// statistics of all K columns (Chan's pairwise update, tiles in order; biased variance),
+// then runs the tile with the BatchNorm + ReLU applied to A on load.
+template <int SPLIT, bool AK, bool BK>
+__global__ __launch_bounds__(64 * SPLIT) void gemm_bn_f32_kernel(GemmArgs g, BnIn bn) {
+    __shared__ GemmLds<SPLIT> L;
+    __shared__ float mu[kBnMaxK], is[kBnMaxK], gm[kBnMaxK], bt[kBnMaxK];
+    const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
+    for (int64_t k = threadIdx.x; k < g.K; k += blockDim.x) {
+        float n = 0.f, mean = 0.f, m2 = 0.f;
+        for (int64_t t = 0; t < bn.tiles; ++t) {
+            const float nb = (float)(bn.rows - 32 * t < 32 ? bn.rows - 32 * t : 32);
+            const float mb = bn.stats[(t * g.K + k) * 2], qb = bn.stats[(t * g.K + k) * 2 + 1];
+            const float nn = n + nb, d = mb - mean;
+            mean = mean + d * (nb / nn);
+            m2 = m2 + qb + d * d * (n * nb / nn);
+            n = nn;
+        }
+        const float var = m2 / (float)bn.rows;
+        const float invstd = 1.f / sqrtf(var + bn.eps);
+        mu[k] = mean;
+        is[k] = invstd;
+        gm[k] = bn.gamma[k];
+        bt[k] = bn.beta[k];
+        if (lead) {
+            if (bn.mean_out) bn.mean_out[k] = mean;
+            if (bn.invstd_out) bn.invstd_out[k] = invstd;
+            if (bn.running_mean) {
+                bn.running_mean[k] = (1.f - bn.momentum) * bn.running_mean[k] + bn.momentum * mean;
+                bn.running_var[k] = (1.f - bn.momentum) * bn.running_var[k] +
+                                    bn.momentum * (var * (float)bn.rows / (float)(bn.rows - 1));
+            }
+        }
+    }
+    if (lead && threadIdx.x == 0 && bn.num_batches) *bn.num_batches += 1;
+    __syncthreads();
+    BnLoad bl{mu, is, gm, bt, blockIdx.y == 0 ? bn.a_out : nullptr, g.sam};
+    gemm_tile<SPLIT, AK, BK, true>(g, blockIdx.x, blockIdx.y, L, &bl);
 }
 
 // Two independent products in one launch (nn.Linear's backward: input gradient and weight
@@ -361,6 +445,25 @@ hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g
     }
     if (hipError_t e = fs_linear_f32_impl(g0, st); e != hipSuccess) return e;
     return fs_linear_f32_impl(g1, st);
+}
+
+hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipStream_t st) {
+    if (!bn) return fs_linear_f32_impl(g, st);
+    if (g.M <= 0 || g.N <= 0) return hipSuccess;
+    const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0;
+    const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0;
+    if (g.K > kBnMaxK || g.rowsum_a) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((g.M + 31) / 32), (unsigned)((g.N + 31) / 32));
+    const int split = gemm_split(g);
+#define FS_GB(S, A, B)                                                                                     \
+    if (split == S && ak == A && bk == B) {                                                                \
+        hipLaunchKernelGGL((gemm_bn_f32_kernel<S, A, B>), grid, dim3(64 * S), 0, st, g, *bn);             \
+        return hipGetLastError();                                                                          \
+    }
+    FS_GB(FS_GEMM_SPLIT, true, true) FS_GB(FS_GEMM_SPLIT, true, false) FS_GB(FS_GEMM_SPLIT, false, true)
+    FS_GB(FS_GEMM_SPLIT, false, false)
+#undef FS_GB
+    return hipErrorInvalidValue;
 }
 
 hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,

@@ -46,6 +46,15 @@ class GemmF32(ctypes.Structure):
                 ("C", ctypes.c_void_p), ("ldc", ctypes.c_int64), ("rowsum_a", ctypes.c_void_p)]
 
 
+class BnIn(ctypes.Structure):
+    """fs_bn_in (include/flowstate.h): BatchNorm1d (train) + ReLU on fs_linear_f32_ex's A."""
+    _fields_ = [("stats", ctypes.c_void_p), ("tiles", ctypes.c_int64), ("rows", ctypes.c_int64),
+                ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("eps", ctypes.c_float),
+                ("momentum", ctypes.c_float), ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p),
+                ("num_batches", ctypes.c_void_p), ("mean_out", ctypes.c_void_p), ("invstd_out", ctypes.c_void_p),
+                ("a_out", ctypes.c_void_p)]
+
+
 class FlowStateError(RuntimeError):
     pass
 
@@ -95,6 +104,7 @@ _SIGS = {
     "fs_linear_f32": (ctypes.c_int, [_I64, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _P, _I64, _P, _I64,
                                      _P, _P]),
     "fs_linear_f32_pair": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(GemmF32), _P]),
+    "fs_linear_f32_ex": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(BnIn), _P, _P]),
     "fs_bn_relu_train_fwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 6 + [ctypes.c_double, ctypes.c_double]
                              + [_P] * 4),
     "fs_bn_relu_train_bwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 11),

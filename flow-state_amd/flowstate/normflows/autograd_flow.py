@@ -294,6 +294,119 @@ class _BnRelu(torch.autograd.Function):
         return gx, gg, gb, None, None
 
 
+def _gemm_desc(x, w, b, r, y):
+    """fs_gemm_f32 of nn.Linear's forward y = x W^T + b (+ r)."""
+    from .. import _lib
+
+    M, K = x.shape
+    N = w.shape[0]
+    p = _lib.ptr
+    return _lib.GemmF32(M, N, K, p(x), K, 1, p(w), 1, K, p(b), p(r), N, p(y), N, None)
+
+
+class _LinearStats(torch.autograd.Function):
+    """_Linear whose epilogue also writes each 32-row tile's column statistics of y (the
+    batch statistics of the BatchNorm that consumes y, fs_linear_f32_ex stats_out)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        from .. import _lib
+
+        x = x.contiguous()
+        M, K = x.shape
+        N = w.shape[0]
+        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        st = torch.empty(((M + 31) // 32, N, 2), dtype=torch.float32, device=x.device)
+        _lib.require_device(x, w, b)
+        _lib.check(_lib.load().fs_linear_f32_ex(_gemm_desc(x, w, b, None, y), None, _lib.ptr(st),
+                                                _lib.stream_ptr()), "fs_linear_f32_ex")
+        ctx.save_for_backward(x, w)
+        ctx.mark_non_differentiable(st)
+        return y, st
+
+    @staticmethod
+    def backward(ctx, gy, gst):
+        from .. import _lib
+
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        M, K = x.shape
+        N = w.shape[0]
+        gx, gw = torch.empty_like(x), torch.empty_like(w)
+        gb = torch.empty((N,), dtype=torch.float32, device=x.device)
+        p = _lib.ptr
+        g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
+        g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
+        _lib.check(_lib.load().fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
+        return gx, gw, gb
+
+
+class _BnReluLinear(torch.autograd.Function):
+    """Linear(relu(BatchNorm1d_train(x))) (+ r) in one launch: the BatchNorm's batch
+    statistics come from the producer's tile statistics (x_stats), the normalisation and
+    ReLU are applied to the GEMM's A operand as it is loaded, running statistics and
+    num_batches_tracked are updated as torch does, and y's own tile statistics are written
+    for the next BatchNorm (fs_linear_f32_ex).  u = relu(BN(x)) is written once for the
+    backward, which is the weight / input gradient pair on u and then the BatchNorm + ReLU
+    backward (fs_bn_relu_train_bwd, with the block's residual gradient added there as in
+    _BnRelu)."""
+
+    @staticmethod
+    def forward(ctx, x, x_stats, gamma, beta, bn, w, b, r, res=None):
+        from .. import _lib
+
+        x = x.contiguous()
+        M, K = x.shape
+        N = w.shape[0]
+        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        st = torch.empty(((M + 31) // 32, N, 2), dtype=torch.float32, device=x.device)
+        mean = torch.empty((K,), dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        u = torch.empty_like(x) if any(ctx.needs_input_grad) else None
+        p = _lib.ptr
+        _lib.require_device(x, x_stats, gamma, beta, w, b, r)
+        bi = _lib.BnIn(p(x_stats), (M + 31) // 32, M, p(gamma), p(beta), float(bn.eps), float(bn.momentum),
+                       p(bn.running_mean), p(bn.running_var), p(bn.num_batches_tracked), p(mean), p(invstd), p(u))
+        _lib.check(_lib.load().fs_linear_f32_ex(_gemm_desc(x, w, b, r, y), bi, p(st), _lib.stream_ptr()),
+                   "fs_linear_f32_ex")
+        ctx.save_for_backward(x, u, gamma, mean, invstd, w)
+        ctx.has_r = r is not None
+        ctx.res = res
+        ctx.mark_non_differentiable(st)
+        return y, st
+
+    @staticmethod
+    def backward(ctx, gy, gst):
+        from .. import _lib
+
+        x, u, gamma, mean, invstd, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        M, K = x.shape
+        N = w.shape[0]
+        L = _lib.load()
+        p = _lib.ptr
+        gu, gw = torch.empty_like(u), torch.empty_like(w)
+        gb = torch.empty((N,), dtype=torch.float32, device=x.device)
+        g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
+        g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
+        _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
+        add = None
+        if ctx.res is not None and ctx.res.g is not None:
+            add, ctx.res.g = ctx.res.g, None
+        gx = torch.empty_like(x)
+        gg = torch.empty_like(gamma)
+        gbeta = torch.empty_like(gamma)
+        _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
+                                          p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
+        gr = None
+        if ctx.has_r and ctx.needs_input_grad[7]:
+            if ctx.res is not None:
+                ctx.res.g = gy  # to the block's first BatchNorm backward (its dx_add)
+            else:
+                gr = gy
+        return gx, None, gg, gbeta, None, gw, gb, gr, None
+
+
 def _fused_ok(net, t):
     """The fused train-mode conditioner applies: f32 device activations, every BatchNorm
     in train mode with affine parameters, running statistics and a momentum, batch >= 2
@@ -329,10 +442,21 @@ class _ResidualGrad:
 
 def _conditioner_fused(net, t):
     """ResidualNet.forward (resnet.py:82-104, blocks :35-51) in train mode: every Linear
-    on fs_linear_f32 (the block's residual add fused into its second Linear), every
-    BatchNorm + ReLU pair on fs_bn_relu_train_fwd; backward: the residual gradient added
-    by the block's first BatchNorm backward."""
+    on fs_linear_f32 kernels; each BatchNorm + ReLU applied inside the Linear that consumes
+    it (its statistics from the producing Linear's epilogue, _BnReluLinear), the block's
+    residual add fused into its second Linear; backward: input / weight gradient pairs,
+    BatchNorm backward with the residual gradient added by the block's first one."""
     li = net.initial_layer
+    if _bn_in_load_ok(net):
+        t, st = _LinearStats.apply(t, li.weight, li.bias)
+        for blk in net.blocks:
+            bn0, bn1 = blk.batch_norm_layers
+            l0, l1 = blk.linear_layers
+            res = _ResidualGrad()
+            u, su = _BnReluLinear.apply(t, st, bn0.weight, bn0.bias, bn0, l0.weight, l0.bias, None, res)
+            t, st = _BnReluLinear.apply(u, su, bn1.weight, bn1.bias, bn1, l1.weight, l1.bias, t, res)
+        lf = net.final_layer
+        return _Linear.apply(t, lf.weight, lf.bias, None)
     t = _Linear.apply(t, li.weight, li.bias, None)
     for blk in net.blocks:
         bn0, bn1 = blk.batch_norm_layers
@@ -344,6 +468,12 @@ def _conditioner_fused(net, t):
         t = _Linear.apply(u, l1.weight, l1.bias, t, res)
     lf = net.final_layer
     return _Linear.apply(t, lf.weight, lf.bias, None)
+
+
+def _bn_in_load_ok(net):
+    """The BatchNorm-in-load GEMM's limit: hidden width <= 256 (its per-column statistics
+    live in LDS)."""
+    return net.initial_layer.weight.shape[0] <= 256
 
 
 def conditioner(net, ident, B):

@@ -258,7 +258,7 @@ int fs_nf_mh_step_banked(const fs_flow_dims *d, const void *packed, const fs_phy
 
 /* Largest batch (rows) the flow passes run on the wide path: phase-by-phase launches
  * spread over the whole chip instead of one 64-row workgroup carrying its rows through
- * every layer, bit-identical results (f32 image only).  Default 8192 or the
+ * every layer, bit-identical results (f32 image only).  Default 12288 or the
  * FS_WIDE_ROWS environment variable; 0 disables it; capped at 65536.  Returns the
  * previous limit.  Process-wide. */
 int64_t fs_set_wide_rows(int64_t rows);
@@ -320,6 +320,27 @@ typedef struct fs_gemm_f32 {
     float *rowsum_a;
 } fs_gemm_f32;
 int fs_linear_f32_pair(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, void *stream);
+
+/* fs_linear_f32 with the ResidualNet's BatchNorm plumbing fused in (resnet.py:35-51):
+ * stats_out (nullable) [ceil(M/32)][N][2] receives each 32-row tile's column mean and sum
+ * of squared deviations of C, the batch statistics of the BatchNorm that consumes C; bn
+ * (nullable) makes A = relu(BatchNorm1d_train(x)) of the raw x the descriptor points at,
+ * from the producer's tile statistics (Chan's combination, tiles in order, biased
+ * variance, eps): bn->mean_out / invstd_out [K] written, running statistics updated with
+ * momentum (unbiased variance) and num_batches += 1 once, u (a_out, nullable, x's layout)
+ * written for the backward.  Replaces the separate BatchNorm + ReLU launch in front of a
+ * Linear (fs_bn_relu_train_fwd).  With bn: K <= 256, A and B contiguous along k. */
+typedef struct fs_bn_in {
+    const float *stats;
+    int64_t tiles, rows;
+    const float *gamma, *beta;
+    float eps, momentum;
+    float *running_mean, *running_var;
+    int64_t *num_batches;
+    float *mean_out, *invstd_out;
+    float *a_out;
+} fs_bn_in;
+int fs_linear_f32_ex(const fs_gemm_f32 *g, const fs_bn_in *bn, float *stats_out, void *stream);
 
 /* BatchNorm1d (training mode) followed by ReLU over x [Bn][H] (row-major):
  * batch mean / biased variance, y = relu(gamma (x - mean) invstd + beta),
