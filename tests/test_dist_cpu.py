@@ -12,6 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from flowstate import parallel
+from oracle import analysis as OA
 
 
 def _free_port():
@@ -24,7 +25,14 @@ def _states(c0, C, N, L):
     # deterministic per-GLOBAL-chain configurations, as the device chains are
     out = np.empty((C, N, 2))
     for c in range(C):
-        out[c] = np.random.default_rng(1000 + c0 + c).random((N, 2)) * L
+        g = c0 + c
+        rng = np.random.default_rng(1000 + g)
+        if g % 3 == 0:    # every particle inside well A (centre (L/4, L/2), radius 1.1 r0)
+            out[c] = np.array([L / 4, L / 2]) + rng.uniform(-0.5, 0.5, (N, 2))
+        elif g % 3 == 1:  # ... well B
+            out[c] = np.array([3 * L / 4, L / 2]) + rng.uniform(-0.5, 0.5, (N, 2))
+        else:
+            out[c] = rng.random((N, 2)) * L
     return out
 
 
@@ -33,7 +41,10 @@ def _stats(states, L):
     edges = np.linspace(-B, B, 100)
     xy = (states - B).reshape(-1, 2)
     hist, _, _ = np.histogram2d(xy[:, 0], xy[:, 1], bins=[edges, edges])
-    wells = np.array([np.sum(states[:, :, 0] < L / 2), np.sum(states[:, :, 0] >= L / 2), len(states)])
+    # the reference's classify_particles (utils.py:104-141, via the oracle): all-in-A,
+    # all-in-B and samples, as BatchedMonteCarlo.well_counts accumulates them per chain
+    _, state, _ = OA.classify(states, L / 2, 1.2)
+    wells = np.array([np.sum(state == 1), np.sum(state == 2), len(states)])
     return torch.from_numpy(hist.astype(np.int64)), torch.from_numpy(wells.astype(np.int64))
 
 
@@ -63,6 +74,7 @@ def test_sharded_reduction_matches_single_process(world, tmp_path):
     want_h, want_w = _stats(_states(0, C * world, N, L), L)
     np.testing.assert_array_equal(got["hist"], want_h.numpy())
     np.testing.assert_array_equal(got["wells"], want_w.numpy())
+    assert got["wells"][0] > 0 and got["wells"][1] > 0
     seeds = np.load(out + ".seeds.npy")
     np.testing.assert_array_equal(seeds, np.arange(42, 42 + C * world, dtype=np.uint64))
 
