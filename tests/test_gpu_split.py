@@ -106,3 +106,25 @@ def test_precision_rejects_unknown():
     m = build_flow(4, L=1, H=32, nb=1, K=5)
     with pytest.raises(ValueError):
         m.set_precision("fp8")
+
+
+@pytest.mark.parametrize("prec", PRECS)
+def test_split_single_pass_log_q(prec):
+    """FS_MH_SINGLE_PASS on the split images: the propose launch's own log q against the
+    density pass of the same image on fl32(config - half_width)."""
+    from flowstate import _lib
+
+    N, C = 16, 1024
+    kw = dict(L=3, H=64, nb=2, K=8)
+    dims = OF.FlowDims(N=N, B=half_box(N), **kw)
+    m = flow_from_state_dict(OF.random_state_dict(dims, seed=13), N, bound=dims.B, **kw).set_precision(prec)
+    lib, p = _lib.load(), _lib.ptr
+    cfg = torch.empty((C, 2 * N), device="cuda")
+    cen = torch.empty_like(cfg)
+    lq1 = torch.empty(C, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    _lib.check(lib.fs_flow_propose_lq(m.dims(), p(m.packed()), C, 3, 0, 0, float(dims.B), p(cfg), p(cen), None,
+                                      p(lq1), p(err), _lib.stream_ptr()))
+    lq2 = m.log_prob(cen)
+    rel = ((lq1.double() - lq2.double()).abs() / lq2.double().abs()).cpu().numpy()
+    assert np.median(rel) < 1e-5 and rel.max() < 1e-3, (np.median(rel), rel.max())
