@@ -761,22 +761,32 @@ def main():
                           "peak_fp64_tflops": PEAK_F64_TFLOPS,
                           "frac": ENERGY_FLOP(N) * C / (t_en * 1e-3) / 1e12 / PEAK_F64_TFLOPS},
     }
+    def leg(name, fn, *a):
+        # a secondary measurement that fails is reported in the line (never silently
+        # dropped) without costing the headline; its kernels' own errors still raise there
+        try:
+            out[name] = fn(*a)
+        except Exception as e:  # noqa: BLE001
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+            print(f"bench.py: {name} failed: {e!r}", file=sys.stderr, flush=True)
+
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        out["acceptance_match"] = acceptance_match(bmc, stepper)
+        leg("acceptance_match", acceptance_match, bmc, stepper)
     if world == 1 and not args.no_alt_precision and args.precision == "f32":
-        out["alt_precision"] = alt_precisions(bmc, stepper)
+        leg("alt_precision", alt_precisions, bmc, stepper)
     if world == 1 and not args.no_single_pass and args.precision == "f32":
-        out["single_pass"] = single_pass(bmc, stepper)
+        leg("single_pass", single_pass, bmc, stepper)
     if world == 1 and not args.no_given_proposal:
-        out["given_proposal"] = given_proposal(bmc, stepper)
+        leg("given_proposal", given_proposal, bmc, stepper)
     if world == 1 and not args.no_config2:
-        out["config2"] = config2()
+        leg("config2", config2)
     if world == 1 and not args.no_config5:
-        out["config5"] = config5()
+        leg("config5", config5)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        out["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
+        leg("cpu_baseline", cpu_baseline, N, args.cpu_budget)
         # vs_baseline stays null: BASELINE.md has no published number for this metric
-        out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+        if "value" in out["cpu_baseline"]:
+            out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
