@@ -176,11 +176,11 @@ def circular_rqs_torch(x, uw, uh, ud, B, inverse):
     return torch.where(inside, o, x), torch.where(inside, l, torch.zeros_like(l))
 
 
-# Output width from which the conditioner's final layer (n (3K+1) columns, 2944 at A2)
-# goes to hipBLASLt for its forward and input gradient: its macro tiles beat the
-# 32 x 32-tile kernel there (7.0 / 11.0 us against 8.7 / 27.9 us at 256 x 2944 x 128,
-# tools/train_gemm_probe.py), while the 128-wide layers run 3x faster on fs_linear_f32.
-_WIDE = 1024
+# The conditioner's final layer (n (3K+1) columns, 2944 at A2) runs on fs_linear_f32 like
+# every other Linear: its forward over 736 output tiles, its input gradient (K = 2944 over 32
+# tiles) as split-K chunks plus an ordered reduction (csrc/train_kernels.hip); in r02 these
+# two went to hipBLASLt, whose macro tiles beat the single-phase kernel there.
+_WIDE = 1 << 62
 
 
 class _Linear(torch.autograd.Function):

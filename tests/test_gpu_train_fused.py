@@ -38,7 +38,7 @@ def gemm(M, N, K, A, sam, sak, B, sbk, sbn, bias=None, R=None, rowsum=None):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 128, 128), (256, 2944, 128), (37, 45, 13), (1, 1, 1), (64, 32, 3000),
-                                   (300, 70, 0)])
+                                   (300, 70, 0), (256, 128, 2944), (40, 24, 2051)])
 def test_linear_f32_layouts(M, N, K):
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
     x = torch.randn(M, K, device="cuda", generator=g)
