@@ -517,6 +517,26 @@ int fs_linear_f32_ex(const fs_gemm_f32 *d, const fs_bn_in *bn, float *stats_out,
     return hip_rc(fs_linear_bn_f32_impl(a, &b, (hipStream_t)stream), "fs_linear_f32_ex");
 }
 
+static bool gemm_desc_ok(const fs_gemm_f32 &g) {
+    return g.M >= 0 && g.N >= 0 && g.K >= 0 && (g.M == 0 || g.N == 0 || (g.C && (g.K == 0 || (g.A && g.B)))) &&
+           g.ldc >= g.N && (!g.R || g.ldr >= g.N) && g.M <= 32LL * 65535 && g.N <= 32LL * 65535;
+}
+
+int64_t fs_linear_f32_splitk_floats(const fs_gemm_f32 *d) {
+    if (!d || !gemm_desc_ok(*d)) return -1;
+    const fs_gemm_f32 &g = *d;
+    fs::GemmArgs a{g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C, g.ldc, g.rowsum_a};
+    return fs_linear_f32_splitk_floats_impl(a);
+}
+
+int fs_linear_f32_splitk(const fs_gemm_f32 *d, float *workspace, int64_t workspace_floats, void *stream) {
+    REQUIRE(d && gemm_desc_ok(*d), "fs_linear_f32_splitk: invalid arguments");
+    const fs_gemm_f32 &g = *d;
+    fs::GemmArgs a{g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C, g.ldc, g.rowsum_a};
+    return hip_rc(fs_linear_f32_splitk_impl(a, workspace, workspace_floats, (hipStream_t)stream),
+                  "fs_linear_f32_splitk");
+}
+
 int fs_bn_relu_train_fwd(int64_t Bn, int32_t H, const float *x, const float *gamma, const float *beta,
                          float *running_mean, float *running_var, int64_t *num_batches, double momentum, double eps,
                          float *y, float *mean, float *invstd, void *stream) {

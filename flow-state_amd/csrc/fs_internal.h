@@ -119,6 +119,8 @@ struct BnIn {
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st);
 hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, hipStream_t st);
 hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipStream_t st);
+int64_t fs_linear_f32_splitk_floats_impl(const fs::GemmArgs &g);
+hipError_t fs_linear_f32_splitk_impl(const fs::GemmArgs &g, float *part, int64_t part_floats, hipStream_t st);
 hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,
                                      float *rm, float *rv, int64_t *nbt, float momentum, float eps, float *y,
                                      float *mean, float *invstd, hipStream_t st);

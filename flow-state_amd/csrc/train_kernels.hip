@@ -21,10 +21,6 @@
 
 #include "fs_internal.h"
 
-#include <map>
-#include <mutex>
-#include <utility>
-
 // Defaults from A/B builds of the A2 training step (tools/gpu_gemm_ab.sh, batch 256,
 // profiles/r02/train/gemm_split_ab.log): 8 waves per tile, one k-block of loads in flight
 // per wave: 113 steps/s against 106 for (4, 4, 2) and 109-112 for the other mixes.
@@ -442,56 +438,49 @@ static int gemm_split(const GemmArgs &g) {
     return g.K > 8 * 4 * 16 ? FS_GEMM_SPLIT_LONG : g.K >= 256 ? FS_GEMM_SPLIT_MID : FS_GEMM_SPLIT;
 }
 
-// Partial-tile workspace of the split-K path, one per (device, stream), allocated once
-// outside stream capture (a captured graph keeps its address); nullptr = not available.
-static float *splitk_workspace(size_t bytes, hipStream_t st) {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, std::pair<float *, size_t>> ws;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    auto &e = ws[{dev, st}];
-    if (e.first) return e.second >= bytes ? e.first : nullptr;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    const size_t cap = bytes > ((size_t)16 << 20) ? bytes : ((size_t)16 << 20);
-    float *p = nullptr;
-    if (hipMalloc(&p, cap) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    e = {p, cap};
-    return p;
+hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st);
+
+// Split-K plan of a product: chunks S and the partial-tile floats it needs (0 = not used):
+// long reductions (K >= 2048) over at most 128 output tiles, no row sum / statistics.
+static int64_t splitk_plan(const GemmArgs &g, int &S, int64_t &kchunk) {
+    const int64_t tiles = ((g.M + 31) / 32) * ((g.N + 31) / 32);
+    if (!(g.K >= 2048 && g.M > 0 && g.N > 0 && tiles <= 128 && !g.rowsum_a && !g.stats)) return 0;
+    S = (int)(g.K / 256);
+    if (S > 16) S = 16;
+    kchunk = ((g.K + S - 1) / S + 7) / 8 * 8;
+    S = (int)((g.K + kchunk - 1) / kchunk);
+    return (int64_t)S * g.M * g.N;
+}
+
+int64_t fs_linear_f32_splitk_floats_impl(const GemmArgs &g) {
+    int S = 0;
+    int64_t kc = 0;
+    return splitk_plan(g, S, kc);
+}
+
+hipError_t fs_linear_f32_splitk_impl(const GemmArgs &g, float *part, int64_t part_floats, hipStream_t st) {
+    int S = 0;
+    int64_t kchunk = 0;
+    const int64_t need = splitk_plan(g, S, kchunk);
+    if (need == 0 || !part || part_floats < need) return fs_linear_f32_impl(g, st);
+    const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0 && kchunk % 4 == 0;
+    const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0 && kchunk % 4 == 0;
+    const dim3 grid((unsigned)((g.M + 31) / 32), (unsigned)((g.N + 31) / 32), (unsigned)S);
+#define FS_SK(A, B)                                                                                                  \
+    if (ak == A && bk == B)                                                                                          \
+        hipLaunchKernelGGL((gemm_splitk_kernel<FS_GEMM_SPLIT, A, B>), grid, dim3(64 * FS_GEMM_SPLIT), 0, st, g, part, \
+                           kchunk);
+    FS_SK(true, true) FS_SK(true, false) FS_SK(false, true) FS_SK(false, false)
+#undef FS_SK
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    const int64_t n = g.M * g.N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g,
+                       (const float *)part, S);
+    return hipGetLastError();
 }
 
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st) {
     if (g.M <= 0 || (g.N <= 0 && !g.rowsum_a)) return hipSuccess;
-    {  // split-K for long reductions over few tiles
-        const int64_t tiles = ((g.M + 31) / 32) * ((g.N + 31) / 32);
-        if (g.K >= 2048 && g.N > 0 && tiles <= 128 && !g.rowsum_a && !g.stats) {
-            int S = (int)(g.K / 256);
-            if (S > 16) S = 16;
-            const int64_t kchunk = ((g.K + S - 1) / S + 7) / 8 * 8;
-            S = (int)((g.K + kchunk - 1) / kchunk);
-            float *part = splitk_workspace((size_t)S * g.M * g.N * 4, st);
-            if (part) {
-                const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0 && kchunk % 4 == 0;
-                const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0 && kchunk % 4 == 0;
-                const dim3 grid((unsigned)((g.M + 31) / 32), (unsigned)((g.N + 31) / 32), (unsigned)S);
-#define FS_SK(A, B)                                                                                                \
-    if (ak == A && bk == B)                                                                                        \
-        hipLaunchKernelGGL((gemm_splitk_kernel<FS_GEMM_SPLIT, A, B>), grid, dim3(64 * FS_GEMM_SPLIT), 0, st, g, part, \
-                           kchunk);
-                FS_SK(true, true) FS_SK(true, false) FS_SK(false, true) FS_SK(false, false)
-#undef FS_SK
-                if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-                const int64_t n = g.M * g.N;
-                hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g,
-                                   (const float *)part, S);
-                return hipGetLastError();
-            }
-        }
-    }
     // one column tile even when N = 0, so that rowsum_a is still written
     const dim3 grid((unsigned)((g.M + 31) / 32), (unsigned)(g.N > 0 ? (g.N + 31) / 32 : 1));
     const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0;

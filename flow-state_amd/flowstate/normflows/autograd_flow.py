@@ -180,13 +180,37 @@ def circular_rqs_torch(x, uw, uh, ud, B, inverse):
 # every other Linear: its forward over 736 output tiles, its input gradient (K = 2944 over 32
 # tiles) as split-K chunks plus an ordered reduction (csrc/train_kernels.hip); in r02 these
 # two went to hipBLASLt, whose macro tiles beat the single-phase kernel there.
-_WIDE = 1 << 62
+
+def _gemm_desc(x, w, b, r, y):
+    """fs_gemm_f32 of nn.Linear's forward y = x W^T + b (+ r)."""
+    from .. import _lib
+
+    M, K = x.shape
+    N = w.shape[0]
+    p = _lib.ptr
+    return _lib.GemmF32(M, N, K, p(x), K, 1, p(w), 1, K, p(b), p(r), N, p(y), N, None)
+
+
+def _gemm(g, device):
+    """One fs_linear_f32 product; long reductions over few tiles take the split-K path with
+    a torch-allocated partial-tile workspace (graph-capture safe: the caching allocator)."""
+    from .. import _lib
+
+    L = _lib.load()
+    n = L.fs_linear_f32_splitk_floats(g)
+    if n > 0:
+        ws = torch.empty(n, dtype=torch.float32, device=device)
+        _lib.check(L.fs_linear_f32_splitk(g, _lib.ptr(ws), n, _lib.stream_ptr()), "fs_linear_f32_splitk")
+    else:
+        _lib.check(L.fs_linear_f32(g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C,
+                                   g.ldc, g.rowsum_a, _lib.stream_ptr()), "fs_linear_f32")
 
 
 class _Linear(torch.autograd.Function):
     """nn.Linear (+ an optional residual added to the output) through fs_linear_f32
-    (csrc/train_kernels.hip): y = x W^T + b (+ r); backward dx = dy W, dW = dy^T x and
-    db = column sums of dy (from the same launch)."""
+    (csrc/train_kernels.hip): y = x W^T + b (+ r); backward: dx = dy W and dW = dy^T x,
+    db = column sums of dy, in one launch (fs_linear_f32_pair) unless dx is a long
+    reduction (the 2944-wide final layer), which takes the split-K path."""
 
     @staticmethod
     def forward(ctx, x, w, b, r, res=None):
@@ -194,17 +218,12 @@ class _Linear(torch.autograd.Function):
 
         x = x.contiguous()
         M, K = x.shape
-        N = w.shape[0]
         ctx.save_for_backward(x, w)
         ctx.has_r = r is not None
         ctx.res = res
-        if N >= _WIDE and r is None:
-            return torch.addmm(b, x, w.t())
-        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
-        L = _lib.load()
+        y = torch.empty((M, w.shape[0]), dtype=torch.float32, device=x.device)
         _lib.require_device(x, w, b, r)
-        _lib.check(L.fs_linear_f32(M, N, K, _lib.ptr(x), K, 1, _lib.ptr(w), 1, K, _lib.ptr(b), _lib.ptr(r),
-                                   N, _lib.ptr(y), N, None, _lib.stream_ptr()), "fs_linear_f32")
+        _gemm(_gemm_desc(x, w, b, r, y), x.device)
         return y
 
     @staticmethod
@@ -216,27 +235,24 @@ class _Linear(torch.autograd.Function):
         M, K = x.shape
         N = w.shape[0]
         L = _lib.load()
+        p = _lib.ptr
         gx = gw = gb = None
-        if ctx.needs_input_grad[0] and N < _WIDE and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]):
-            # input gradient dY W and weight / bias gradients dY^T X in one launch
+        need_x = ctx.needs_input_grad[0]
+        need_w = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        if need_x:
             gx = torch.empty_like(x)
-            gw = torch.empty_like(w)
-            gb = torch.empty((N,), dtype=torch.float32, device=x.device)
-            p = _lib.ptr
             g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
-            g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
-            _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
-        elif ctx.needs_input_grad[0] and N >= _WIDE:
-            gx = torch.mm(gy, w)
-        elif ctx.needs_input_grad[0]:
-            gx = torch.empty_like(x)
-            _lib.check(L.fs_linear_f32(M, K, N, _lib.ptr(gy), N, 1, _lib.ptr(w), K, 1, None, None, 0, _lib.ptr(gx),
-                                       K, None, _lib.stream_ptr()), "fs_linear_f32")
-        if (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]) and gw is None:
+        if need_w:
             gw = torch.empty_like(w)
             gb = torch.empty((N,), dtype=torch.float32, device=x.device)
-            _lib.check(L.fs_linear_f32(N, K, M, _lib.ptr(gy), 1, N, _lib.ptr(x), K, 1, None, None, 0, _lib.ptr(gw),
-                                       K, _lib.ptr(gb), _lib.stream_ptr()), "fs_linear_f32")
+            g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
+        if need_x and need_w and L.fs_linear_f32_splitk_floats(g0) == 0:
+            _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
+        else:
+            if need_x:
+                _gemm(g0, x.device)
+            if need_w:
+                _gemm(g1, x.device)
         if ctx.res is not None and ctx.needs_input_grad[3]:
             # the residual's gradient goes to the block's first BatchNorm backward, which
             # adds it in its own launch (no autograd accumulation kernel)
@@ -292,16 +308,6 @@ class _BnRelu(torch.autograd.Function):
                                                     _lib.ptr(gg), _lib.ptr(gb), _lib.stream_ptr()),
                    "fs_bn_relu_train_bwd")
         return gx, gg, gb, None, None
-
-
-def _gemm_desc(x, w, b, r, y):
-    """fs_gemm_f32 of nn.Linear's forward y = x W^T + b (+ r)."""
-    from .. import _lib
-
-    M, K = x.shape
-    N = w.shape[0]
-    p = _lib.ptr
-    return _lib.GemmF32(M, N, K, p(x), K, 1, p(w), 1, K, p(b), p(r), N, p(y), N, None)
 
 
 class _LinearStats(torch.autograd.Function):

@@ -342,6 +342,15 @@ typedef struct fs_bn_in {
 } fs_bn_in;
 int fs_linear_f32_ex(const fs_gemm_f32 *g, const fs_bn_in *bn, float *stats_out, void *stream);
 
+/* Long reductions over few output tiles (K >= 2048, <= 128 tiles of 32 x 32, no rowsum:
+ * the input gradient of the 2944-wide final layer, 256 x 128 over K = 2944): the reduction
+ * runs as S chunks of the grid, each a partial tile by fs_linear_f32's arithmetic, then one
+ * launch adds the partials in chunk order (+ bias, + R).  workspace: caller-owned, at least
+ * fs_linear_f32_splitk_floats(g) floats (0 = this product does not take the split-K path;
+ * with a smaller or NULL workspace the call is plain fs_linear_f32). */
+int64_t fs_linear_f32_splitk_floats(const fs_gemm_f32 *g);
+int fs_linear_f32_splitk(const fs_gemm_f32 *g, float *workspace, int64_t workspace_floats, void *stream);
+
 /* BatchNorm1d (training mode) followed by ReLU over x [Bn][H] (row-major):
  * batch mean / biased variance, y = relu(gamma (x - mean) invstd + beta),
  * running_mean / running_var updated with `momentum` (unbiased variance) and
