@@ -89,13 +89,20 @@ def _fused_vs_oracle(N, dims_kw, C, steps, seed_w=11, precision="f32"):
         nll_o = np.where(a, -lq.astype(np.float64), nll_o)
         np.testing.assert_allclose(bmc.E_old.cpu().numpy(), E_o, rtol=1e-12)
         np.testing.assert_array_equal(bmc.state.cpu().numpy(), state_o)
-        # the accepted chains cache the kernel's log q (knots normalised in double): within the
-        # measured bound of the reference-order float32 value (bench acceptance_match: max 2.8e-5)
+        # the accepted chains cache the kernel's log q (knots normalised in double): each
+        # within 5e-5 relative of the reference-order float32 value, or no further from the
+        # exact (float64) value than that float32 value is (flow samples are where the
+        # reference's own float32 drifts)
         nll_g = bmc.nll_old.cpu().numpy()
         fin = a & np.isfinite(lq)
         if fin.any():
             rel = np.abs(nll_g[fin] + lq[fin]) / np.abs(lq[fin])
-            assert rel.max() <= 5e-5, rel.max()
+            sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+            ex = OF.log_prob(sd64, cen[torch.from_numpy(fin)].double(), dims).numpy()
+            e_gpu = np.abs(-nll_g[fin] - ex)
+            e_ref = np.abs(lq[fin].astype(np.float64) - ex)
+            ok = (rel <= 5e-5) | (e_gpu <= 1.1 * e_ref)
+            assert ok.all(), (rel[~ok], e_gpu[~ok], e_ref[~ok])
     bmc.check_errors()
     assert int(bmc.n_accept.item()) == total_acc
     return flips, total_acc, C * steps
