@@ -309,6 +309,7 @@ def test_banked_hybrid_steps_match_single_steps():
     # no NaN discriminant in either path (a bank reports its proposals' errors when it is
     # made, as the reference's batch pre-generation does)
     assert int(banked.err.item()) == int(single.err.item()) == 0
+    assert int(banked.accepted.sum().item()) > 0
 
 
 def test_sharded_seeds_warning():
