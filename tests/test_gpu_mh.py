@@ -329,7 +329,6 @@ def test_sharded_seeds_warning():
     assert not [w for w in rec if "proposal_seed" in str(w.message)]
     with pytest.warns(UserWarning, match="proposal_seed"):
         BatchedMonteCarlo(model, init, Physics(L, L), np.arange(C, dtype=np.uint64)[::-1].copy() + 50, chain_offset=8)
-    assert int(banked.accepted.sum().item()) > 0
 
 
 def test_nf_big_move_with_precomputed_terms():
