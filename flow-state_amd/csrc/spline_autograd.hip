@@ -388,8 +388,11 @@ __global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
     CouplingArgs c, const float *__restrict__ x, const float *__restrict__ params, const float *__restrict__ uw,
     const float *__restrict__ uh, const float *__restrict__ ud, const float *__restrict__ g_out,
     const float *__restrict__ g_lq, float *gx, float *g_params, float *g_u) {
+    // two waves per row: wave part 0 takes the conditional spline's adjoints, part 1 the
+    // unconditional one's (each lane one feature), so the row's work is spread twice as wide
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
+    const int wv = threadIdx.x >> 6, part = wv & 1;
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (wv >> 1);
     if (row >= c.rows) return;
     const float *xr = x + row * c.D;
     const float gl = g_lq ? g_lq[row] : 0.f;
@@ -405,7 +408,8 @@ __global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
         float *guh = guw + c.n * K;
         float *gud = g_u + row * c.n * P + 2 * c.n * K + j * (K + 1);
         float gw[K], gh[K], gd[K + 1];
-        if (xt >= -c.bound && xt <= c.bound) {
+        if (part == 1) {
+        } else if (xt >= -c.bound && xt <= c.bound) {
             const float *p = params + (row * c.n + j) * P;
             float w[K], h[K];
             cond_params<K>(p, c.sq, w, h);
@@ -424,7 +428,8 @@ __global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
 #pragma unroll
             for (int k = 0; k < P; ++k) gp[k] = 0.f;
         }
-        if (xi >= -c.bound && xi <= c.bound) {
+        if (part == 0) {
+        } else if (xi >= -c.bound && xi <= c.bound) {
             float g;
             rqs_point_bwd<K, false>(xi, uw + j * K, uh + j * K, ud + j * (K + 1), c.bound, goi, gl, g, gw, gh, gd);
             gx[row * c.D + pi] = g;
@@ -620,7 +625,19 @@ hipError_t fs_coupling_density_fwd_impl(const fs_coupling *cp, const float *x, c
 hipError_t fs_coupling_density_bwd_impl(const fs_coupling *cp, const float *x, const float *params, const float *uw,
                                         const float *uh, const float *ud, const float *g_out, const float *g_lq,
                                         float *gx, float *g_params, float *g_u, hipStream_t st) {
-    FS_COUPLING_LAUNCH(coupling_density_bwd_kernel, x, params, uw, uh, ud, g_out, g_lq, gx, g_params, g_u)
+    static_assert(2 * kCplRows <= 4, "launch bounds: two waves per row");
+    const fs::CouplingArgs a = coupling_args(cp);
+    if (a.rows <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((a.rows + kCplRows - 1) / kCplRows);
+#define FS_DB(KK)                                                                                                  \
+    if (cp->K == KK) {                                                                                             \
+        hipLaunchKernelGGL(coupling_density_bwd_kernel<KK>, dim3(grid), dim3(128 * kCplRows), 0, st, a, x, params, uw, \
+                           uh, ud, g_out, g_lq, gx, g_params, g_u);                                                \
+        return hipGetLastError();                                                                                  \
+    }
+    FS_DB(5) FS_DB(8) FS_DB(15) FS_DB(32)
+#undef FS_DB
+    return hipErrorInvalidValue;
 }
 
 hipError_t fs_coupling_sample_pre_impl(const fs_coupling *cp, const float *z, const float *uw, const float *uh,
