@@ -15,7 +15,7 @@ def main(d):
     per = {}
     for f in files:
         for r in csv.DictReader(open(f)):
-            k = (r["Kernel_Name"], int(r["Grid_Size"]))
+            k = (r["Kernel_Name"], int(r.get("Grid_Size") or r["Grid_Size_X"]))
             per.setdefault(k, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     out = []
     for (name, grid), ms in sorted(per.items(), key=lambda kv: -sum(kv[1])):
