@@ -499,6 +499,17 @@ int fs_linear_f32_pair(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, void *strea
     return hip_rc(fs_linear_f32_pair_impl(a[0], a[1], (hipStream_t)stream), "fs_linear_f32_pair");
 }
 
+static bool bn_in_ok(const fs_gemm_f32 &g, const fs_bn_in *bn) {
+    return bn->stats && bn->gamma && bn->beta && bn->rows >= 2 && bn->tiles == (bn->rows + 31) / 32 &&
+           bn->rows == g.M && g.K <= 256 && bn->eps > 0.f && (!bn->running_mean) == (!bn->running_var);
+}
+
+static fs::BnIn bn_in_args(const fs_bn_in *bn) {
+    return fs::BnIn{bn->stats,        bn->tiles,      bn->rows,         bn->gamma,     bn->beta,
+                    bn->eps,          bn->momentum,   bn->running_mean, bn->running_var, bn->num_batches,
+                    bn->mean_out,     bn->invstd_out, bn->a_out,        bn->var_out};
+}
+
 int fs_linear_f32_ex(const fs_gemm_f32 *d, const fs_bn_in *bn, float *stats_out, void *stream) {
     REQUIRE(d, "fs_linear_f32_ex: NULL descriptor");
     const fs_gemm_f32 &g = *d;
@@ -509,12 +520,51 @@ int fs_linear_f32_ex(const fs_gemm_f32 *d, const fs_bn_in *bn, float *stats_out,
     fs::GemmArgs a{g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C, g.ldc, g.rowsum_a};
     a.stats = stats_out;
     if (!bn) return hip_rc(fs_linear_f32_impl(a, (hipStream_t)stream), "fs_linear_f32_ex");
-    REQUIRE(bn->stats && bn->gamma && bn->beta && bn->rows >= 2 && bn->tiles == (bn->rows + 31) / 32 &&
-                bn->rows == g.M && g.K <= 256 && bn->eps > 0.f && (!bn->running_mean) == (!bn->running_var),
-            "fs_linear_f32_ex: invalid BatchNorm arguments");
-    fs::BnIn b{bn->stats, bn->tiles, bn->rows, bn->gamma, bn->beta, bn->eps, bn->momentum, bn->running_mean,
-               bn->running_var, bn->num_batches, bn->mean_out, bn->invstd_out, bn->a_out};
+    REQUIRE(bn_in_ok(g, bn), "fs_linear_f32_ex: invalid BatchNorm arguments");
+    const fs::BnIn b = bn_in_args(bn);
     return hip_rc(fs_linear_bn_f32_impl(a, &b, (hipStream_t)stream), "fs_linear_f32_ex");
+}
+
+int fs_linear_f32_ex2(const fs_gemm_f32 *d0, const fs_bn_in *bn0, float *stats0, const fs_gemm_f32 *d1,
+                      const fs_bn_in *bn1, float *stats1, void *stream) {
+    REQUIRE(d0 && d1, "fs_linear_f32_ex2: NULL descriptor");
+    const fs_gemm_f32 *d[2] = {d0, d1};
+    const fs_bn_in *bn[2] = {bn0, bn1};
+    float *so[2] = {stats0, stats1};
+    fs::GemmArgs a[2];
+    fs::BnIn b[2];
+    for (int i = 0; i < 2; ++i) {
+        const fs_gemm_f32 &g = *d[i];
+        REQUIRE(g.M >= 0 && g.N >= 0 && g.K >= 0 && (g.M == 0 || g.N == 0 || (g.C && (g.K == 0 || (g.A && g.B)))) &&
+                    g.ldc >= g.N && (!g.R || g.ldr >= g.N) && g.M <= 32LL * 65535 && g.N <= 32LL * 65535,
+                "fs_linear_f32_ex2: invalid arguments (problem %d)", i);
+        REQUIRE(!bn[i] || bn_in_ok(g, bn[i]), "fs_linear_f32_ex2: invalid BatchNorm arguments (problem %d)", i);
+        a[i] = fs::GemmArgs{g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C, g.ldc,
+                            g.rowsum_a};
+        a[i].stats = so[i];
+        if (bn[i]) b[i] = bn_in_args(bn[i]);
+    }
+    if (fs_linear_ex2_ok(a[0], bn0 ? &b[0] : nullptr, a[1], bn1 ? &b[1] : nullptr))
+        return hip_rc(fs_linear_ex2_impl(a[0], bn0 ? &b[0] : nullptr, a[1], bn1 ? &b[1] : nullptr, (hipStream_t)stream),
+                      "fs_linear_f32_ex2");
+    for (int i = 0; i < 2; ++i) {  // shapes the two-problem kernel does not take: one launch each
+        const hipError_t e = bn[i] ? fs_linear_bn_f32_impl(a[i], &b[i], (hipStream_t)stream)
+                                   : fs_linear_f32_impl(a[i], (hipStream_t)stream);
+        if (int rc = hip_rc(e, "fs_linear_f32_ex2")) return rc;
+    }
+    return 0;
+}
+
+int fs_bn_running_update(int32_t nbn, int32_t H, float *running_mean, float *running_var, int64_t *num_batches,
+                         const float *stats, int32_t passes, int64_t rows0, int64_t rows1, double momentum,
+                         void *stream) {
+    REQUIRE(nbn >= 0 && H >= 0 && passes >= 1 && passes <= 2 && rows0 >= 2 && (passes < 2 || rows1 >= 2),
+            "fs_bn_running_update: invalid arguments");
+    REQUIRE(nbn == 0 || H == 0 || (running_mean && running_var && num_batches && stats),
+            "fs_bn_running_update: NULL buffer");
+    return hip_rc(fs_bn_running_update_impl(nbn, H, running_mean, running_var, num_batches, stats, passes, rows0,
+                                            rows1, (float)momentum, (hipStream_t)stream),
+                  "fs_bn_running_update");
 }
 
 static bool gemm_desc_ok(const fs_gemm_f32 &g) {
@@ -623,4 +673,34 @@ int fs_coupling_sample_post(const fs_coupling *c, const float *params, const flo
     REQUIRE(c->rows == 0 || (params && lad_u && out && lq_out), "fs_coupling_sample_post: invalid arguments");
     return hip_rc(fs_coupling_sample_post_impl(c, params, lad_u, lq_in, out, lq_out, nan_flag, (hipStream_t)stream),
                   "fs_coupling_sample_post");
+}
+
+int fs_coupling_pair_pre(const fs_coupling *s, const float *z, const float *uw, const float *uh, const float *ud,
+                         float *t, float *out, float *lad_u, int32_t *nan_flag, const fs_coupling *d, const float *x,
+                         float *t_density, void *stream) {
+    int rc = check_coupling(s, "fs_coupling_pair_pre");
+    if (rc || (rc = check_coupling(d, "fs_coupling_pair_pre"))) return rc;
+    REQUIRE(s->K == d->K && s->D == d->D, "fs_coupling_pair_pre: the two layers differ in K or D");
+    REQUIRE(s->rows == 0 || (z && uw && uh && ud && t && out && lad_u), "fs_coupling_pair_pre: invalid arguments");
+    REQUIRE(z != out, "fs_coupling_pair_pre: out must not alias z");
+    REQUIRE(d->rows == 0 || (x && t_density), "fs_coupling_pair_pre: invalid density arguments");
+    return hip_rc(fs_coupling_pair_pre_impl(s, z, uw, uh, ud, t, out, lad_u, nan_flag, d, x, t_density,
+                                            (hipStream_t)stream),
+                  "fs_coupling_pair_pre");
+}
+
+int fs_coupling_pair_post(const fs_coupling *s, const float *params, const float *lad_u, const float *lq_in,
+                          float *out, float *lq_out, int32_t *nan_flag, const fs_coupling *d, const float *x,
+                          const float *params_d, const float *uw, const float *uh, const float *ud,
+                          const float *lq_in_d, float *out_d, float *lq_out_d, void *stream) {
+    int rc = check_coupling(s, "fs_coupling_pair_post");
+    if (rc || (rc = check_coupling(d, "fs_coupling_pair_post"))) return rc;
+    REQUIRE(s->K == d->K && s->D == d->D, "fs_coupling_pair_post: the two layers differ in K or D");
+    REQUIRE(s->rows == 0 || (params && lad_u && out && lq_out), "fs_coupling_pair_post: invalid arguments");
+    REQUIRE(d->rows == 0 || (x && params_d && uw && uh && ud && out_d && lq_out_d),
+            "fs_coupling_pair_post: invalid density arguments");
+    REQUIRE(x != out_d, "fs_coupling_pair_post: out must not alias x");
+    return hip_rc(fs_coupling_pair_post_impl(s, params, lad_u, lq_in, out, lq_out, nan_flag, d, x, params_d, uw, uh,
+                                             ud, lq_in_d, out_d, lq_out_d, (hipStream_t)stream),
+                  "fs_coupling_pair_post");
 }

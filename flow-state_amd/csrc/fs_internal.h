@@ -114,11 +114,17 @@ struct BnIn {
     int64_t *num_batches;
     float *mean_out, *invstd_out;
     float *a_out;
+    float *var_out;  // nullable: the biased batch variance [K] (deferred running-statistics updates)
 };
 }  // namespace fs
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st);
 hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, hipStream_t st);
 hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipStream_t st);
+bool fs_linear_ex2_ok(const fs::GemmArgs &g0, const fs::BnIn *b0, const fs::GemmArgs &g1, const fs::BnIn *b1);
+hipError_t fs_linear_ex2_impl(const fs::GemmArgs &g0, const fs::BnIn *b0, const fs::GemmArgs &g1, const fs::BnIn *b1,
+                              hipStream_t st);
+hipError_t fs_bn_running_update_impl(int nbn, int H, float *rm, float *rv, int64_t *nbt, const float *stats,
+                                     int passes, int64_t rows0, int64_t rows1, float momentum, hipStream_t st);
 int64_t fs_linear_f32_splitk_floats_impl(const fs::GemmArgs &g);
 hipError_t fs_linear_f32_splitk_impl(const fs::GemmArgs &g, float *part, int64_t part_floats, hipStream_t st);
 hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,
@@ -131,6 +137,14 @@ hipError_t fs_coupling_density_fwd_impl(const fs_coupling *cp, const float *x, c
                                         const float *uh, const float *ud, const float *lq_in, float *out, float *lq_out,
                                         hipStream_t st);
 hipError_t fs_coupling_features_fwd_impl(const fs_coupling *cp, const float *x, float *t, hipStream_t st);
+hipError_t fs_coupling_pair_pre_impl(const fs_coupling *sp, const float *z, const float *uw, const float *uh,
+                                     const float *ud, float *t, float *out, float *lad_u, int32_t *nan_flag,
+                                     const fs_coupling *dp, const float *x, float *td, hipStream_t st);
+hipError_t fs_coupling_pair_post_impl(const fs_coupling *sp, const float *params, const float *lad_u,
+                                      const float *lq_in, float *out, float *lq_out, int32_t *nan_flag,
+                                      const fs_coupling *dp, const float *x, const float *params_d, const float *uw,
+                                      const float *uh, const float *ud, const float *lq_in_d, float *out_d,
+                                      float *lq_out_d, hipStream_t st);
 hipError_t fs_coupling_density_bwd_impl(const fs_coupling *cp, const float *x, const float *params, const float *uw,
                                         const float *uh, const float *ud, const float *g_out, const float *g_lq,
                                         float *gx, float *g_params, float *g_u, hipStream_t st);

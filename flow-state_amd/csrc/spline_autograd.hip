@@ -345,40 +345,43 @@ constexpr int kCplRows = FS_CPL_ROWS;
 
 // density direction forward (Coupling.forward), after the conditioner: both splines,
 // rolled output, lq_out = lq_in + (sum lad_cond + sum lad_uncond)
+struct DensityFwdArgs {
+    const float *x, *params, *uw, *uh, *ud, *lq_in;
+    float *out, *lq_out;
+};
+
 template <int K>
-__global__ __launch_bounds__(256) void coupling_density_fwd_kernel(CouplingArgs c, const float *__restrict__ x,
-                                                                   const float *__restrict__ params,
-                                                                   const float *__restrict__ uw,
-                                                                   const float *__restrict__ uh,
-                                                                   const float *__restrict__ ud,
-                                                                   const float *__restrict__ lq_in, float *out,
-                                                                   float *lq_out) {
+__device__ __forceinline__ void density_fwd_row(const CouplingArgs &c, const DensityFwdArgs &d, int64_t row) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
-    if (row >= c.rows) return;
-    const float *xr = x + row * c.D;
+    const float *xr = d.x + row * c.D;
     float sc = 0.f, su = 0.f;
     for (int j = lane; j < c.n; j += 64) {
         const int pi = (int)c.id[j], pt = (int)c.tr[j];
         const float xi = xr[pi], xt = xr[pt];
         float yt = xt, lt = 0.f;
         if (xt >= -c.bound && xt <= c.bound) {
-            const float *p = params + (row * c.n + j) * (3 * K + 1);
+            const float *p = d.params + (row * c.n + j) * (3 * K + 1);
             float w[K], h[K];
             cond_params<K>(p, c.sq, w, h);
             rqs_point<K, false>(xt, w, h, p + 2 * K, c.bound, yt, lt, nullptr);
         }
         float yi = xi, li = 0.f;
         if (xi >= -c.bound && xi <= c.bound)
-            rqs_point<K, false>(xi, uw + j * K, uh + j * K, ud + j * (K + 1), c.bound, yi, li, nullptr);
-        out[row * c.D + (pt + c.D - c.split) % c.D] = yt;
-        out[row * c.D + (pi + c.D - c.split) % c.D] = yi;
+            rqs_point<K, false>(xi, d.uw + j * K, d.uh + j * K, d.ud + j * (K + 1), c.bound, yi, li, nullptr);
+        d.out[row * c.D + (pt + c.D - c.split) % c.D] = yt;
+        d.out[row * c.D + (pi + c.D - c.split) % c.D] = yi;
         sc += lt;
         su += li;
     }
     sc = wave_sum(sc);
     su = wave_sum(su);
-    if (lane == 0) lq_out[row] = (lq_in ? lq_in[row] : 0.f) + (sc + su);
+    if (lane == 0) d.lq_out[row] = (d.lq_in ? d.lq_in[row] : 0.f) + (sc + su);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void coupling_density_fwd_kernel(CouplingArgs c, DensityFwdArgs d) {
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
+    if (row < c.rows) density_fwd_row<K>(c, d, row);
 }
 
 // its adjoints: gx (both halves, spline part), g_params [rows][n][3K+1], g_u the per-row
@@ -454,16 +457,19 @@ __global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
 }
 
 // density direction, before the conditioner: t = [cos(s x_id), sin(s x_id)]
-__global__ __launch_bounds__(256) void coupling_features_fwd_kernel(CouplingArgs c, const float *__restrict__ x,
-                                                                    float *t) {
+__device__ __forceinline__ void features_row(const CouplingArgs &c, const float *__restrict__ x, float *t, int64_t row) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
-    if (row >= c.rows) return;
     for (int j = lane; j < c.n; j += 64) {
         const float v = c.scale * x[row * c.D + c.id[j]];
         t[row * 2 * c.n + j] = cosf(v);
         t[row * 2 * c.n + c.n + j] = sinf(v);
     }
+}
+
+__global__ __launch_bounds__(256) void coupling_features_fwd_kernel(CouplingArgs c, const float *__restrict__ x,
+                                                                    float *t) {
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
+    if (row < c.rows) features_row(c, x, t, row);
 }
 
 // adjoint of the periodic features t = [cos(s x_id), sin(s x_id)]: gx at the identity
@@ -487,60 +493,100 @@ __global__ __launch_bounds__(256) void coupling_features_bwd_kernel(CouplingArgs
 // sampling direction (Coupling.inverse), forward only: roll, unconditional inverse spline
 // of the identity half, features of its output; out holds the new identity values and
 // the untouched transform half; lad_u[row] = its log-det sum
+struct SamplePreArgs {
+    const float *z, *uw, *uh, *ud;
+    float *t, *out, *lad_u;
+    int32_t *nan_flag;
+};
+
 template <int K>
-__global__ __launch_bounds__(256) void coupling_sample_pre_kernel(CouplingArgs c, const float *__restrict__ z,
-                                                                  const float *__restrict__ uw,
-                                                                  const float *__restrict__ uh,
-                                                                  const float *__restrict__ ud, float *t, float *out,
-                                                                  float *lad_u, int32_t *nan_flag) {
+__device__ __forceinline__ void sample_pre_row(const CouplingArgs &c, const SamplePreArgs &s, int64_t row) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
-    if (row >= c.rows) return;
-    const float *zr = z + row * c.D;
+    const float *zr = s.z + row * c.D;
     float su = 0.f;
     for (int j = lane; j < c.n; j += 64) {
         const int pi = (int)c.id[j], pt = (int)c.tr[j];
         const float xi = zr[(pi + c.split) % c.D];
         float yi = xi, li = 0.f;
         if (xi >= -c.bound && xi <= c.bound)
-            rqs_point<K, true>(xi, uw + j * K, uh + j * K, ud + j * (K + 1), c.bound, yi, li, nan_flag);
+            rqs_point<K, true>(xi, s.uw + j * K, s.uh + j * K, s.ud + j * (K + 1), c.bound, yi, li, s.nan_flag);
         const float v = c.scale * yi;
-        t[row * 2 * c.n + j] = cosf(v);
-        t[row * 2 * c.n + c.n + j] = sinf(v);
-        out[row * c.D + pi] = yi;
-        out[row * c.D + pt] = zr[(pt + c.split) % c.D];
+        s.t[row * 2 * c.n + j] = cosf(v);
+        s.t[row * 2 * c.n + c.n + j] = sinf(v);
+        s.out[row * c.D + pi] = yi;
+        s.out[row * c.D + pt] = zr[(pt + c.split) % c.D];
         su += li;
     }
     su = wave_sum(su);
-    if (lane == 0) lad_u[row] = su;
+    if (lane == 0) s.lad_u[row] = su;
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void coupling_sample_pre_kernel(CouplingArgs c, SamplePreArgs s) {
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
+    if (row < c.rows) sample_pre_row<K>(c, s, row);
 }
 
 // ... then the conditional inverse spline of the transform half in place;
 // lq_out = lq_in - (lad_u + sum lad_cond)
+struct SamplePostArgs {
+    const float *params, *lad_u, *lq_in;
+    float *out, *lq_out;
+    int32_t *nan_flag;
+};
+
 template <int K>
-__global__ __launch_bounds__(256) void coupling_sample_post_kernel(CouplingArgs c, const float *__restrict__ params,
-                                                                   const float *__restrict__ lad_u,
-                                                                   const float *__restrict__ lq_in, float *out,
-                                                                   float *lq_out, int32_t *nan_flag) {
+__device__ __forceinline__ void sample_post_row(const CouplingArgs &c, const SamplePostArgs &s, int64_t row) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
-    if (row >= c.rows) return;
     float sc = 0.f;
     for (int j = lane; j < c.n; j += 64) {
         const int pt = (int)c.tr[j];
-        const float xt = out[row * c.D + pt];
+        const float xt = s.out[row * c.D + pt];
         float yt = xt, lt = 0.f;
         if (xt >= -c.bound && xt <= c.bound) {
-            const float *p = params + (row * c.n + j) * (3 * K + 1);
+            const float *p = s.params + (row * c.n + j) * (3 * K + 1);
             float w[K], h[K];
             cond_params<K>(p, c.sq, w, h);
-            rqs_point<K, true>(xt, w, h, p + 2 * K, c.bound, yt, lt, nan_flag);
+            rqs_point<K, true>(xt, w, h, p + 2 * K, c.bound, yt, lt, s.nan_flag);
         }
-        out[row * c.D + pt] = yt;
+        s.out[row * c.D + pt] = yt;
         sc += lt;
     }
     sc = wave_sum(sc);
-    if (lane == 0) lq_out[row] = (lq_in ? lq_in[row] : 0.f) - (lad_u[row] + sc);
+    if (lane == 0) s.lq_out[row] = (s.lq_in ? s.lq_in[row] : 0.f) - (s.lad_u[row] + sc);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void coupling_sample_post_kernel(CouplingArgs c, SamplePostArgs s) {
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
+    if (row < c.rows) sample_post_row<K>(c, s, row);
+}
+
+// The training step's two passes side by side (fs_coupling_pair_pre / _post): workgroups
+// [0, nb0) run the sampling pass's layer (rows of cs), the rest the density pass's layer
+// (rows of cd), each row exactly as the single-pass kernels compute it.
+template <int K>
+__global__ __launch_bounds__(256) void coupling_pair_pre_kernel(CouplingArgs cs, SamplePreArgs s, CouplingArgs cd,
+                                                                const float *__restrict__ x, float *t, unsigned nb0) {
+    const bool dens = blockIdx.x >= nb0;
+    const int64_t row = (int64_t)(dens ? blockIdx.x - nb0 : blockIdx.x) * kCplRows + (threadIdx.x >> 6);
+    if (!dens) {
+        if (row < cs.rows) sample_pre_row<K>(cs, s, row);
+    } else if (row < cd.rows) {
+        features_row(cd, x, t, row);
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void coupling_pair_post_kernel(CouplingArgs cs, SamplePostArgs s, CouplingArgs cd,
+                                                                 DensityFwdArgs d, unsigned nb0) {
+    const bool dens = blockIdx.x >= nb0;
+    const int64_t row = (int64_t)(dens ? blockIdx.x - nb0 : blockIdx.x) * kCplRows + (threadIdx.x >> 6);
+    if (!dens) {
+        if (row < cs.rows) sample_post_row<K>(cs, s, row);
+    } else if (row < cd.rows) {
+        density_fwd_row<K>(cd, d, row);
+    }
 }
 
 }  // namespace fs
@@ -619,7 +665,8 @@ static fs::CouplingArgs coupling_args(const fs_coupling *c) {
 hipError_t fs_coupling_density_fwd_impl(const fs_coupling *cp, const float *x, const float *params, const float *uw,
                                         const float *uh, const float *ud, const float *lq_in, float *out, float *lq_out,
                                         hipStream_t st) {
-    FS_COUPLING_LAUNCH(coupling_density_fwd_kernel, x, params, uw, uh, ud, lq_in, out, lq_out)
+    const DensityFwdArgs d{x, params, uw, uh, ud, lq_in, out, lq_out};
+    FS_COUPLING_LAUNCH(coupling_density_fwd_kernel, d)
 }
 
 hipError_t fs_coupling_density_bwd_impl(const fs_coupling *cp, const float *x, const float *params, const float *uw,
@@ -643,15 +690,51 @@ hipError_t fs_coupling_density_bwd_impl(const fs_coupling *cp, const float *x, c
 hipError_t fs_coupling_sample_pre_impl(const fs_coupling *cp, const float *z, const float *uw, const float *uh,
                                        const float *ud, float *t, float *out, float *lad_u, int32_t *nan_flag,
                                        hipStream_t st) {
-    FS_COUPLING_LAUNCH(coupling_sample_pre_kernel, z, uw, uh, ud, t, out, lad_u, nan_flag)
+    const SamplePreArgs s{z, uw, uh, ud, t, out, lad_u, nan_flag};
+    FS_COUPLING_LAUNCH(coupling_sample_pre_kernel, s)
 }
 
 hipError_t fs_coupling_sample_post_impl(const fs_coupling *cp, const float *params, const float *lad_u,
                                         const float *lq_in, float *out, float *lq_out, int32_t *nan_flag,
                                         hipStream_t st) {
-    FS_COUPLING_LAUNCH(coupling_sample_post_kernel, params, lad_u, lq_in, out, lq_out, nan_flag)
+    const SamplePostArgs s{params, lad_u, lq_in, out, lq_out, nan_flag};
+    FS_COUPLING_LAUNCH(coupling_sample_post_kernel, s)
 }
 #undef FS_COUPLING_LAUNCH
+
+#define FS_PAIR_LAUNCH(KERNEL, ...)                                                                     \
+    const fs::CouplingArgs as = coupling_args(sp), ad = coupling_args(dp);                              \
+    if (sp->K != dp->K || as.rows < 0 || ad.rows < 0) return hipErrorInvalidValue;                     \
+    const unsigned nb0 = (unsigned)((as.rows + kCplRows - 1) / kCplRows);                              \
+    const unsigned nb = nb0 + (unsigned)((ad.rows + kCplRows - 1) / kCplRows);                         \
+    if (nb == 0) return hipSuccess;                                                                     \
+    const dim3 block(64 * kCplRows);                                                                    \
+    switch (sp->K) {                                                                                    \
+    case 5: hipLaunchKernelGGL((KERNEL<5>), dim3(nb), block, 0, st, __VA_ARGS__, nb0); break;           \
+    case 8: hipLaunchKernelGGL((KERNEL<8>), dim3(nb), block, 0, st, __VA_ARGS__, nb0); break;           \
+    case 15: hipLaunchKernelGGL((KERNEL<15>), dim3(nb), block, 0, st, __VA_ARGS__, nb0); break;         \
+    case 32: hipLaunchKernelGGL((KERNEL<32>), dim3(nb), block, 0, st, __VA_ARGS__, nb0); break;         \
+    default: return hipErrorInvalidValue;                                                               \
+    }                                                                                                   \
+    return hipGetLastError();
+
+hipError_t fs_coupling_pair_pre_impl(const fs_coupling *sp, const float *z, const float *uw, const float *uh,
+                                     const float *ud, float *t, float *out, float *lad_u, int32_t *nan_flag,
+                                     const fs_coupling *dp, const float *x, float *td, hipStream_t st) {
+    const SamplePreArgs s{z, uw, uh, ud, t, out, lad_u, nan_flag};
+    FS_PAIR_LAUNCH(coupling_pair_pre_kernel, as, s, ad, x, td)
+}
+
+hipError_t fs_coupling_pair_post_impl(const fs_coupling *sp, const float *params, const float *lad_u,
+                                      const float *lq_in, float *out, float *lq_out, int32_t *nan_flag,
+                                      const fs_coupling *dp, const float *x, const float *params_d, const float *uw,
+                                      const float *uh, const float *ud, const float *lq_in_d, float *out_d,
+                                      float *lq_out_d, hipStream_t st) {
+    const SamplePostArgs s{params, lad_u, lq_in, out, lq_out, nan_flag};
+    const DensityFwdArgs d{x, params_d, uw, uh, ud, lq_in_d, out_d, lq_out_d};
+    FS_PAIR_LAUNCH(coupling_pair_post_kernel, as, s, ad, d)
+}
+#undef FS_PAIR_LAUNCH
 
 hipError_t fs_coupling_features_fwd_impl(const fs_coupling *cp, const float *x, float *t, hipStream_t st) {
     const fs::CouplingArgs a = coupling_args(cp);

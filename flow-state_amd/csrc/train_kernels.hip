@@ -68,6 +68,7 @@ struct GemmLds {
 };
 
 constexpr int kBnMaxK = 256;  // BatchNorm-in-load: widest A (the conditioner's hidden width)
+constexpr int kBnStTiles = 8;  // producer tile statistics staged per LDS round (batch 256 = one round)
 
 // A operand with BatchNorm + ReLU applied on load (bn_relu_train_fwd's arithmetic).
 struct BnLoad {
@@ -190,33 +191,49 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_f32_kernel(GemmArgs g) {
     gemm_tile<SPLIT, AK, BK>(g, blockIdx.x, blockIdx.y, L);
 }
 
-// nn.Linear of relu(BatchNorm1d_train(x)): every workgroup combines the producer's tile
-// statistics of all K columns (Chan's pairwise update, tiles in order; biased variance),
-// then runs the tile with the BatchNorm + ReLU applied to A on load.
-template <int SPLIT, bool AK, bool BK>
-__global__ __launch_bounds__(64 * SPLIT) void gemm_bn_f32_kernel(GemmArgs g, BnIn bn) {
-    __shared__ GemmLds<SPLIT> L;
-    __shared__ float mu[kBnMaxK], is[kBnMaxK], gm[kBnMaxK], bt[kBnMaxK];
-    const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
-    for (int64_t k = threadIdx.x; k < g.K; k += blockDim.x) {
-        float n = 0.f, mean = 0.f, m2 = 0.f;
-        for (int64_t t = 0; t < bn.tiles; ++t) {
-            const float nb = (float)(bn.rows - 32 * t < 32 ? bn.rows - 32 * t : 32);
-            const float mb = bn.stats[(t * g.K + k) * 2], qb = bn.stats[(t * g.K + k) * 2 + 1];
-            const float nn = n + nb, d = mb - mean;
-            mean = mean + d * (nb / nn);
-            m2 = m2 + qb + d * d * (n * nb / nn);
-            n = nn;
+// The BatchNorm of a BatchNorm-in-load product: every workgroup combines the producer's
+// tile statistics of all K columns (Chan's pairwise update, tiles in order; biased
+// variance) into LDS; the problem's lead workgroup writes mean / invstd (/ var) and updates
+// the running statistics.  The producer's statistics are staged through LDS kBnStTiles
+// tiles at a time (all of a round's loads in flight together, instead of one dependent L2
+// read per tile); the host guarantees blockDim.x >= K, so thread k owns column k.
+struct BnLds {
+    float mu[kBnMaxK], is[kBnMaxK], gm[kBnMaxK], bt[kBnMaxK];
+    float sst[kBnStTiles * kBnMaxK * 2];
+};
+
+__device__ __forceinline__ void bn_prologue(const GemmArgs &g, const BnIn &bn, bool lead, BnLds &S) {
+    const int k = threadIdx.x;
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    for (int64_t t0 = 0; t0 < bn.tiles; t0 += kBnStTiles) {
+        const int nt = (int)(bn.tiles - t0 < kBnStTiles ? bn.tiles - t0 : kBnStTiles);
+        const float *src = bn.stats + t0 * g.K * 2;
+        for (int64_t i = threadIdx.x; i < nt * g.K * 2; i += blockDim.x) S.sst[i] = src[i];
+        __syncthreads();
+        if (k < g.K) {
+            for (int t = 0; t < nt; ++t) {  // Chan's pairwise update, tiles in order
+                const int64_t row0 = 32 * (t0 + t);
+                const float nb = (float)(bn.rows - row0 < 32 ? bn.rows - row0 : 32);
+                const float mb = S.sst[(t * g.K + k) * 2], qb = S.sst[(t * g.K + k) * 2 + 1];
+                const float nn = n + nb, d = mb - mean;
+                mean = mean + d * (nb / nn);
+                m2 = m2 + qb + d * d * (n * nb / nn);
+                n = nn;
+            }
         }
+        __syncthreads();
+    }
+    if (k < g.K) {
         const float var = m2 / (float)bn.rows;
         const float invstd = 1.f / sqrtf(var + bn.eps);
-        mu[k] = mean;
-        is[k] = invstd;
-        gm[k] = bn.gamma[k];
-        bt[k] = bn.beta[k];
+        S.mu[k] = mean;
+        S.is[k] = invstd;
+        S.gm[k] = bn.gamma[k];
+        S.bt[k] = bn.beta[k];
         if (lead) {
             if (bn.mean_out) bn.mean_out[k] = mean;
             if (bn.invstd_out) bn.invstd_out[k] = invstd;
+            if (bn.var_out) bn.var_out[k] = var;
             if (bn.running_mean) {
                 bn.running_mean[k] = (1.f - bn.momentum) * bn.running_mean[k] + bn.momentum * mean;
                 bn.running_var[k] = (1.f - bn.momentum) * bn.running_var[k] +
@@ -226,8 +243,64 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_bn_f32_kernel(GemmArgs g, BnI
     }
     if (lead && threadIdx.x == 0 && bn.num_batches) *bn.num_batches += 1;
     __syncthreads();
-    BnLoad bl{mu, is, gm, bt, blockIdx.y == 0 ? bn.a_out : nullptr, g.sam};
+}
+
+// nn.Linear of relu(BatchNorm1d_train(x)): bn_prologue, then the tile with the BatchNorm +
+// ReLU applied to A on load.
+template <int SPLIT, bool AK, bool BK>
+__global__ __launch_bounds__(64 * SPLIT) void gemm_bn_f32_kernel(GemmArgs g, BnIn bn) {
+    __shared__ GemmLds<SPLIT> L;
+    __shared__ BnLds S;
+    bn_prologue(g, bn, blockIdx.x == 0 && blockIdx.y == 0, S);
+    BnLoad bl{S.mu, S.is, S.gm, S.bt, blockIdx.y == 0 ? bn.a_out : nullptr, g.sam};
     gemm_tile<SPLIT, AK, BK, true>(g, blockIdx.x, blockIdx.y, L, &bl);
+}
+
+// Two independent forward products in one launch (the training step's two passes: the
+// density pass's Linear and the sampling pass's, of other layers): workgroups [0, t0) take
+// the tiles of g0 (column-major over its mt0 row tiles), the rest those of g1; each problem
+// with or without its BatchNorm-in-load (bit b of bnmask), each tile exactly as the
+// single-problem kernels compute it.  A and B contiguous along k.
+template <int SPLIT>
+__global__ __launch_bounds__(64 * SPLIT) void gemm_ex2_kernel(GemmArgs g0, BnIn b0, GemmArgs g1, BnIn b1, unsigned t0,
+                                                             unsigned mt0, unsigned mt1, int bnmask) {
+    __shared__ GemmLds<SPLIT> L;
+    __shared__ BnLds S;
+    const bool second = blockIdx.x >= t0;
+    const unsigned b = second ? blockIdx.x - t0 : blockIdx.x;
+    const unsigned mt = second ? mt1 : mt0;
+    const GemmArgs &g = second ? g1 : g0;
+    const BnIn &bn = second ? b1 : b0;
+    const unsigned bx = b % mt, by = b / mt;
+    if (bnmask & (second ? 2 : 1)) {
+        bn_prologue(g, bn, bx == 0 && by == 0, S);
+        BnLoad bl{S.mu, S.is, S.gm, S.bt, by == 0 ? bn.a_out : nullptr, g.sam};
+        gemm_tile<SPLIT, true, true, true>(g, bx, by, L, &bl);
+    } else {
+        gemm_tile<SPLIT, true, true, false>(g, bx, by, L);
+    }
+}
+
+// Deferred BatchNorm running statistics: for each of nbn BatchNorms of width H (flat
+// running buffers rm / rv [nbn][H], counters nbt [nbn]) the momentum updates of `passes`
+// passes in pass order, from stats [passes][nbn][2][H] (batch mean, biased variance;
+// rows of the pass), exactly as the in-launch update computes them; nbt += passes.
+__global__ void __launch_bounds__(256) bn_running_update_kernel(int nbn, int H, float *rm, float *rv, int64_t *nbt,
+                                                                const float *stats, int passes, int64_t rows0,
+                                                                int64_t rows1, float m) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)nbn * H) return;
+    const int64_t bnx = i / H, h = i - bnx * H;
+    float a = rm[i], v = rv[i];
+    for (int p = 0; p < passes; ++p) {
+        const int64_t rows = p == 0 ? rows0 : rows1;
+        const float *s = stats + (((int64_t)p * nbn + bnx) * 2) * H;
+        a = (1.f - m) * a + m * s[h];
+        v = (1.f - m) * v + m * (s[H + h] * (float)rows / (float)(rows - 1));
+    }
+    rm[i] = a;
+    rv[i] = v;
+    if (h == 0) nbt[bnx] += passes;
 }
 
 // Two independent products in one launch (nn.Linear's backward: input gradient and weight
@@ -529,6 +602,7 @@ hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipS
     if (g.K > kBnMaxK || g.rowsum_a) return hipErrorInvalidValue;
     const dim3 grid((unsigned)((g.M + 31) / 32), (unsigned)((g.N + 31) / 32));
     const int split = gemm_split(g);
+    if (64 * split < g.K) return hipErrorInvalidValue;  // one thread per column in the statistics prologue
 #define FS_GB(S, A, B)                                                                                     \
     if (split == S && ak == A && bk == B) {                                                                \
         hipLaunchKernelGGL((gemm_bn_f32_kernel<S, A, B>), grid, dim3(64 * S), 0, st, g, *bn);             \
@@ -538,6 +612,36 @@ hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipS
     FS_GB(FS_GEMM_SPLIT, false, false)
 #undef FS_GB
     return hipErrorInvalidValue;
+}
+
+static bool ex2_operand_ok(const GemmArgs &g, const BnIn *bn) {
+    const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0;
+    const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0;
+    return ak && bk && g.M > 0 && g.N > 0 && !g.rowsum_a && (!bn || (g.K <= kBnMaxK && 64 * gemm_split(g) >= g.K));
+}
+
+bool fs_linear_ex2_ok(const GemmArgs &g0, const BnIn *b0, const GemmArgs &g1, const BnIn *b1) {
+    return ex2_operand_ok(g0, b0) && ex2_operand_ok(g1, b1) && gemm_split(g0) == FS_GEMM_SPLIT &&
+           gemm_split(g1) == FS_GEMM_SPLIT;
+}
+
+hipError_t fs_linear_ex2_impl(const GemmArgs &g0, const BnIn *b0, const GemmArgs &g1, const BnIn *b1, hipStream_t st) {
+    if (!fs_linear_ex2_ok(g0, b0, g1, b1)) return hipErrorInvalidValue;
+    const unsigned mt0 = (unsigned)((g0.M + 31) / 32), mt1 = (unsigned)((g1.M + 31) / 32);
+    const unsigned t0 = mt0 * (unsigned)((g0.N + 31) / 32), t1 = mt1 * (unsigned)((g1.N + 31) / 32);
+    const BnIn none{};
+    hipLaunchKernelGGL(gemm_ex2_kernel<FS_GEMM_SPLIT>, dim3(t0 + t1), dim3(64 * FS_GEMM_SPLIT), 0, st, g0,
+                       b0 ? *b0 : none, g1, b1 ? *b1 : none, t0, mt0, mt1, (b0 ? 1 : 0) | (b1 ? 2 : 0));
+    return hipGetLastError();
+}
+
+hipError_t fs_bn_running_update_impl(int nbn, int H, float *rm, float *rv, int64_t *nbt, const float *stats,
+                                     int passes, int64_t rows0, int64_t rows1, float momentum, hipStream_t st) {
+    if (nbn <= 0 || H <= 0 || passes <= 0) return hipSuccess;
+    const int64_t n = (int64_t)nbn * H;
+    hipLaunchKernelGGL(bn_running_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nbn, H, rm, rv,
+                       nbt, stats, passes, rows0, rows1, momentum);
+    return hipGetLastError();
 }
 
 hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,

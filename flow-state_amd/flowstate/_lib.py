@@ -52,7 +52,7 @@ class BnIn(ctypes.Structure):
                 ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("eps", ctypes.c_float),
                 ("momentum", ctypes.c_float), ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p),
                 ("num_batches", ctypes.c_void_p), ("mean_out", ctypes.c_void_p), ("invstd_out", ctypes.c_void_p),
-                ("a_out", ctypes.c_void_p)]
+                ("a_out", ctypes.c_void_p), ("var_out", ctypes.c_void_p)]
 
 
 class FlowStateError(RuntimeError):
@@ -107,6 +107,10 @@ _SIGS = {
     "fs_linear_f32_splitk_floats": (_I64, [ctypes.POINTER(GemmF32)]),
     "fs_linear_f32_splitk": (ctypes.c_int, [ctypes.POINTER(GemmF32), _P, _I64, _P]),
     "fs_linear_f32_ex": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(BnIn), _P, _P]),
+    "fs_linear_f32_ex2": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(BnIn), _P, ctypes.POINTER(GemmF32),
+                                         ctypes.POINTER(BnIn), _P, _P]),
+    "fs_bn_running_update": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, ctypes.c_int32, _I64, _I64,
+                                            ctypes.c_double, _P]),
     "fs_bn_relu_train_fwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 6 + [ctypes.c_double, ctypes.c_double]
                              + [_P] * 4),
     "fs_bn_relu_train_bwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 11),
@@ -116,6 +120,8 @@ _SIGS = {
     "fs_coupling_features_bwd": (ctypes.c_int, [_CP] + [_P] * 5),
     "fs_coupling_sample_pre": (ctypes.c_int, [_CP] + [_P] * 9),
     "fs_coupling_sample_post": (ctypes.c_int, [_CP] + [_P] * 7),
+    "fs_coupling_pair_pre": (ctypes.c_int, [_CP] + [_P] * 8 + [_CP, _P, _P, _P]),
+    "fs_coupling_pair_post": (ctypes.c_int, [_CP] + [_P] * 6 + [_CP] + [_P] * 9),
     "fs_set_wide_rows": (_I64, [_I64]),
     "fs_target_energy": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_int32]
                          + [ctypes.c_double] * 4 + [_P, _P, _P]),

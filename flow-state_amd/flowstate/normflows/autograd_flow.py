@@ -213,7 +213,7 @@ class _Linear(torch.autograd.Function):
     reduction (the 2944-wide final layer), which takes the split-K path."""
 
     @staticmethod
-    def forward(ctx, x, w, b, r, res=None):
+    def forward(ctx, x, w, b, r, res=None, pair=None):
         from .. import _lib
 
         x = x.contiguous()
@@ -223,7 +223,16 @@ class _Linear(torch.autograd.Function):
         ctx.res = res
         y = torch.empty((M, w.shape[0]), dtype=torch.float32, device=x.device)
         _lib.require_device(x, w, b, r)
-        _gemm(_gemm_desc(x, w, b, r, y), x.device)
+        g = _gemm_desc(x, w, b, r, y)
+        if pair is not None and _lib.load().fs_linear_f32_splitk_floats(g) == 0:
+            gs, _, _ = pair.gemm("final")
+            _lib.check(_lib.load().fs_linear_f32_ex2(g, None, None, gs, None, None, _lib.stream_ptr()),
+                       "fs_linear_f32_ex2")
+            pair.commit()
+        else:
+            _gemm(g, x.device)
+            if pair is not None:
+                pair.gemm_alone("final")
         return y
 
     @staticmethod
@@ -259,8 +268,8 @@ class _Linear(torch.autograd.Function):
             if ctx.res.g is not None:
                 raise RuntimeError("residual gradient stash was never consumed by its BatchNorm backward")
             ctx.res.g = gy
-            return gx, gw, gb, None, None
-        return gx, gw, gb, (gy if ctx.has_r and ctx.needs_input_grad[3] else None), None
+            return gx, gw, gb, None, None, None
+        return gx, gw, gb, (gy if ctx.has_r and ctx.needs_input_grad[3] else None), None, None
 
 
 class _BnRelu(torch.autograd.Function):
@@ -315,7 +324,7 @@ class _LinearStats(torch.autograd.Function):
     batch statistics of the BatchNorm that consumes y, fs_linear_f32_ex stats_out)."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, pair=None):
         from .. import _lib
 
         x = x.contiguous()
@@ -324,10 +333,17 @@ class _LinearStats(torch.autograd.Function):
         y = torch.empty((M, N), dtype=torch.float32, device=x.device)
         st = torch.empty(((M + 31) // 32, N, 2), dtype=torch.float32, device=x.device)
         _lib.require_device(x, w, b)
-        _lib.check(_lib.load().fs_linear_f32_ex(_gemm_desc(x, w, b, None, y), None, _lib.ptr(st),
-                                                _lib.stream_ptr()), "fs_linear_f32_ex")
+        if pair is None:
+            _lib.check(_lib.load().fs_linear_f32_ex(_gemm_desc(x, w, b, None, y), None, _lib.ptr(st),
+                                                    _lib.stream_ptr()), "fs_linear_f32_ex")
+        else:
+            gs, bs, sts = pair.gemm("init")
+            _lib.check(_lib.load().fs_linear_f32_ex2(_gemm_desc(x, w, b, None, y), None, _lib.ptr(st), gs, bs,
+                                                     _lib.ptr(sts), _lib.stream_ptr()), "fs_linear_f32_ex2")
+            pair.commit()
         ctx.save_for_backward(x, w)
         ctx.mark_non_differentiable(st)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for st (a fill kernel per call)
         return y, st
 
     @staticmethod
@@ -335,6 +351,8 @@ class _LinearStats(torch.autograd.Function):
         from .. import _lib
 
         x, w = ctx.saved_tensors
+        if gy is None:  # y unused by the loss
+            return None, None, None, None
         gy = gy.contiguous()
         M, K = x.shape
         N = w.shape[0]
@@ -344,7 +362,7 @@ class _LinearStats(torch.autograd.Function):
         g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
         g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
         _lib.check(_lib.load().fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
-        return gx, gw, gb
+        return gx, gw, gb, None
 
 
 class _BnReluLinear(torch.autograd.Function):
@@ -358,7 +376,7 @@ class _BnReluLinear(torch.autograd.Function):
     _BnRelu)."""
 
     @staticmethod
-    def forward(ctx, x, x_stats, gamma, beta, bn, w, b, r, res=None):
+    def forward(ctx, x, x_stats, gamma, beta, bn, w, b, r, res=None, pair=None, op=None):
         from .. import _lib
 
         x = x.contiguous()
@@ -366,19 +384,31 @@ class _BnReluLinear(torch.autograd.Function):
         N = w.shape[0]
         y = torch.empty((M, N), dtype=torch.float32, device=x.device)
         st = torch.empty(((M + 31) // 32, N, 2), dtype=torch.float32, device=x.device)
-        mean = torch.empty((K,), dtype=torch.float32, device=x.device)
-        invstd = torch.empty_like(mean)
+        invstd = torch.empty((K,), dtype=torch.float32, device=x.device)
         u = torch.empty_like(x) if any(ctx.needs_input_grad) else None
         p = _lib.ptr
         _lib.require_device(x, x_stats, gamma, beta, w, b, r)
-        bi = _lib.BnIn(p(x_stats), (M + 31) // 32, M, p(gamma), p(beta), float(bn.eps), float(bn.momentum),
-                       p(bn.running_mean), p(bn.running_var), p(bn.num_batches_tracked), p(mean), p(invstd), p(u))
-        _lib.check(_lib.load().fs_linear_f32_ex(_gemm_desc(x, w, b, r, y), bi, p(st), _lib.stream_ptr()),
-                   "fs_linear_f32_ex")
+        if pair is None:
+            mean = torch.empty((K,), dtype=torch.float32, device=x.device)
+            bi = _lib.BnIn(p(x_stats), (M + 31) // 32, M, p(gamma), p(beta), float(bn.eps), float(bn.momentum),
+                           p(bn.running_mean), p(bn.running_var), p(bn.num_batches_tracked), p(mean), p(invstd),
+                           p(u), None)
+            _lib.check(_lib.load().fs_linear_f32_ex(_gemm_desc(x, w, b, r, y), bi, p(st), _lib.stream_ptr()),
+                       "fs_linear_f32_ex")
+        else:
+            # running statistics deferred to the end of the pass pair (_SamplingRider)
+            mean, var = pair.bn_slots(bn, 1)
+            bi = _lib.BnIn(p(x_stats), (M + 31) // 32, M, p(gamma), p(beta), float(bn.eps), float(bn.momentum),
+                           None, None, None, p(mean), p(invstd), p(u), p(var))
+            gs, bs, sts = pair.gemm(op)
+            _lib.check(_lib.load().fs_linear_f32_ex2(_gemm_desc(x, w, b, r, y), bi, p(st), gs, bs, p(sts),
+                                                     _lib.stream_ptr()), "fs_linear_f32_ex2")
+            pair.commit()
         ctx.save_for_backward(x, u, gamma, mean, invstd, w)
         ctx.has_r = r is not None
         ctx.res = res
         ctx.mark_non_differentiable(st)
+        ctx.set_materialize_grads(False)
         return y, st
 
     @staticmethod
@@ -386,6 +416,8 @@ class _BnReluLinear(torch.autograd.Function):
         from .. import _lib
 
         x, u, gamma, mean, invstd, w = ctx.saved_tensors
+        if gy is None:
+            return (None,) * 11
         gy = gy.contiguous()
         M, K = x.shape
         N = w.shape[0]
@@ -410,7 +442,7 @@ class _BnReluLinear(torch.autograd.Function):
                 ctx.res.g = gy  # to the block's first BatchNorm backward (its dx_add)
             else:
                 gr = gy
-        return gx, None, gg, gbeta, None, gw, gb, gr, None
+        return gx, None, gg, gbeta, None, gw, gb, gr, None, None, None
 
 
 def _fused_ok(net, t):
@@ -446,7 +478,7 @@ class _ResidualGrad:
         self.g = None
 
 
-def _conditioner_fused(net, t):
+def _conditioner_fused(net, t, pair=None):
     """ResidualNet.forward (resnet.py:82-104, blocks :35-51) in train mode: every Linear
     on fs_linear_f32 kernels; each BatchNorm + ReLU applied inside the Linear that consumes
     it (its statistics from the producing Linear's epilogue, _BnReluLinear), the block's
@@ -454,15 +486,17 @@ def _conditioner_fused(net, t):
     BatchNorm backward with the residual gradient added by the block's first one."""
     li = net.initial_layer
     if _bn_in_load_ok(net):
-        t, st = _LinearStats.apply(t, li.weight, li.bias)
-        for blk in net.blocks:
+        t, st = _LinearStats.apply(t, li.weight, li.bias, pair)
+        for i, blk in enumerate(net.blocks):
             bn0, bn1 = blk.batch_norm_layers
             l0, l1 = blk.linear_layers
             res = _ResidualGrad()
-            u, su = _BnReluLinear.apply(t, st, bn0.weight, bn0.bias, bn0, l0.weight, l0.bias, None, res)
-            t, st = _BnReluLinear.apply(u, su, bn1.weight, bn1.bias, bn1, l1.weight, l1.bias, t, res)
+            u, su = _BnReluLinear.apply(t, st, bn0.weight, bn0.bias, bn0, l0.weight, l0.bias, None, res, pair, (i, 0))
+            t, st = _BnReluLinear.apply(u, su, bn1.weight, bn1.bias, bn1, l1.weight, l1.bias, t, res, pair, (i, 1))
         lf = net.final_layer
-        return _Linear.apply(t, lf.weight, lf.bias, None)
+        return _Linear.apply(t, lf.weight, lf.bias, None, None, pair)
+    if pair is not None:
+        raise ValueError("the paired passes need the BatchNorm-in-load conditioner")
     t = _Linear.apply(t, li.weight, li.bias, None)
     for blk in net.blocks:
         bn0, bn1 = blk.batch_norm_layers
@@ -600,15 +634,18 @@ class _Features(torch.autograd.Function):
     """t = [cos(s x_id), sin(s x_id)] (nn.py:120-137) and its adjoint."""
 
     @staticmethod
-    def forward(ctx, x, layer, res=None):
+    def forward(ctx, x, layer, res=None, pair=None):
         from .. import _lib
 
         x = x.contiguous()
         t = torch.empty_like(x)
         c = _coupling_desc(layer, x.shape[0])
         _lib.require_device(x)
-        _lib.check(_lib.load().fs_coupling_features_fwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(t), _lib.stream_ptr()),
-                   "fs_coupling_features_fwd")
+        if pair is None:
+            _lib.check(_lib.load().fs_coupling_features_fwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(t),
+                                                            _lib.stream_ptr()), "fs_coupling_features_fwd")
+        else:
+            pair.pre(c, x, t)
         ctx.save_for_backward(x)
         ctx.layer = layer
         ctx.res = res
@@ -629,7 +666,7 @@ class _Features(torch.autograd.Function):
         c = _coupling_desc(ctx.layer, x.shape[0])
         _lib.check(_lib.load().fs_coupling_features_bwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(gt), _lib.ptr(gx),
                                                         _lib.ptr(add), _lib.stream_ptr()), "fs_coupling_features_bwd")
-        return gx, None, None
+        return gx, None, None, None
 
 
 class _DensitySplines(torch.autograd.Function):
@@ -638,7 +675,7 @@ class _DensitySplines(torch.autograd.Function):
     lq_out = lq_in + both log-det sums; backward through both splines."""
 
     @staticmethod
-    def forward(ctx, x, params, uw, uh, ud, lq_in, layer, res=None):
+    def forward(ctx, x, params, uw, uh, ud, lq_in, layer, res=None, pair=None):
         from .. import _lib
 
         x = x.contiguous()
@@ -651,9 +688,13 @@ class _DensitySplines(torch.autograd.Function):
         lq = torch.empty((x.shape[0],), dtype=torch.float32, device=x.device)
         c = _coupling_desc(layer, x.shape[0])
         _lib.require_device(x, params, uw, lq_in)
-        _lib.check(_lib.load().fs_coupling_density_fwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(params), _lib.ptr(uw),
-                                                       _lib.ptr(uh), _lib.ptr(ud), _lib.ptr(lq_in), _lib.ptr(out),
-                                                       _lib.ptr(lq), _lib.stream_ptr()), "fs_coupling_density_fwd")
+        if pair is None:
+            _lib.check(_lib.load().fs_coupling_density_fwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(params),
+                                                           _lib.ptr(uw), _lib.ptr(uh), _lib.ptr(ud), _lib.ptr(lq_in),
+                                                           _lib.ptr(out), _lib.ptr(lq), _lib.stream_ptr()),
+                       "fs_coupling_density_fwd")
+        else:
+            pair.post(c, x, params, uw, uh, ud, lq_in, out, lq)
         ctx.save_for_backward(x, params, uw, uh, ud)
         ctx.layer = layer
         ctx.has_lq = lq_in is not None
@@ -694,13 +735,15 @@ class _DensitySplines(torch.autograd.Function):
             # runs after this one (it needs the conditioner's adjoint, which needs gp)
             ctx.res.g = gx
             gx = None
-        return (gx, gp, guw, guh, gud, g_lq if ctx.has_lq else None, None, None)
+        return (gx, gp, guw, guh, gud, g_lq if ctx.has_lq else None, None, None, None)
 
 
-def conditioner_from_features(net, t):
+def conditioner_from_features(net, t, pair=None):
     """ResidualNet.forward from the periodic features t (the rest of conditioner())."""
     if _fused_ok(net, t):
-        return _conditioner_fused(net, t)
+        return _conditioner_fused(net, t, pair)
+    if pair is not None:
+        raise ValueError("the paired passes need the fused train-mode conditioner")
     t = net.initial_layer(t)
     for blk in net.blocks:
         u = blk.batch_norm_layers[0](t)
@@ -713,17 +756,18 @@ def conditioner_from_features(net, t):
     return net.final_layer(t)
 
 
-def density_step(layer, x, log_q):
-    """One layer of forward_kld on the device: (z, log_q + log_det), differentiable."""
+def density_step(layer, x, log_q, pair=None):
+    """One layer of forward_kld on the device: (z, log_q + log_det), differentiable.
+    pair: a _SamplingRider whose sampling-pass layer runs in the same launches."""
     p = layer.prqct
     # x feeds the features and the splines: the features backward adds the splines' x
     # gradient in its own launch (no autograd accumulation kernel)
     res = _ResidualGrad() if x.requires_grad and torch.is_grad_enabled() else None
-    t = _Features.apply(x, layer, res)
-    params = conditioner_from_features(p.transform_net, t)
+    t = _Features.apply(x, layer, res, pair)
+    params = conditioner_from_features(p.transform_net, t, pair)
     u = p.unconditional_transform
     return _DensitySplines.apply(x, params, u.unnormalized_widths, u.unnormalized_heights,
-                                 u.unnormalized_derivatives, log_q, layer, res)
+                                 u.unnormalized_derivatives, log_q, layer, res, pair)
 
 
 @torch.no_grad()
@@ -757,3 +801,213 @@ def sample_step(layer, z, log_q, nan_flag):
                                          _lib.ptr(out), _lib.ptr(lq), _lib.ptr(nan_flag), _lib.stream_ptr()),
                "fs_coupling_sample_post")
     return out, lq
+
+
+# ---------------------------------------------------------------------------
+# The training step's two passes in shared launches.  With ALPHA = 1 a step runs
+# reverse_kld's sampling pass (no autograd: its loss only gates the step and its
+# BatchNorms update their running statistics) and then forward_kld's density pass
+# (main_algorithm_2.py:446-447).  The two are independent apart from those running
+# statistics, and each launch of either is a few dozen workgroups on a 256-CU chip, so
+# they run side by side: at step s the sampling pass is at layer s and the density pass at
+# layer L-1-s, and every launch carries one problem of each (fs_linear_f32_ex2,
+# fs_coupling_pair_pre / _post).  Each problem is computed exactly as alone.  The
+# running-statistics updates, whose order the interleaving would change, are deferred:
+# the batch mean / variance of every BatchNorm of both passes go to one buffer and
+# fs_bn_running_update applies them at the end, sampling pass first, as the reference.
+
+
+class FlatBatchNorm:
+    """Every BatchNorm1d of a flow with its running buffers re-homed as rows of flat
+    buffers (values unchanged), so that fs_bn_running_update can update all of them in one
+    launch.  Needs one width and one momentum for all of them (the ResidualNets of a flow)."""
+
+    def __init__(self, model):
+        bns = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm1d)]
+        if not bns:
+            raise ValueError("no BatchNorm1d in the model")
+        H, mom = bns[0].num_features, bns[0].momentum
+        for bn in bns:
+            if (bn.num_features != H or bn.momentum != mom or mom is None or not bn.track_running_stats
+                    or bn.running_mean is None or not bn.affine):
+                raise ValueError("BatchNorms of one width, one momentum, with running statistics")
+        with torch.no_grad():
+            self.rm = torch.stack([bn.running_mean.detach() for bn in bns]).contiguous()
+            self.rv = torch.stack([bn.running_var.detach() for bn in bns]).contiguous()
+            self.nbt = torch.stack([bn.num_batches_tracked.detach().reshape(()) for bn in bns]).contiguous()
+        for i, bn in enumerate(bns):
+            bn._buffers["running_mean"] = self.rm[i]
+            bn._buffers["running_var"] = self.rv[i]
+            bn._buffers["num_batches_tracked"] = self.nbt[i]
+        self.bns = bns
+        self.index = {id(bn): i for i, bn in enumerate(bns)}
+        self.H, self.momentum = H, float(mom)
+
+    @classmethod
+    def try_build(cls, model):
+        try:
+            return cls(model)
+        except ValueError:
+            return None
+
+    def intact(self):
+        """Still the flat buffers (a .to() to another device re-allocates them)."""
+        return all(bn.running_mean.data_ptr() == self.rm[i].data_ptr() and
+                   bn.running_var.data_ptr() == self.rv[i].data_ptr() and
+                   bn.num_batches_tracked.data_ptr() == self.nbt[i].data_ptr() for i, bn in enumerate(self.bns))
+
+    def update(self, stats, rows0, rows1):
+        from .. import _lib
+
+        _lib.check(_lib.load().fs_bn_running_update(len(self.bns), self.H, _lib.ptr(self.rm), _lib.ptr(self.rv),
+                                                    _lib.ptr(self.nbt), _lib.ptr(stats), 2, int(rows0), int(rows1),
+                                                    self.momentum, _lib.stream_ptr()), "fs_bn_running_update")
+
+
+class _SamplingRider:
+    """reverse_kld's sampling pass, carried by the density pass's launches (see above):
+    holds its state (rows z, log q, NaN flag, the current layer's activations) and builds
+    its half of each shared launch."""
+
+    def __init__(self, z, flat_bn):
+        self.z = z.contiguous()
+        self.lq = None
+        self.nan_flag = torch.zeros(1, dtype=torch.int32, device=z.device)
+        self.fbn = flat_bn
+        # [pass][BatchNorm][mean | biased variance][H]; pass 0 sampling, 1 density
+        self.bnstats = torch.empty((2, len(flat_bn.bns), 2, flat_bn.H), dtype=torch.float32, device=z.device)
+        self.layer = None
+
+    def bn_slots(self, bn, p):
+        i = self.fbn.index[id(bn)]
+        return self.bnstats[p, i, 0], self.bnstats[p, i, 1]
+
+    def begin(self, layer):
+        self.layer = layer
+        u = layer.prqct.unconditional_transform
+        self.u = tuple(v.detach().contiguous() for v in (u.unnormalized_widths, u.unnormalized_heights,
+                                                         u.unnormalized_derivatives))
+        _check_shapes(layer, self.z.shape[0], None, *self.u)
+
+    def pre(self, c_density, x, t_density):
+        """fs_coupling_sample_pre of this layer + fs_coupling_features_fwd of the density's."""
+        from .. import _lib
+
+        z = self.z
+        self.t = torch.empty_like(z)
+        self.out = torch.empty_like(z)
+        self.lad_u = torch.empty((z.shape[0],), dtype=torch.float32, device=z.device)
+        self.cs = _coupling_desc(self.layer, z.shape[0])
+        p = _lib.ptr
+        _lib.check(_lib.load().fs_coupling_pair_pre(ctypes.byref(self.cs), p(z), p(self.u[0]), p(self.u[1]),
+                                                    p(self.u[2]), p(self.t), p(self.out), p(self.lad_u),
+                                                    p(self.nan_flag), ctypes.byref(c_density), p(x), p(t_density),
+                                                    _lib.stream_ptr()), "fs_coupling_pair_pre")
+        self.h, self.hst = self.t, None
+
+    def gemm(self, op):
+        """This pass's half of a shared conditioner launch: (descriptor, BatchNorm or None,
+        statistics output or None); commit() takes the result after the launch."""
+        from .. import _lib
+
+        net = self.layer.prqct.transform_net
+        p = _lib.ptr
+        bi = None
+        r = None
+        if op == "init":
+            lin, x = net.initial_layer, self.h
+        elif op == "final":
+            lin, x = net.final_layer, self.h
+        else:
+            b, j = op
+            blk = net.blocks[b]
+            lin, bn = blk.linear_layers[j], blk.batch_norm_layers[j]
+            x, xs = (self.h, self.hst) if j == 0 else (self.u0, self.u0st)
+            if j == 1:
+                r = self.h
+            mean, var = self.bn_slots(bn, 0)
+            M = x.shape[0]
+            bi = _lib.BnIn(p(xs), (M + 31) // 32, M, p(bn.weight), p(bn.bias), float(bn.eps), float(bn.momentum),
+                           None, None, None, p(mean), None, None, p(var))
+        M, N = x.shape[0], lin.weight.shape[0]
+        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        st = None if op == "final" else torch.empty(((M + 31) // 32, N, 2), dtype=torch.float32, device=x.device)
+        self._pending = (op, y, st)
+        return _gemm_desc(x, lin.weight.detach(), lin.bias.detach(), r, y), bi, st
+
+    def commit(self):
+        op, y, st = self._pending
+        self._pending = None
+        if op == "final":
+            self.params = y
+        elif op == "init" or op[1] == 1:
+            self.h, self.hst = y, st
+        else:
+            self.u0, self.u0st = y, st
+
+    def gemm_alone(self, op):
+        """The final Linear on its own when the density's takes another path (split-K)."""
+        from .. import _lib
+
+        g, _, _ = self.gemm(op)
+        _gemm(g, self.z.device)
+        self.commit()
+
+    def post(self, c_density, x, params, uw, uh, ud, lq_in, out, lq):
+        """fs_coupling_sample_post of this layer + fs_coupling_density_fwd of the density's."""
+        from .. import _lib
+
+        params_s = self.params.contiguous()
+        _check_shapes(self.layer, self.z.shape[0], params_s, *self.u)
+        lq_s = torch.empty_like(self.lad_u)
+        p = _lib.ptr
+        _lib.check(_lib.load().fs_coupling_pair_post(ctypes.byref(self.cs), p(params_s), p(self.lad_u), p(self.lq),
+                                                     p(self.out), p(lq_s), p(self.nan_flag), ctypes.byref(c_density),
+                                                     p(x), p(params), p(uw), p(uh), p(ud), p(lq_in), p(out), p(lq),
+                                                     _lib.stream_ptr()), "fs_coupling_pair_post")
+        self.z, self.lq = self.out, lq_s
+        self.t = self.out = self.h = self.hst = self.u0 = self.u0st = self.params = None
+
+
+def paired_ok(model, x, z, flat_bn):
+    """The shared-launch passes apply: device f32 rows, every layer on the fused coupling
+    kernels with the BatchNorm-in-load conditioner, one layer shape throughout, the flat
+    BatchNorm buffers intact."""
+    if flat_bn is None or not flat_bn.intact() or not torch.is_grad_enabled():
+        return False
+    flows = list(model.flows)
+    if not flows or z.shape[0] < 2 or x.shape[0] < 2:
+        return False
+    f0 = flows[0]
+    for f in flows:
+        net = f.prqct.transform_net
+        if not (fused_coupling_ok(f, x) and fused_coupling_ok(f, z) and _bn_in_load_ok(net)):
+            return False
+        if (f.num_bins, f.num_input_channels, f.num_hidden_channels, len(net.blocks)) != \
+                (f0.num_bins, f0.num_input_channels, f0.num_hidden_channels, len(f0.prqct.transform_net.blocks)):
+            return False
+        for blk in net.blocks:
+            for bn in blk.batch_norm_layers:
+                if not (bn.training and id(bn) in flat_bn.index):
+                    return False
+    return True
+
+
+def paired_kld(model, x, z, flat_bn):
+    """forward_kld(x) (differentiable) and reverse_kld's sampling pass of the base draws z
+    (no autograd) in shared launches; returns (forward_kld loss, samples, their log q)."""
+    from .. import _lib
+
+    flows = model.flows
+    L = len(flows)
+    rider = _SamplingRider(z, flat_bn)
+    log_q = None
+    xd = x
+    with _lib.on_device(x):
+        for s in range(L):
+            rider.begin(flows[s])
+            xd, log_q = density_step(flows[L - 1 - s], xd, log_q, pair=rider)
+        flat_bn.update(rider.bnstats, z.shape[0], x.shape[0])
+    _nan_flags.append(rider.nan_flag[0] != 0)
+    check_nan_flags()
+    return -torch.mean(log_q), rider.z, rider.lq

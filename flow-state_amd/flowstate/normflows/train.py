@@ -29,14 +29,28 @@ import torch
 from . import autograd_flow as AF
 
 
-def step_loss(model, x, n_reverse, alpha):
+def step_loss(model, x, n_reverse, alpha, flat_bn=None):
     """loss = ALPHA * forward_kld(x) + (1 - ALPHA) * reverse_kld(n_reverse)
     (main_algorithm_2.py:316-318).  With ALPHA = 1 (the reference's setting) the
     reverse term only contributes its value (0 * e: NaN / inf when e is, so the skip
     rule sees it) and its BatchNorm statistics, so it runs without autograd: its
     gradient 0 * de/dtheta is exactly zero whenever the loss is finite.  Likewise the
-    forward term when ALPHA = 0."""
+    forward term when ALPHA = 0.  With ALPHA = 1 and the model's BatchNorm buffers flat
+    (flat_bn, autograd_flow.FlatBatchNorm) the two passes share their launches
+    (autograd_flow.paired_kld): same values, same running statistics, half the launches
+    of the forward half of the step."""
     if alpha == 1.0:
+        if flat_bn is not None:
+            dev = next(model.parameters()).device
+            z = model.q0(n_reverse).to(dev)  # reverse_kld's base draws, first as in the reference
+            if AF.paired_ok(model, x, z, flat_bn):
+                sample_loss, zs, lqs = AF.paired_kld(model, x, z, flat_bn)
+                with torch.no_grad():
+                    energy_loss = torch.mean(model.p._energy(zs)) + torch.mean(lqs)
+                return sample_loss + 0.0 * energy_loss
+            with torch.no_grad():
+                energy_loss, _ = model._reverse_kld_from(z)
+            return model.forward_kld(x) + 0.0 * energy_loss
         with torch.no_grad():
             energy_loss, _ = model.reverse_kld(n_reverse)
         return model.forward_kld(x) + 0.0 * energy_loss
@@ -59,7 +73,7 @@ class _Captured:
 
 class GraphedTrainStep:
     def __init__(self, model, batch_size, lr, weight_decay=0.0, alpha=1.0, warmup=3, example=None,
-                 extra_batch_sizes=()):
+                 extra_batch_sizes=(), paired=True):
         """Captures the step for `batch_size` (reverse_kld always draws `batch_size`
         samples, as the reference's reverse_kld(BATCH_SIZE)) and for every size in
         extra_batch_sizes (e.g. the epoch's partial last batch); all graphs share the
@@ -77,6 +91,9 @@ class GraphedTrainStep:
         self.D = model.flows[0].num_input_channels
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.opt = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay, capturable=True)
+        # BatchNorm running buffers re-homed flat: the step's two passes share launches
+        # (step_loss, autograd_flow.paired_kld); None keeps them separate
+        self.flat_bn = AF.FlatBatchNorm.try_build(model) if paired else None
         model.train()
         self.graphs = {}
         for bs in [self.batch_size] + [int(b) for b in extra_batch_sizes if int(b) != self.batch_size]:
@@ -121,7 +138,7 @@ class GraphedTrainStep:
         try:
             with torch.cuda.graph(graph):  # own pool: graphs replay in any order
                 self._zero_grad()
-                loss = step_loss(model, x, self.batch_size, self.alpha)
+                loss = step_loss(model, x, self.batch_size, self.alpha, self.flat_bn)
                 loss.backward()
                 self._gather_grads()
                 finite = ~(torch.isnan(loss) | torch.isinf(loss))
@@ -212,7 +229,7 @@ class GraphedTrainStep:
 
     def _eager_step(self, x):
         self._zero_grad()
-        loss = step_loss(self.model, x, self.batch_size, self.alpha)
+        loss = step_loss(self.model, x, self.batch_size, self.alpha, self.flat_bn)
         if bool(~(torch.isnan(loss) | torch.isinf(loss))):
             loss.backward()
             self._gather_grads()

@@ -339,8 +339,28 @@ typedef struct fs_bn_in {
     int64_t *num_batches;
     float *mean_out, *invstd_out;
     float *a_out;
+    float *var_out; /* nullable: the biased batch variance [K] (for deferred running statistics) */
 } fs_bn_in;
 int fs_linear_f32_ex(const fs_gemm_f32 *g, const fs_bn_in *bn, float *stats_out, void *stream);
+
+/* Two independent fs_linear_f32_ex products in one launch (the Algorithm-2 training step's
+ * two passes, main_algorithm_2.py:446-447: reverse_kld's sampling pass and forward_kld's
+ * density pass run layer by layer side by side, each launch carrying one Linear of each).
+ * Each problem is computed exactly as fs_linear_f32_ex computes it alone; shapes the shared
+ * kernel does not take (non-contiguous operands, long reductions) run as two launches. */
+int fs_linear_f32_ex2(const fs_gemm_f32 *g0, const fs_bn_in *bn0, float *stats0, const fs_gemm_f32 *g1,
+                      const fs_bn_in *bn1, float *stats1, void *stream);
+
+/* BatchNorm running statistics applied after the fact (torch.nn.BatchNorm1d.forward's
+ * momentum update, unbiased variance): nbn BatchNorms of width H whose running buffers are
+ * flat [nbn][H] (num_batches [nbn]); stats [passes][nbn][2][H] = each pass's batch mean and
+ * biased variance (fs_bn_in mean_out / var_out of launches that left running_mean NULL);
+ * the passes' updates are applied in pass order (rows0 / rows1 = their batch sizes) and
+ * num_batches += passes.  With passes = 2 this is the reference's order when pass 0 is
+ * reverse_kld's sampling pass and pass 1 forward_kld's density pass. */
+int fs_bn_running_update(int32_t nbn, int32_t H, float *running_mean, float *running_var, int64_t *num_batches,
+                         const float *stats, int32_t passes, int64_t rows0, int64_t rows1, double momentum,
+                         void *stream);
 
 /* Long reductions over few output tiles (K >= 2048, <= 128 tiles of 32 x 32, no rowsum:
  * the input gradient of the 2944-wide final layer, 256 x 128 over K = 2944): the reduction
@@ -413,6 +433,17 @@ int fs_coupling_sample_pre(const fs_coupling *c, const float *z, const float *uw
                            float *t, float *out, float *lad_u, int32_t *nan_flag, void *stream);
 int fs_coupling_sample_post(const fs_coupling *c, const float *params, const float *lad_u, const float *lq_in,
                             float *out, float *lq_out, int32_t *nan_flag, void *stream);
+/* The training step's two passes side by side (see fs_linear_f32_ex2): one launch runs
+ * fs_coupling_sample_pre on layer s and fs_coupling_features_fwd on layer d; the other
+ * fs_coupling_sample_post on s and fs_coupling_density_fwd on d (same K and D), each row
+ * exactly as the single-layer entry points compute it. */
+int fs_coupling_pair_pre(const fs_coupling *s, const float *z, const float *uw, const float *uh, const float *ud,
+                         float *t, float *out, float *lad_u, int32_t *nan_flag, const fs_coupling *d, const float *x,
+                         float *t_density, void *stream);
+int fs_coupling_pair_post(const fs_coupling *s, const float *params, const float *lad_u, const float *lq_in,
+                          float *out, float *lq_out, int32_t *nan_flag, const fs_coupling *d, const float *x,
+                          const float *params_d, const float *uw, const float *uh, const float *ud,
+                          const float *lq_in_d, float *out_d, float *lq_out_d, void *stream);
 
 /* ------------------------------------------------------------------ */
 /* Local moves (MCMC/monte_carlo.py)                                   */

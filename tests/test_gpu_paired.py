@@ -1,0 +1,111 @@
+"""The training step's two passes in shared launches (autograd_flow.paired_kld,
+fs_linear_f32_ex2, fs_coupling_pair_pre / _post, fs_bn_running_update): reverse_kld's
+sampling pass rides along forward_kld's density pass.  Every problem is computed as it
+is alone and the BatchNorm running statistics are applied afterwards in the reference's
+order (sampling pass first, main_algorithm_2.py:446-447), so a step must give exactly
+what the separate passes give: loss, every gradient, running statistics and counters."""
+import numpy as np
+import pytest
+import torch
+
+from flowstate import _lib
+from flowstate.models import A2, build_flow, half_box
+from flowstate.normflows import autograd_flow as AF
+from flowstate.normflows.Energy import DoubleWellLJ
+from flowstate.normflows.train import GraphedTrainStep, step_loss
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(N, kw, seed=0):
+    torch.manual_seed(seed)
+    B = half_box(N)
+    m = build_flow(N, bound=B, device="cpu", **kw)
+    m.p = DoubleWellLJ(2 * N, N, 1.0, B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+    m = m.cuda().train()
+    m.q0.device = torch.device("cuda")
+    return m
+
+
+def _batch(N, rows, seed=3):
+    B = half_box(N)
+    g = np.random.default_rng(seed)
+    return torch.from_numpy(((g.random((rows, 2 * N)) * 2 - 1) * B * 0.9).astype(np.float32)).cuda()
+
+
+def _state(m):
+    return [t.detach().clone() for t in list(m.parameters()) + list(m.buffers())]
+
+
+@pytest.mark.parametrize("N,kw,rows", [(16, dict(L=4, H=64, nb=2, K=8), 96), (64, A2, 256), (16, dict(L=3, H=32, nb=1,
+                                                                                                     K=5), 37)],
+                         ids=["n16-h64", "a2-n64", "n16-ragged"])
+def test_paired_step_matches_separate_passes(N, kw, rows):
+    ma, mb = _model(N, kw), _model(N, kw)
+    fbn = AF.FlatBatchNorm(mb)
+    x = _batch(N, rows)
+    z = mb.q0(rows).cuda()
+    assert AF.paired_ok(mb, x, z, fbn)
+    for m in (ma, mb):
+        for p in m.parameters():
+            p.grad = None
+    torch.cuda.manual_seed(11)
+    la = step_loss(ma, x, rows, 1.0)
+    la.backward()
+    torch.cuda.manual_seed(11)
+    lb = step_loss(mb, x, rows, 1.0, fbn)
+    lb.backward()
+    torch.cuda.synchronize()
+    assert torch.equal(la, lb)
+    for (na, pa), (nb_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+        assert (pa.grad is None) == (pb.grad is None), na
+        if pa.grad is not None:
+            assert torch.equal(pa.grad, pb.grad), na
+    for (na, ba), (nb_, bb) in zip(ma.named_buffers(), mb.named_buffers()):
+        assert torch.equal(ba, bb), na  # running statistics in the reference's order, counters +2
+    assert int(fbn.nbt[0]) == 2
+
+
+def test_paired_graphed_steps_match_separate():
+    """GraphedTrainStep with the shared launches (the default) against paired=False over a
+    few replays: parameters, Adam moments and BatchNorm buffers identical."""
+    N, rows = 16, 128
+    kw = dict(L=4, H=64, nb=2, K=8)
+    out = []
+    for paired in (True, False):
+        m = _model(N, kw, seed=4)
+        x = _batch(N, rows, seed=5)
+        torch.cuda.manual_seed(7)
+        g = GraphedTrainStep(m, rows, lr=1e-3, weight_decay=1e-4, alpha=1.0, example=x, paired=paired)
+        assert (g.flat_bn is not None) == paired
+        for k in range(3):
+            g.step(_batch(N, rows, seed=10 + k))
+        torch.cuda.synchronize()
+        out.append(_state(m) + [t.clone() for t in g._state_tensors])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
+def test_paired_launch_count():
+    """The paired step's forward half: per layer step 8 launches carry both passes
+    (2 coupling + 6 conditioner), against 16 when the passes run one after the other."""
+    from torch.profiler import ProfilerActivity, profile
+
+    N, rows = 16, 64
+    kw = dict(L=4, H=64, nb=2, K=8)
+    m = _model(N, kw)
+    fbn = AF.FlatBatchNorm(m)
+    x = _batch(N, rows)
+    counts = {}
+    for mode in ("paired", "separate"):
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            loss = step_loss(m, x, rows, 1.0, fbn if mode == "paired" else None)
+            torch.cuda.synchronize()
+        names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+        if not names:
+            pytest.skip("the profiler recorded no device kernels")
+        counts[mode] = sum(1 for n in names if "gemm" in n or "coupling" in n)
+        del loss
+    L = kw["L"]
+    assert counts["paired"] == 8 * L, counts
+    assert counts["separate"] == 16 * L, counts
