@@ -61,6 +61,15 @@ __device__ __forceinline__ t4 load4(const float *p, int64_t stride, int64_t k0, 
     return v;
 }
 
+// BatchNorm running statistics, torch's momentum form (1 - m) r + m v, rounded per
+// operation (no contraction: the in-launch and the deferred update agree bit for bit)
+__device__ __forceinline__ float running_update(float r, float v, float m) {
+    return __fadd_rn(__fmul_rn(1.f - m, r), __fmul_rn(m, v));
+}
+__device__ __forceinline__ float unbiased(float var, int64_t rows) {
+    return __fdiv_rn(__fmul_rn(var, (float)rows), (float)(rows - 1));
+}
+
 template <int SPLIT>
 struct GemmLds {
     t16 part[SPLIT > 1 ? SPLIT - 1 : 1][64];
@@ -235,9 +244,8 @@ __device__ __forceinline__ void bn_prologue(const GemmArgs &g, const BnIn &bn, b
             if (bn.invstd_out) bn.invstd_out[k] = invstd;
             if (bn.var_out) bn.var_out[k] = var;
             if (bn.running_mean) {
-                bn.running_mean[k] = (1.f - bn.momentum) * bn.running_mean[k] + bn.momentum * mean;
-                bn.running_var[k] = (1.f - bn.momentum) * bn.running_var[k] +
-                                    bn.momentum * (var * (float)bn.rows / (float)(bn.rows - 1));
+                bn.running_mean[k] = running_update(bn.running_mean[k], mean, bn.momentum);
+                bn.running_var[k] = running_update(bn.running_var[k], unbiased(var, bn.rows), bn.momentum);
             }
         }
     }
@@ -295,8 +303,8 @@ __global__ void __launch_bounds__(256) bn_running_update_kernel(int nbn, int H, 
     for (int p = 0; p < passes; ++p) {
         const int64_t rows = p == 0 ? rows0 : rows1;
         const float *s = stats + (((int64_t)p * nbn + bnx) * 2) * H;
-        a = (1.f - m) * a + m * s[h];
-        v = (1.f - m) * v + m * (s[H + h] * (float)rows / (float)(rows - 1));
+        a = running_update(a, s[h], m);
+        v = running_update(v, unbiased(s[H + h], rows), m);
     }
     rm[i] = a;
     rv[i] = v;
@@ -403,8 +411,8 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_fwd_kernel(
         mean_out[col] = mean;
         invstd_out[col] = invstd;
         if (running_mean) {
-            running_mean[col] = (1.f - momentum) * running_mean[col] + momentum * mean;
-            running_var[col] = (1.f - momentum) * running_var[col] + momentum * (var * (float)B / (float)(B - 1));
+            running_mean[col] = running_update(running_mean[col], mean, momentum);
+            running_var[col] = running_update(running_var[col], unbiased(var, B), momentum);
         }
         if (num_batches && col == 0) *num_batches += 1;
     }
