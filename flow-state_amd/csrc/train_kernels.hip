@@ -62,12 +62,18 @@ __device__ __forceinline__ t4 load4(const float *p, int64_t stride, int64_t k0, 
 }
 
 // BatchNorm running statistics, torch's momentum form (1 - m) r + m v, rounded per
-// operation (no contraction: the in-launch and the deferred update agree bit for bit)
+// operation: no contraction into an FMA (which hipcc otherwise chooses per call site), so
+// the in-launch and the deferred update agree bit for bit
 __device__ __forceinline__ float running_update(float r, float v, float m) {
-    return __fadd_rn(__fmul_rn(1.f - m, r), __fmul_rn(m, v));
+#pragma clang fp contract(off)
+    const float a = (1.f - m) * r;
+    const float b = m * v;
+    return a + b;
 }
 __device__ __forceinline__ float unbiased(float var, int64_t rows) {
-    return __fdiv_rn(__fmul_rn(var, (float)rows), (float)(rows - 1));
+#pragma clang fp contract(off)
+    const float p = var * (float)rows;
+    return p / (float)(rows - 1);
 }
 
 template <int SPLIT>
