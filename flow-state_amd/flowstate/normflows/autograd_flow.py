@@ -835,10 +835,10 @@ class FlatBatchNorm:
             self.rm = torch.stack([bn.running_mean.detach() for bn in bns]).contiguous()
             self.rv = torch.stack([bn.running_var.detach() for bn in bns]).contiguous()
             self.nbt = torch.stack([bn.num_batches_tracked.detach().reshape(()) for bn in bns]).contiguous()
-        for i, bn in enumerate(bns):
-            bn._buffers["running_mean"] = self.rm[i]
-            bn._buffers["running_var"] = self.rv[i]
-            bn._buffers["num_batches_tracked"] = self.nbt[i]
+        for i, bn in enumerate(bns):  # through register_buffer: the packed-image cache sees the new tensors
+            bn.running_mean = self.rm[i]
+            bn.running_var = self.rv[i]
+            bn.num_batches_tracked = self.nbt[i]
         self.bns = bns
         self.index = {id(bn): i for i, bn in enumerate(bns)}
         self.H, self.momentum = H, float(mom)
