@@ -587,6 +587,33 @@ int fs_linear_f32_splitk(const fs_gemm_f32 *d, float *workspace, int64_t workspa
                   "fs_linear_f32_splitk");
 }
 
+int fs_linear_f32_group(const fs_gemm_f32 *const *gs, int32_t n, float *workspace, int64_t workspace_floats,
+                        void *stream) {
+    REQUIRE(gs && n >= 0 && n <= 4, "fs_linear_f32_group: 0..4 products");
+    fs::GemmArgs a[4];
+    for (int i = 0; i < n; ++i) {
+        REQUIRE(gs[i] && gemm_desc_ok(*gs[i]), "fs_linear_f32_group: invalid product %d", i);
+        const fs_gemm_f32 &g = *gs[i];
+        a[i] = fs::GemmArgs{g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C, g.ldc,
+                            g.rowsum_a};
+    }
+    hipError_t e = fs_linear_f32_group_impl(a, n, workspace, workspace_floats, (hipStream_t)stream);
+    if (e == hipErrorNotSupported) {  // one by one
+        int64_t off = 0;
+        for (int i = 0; i < n; ++i) {
+            const int64_t f = fs_linear_f32_splitk_floats_impl(a[i]);
+            if (f > 0 && workspace && workspace_floats - off >= f) {
+                e = fs_linear_f32_splitk_impl(a[i], workspace + off, f, (hipStream_t)stream);
+                off += f;
+            } else {
+                e = fs_linear_f32_impl(a[i], (hipStream_t)stream);
+            }
+            if (e != hipSuccess) break;
+        }
+    }
+    return hip_rc(e, "fs_linear_f32_group");
+}
+
 int fs_bn_relu_train_fwd(int64_t Bn, int32_t H, const float *x, const float *gamma, const float *beta,
                          float *running_mean, float *running_var, int64_t *num_batches, double momentum, double eps,
                          float *y, float *mean, float *invstd, void *stream) {

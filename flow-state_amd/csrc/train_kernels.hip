@@ -84,6 +84,12 @@ struct GemmLds {
 
 constexpr int kBnMaxK = 256;  // BatchNorm-in-load: widest A (the conditioner's hidden width)
 constexpr int kBnStTiles = 8;  // producer tile statistics staged per LDS round (batch 256 = one round)
+// k-blocks in flight per wave in the forward products (the A2 shapes: K = 128 over 8 waves
+// = 2 k-blocks each, so all of a wave's operand loads go out before the prologue)
+#ifndef FS_GEMM_BN_PF
+#define FS_GEMM_BN_PF 2
+#endif
+constexpr int kBnPF = FS_GEMM_BN_PF;
 
 // A operand with BatchNorm + ReLU applied on load (bn_relu_train_fwd's arithmetic).
 struct BnLoad {
@@ -92,10 +98,16 @@ struct BnLoad {
     int64_t lda;
 };
 
-// One 32 x 32 output tile (bx, by) of g by the workgroup's SPLIT waves.
-template <int SPLIT, bool AK, bool BK, bool BNA = false>
+struct NoPrologue {
+    __device__ void operator()() const {}
+};
+
+// One 32 x 32 output tile (bx, by) of g by the workgroup's SPLIT waves.  pro() runs after
+// the first PF k-blocks of operand loads are issued and before they are used (the
+// BatchNorm-in-load statistics prologue, whose own loads then share their round trip).
+template <int SPLIT, bool AK, bool BK, bool BNA = false, int PF = FS_GEMM_PF, class Pro = NoPrologue>
 __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t by, GemmLds<SPLIT> &L,
-                                          const BnLoad *bnl = nullptr) {
+                                          const BnLoad *bnl = nullptr, Pro pro = {}) {
     auto &part = L.part;
     auto &rs_part = L.rs_part;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -111,7 +123,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
     float rs = 0.f;
     // PF k-blocks of loads in flight per wave (the operands come from L2 / the last
     // kernel's output, so the loop is latency-bound without them)
-    constexpr int PF = FS_GEMM_PF;
     const int64_t step = 8 * SPLIT;
     const int64_t kb0 = 8 * w;
     t4 a[PF], b[PF];
@@ -134,8 +145,16 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
 #pragma unroll
     for (int s = 0; s < PF; ++s) {
         const int64_t k = kb0 + s * step;
-        a[s] = bn(load4<AK>(Ap, g.sak, k + 4 * h, g.K, aok && k < g.K), k + 4 * h, aok && k < g.K);
+        a[s] = load4<AK>(Ap, g.sak, k + 4 * h, g.K, aok && k < g.K);
         b[s] = load4<BK>(Bp, g.sbk, k + 4 * h, g.K, bok && k < g.K);
+    }
+    pro();
+    if constexpr (BNA) {
+#pragma unroll
+        for (int s = 0; s < PF; ++s) {
+            const int64_t k = kb0 + s * step;
+            a[s] = bn(a[s], k + 4 * h, aok && k < g.K);
+        }
     }
     for (int64_t kb = kb0; kb < g.K; kb += PF * step) {
 #pragma unroll
@@ -219,6 +238,8 @@ struct BnLds {
 
 __device__ __forceinline__ void bn_prologue(const GemmArgs &g, const BnIn &bn, bool lead, BnLds &S) {
     const int k = threadIdx.x;
+    // gamma / beta loads issued with the statistics' (one round trip for all)
+    const float gk = k < g.K ? bn.gamma[k] : 0.f, bk = k < g.K ? bn.beta[k] : 0.f;
     float n = 0.f, mean = 0.f, m2 = 0.f;
     for (int64_t t0 = 0; t0 < bn.tiles; t0 += kBnStTiles) {
         const int nt = (int)(bn.tiles - t0 < kBnStTiles ? bn.tiles - t0 : kBnStTiles);
@@ -243,8 +264,8 @@ __device__ __forceinline__ void bn_prologue(const GemmArgs &g, const BnIn &bn, b
         const float invstd = 1.f / sqrtf(var + bn.eps);
         S.mu[k] = mean;
         S.is[k] = invstd;
-        S.gm[k] = bn.gamma[k];
-        S.bt[k] = bn.beta[k];
+        S.gm[k] = gk;
+        S.bt[k] = bk;
         if (lead) {
             if (bn.mean_out) bn.mean_out[k] = mean;
             if (bn.invstd_out) bn.invstd_out[k] = invstd;
@@ -265,9 +286,9 @@ template <int SPLIT, bool AK, bool BK>
 __global__ __launch_bounds__(64 * SPLIT) void gemm_bn_f32_kernel(GemmArgs g, BnIn bn) {
     __shared__ GemmLds<SPLIT> L;
     __shared__ BnLds S;
-    bn_prologue(g, bn, blockIdx.x == 0 && blockIdx.y == 0, S);
-    BnLoad bl{S.mu, S.is, S.gm, S.bt, blockIdx.y == 0 ? bn.a_out : nullptr, g.sam};
-    gemm_tile<SPLIT, AK, BK, true>(g, blockIdx.x, blockIdx.y, L, &bl);
+    const BnLoad bl{S.mu, S.is, S.gm, S.bt, blockIdx.y == 0 ? bn.a_out : nullptr, g.sam};
+    gemm_tile<SPLIT, AK, BK, true, kBnPF>(g, blockIdx.x, blockIdx.y, L, &bl,
+                                         [&] { bn_prologue(g, bn, blockIdx.x == 0 && blockIdx.y == 0, S); });
 }
 
 // Two independent forward products in one launch (the training step's two passes: the
@@ -287,11 +308,10 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_ex2_kernel(GemmArgs g0, BnIn 
     const BnIn &bn = second ? b1 : b0;
     const unsigned bx = b % mt, by = b / mt;
     if (bnmask & (second ? 2 : 1)) {
-        bn_prologue(g, bn, bx == 0 && by == 0, S);
-        BnLoad bl{S.mu, S.is, S.gm, S.bt, by == 0 ? bn.a_out : nullptr, g.sam};
-        gemm_tile<SPLIT, true, true, true>(g, bx, by, L, &bl);
+        const BnLoad bl{S.mu, S.is, S.gm, S.bt, by == 0 ? bn.a_out : nullptr, g.sam};
+        gemm_tile<SPLIT, true, true, true, kBnPF>(g, bx, by, L, &bl, [&] { bn_prologue(g, bn, bx == 0 && by == 0, S); });
     } else {
-        gemm_tile<SPLIT, true, true, false>(g, bx, by, L);
+        gemm_tile<SPLIT, true, true, false, kBnPF>(g, bx, by, L);
     }
 }
 
@@ -517,6 +537,60 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs g, const fl
     g.C[m * g.ldc + n] = v;
 }
 
+// Up to kGroupMax independent products in one launch, each plain or split-K (partial tiles
+// into its workspace slice, added by splitk_reduce_kernel after the launch): the backward
+// of a coupling layer's final Linear (input gradient over K = n (3K+1), weight + bias
+// gradient) together with the unconditional spline parameters' row sum.  Each tile is
+// computed exactly as gemm_f32_kernel / gemm_splitk_kernel compute it alone.
+constexpr int kGroupMax = 4;
+struct GroupProblem {
+    GemmArgs g;
+    float *part;  // split-K partial tiles (S > 1)
+    int64_t kchunk;
+    unsigned S, mt, nt, begin;
+    int ak, bk;
+};
+struct GroupArgs {
+    GroupProblem p[kGroupMax];
+    int n;
+};
+
+template <int SPLIT>
+__global__ __launch_bounds__(64 * SPLIT) void gemm_group_kernel(GroupArgs ga) {
+    __shared__ GemmLds<SPLIT> L;
+    int i = 0;
+    while (i + 1 < ga.n && blockIdx.x >= ga.p[i + 1].begin) ++i;
+    const GroupProblem &P = ga.p[i];
+    unsigned b = blockIdx.x - P.begin;
+    const unsigned per = P.mt * P.nt, z = b / per;
+    b -= z * per;
+    const unsigned bx = b % P.mt, by = b / P.mt;
+    GemmArgs c = P.g;
+    if (P.S > 1) {
+        const int64_t k0 = (int64_t)z * P.kchunk;
+        c.A = P.g.A + k0 * P.g.sak;
+        c.B = P.g.B + k0 * P.g.sbk;
+        c.K = (P.g.K - k0 < P.kchunk ? P.g.K - k0 : P.kchunk);
+        c.bias = nullptr;
+        c.R = nullptr;
+        c.rowsum_a = nullptr;
+        c.stats = nullptr;
+        c.C = P.part + (int64_t)z * P.g.M * P.g.N;
+        c.ldc = P.g.N;
+    }
+    if (P.ak) {
+        if (P.bk)
+            gemm_tile<SPLIT, true, true>(c, bx, by, L);
+        else
+            gemm_tile<SPLIT, true, false>(c, bx, by, L);
+    } else {
+        if (P.bk)
+            gemm_tile<SPLIT, false, true>(c, bx, by, L);
+        else
+            gemm_tile<SPLIT, false, false>(c, bx, by, L);
+    }
+}
+
 }  // namespace fs
 
 using namespace fs;
@@ -564,6 +638,56 @@ hipError_t fs_linear_f32_splitk_impl(const GemmArgs &g, float *part, int64_t par
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g,
                        (const float *)part, S);
     return hipGetLastError();
+}
+
+// A group launch (gemm_group_kernel) of n <= kGroupMax products: those with a split-K plan
+// whose partials fit the workspace take it, the others run whole; every product must take
+// FS_GEMM_SPLIT waves per tile (K <= 512 or split).  hipErrorNotSupported: run them one
+// by one (the caller's fallback).
+hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_t ws_floats, hipStream_t st) {
+    if (n < 0 || n > kGroupMax) return hipErrorInvalidValue;
+    GroupArgs ga{};
+    unsigned wg = 0;
+    int64_t used = 0;
+    for (int i = 0; i < n; ++i) {
+        const GemmArgs &g = gs[i];
+        if (g.M <= 0 || (g.N <= 0 && !g.rowsum_a)) continue;  // nothing to compute
+        GroupProblem &P = ga.p[ga.n];
+        P.g = g;
+        P.part = nullptr;
+        P.S = 1;
+        P.kchunk = g.K;
+        int S = 0;
+        int64_t kchunk = 0;
+        const int64_t need = splitk_plan(g, S, kchunk);
+        if (need > 0 && ws && ws_floats - used >= need) {
+            P.part = ws + used;
+            used += need;
+            P.S = (unsigned)S;
+            P.kchunk = kchunk;
+        } else if (gemm_split(g) != FS_GEMM_SPLIT) {
+            return hipErrorNotSupported;
+        }
+        P.ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0 && (P.S == 1 || P.kchunk % 4 == 0);
+        P.bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0 && (P.S == 1 || P.kchunk % 4 == 0);
+        P.mt = (unsigned)((g.M + 31) / 32);
+        P.nt = (unsigned)(g.N > 0 ? (g.N + 31) / 32 : 1);
+        P.begin = wg;
+        wg += P.mt * P.nt * P.S;
+        ++ga.n;
+    }
+    if (ga.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gemm_group_kernel<FS_GEMM_SPLIT>, dim3(wg), dim3(64 * FS_GEMM_SPLIT), 0, st, ga);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    for (int i = 0; i < ga.n; ++i) {
+        const GroupProblem &P = ga.p[i];
+        if (P.S <= 1) continue;
+        const int64_t m = P.g.M * P.g.N;
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, P.g,
+                           (const float *)P.part, (int)P.S);
+        if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st) {

@@ -478,7 +478,7 @@ class _ResidualGrad:
         self.g = None
 
 
-def _conditioner_fused(net, t, pair=None):
+def _conditioner_fused(net, t, pair=None, final=True):
     """ResidualNet.forward (resnet.py:82-104, blocks :35-51) in train mode: every Linear
     on fs_linear_f32 kernels; each BatchNorm + ReLU applied inside the Linear that consumes
     it (its statistics from the producing Linear's epilogue, _BnReluLinear), the block's
@@ -493,6 +493,8 @@ def _conditioner_fused(net, t, pair=None):
             res = _ResidualGrad()
             u, su = _BnReluLinear.apply(t, st, bn0.weight, bn0.bias, bn0, l0.weight, l0.bias, None, res, pair, (i, 0))
             t, st = _BnReluLinear.apply(u, su, bn1.weight, bn1.bias, bn1, l1.weight, l1.bias, t, res, pair, (i, 1))
+        if not final:  # the caller fuses the final Linear into its next Function (_FinalSplines)
+            return t
         lf = net.final_layer
         return _Linear.apply(t, lf.weight, lf.bias, None, None, pair)
     if pair is not None:
@@ -738,6 +740,91 @@ class _DensitySplines(torch.autograd.Function):
         return (gx, gp, guw, guh, gud, g_lq if ctx.has_lq else None, None, None, None)
 
 
+class _FinalSplines(torch.autograd.Function):
+    """The conditioner's final Linear (params = h W^T + b, nn.Linear) and the layer's
+    density-direction splines (as _DensitySplines) in one Function, so that the backward's
+    three products run as one group launch (fs_linear_f32_group): dh = dparams W (split-K
+    over the n (3K+1) columns), dW = dparams^T h with db, and the unconditional spline
+    parameters' gradient (the row sum of the per-row adjoints).  Values are those of
+    _Linear + _DensitySplines."""
+
+    @staticmethod
+    def forward(ctx, h, w, b, x, uw, uh, ud, lq_in, layer, res=None, pair=None):
+        from .. import _lib
+
+        h = h.contiguous()
+        x = x.contiguous()
+        uw, uh, ud = uw.contiguous(), uh.contiguous(), ud.contiguous()
+        L = _lib.load()
+        params = torch.empty((h.shape[0], w.shape[0]), dtype=torch.float32, device=h.device)
+        _lib.require_device(h, w, b, x, uw, lq_in)
+        g = _gemm_desc(h, w, b, None, params)
+        if pair is not None and L.fs_linear_f32_splitk_floats(g) == 0:
+            gs, _, _ = pair.gemm("final")
+            _lib.check(L.fs_linear_f32_ex2(g, None, None, gs, None, None, _lib.stream_ptr()), "fs_linear_f32_ex2")
+            pair.commit()
+        else:
+            _gemm(g, h.device)
+            if pair is not None:
+                pair.gemm_alone("final")
+        _check_shapes(layer, x.shape[0], params, uw, uh, ud)
+        if lq_in is not None and tuple(lq_in.shape) != (x.shape[0],):
+            raise ValueError("log_q must be [rows]")
+        out = torch.empty_like(x)
+        lq = torch.empty((x.shape[0],), dtype=torch.float32, device=x.device)
+        c = _coupling_desc(layer, x.shape[0])
+        if pair is None:
+            _lib.check(L.fs_coupling_density_fwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(params), _lib.ptr(uw),
+                                                 _lib.ptr(uh), _lib.ptr(ud), _lib.ptr(lq_in), _lib.ptr(out),
+                                                 _lib.ptr(lq), _lib.stream_ptr()), "fs_coupling_density_fwd")
+        else:
+            pair.post(c, x, params, uw, uh, ud, lq_in, out, lq)
+        ctx.save_for_backward(h, w, x, params, uw, uh, ud)
+        ctx.layer = layer
+        ctx.has_lq = lq_in is not None
+        ctx.res = res
+        return out, lq
+
+    @staticmethod
+    def backward(ctx, g_out, g_lq):
+        from .. import _lib
+
+        h, w, x, params, uw, uh, ud = ctx.saved_tensors
+        layer = ctx.layer
+        K = layer.num_bins
+        L = _lib.load()
+        p = _lib.ptr
+        g_out = g_out.contiguous() if g_out is not None else None
+        g_lq = g_lq.contiguous() if g_lq is not None else None
+        M, H = h.shape
+        n = x.shape[1] // 2
+        P = n * (3 * K + 1)
+        gx = torch.empty_like(x)
+        gp = torch.empty_like(params)
+        gu = torch.empty((M, P), dtype=torch.float32, device=x.device)
+        c = _coupling_desc(layer, M)
+        _lib.check(L.fs_coupling_density_bwd(ctypes.byref(c), p(x), p(params), p(uw), p(uh), p(ud), p(g_out),
+                                             p(g_lq), p(gx), p(gp), p(gu), _lib.stream_ptr()),
+                   "fs_coupling_density_bwd")
+        gh, gw = torch.empty_like(h), torch.empty_like(w)
+        gb = torch.empty((P,), dtype=torch.float32, device=x.device)
+        gs = torch.empty((P,), dtype=torch.float32, device=x.device)
+        descs = [_lib.GemmF32(M, H, P, p(gp), P, 1, p(w), H, 1, None, None, 0, p(gh), H, None),  # dh = dparams W
+                 _lib.GemmF32(P, H, M, p(gp), 1, P, p(h), H, 1, None, None, 0, p(gw), H, p(gb)),  # dW, db
+                 _lib.GemmF32(P, 0, M, p(gu), 1, P, None, 0, 0, None, None, 0, None, 0, p(gs))]  # row sum of gu
+        nws = sum(max(0, L.fs_linear_f32_splitk_floats(d)) for d in descs)
+        ws = torch.empty((max(nws, 1),), dtype=torch.float32, device=x.device)
+        arr = (ctypes.POINTER(_lib.GemmF32) * 3)(*[ctypes.pointer(d) for d in descs])
+        _lib.check(L.fs_linear_f32_group(arr, 3, p(ws), nws, _lib.stream_ptr()), "fs_linear_f32_group")
+        guw = gs[:n * K].view(n, K)
+        guh = gs[n * K:2 * n * K].view(n, K)
+        gud = gs[2 * n * K:].view(n, K + 1)
+        if ctx.res is not None and ctx.needs_input_grad[3]:
+            ctx.res.g = gx  # added by the layer's features backward (as _DensitySplines)
+            gx = None
+        return (gh, gw, gb, gx, guw, guh, gud, g_lq if ctx.has_lq else None, None, None, None)
+
+
 def conditioner_from_features(net, t, pair=None):
     """ResidualNet.forward from the periodic features t (the rest of conditioner())."""
     if _fused_ok(net, t):
@@ -764,8 +851,14 @@ def density_step(layer, x, log_q, pair=None):
     # gradient in its own launch (no autograd accumulation kernel)
     res = _ResidualGrad() if x.requires_grad and torch.is_grad_enabled() else None
     t = _Features.apply(x, layer, res, pair)
-    params = conditioner_from_features(p.transform_net, t, pair)
     u = p.unconditional_transform
+    net = p.transform_net
+    if _fused_ok(net, t) and _bn_in_load_ok(net):
+        h = _conditioner_fused(net, t, pair, final=False)
+        lf = net.final_layer
+        return _FinalSplines.apply(h, lf.weight, lf.bias, x, u.unnormalized_widths, u.unnormalized_heights,
+                                   u.unnormalized_derivatives, log_q, layer, res, pair)
+    params = conditioner_from_features(net, t, pair)
     return _DensitySplines.apply(x, params, u.unnormalized_widths, u.unnormalized_heights,
                                  u.unnormalized_derivatives, log_q, layer, res, pair)
 

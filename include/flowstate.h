@@ -371,6 +371,14 @@ int fs_bn_running_update(int32_t nbn, int32_t H, float *running_mean, float *run
 int64_t fs_linear_f32_splitk_floats(const fs_gemm_f32 *g);
 int fs_linear_f32_splitk(const fs_gemm_f32 *g, float *workspace, int64_t workspace_floats, void *stream);
 
+/* Up to 4 independent fs_linear_f32 products in one launch (a coupling layer's final
+ * Linear backward: input gradient, weight + bias gradient, and the unconditional spline
+ * parameters' row sum).  Products with a split-K plan take it while the workspace
+ * (sum of their fs_linear_f32_splitk_floats, in order) lasts, followed by their ordered
+ * reductions; each product's values are those of fs_linear_f32 / fs_linear_f32_splitk. */
+int fs_linear_f32_group(const fs_gemm_f32 *const *gs, int32_t n, float *workspace, int64_t workspace_floats,
+                        void *stream);
+
 /* BatchNorm1d (training mode) followed by ReLU over x [Bn][H] (row-major):
  * batch mean / biased variance, y = relu(gamma (x - mean) invstd + beta),
  * running_mean / running_var updated with `momentum` (unbiased variance) and

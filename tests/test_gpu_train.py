@@ -102,3 +102,46 @@ def test_linear_pair_launch_matches_two_launches():
         torch.testing.assert_close(outs[0][0], gy @ w, rtol=1e-5, atol=1e-4)
         torch.testing.assert_close(outs[0][1], gy.t() @ x, rtol=1e-5, atol=1e-4)
         torch.testing.assert_close(outs[0][2], gy.sum(0), rtol=1e-5, atol=1e-4)
+
+
+def test_linear_group_launch_matches_single_launches():
+    """fs_linear_f32_group (the final Linear's backward + the unconditional row sum in one
+    launch, split-K included) gives exactly what the products give one by one."""
+    import ctypes
+
+    from flowstate import _lib
+
+    L, p = _lib.load(), _lib.ptr
+    g = torch.Generator().manual_seed(2)
+    for M, H, P in ((256, 128, 2944), (100, 64, 1040), (37, 24, 300)):
+        h = torch.randn((M, H), generator=g).cuda()
+        w = torch.randn((P, H), generator=g).cuda()
+        gp = torch.randn((M, P), generator=g).cuda()
+        gu = torch.randn((M, P), generator=g).cuda()
+        outs = []
+        for grouped in (True, False):
+            gh, gw = torch.empty_like(h), torch.empty_like(w)
+            gb, gs = torch.empty(P, device="cuda"), torch.empty(P, device="cuda")
+            descs = [_lib.GemmF32(M, H, P, p(gp), P, 1, p(w), H, 1, None, None, 0, p(gh), H, None),
+                     _lib.GemmF32(P, H, M, p(gp), 1, P, p(h), H, 1, None, None, 0, p(gw), H, p(gb)),
+                     _lib.GemmF32(P, 0, M, p(gu), 1, P, None, 0, 0, None, None, 0, None, 0, p(gs))]
+            nws = sum(max(0, L.fs_linear_f32_splitk_floats(d)) for d in descs)
+            ws = torch.empty((max(nws, 1),), device="cuda")
+            if grouped:
+                arr = (ctypes.POINTER(_lib.GemmF32) * 3)(*[ctypes.pointer(d) for d in descs])
+                _lib.check(L.fs_linear_f32_group(arr, 3, p(ws), nws, _lib.stream_ptr()))
+            else:
+                for d in descs:
+                    f = L.fs_linear_f32_splitk_floats(d)
+                    if f > 0:
+                        _lib.check(L.fs_linear_f32_splitk(d, p(ws), f, _lib.stream_ptr()))
+                    else:
+                        _lib.check(L.fs_linear_f32(d.M, d.N, d.K, d.A, d.sam, d.sak, d.B, d.sbk, d.sbn, None, None, 0,
+                                                   d.C, d.ldc, d.rowsum_a, _lib.stream_ptr()))
+            outs.append((gh, gw, gb, gs))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b)
+        torch.testing.assert_close(outs[0][0], gp @ w, rtol=1e-5, atol=2e-3)
+        torch.testing.assert_close(outs[0][1], gp.t() @ h, rtol=1e-5, atol=2e-3)
+        torch.testing.assert_close(outs[0][2], gp.sum(0), rtol=1e-5, atol=1e-3)
+        torch.testing.assert_close(outs[0][3], gu.sum(0), rtol=1e-5, atol=1e-3)
