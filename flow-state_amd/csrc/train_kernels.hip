@@ -591,6 +591,111 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_group_kernel(GroupArgs ga) {
     }
 }
 
+// Backward of y = Linear(u) (+ r) with u = relu(BatchNorm1d_train(x)), batch M <= 256, in
+// one launch (replaces the input / weight gradient pair and bn_relu_train_bwd):
+//  * workgroups [0, ns): column strip c of gu = dY W (32 columns of u, all M rows): wave w
+//    computes row tile w over the whole reduction (16 k-blocks at N = 128), so the strip's
+//    column sums of the BatchNorm backward are workgroup-local: dz = gu (u > 0),
+//    dbeta = sum dz, dgamma = sum dz xhat (per wave over its rows, then waves in order),
+//    dx = gamma invstd (dz - dbeta / M - xhat dgamma / M) (+ dx_add), as
+//    bn_relu_train_bwd_kernel's formula;
+//  * the rest: the tiles of dW = dY^T u with db = column sums of dY (gemm_tile).
+struct LinBnBwdArgs {
+    GemmArgs gdx;  // gu = dY W: M x K over N (A = dY contiguous along N, B = W [N][K])
+    GemmArgs gdw;  // dW = dY^T u (+ rowsum_a = db)
+    const float *x, *u, *gamma, *mean, *invstd, *dx_add;
+    float *dx, *dgamma, *dbeta;
+    unsigned ns;
+};
+
+constexpr int kLbPF = 4;  // k-blocks in flight per wave in the strip's full-K walk
+
+template <int SPLIT>
+__global__ __launch_bounds__(64 * SPLIT) void linear_bn_bwd_kernel(LinBnBwdArgs a) {
+    __shared__ GemmLds<SPLIT> L;
+    __shared__ float red[SPLIT][32][2];
+    if (blockIdx.x >= a.ns) {
+        const GemmArgs &g = a.gdw;
+        const unsigned b = blockIdx.x - a.ns, mt = (unsigned)((g.M + 31) / 32);
+        gemm_tile<SPLIT, false, false>(g, b % mt, b / mt, L);
+        return;
+    }
+    const GemmArgs &g = a.gdx;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t m0 = (int64_t)w * 32, n0 = (int64_t)blockIdx.x * 32;
+    const bool aok = m0 + r < g.M, bok = n0 + r < g.N;
+    const float *Ap = aok ? g.A + (m0 + r) * g.sam : g.A;
+    const float *Bp = bok ? g.B + (n0 + r) * g.sbn : g.B;
+    t16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    if (m0 < g.M) {  // wave-uniform: this wave's row tile exists
+        t4 av[kLbPF], bv[kLbPF];
+#pragma unroll
+        for (int s = 0; s < kLbPF; ++s) {
+            const int64_t k = 8 * s;
+            av[s] = load4<true>(Ap, 1, k + 4 * h, g.K, aok && k < g.K);
+            bv[s] = load4<false>(Bp, g.sbk, k + 4 * h, g.K, bok && k < g.K);
+        }
+        for (int64_t kb = 0; kb < g.K; kb += 8 * kLbPF) {
+#pragma unroll
+            for (int s = 0; s < kLbPF; ++s) {
+                const int64_t k = kb + 8 * s;
+                if (k < g.K) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s][j], bv[s][j], acc, 0, 0, 0);
+                    const int64_t kn = k + 8 * kLbPF;
+                    av[s] = load4<true>(Ap, 1, kn + 4 * h, g.K, aok && kn < g.K);
+                    bv[s] = load4<false>(Bp, g.sbk, kn + 4 * h, g.K, bok && kn < g.K);
+                }
+            }
+        }
+    }
+    // BatchNorm + ReLU backward of the strip's columns (column n0 + r of u / x)
+    const int64_t col = n0 + r, H = g.N;
+    const float mu = bok ? a.mean[col] : 0.f, is = bok ? a.invstd[col] : 0.f;
+    float dz[16], xh[16];
+    float sd = 0.f, sdx = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
+        const bool in = bok && row < g.M;
+        const float uv = in ? a.u[row * H + col] : 0.f, xv = in ? a.x[row * H + col] : mu;
+        dz[i] = uv > 0.f ? acc[i] : 0.f;
+        xh[i] = (xv - mu) * is;
+        sd += dz[i];
+        sdx += dz[i] * xh[i];
+    }
+    sd += __shfl_xor(sd, 32);
+    sdx += __shfl_xor(sdx, 32);
+    if (h == 0) {
+        red[w][r][0] = sd;
+        red[w][r][1] = sdx;
+    }
+    __syncthreads();
+    float db = 0.f, dg = 0.f;
+#pragma unroll
+    for (int q = 0; q < SPLIT; ++q) {
+        db += red[q][r][0];
+        dg += red[q][r][1];
+    }
+    if (!bok) return;
+    const float gm = a.gamma[col];
+    const float mdb = db / (float)g.M, mdg = dg / (float)g.M;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
+        if (row < g.M)
+            a.dx[row * H + col] = (dz[i] - mdb - xh[i] * mdg) * (is * gm) + (a.dx_add ? a.dx_add[row * H + col] : 0.f);
+    }
+    if (w == 0 && h == 0) {
+        if (a.dgamma) a.dgamma[col] = dg;
+        if (a.dbeta) a.dbeta[col] = db;
+    }
+}
+
 }  // namespace fs
 
 using namespace fs;
@@ -779,6 +884,32 @@ hipError_t fs_bn_running_update_impl(int nbn, int H, float *rm, float *rv, int64
     const int64_t n = (int64_t)nbn * H;
     hipLaunchKernelGGL(bn_running_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nbn, H, rm, rv,
                        nbt, stats, passes, rows0, rows1, momentum);
+    return hipGetLastError();
+}
+
+// fs_linear_bn_relu_bwd: M <= 32 FS_GEMM_SPLIT rows (one row tile per wave of a strip).
+hipError_t fs_linear_bn_relu_bwd_impl(int64_t M, int K, int N, const float *gy, const float *w, const float *u,
+                                      const float *x, const float *gamma, const float *mean, const float *invstd,
+                                      const float *dx_add, float *gx, float *gw, float *gb, float *dgamma,
+                                      float *dbeta, hipStream_t st) {
+    if (M <= 0 || K <= 0) return hipSuccess;
+    if (M > 32 * FS_GEMM_SPLIT || N <= 0 || ((uintptr_t)gy & 15) != 0 || N % 4 != 0) return hipErrorNotSupported;
+    LinBnBwdArgs a{};
+    a.gdx = GemmArgs{M, K, N, gy, N, 1, w, K, 1, nullptr, nullptr, 0, nullptr, K, nullptr};
+    a.gdw = GemmArgs{N, K, M, gy, 1, N, u, K, 1, nullptr, nullptr, 0, gw, K, gb};
+    if (gemm_split(a.gdw) != FS_GEMM_SPLIT) return hipErrorNotSupported;
+    a.x = x;
+    a.u = u;
+    a.gamma = gamma;
+    a.mean = mean;
+    a.invstd = invstd;
+    a.dx_add = dx_add;
+    a.dx = gx;
+    a.dgamma = dgamma;
+    a.dbeta = dbeta;
+    a.ns = (unsigned)((K + 31) / 32);
+    const unsigned tw = (unsigned)(((N + 31) / 32) * ((K + 31) / 32));
+    hipLaunchKernelGGL(linear_bn_bwd_kernel<FS_GEMM_SPLIT>, dim3(a.ns + tw), dim3(64 * FS_GEMM_SPLIT), 0, st, a);
     return hipGetLastError();
 }
 

@@ -423,19 +423,26 @@ class _BnReluLinear(torch.autograd.Function):
         N = w.shape[0]
         L = _lib.load()
         p = _lib.ptr
-        gu, gw = torch.empty_like(u), torch.empty_like(w)
+        gw = torch.empty_like(w)
         gb = torch.empty((N,), dtype=torch.float32, device=x.device)
-        g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
-        g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
-        _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
         add = None
         if ctx.res is not None and ctx.res.g is not None:
             add, ctx.res.g = ctx.res.g, None
         gx = torch.empty_like(x)
         gg = torch.empty_like(gamma)
         gbeta = torch.empty_like(gamma)
-        _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
-                                          p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
+        # one launch: input / weight gradients and the BatchNorm + ReLU backward (batch <= 256)
+        rc = L.fs_linear_bn_relu_bwd(M, K, N, p(gy), p(w), p(u), p(x), p(gamma), p(mean), p(invstd), p(add), p(gx),
+                                     p(gw), p(gb), p(gg), p(gbeta), _lib.stream_ptr())
+        if rc == _lib.FS_EUNSUPPORTED:
+            gu = torch.empty_like(u)
+            g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
+            g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
+            _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
+            _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
+                                              p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
+        else:
+            _lib.check(rc, "fs_linear_bn_relu_bwd")
         gr = None
         if ctx.has_r and ctx.needs_input_grad[7]:
             if ctx.res is not None:
