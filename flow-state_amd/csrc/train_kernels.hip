@@ -236,6 +236,7 @@ struct BnLds {
     float sst[kBnStTiles * kBnMaxK * 2];
 };
 
+template <int NT>
 __device__ __forceinline__ void bn_prologue(const GemmArgs &g, const BnIn &bn, bool lead, BnLds &S) {
     const int k = threadIdx.x;
     // gamma / beta loads issued with the statistics' (one round trip for all)
@@ -244,7 +245,21 @@ __device__ __forceinline__ void bn_prologue(const GemmArgs &g, const BnIn &bn, b
     for (int64_t t0 = 0; t0 < bn.tiles; t0 += kBnStTiles) {
         const int nt = (int)(bn.tiles - t0 < kBnStTiles ? bn.tiles - t0 : kBnStTiles);
         const float *src = bn.stats + t0 * g.K * 2;
-        for (int64_t i = threadIdx.x; i < nt * g.K * 2; i += blockDim.x) S.sst[i] = src[i];
+        const int cnt = nt * (int)g.K * 2;
+        // all of a thread's loads first (a runtime-trip loop of load -> LDS store would wait
+        // for each load in turn)
+        constexpr int PER = (kBnStTiles * kBnMaxK * 2 + NT - 1) / NT;
+        float v[PER];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int i = (int)threadIdx.x + q * NT;
+            v[q] = i < cnt ? src[i] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int i = (int)threadIdx.x + q * NT;
+            if (i < cnt) S.sst[i] = v[q];
+        }
         __syncthreads();
         if (k < g.K) {
             for (int t = 0; t < nt; ++t) {  // Chan's pairwise update, tiles in order
@@ -288,7 +303,7 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_bn_f32_kernel(GemmArgs g, BnI
     __shared__ BnLds S;
     const BnLoad bl{S.mu, S.is, S.gm, S.bt, blockIdx.y == 0 ? bn.a_out : nullptr, g.sam};
     gemm_tile<SPLIT, AK, BK, true, kBnPF>(g, blockIdx.x, blockIdx.y, L, &bl,
-                                         [&] { bn_prologue(g, bn, blockIdx.x == 0 && blockIdx.y == 0, S); });
+                                         [&] { bn_prologue<64 * SPLIT>(g, bn, blockIdx.x == 0 && blockIdx.y == 0, S); });
 }
 
 // Two independent forward products in one launch (the training step's two passes: the
@@ -309,7 +324,7 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_ex2_kernel(GemmArgs g0, BnIn 
     const unsigned bx = b % mt, by = b / mt;
     if (bnmask & (second ? 2 : 1)) {
         const BnLoad bl{S.mu, S.is, S.gm, S.bt, by == 0 ? bn.a_out : nullptr, g.sam};
-        gemm_tile<SPLIT, true, true, true, kBnPF>(g, bx, by, L, &bl, [&] { bn_prologue(g, bn, bx == 0 && by == 0, S); });
+        gemm_tile<SPLIT, true, true, true, kBnPF>(g, bx, by, L, &bl, [&] { bn_prologue<64 * SPLIT>(g, bn, bx == 0 && by == 0, S); });
     } else {
         gemm_tile<SPLIT, true, true, false, kBnPF>(g, bx, by, L);
     }
@@ -608,7 +623,8 @@ struct LinBnBwdArgs {
     unsigned ns;
 };
 
-constexpr int kLbPF = 4;  // k-blocks in flight per wave in the strip's full-K walk
+constexpr int kLbPF = 16;  // k-blocks in flight per wave in the strip's full-K walk (all of N = 128)
+constexpr int kLbWPF = 4;  // ... in the weight-gradient tiles (K = batch 256 over 8 waves: all 4)
 
 template <int SPLIT>
 __global__ __launch_bounds__(64 * SPLIT) void linear_bn_bwd_kernel(LinBnBwdArgs a) {
@@ -617,7 +633,7 @@ __global__ __launch_bounds__(64 * SPLIT) void linear_bn_bwd_kernel(LinBnBwdArgs 
     if (blockIdx.x >= a.ns) {
         const GemmArgs &g = a.gdw;
         const unsigned b = blockIdx.x - a.ns, mt = (unsigned)((g.M + 31) / 32);
-        gemm_tile<SPLIT, false, false>(g, b % mt, b / mt, L);
+        gemm_tile<SPLIT, false, false, false, kLbWPF>(g, b % mt, b / mt, L);
         return;
     }
     const GemmArgs &g = a.gdx;
@@ -627,6 +643,18 @@ __global__ __launch_bounds__(64 * SPLIT) void linear_bn_bwd_kernel(LinBnBwdArgs 
     const bool aok = m0 + r < g.M, bok = n0 + r < g.N;
     const float *Ap = aok ? g.A + (m0 + r) * g.sam : g.A;
     const float *Bp = bok ? g.B + (n0 + r) * g.sbn : g.B;
+    // the BatchNorm backward's operands, loaded ahead of the product (they do not depend on it)
+    const int64_t col = n0 + r, H = g.N;
+    const float mu = bok ? a.mean[col] : 0.f, is = bok ? a.invstd[col] : 0.f, gm = bok ? a.gamma[col] : 0.f;
+    float uv[16], xv[16], av_add[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
+        const bool in = bok && row < g.M;
+        uv[i] = in ? a.u[row * H + col] : 0.f;
+        xv[i] = in ? a.x[row * H + col] : 0.f;
+        av_add[i] = (in && a.dx_add) ? a.dx_add[row * H + col] : 0.f;
+    }
     t16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
@@ -654,17 +682,14 @@ __global__ __launch_bounds__(64 * SPLIT) void linear_bn_bwd_kernel(LinBnBwdArgs 
         }
     }
     // BatchNorm + ReLU backward of the strip's columns (column n0 + r of u / x)
-    const int64_t col = n0 + r, H = g.N;
-    const float mu = bok ? a.mean[col] : 0.f, is = bok ? a.invstd[col] : 0.f;
     float dz[16], xh[16];
     float sd = 0.f, sdx = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
         const bool in = bok && row < g.M;
-        const float uv = in ? a.u[row * H + col] : 0.f, xv = in ? a.x[row * H + col] : mu;
-        dz[i] = uv > 0.f ? acc[i] : 0.f;
-        xh[i] = (xv - mu) * is;
+        dz[i] = uv[i] > 0.f ? acc[i] : 0.f;
+        xh[i] = in ? (xv[i] - mu) * is : 0.f;
         sd += dz[i];
         sdx += dz[i] * xh[i];
     }
@@ -682,13 +707,11 @@ __global__ __launch_bounds__(64 * SPLIT) void linear_bn_bwd_kernel(LinBnBwdArgs 
         dg += red[q][r][1];
     }
     if (!bok) return;
-    const float gm = a.gamma[col];
     const float mdb = db / (float)g.M, mdg = dg / (float)g.M;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
-        if (row < g.M)
-            a.dx[row * H + col] = (dz[i] - mdb - xh[i] * mdg) * (is * gm) + (a.dx_add ? a.dx_add[row * H + col] : 0.f);
+        if (row < g.M) a.dx[row * H + col] = (dz[i] - mdb - xh[i] * mdg) * (is * gm) + av_add[i];
     }
     if (w == 0 && h == 0) {
         if (a.dgamma) a.dgamma[col] = dg;
