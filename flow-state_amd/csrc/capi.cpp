@@ -635,22 +635,6 @@ int fs_bn_relu_train_bwd(int64_t Bn, int32_t H, const float *x, const float *y, 
                   "fs_bn_relu_train_bwd");
 }
 
-int fs_linear_bn_relu_bwd(int64_t M, int32_t K, int32_t N, const float *gy, const float *w, const float *u,
-                          const float *x, const float *gamma, const float *mean, const float *invstd,
-                          const float *dx_add, float *gx, float *gw, float *gb, float *dgamma, float *dbeta,
-                          void *stream) {
-    REQUIRE(M >= 2 && K >= 1 && N >= 1 && gy && w && u && x && gamma && mean && invstd && gx && gw && gb,
-            "fs_linear_bn_relu_bwd: invalid arguments");
-    hipError_t e = fs_linear_bn_relu_bwd_impl(M, K, N, gy, w, u, x, gamma, mean, invstd, dx_add, gx, gw, gb, dgamma,
-                                              dbeta, (hipStream_t)stream);
-    if (e == hipErrorNotSupported) {  // the caller runs fs_linear_f32_pair + fs_bn_relu_train_bwd instead
-        fs_set_error("fs_linear_bn_relu_bwd: batch %lld above 256 or a weight-gradient reduction above 512",
-                     (long long)M);
-        return FS_EUNSUPPORTED;
-    }
-    return hip_rc(e, "fs_linear_bn_relu_bwd");
-}
-
 static int check_coupling(const fs_coupling *c, const char *what) {
     REQUIRE(c && c->rows >= 0 && c->D >= 2 && c->D % 2 == 0 && c->hidden >= 1 && c->tail_bound > 0.0,
             "%s: invalid coupling description", what);

@@ -127,10 +127,6 @@ hipError_t fs_bn_running_update_impl(int nbn, int H, float *rm, float *rv, int64
                                      int passes, int64_t rows0, int64_t rows1, float momentum, hipStream_t st);
 int64_t fs_linear_f32_splitk_floats_impl(const fs::GemmArgs &g);
 hipError_t fs_linear_f32_splitk_impl(const fs::GemmArgs &g, float *part, int64_t part_floats, hipStream_t st);
-hipError_t fs_linear_bn_relu_bwd_impl(int64_t M, int K, int N, const float *gy, const float *w, const float *u,
-                                      const float *x, const float *gamma, const float *mean, const float *invstd,
-                                      const float *dx_add, float *gx, float *gw, float *gb, float *dgamma,
-                                      float *dbeta, hipStream_t st);
 hipError_t fs_linear_f32_group_impl(const fs::GemmArgs *gs, int n, float *ws, int64_t ws_floats, hipStream_t st);
 hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,
                                      float *rm, float *rv, int64_t *nbt, float momentum, float eps, float *y,

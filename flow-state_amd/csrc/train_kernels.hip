@@ -83,7 +83,7 @@ struct GemmLds {
 };
 
 constexpr int kBnMaxK = 256;  // BatchNorm-in-load: widest A (the conditioner's hidden width)
-constexpr int kBnStTiles = 8;  // producer tile statistics staged per LDS round (batch 256 = one round)
+constexpr int kBnStTiles = 8;  // producer tile statistics loaded per round (batch 256 = one round)
 // k-blocks in flight per wave in the forward products (the A2 shapes: K = 128 over 8 waves
 // = 2 k-blocks each, so all of a wave's operand loads go out before the prologue)
 #ifndef FS_GEMM_BN_PF
@@ -94,8 +94,11 @@ constexpr int kBnPF = FS_GEMM_BN_PF;
 // A operand with BatchNorm + ReLU applied on load (bn_relu_train_fwd's arithmetic).
 struct BnLoad {
     const float *mu, *is, *gm, *bt;  // LDS, per k
-    float *a_out;                    // nullable: u written back (column tile 0 only)
+    float *a_out;                    // nullable: u written back, [M][K] row-major
     int64_t lda;
+    // the workgroups of column tile `by` of `nt` write u's 32-wide k slices ks with
+    // ks % nt == by, so the write-back is spread over every column tile
+    int64_t by, nt;
 };
 
 struct NoPrologue {
@@ -136,9 +139,21 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
                 if (k < g.K) {
                     const float o = bnl->gm[k] * ((v[j] - bnl->mu[k]) * bnl->is[k]) + bnl->bt[k];
                     v[j] = o > 0.f ? o : 0.f;
-                    if (bnl->a_out) bnl->a_out[(m0 + r) * bnl->lda + k] = v[j];
                 }
             }
+#ifndef FS_PROBE_NOAOUT
+            // k0 is a multiple of 4: the four elements sit in one 32-wide k slice
+            if (bnl->a_out && (k0 >> 5) % bnl->nt == bnl->by) {
+                float *dst = bnl->a_out + (m0 + r) * bnl->lda + k0;
+                if (AK && k0 + 3 < g.K) {
+                    *(t4 *)dst = v;  // 16-byte aligned: the host checks a_out and lda
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (k0 + j < g.K) dst[j] = v[j];
+                }
+            }
+#endif
         }
         return v;
     };
@@ -228,51 +243,48 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_f32_kernel(GemmArgs g) {
 // The BatchNorm of a BatchNorm-in-load product: every workgroup combines the producer's
 // tile statistics of all K columns (Chan's pairwise update, tiles in order; biased
 // variance) into LDS; the problem's lead workgroup writes mean / invstd (/ var) and updates
-// the running statistics.  The producer's statistics are staged through LDS kBnStTiles
-// tiles at a time (all of a round's loads in flight together, instead of one dependent L2
-// read per tile); the host guarantees blockDim.x >= K, so thread k owns column k.
+// the running statistics.  Thread k owns column k (the host guarantees blockDim.x >= K) and
+// loads its kBnStTiles (mean, M2) pairs of a round at once, straight into registers: one
+// round trip per round and a single barrier, where staging the statistics through LDS
+// cost two more barriers (tools/linbn_probe.py, profiles/r03/).
 struct BnLds {
     float mu[kBnMaxK], is[kBnMaxK], gm[kBnMaxK], bt[kBnMaxK];
-    float sst[kBnStTiles * kBnMaxK * 2];
 };
 
+#ifndef FS_PROBE_PRO
+#define FS_PROBE_PRO 0  // timing-only builds (tools/linbn_probe.py): 1 = no Chan loop, 2 = no statistics loads
+#endif
 template <int NT>
 __device__ __forceinline__ void bn_prologue(const GemmArgs &g, const BnIn &bn, bool lead, BnLds &S) {
     const int k = threadIdx.x;
+#if FS_PROBE_PRO == 2
+    if (k < g.K) { S.mu[k] = 0.f; S.is[k] = 1.f; S.gm[k] = 1.f; S.bt[k] = 0.f; }
+    __syncthreads();
+    return;
+#endif
+    typedef float f2 __attribute__((ext_vector_type(2)));
     // gamma / beta loads issued with the statistics' (one round trip for all)
     const float gk = k < g.K ? bn.gamma[k] : 0.f, bk = k < g.K ? bn.beta[k] : 0.f;
     float n = 0.f, mean = 0.f, m2 = 0.f;
-    for (int64_t t0 = 0; t0 < bn.tiles; t0 += kBnStTiles) {
-        const int nt = (int)(bn.tiles - t0 < kBnStTiles ? bn.tiles - t0 : kBnStTiles);
-        const float *src = bn.stats + t0 * g.K * 2;
-        const int cnt = nt * (int)g.K * 2;
-        // all of a thread's loads first (a runtime-trip loop of load -> LDS store would wait
-        // for each load in turn)
-        constexpr int PER = (kBnStTiles * kBnMaxK * 2 + NT - 1) / NT;
-        float v[PER];
+    if (k < g.K) {
+        for (int64_t t0 = 0; t0 < bn.tiles; t0 += kBnStTiles) {
+            const int nt = (int)(bn.tiles - t0 < kBnStTiles ? bn.tiles - t0 : kBnStTiles);
+            const f2 *src = (const f2 *)bn.stats + t0 * g.K + k;  // [tile][K] pairs, 8-byte aligned
+            f2 v[kBnStTiles];
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            const int i = (int)threadIdx.x + q * NT;
-            v[q] = i < cnt ? src[i] : 0.f;
-        }
+            for (int t = 0; t < kBnStTiles; ++t) v[t] = t < nt ? src[t * g.K] : f2{0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            const int i = (int)threadIdx.x + q * NT;
-            if (i < cnt) S.sst[i] = v[q];
-        }
-        __syncthreads();
-        if (k < g.K) {
-            for (int t = 0; t < nt; ++t) {  // Chan's pairwise update, tiles in order
-                const int64_t row0 = 32 * (t0 + t);
-                const float nb = (float)(bn.rows - row0 < 32 ? bn.rows - row0 : 32);
-                const float mb = S.sst[(t * g.K + k) * 2], qb = S.sst[(t * g.K + k) * 2 + 1];
-                const float nn = n + nb, d = mb - mean;
-                mean = mean + d * (nb / nn);
-                m2 = m2 + qb + d * d * (n * nb / nn);
-                n = nn;
+            for (int t = 0; t < kBnStTiles; ++t) {  // Chan's pairwise update, tiles in order
+                if (t < (FS_PROBE_PRO == 1 ? 1 : nt)) {
+                    const int64_t row0 = 32 * (t0 + t);
+                    const float nb = (float)(bn.rows - row0 < 32 ? bn.rows - row0 : 32);
+                    const float nn = n + nb, d = v[t][0] - mean;
+                    mean = mean + d * (nb / nn);
+                    m2 = m2 + v[t][1] + d * d * (n * nb / nn);
+                    n = nn;
+                }
             }
         }
-        __syncthreads();
     }
     if (k < g.K) {
         const float var = m2 / (float)bn.rows;
@@ -301,7 +313,7 @@ template <int SPLIT, bool AK, bool BK>
 __global__ __launch_bounds__(64 * SPLIT) void gemm_bn_f32_kernel(GemmArgs g, BnIn bn) {
     __shared__ GemmLds<SPLIT> L;
     __shared__ BnLds S;
-    const BnLoad bl{S.mu, S.is, S.gm, S.bt, blockIdx.y == 0 ? bn.a_out : nullptr, g.sam};
+    const BnLoad bl{S.mu, S.is, S.gm, S.bt, bn.a_out, g.sam, blockIdx.y, gridDim.y};
     gemm_tile<SPLIT, AK, BK, true, kBnPF>(g, blockIdx.x, blockIdx.y, L, &bl,
                                          [&] { bn_prologue<64 * SPLIT>(g, bn, blockIdx.x == 0 && blockIdx.y == 0, S); });
 }
@@ -323,7 +335,7 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_ex2_kernel(GemmArgs g0, BnIn 
     const BnIn &bn = second ? b1 : b0;
     const unsigned bx = b % mt, by = b / mt;
     if (bnmask & (second ? 2 : 1)) {
-        const BnLoad bl{S.mu, S.is, S.gm, S.bt, by == 0 ? bn.a_out : nullptr, g.sam};
+        const BnLoad bl{S.mu, S.is, S.gm, S.bt, bn.a_out, g.sam, by, (g.N + 31) / 32};
         gemm_tile<SPLIT, true, true, true, kBnPF>(g, bx, by, L, &bl, [&] { bn_prologue<64 * SPLIT>(g, bn, bx == 0 && by == 0, S); });
     } else {
         gemm_tile<SPLIT, true, true, false, kBnPF>(g, bx, by, L);
@@ -606,119 +618,6 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_group_kernel(GroupArgs ga) {
     }
 }
 
-// Backward of y = Linear(u) (+ r) with u = relu(BatchNorm1d_train(x)), batch M <= 256, in
-// one launch (replaces the input / weight gradient pair and bn_relu_train_bwd):
-//  * workgroups [0, ns): column strip c of gu = dY W (32 columns of u, all M rows): wave w
-//    computes row tile w over the whole reduction (16 k-blocks at N = 128), so the strip's
-//    column sums of the BatchNorm backward are workgroup-local: dz = gu (u > 0),
-//    dbeta = sum dz, dgamma = sum dz xhat (per wave over its rows, then waves in order),
-//    dx = gamma invstd (dz - dbeta / M - xhat dgamma / M) (+ dx_add), as
-//    bn_relu_train_bwd_kernel's formula;
-//  * the rest: the tiles of dW = dY^T u with db = column sums of dY (gemm_tile).
-struct LinBnBwdArgs {
-    GemmArgs gdx;  // gu = dY W: M x K over N (A = dY contiguous along N, B = W [N][K])
-    GemmArgs gdw;  // dW = dY^T u (+ rowsum_a = db)
-    const float *x, *u, *gamma, *mean, *invstd, *dx_add;
-    float *dx, *dgamma, *dbeta;
-    unsigned ns;
-};
-
-constexpr int kLbPF = 16;  // k-blocks in flight per wave in the strip's full-K walk (all of N = 128)
-constexpr int kLbWPF = 4;  // ... in the weight-gradient tiles (K = batch 256 over 8 waves: all 4)
-
-template <int SPLIT>
-__global__ __launch_bounds__(64 * SPLIT) void linear_bn_bwd_kernel(LinBnBwdArgs a) {
-    __shared__ GemmLds<SPLIT> L;
-    __shared__ float red[SPLIT][32][2];
-    if (blockIdx.x >= a.ns) {
-        const GemmArgs &g = a.gdw;
-        const unsigned b = blockIdx.x - a.ns, mt = (unsigned)((g.M + 31) / 32);
-        gemm_tile<SPLIT, false, false, false, kLbWPF>(g, b % mt, b / mt, L);
-        return;
-    }
-    const GemmArgs &g = a.gdx;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int r = lane & 31, h = lane >> 5;
-    const int64_t m0 = (int64_t)w * 32, n0 = (int64_t)blockIdx.x * 32;
-    const bool aok = m0 + r < g.M, bok = n0 + r < g.N;
-    const float *Ap = aok ? g.A + (m0 + r) * g.sam : g.A;
-    const float *Bp = bok ? g.B + (n0 + r) * g.sbn : g.B;
-    // the BatchNorm backward's operands, loaded ahead of the product (they do not depend on it)
-    const int64_t col = n0 + r, H = g.N;
-    const float mu = bok ? a.mean[col] : 0.f, is = bok ? a.invstd[col] : 0.f, gm = bok ? a.gamma[col] : 0.f;
-    float uv[16], xv[16], av_add[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
-        const bool in = bok && row < g.M;
-        uv[i] = in ? a.u[row * H + col] : 0.f;
-        xv[i] = in ? a.x[row * H + col] : 0.f;
-        av_add[i] = (in && a.dx_add) ? a.dx_add[row * H + col] : 0.f;
-    }
-    t16 acc;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    if (m0 < g.M) {  // wave-uniform: this wave's row tile exists
-        t4 av[kLbPF], bv[kLbPF];
-#pragma unroll
-        for (int s = 0; s < kLbPF; ++s) {
-            const int64_t k = 8 * s;
-            av[s] = load4<true>(Ap, 1, k + 4 * h, g.K, aok && k < g.K);
-            bv[s] = load4<false>(Bp, g.sbk, k + 4 * h, g.K, bok && k < g.K);
-        }
-        for (int64_t kb = 0; kb < g.K; kb += 8 * kLbPF) {
-#pragma unroll
-            for (int s = 0; s < kLbPF; ++s) {
-                const int64_t k = kb + 8 * s;
-                if (k < g.K) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s][j], bv[s][j], acc, 0, 0, 0);
-                    const int64_t kn = k + 8 * kLbPF;
-                    av[s] = load4<true>(Ap, 1, kn + 4 * h, g.K, aok && kn < g.K);
-                    bv[s] = load4<false>(Bp, g.sbk, kn + 4 * h, g.K, bok && kn < g.K);
-                }
-            }
-        }
-    }
-    // BatchNorm + ReLU backward of the strip's columns (column n0 + r of u / x)
-    float dz[16], xh[16];
-    float sd = 0.f, sdx = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
-        const bool in = bok && row < g.M;
-        dz[i] = uv[i] > 0.f ? acc[i] : 0.f;
-        xh[i] = in ? (xv[i] - mu) * is : 0.f;
-        sd += dz[i];
-        sdx += dz[i] * xh[i];
-    }
-    sd += __shfl_xor(sd, 32);
-    sdx += __shfl_xor(sdx, 32);
-    if (h == 0) {
-        red[w][r][0] = sd;
-        red[w][r][1] = sdx;
-    }
-    __syncthreads();
-    float db = 0.f, dg = 0.f;
-#pragma unroll
-    for (int q = 0; q < SPLIT; ++q) {
-        db += red[q][r][0];
-        dg += red[q][r][1];
-    }
-    if (!bok) return;
-    const float mdb = db / (float)g.M, mdg = dg / (float)g.M;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
-        if (row < g.M) a.dx[row * H + col] = (dz[i] - mdb - xh[i] * mdg) * (is * gm) + av_add[i];
-    }
-    if (w == 0 && h == 0) {
-        if (a.dgamma) a.dgamma[col] = dg;
-        if (a.dbeta) a.dbeta[col] = db;
-    }
-}
-
 }  // namespace fs
 
 using namespace fs;
@@ -860,12 +759,17 @@ hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g
     return fs_linear_f32_impl(g1, st);
 }
 
+// u's write-back stores 4 floats at once where A is contiguous along k
+static bool bn_out_ok(const GemmArgs &g, const BnIn *bn) {
+    return !bn || !bn->a_out || (((uintptr_t)bn->a_out & 15) == 0 && g.sam % 4 == 0);
+}
+
 hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipStream_t st) {
     if (!bn) return fs_linear_f32_impl(g, st);
     if (g.M <= 0 || g.N <= 0) return hipSuccess;
     const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0;
     const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0;
-    if (g.K > kBnMaxK || g.rowsum_a) return hipErrorInvalidValue;
+    if (g.K > kBnMaxK || g.rowsum_a || !bn_out_ok(g, bn)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)((g.M + 31) / 32), (unsigned)((g.N + 31) / 32));
     const int split = gemm_split(g);
     if (64 * split < g.K) return hipErrorInvalidValue;  // one thread per column in the statistics prologue
@@ -883,7 +787,8 @@ hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipS
 static bool ex2_operand_ok(const GemmArgs &g, const BnIn *bn) {
     const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0;
     const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0;
-    return ak && bk && g.M > 0 && g.N > 0 && !g.rowsum_a && (!bn || (g.K <= kBnMaxK && 64 * gemm_split(g) >= g.K));
+    return ak && bk && g.M > 0 && g.N > 0 && !g.rowsum_a && bn_out_ok(g, bn) &&
+           (!bn || (g.K <= kBnMaxK && 64 * gemm_split(g) >= g.K));
 }
 
 bool fs_linear_ex2_ok(const GemmArgs &g0, const BnIn *b0, const GemmArgs &g1, const BnIn *b1) {
@@ -907,32 +812,6 @@ hipError_t fs_bn_running_update_impl(int nbn, int H, float *rm, float *rv, int64
     const int64_t n = (int64_t)nbn * H;
     hipLaunchKernelGGL(bn_running_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nbn, H, rm, rv,
                        nbt, stats, passes, rows0, rows1, momentum);
-    return hipGetLastError();
-}
-
-// fs_linear_bn_relu_bwd: M <= 32 FS_GEMM_SPLIT rows (one row tile per wave of a strip).
-hipError_t fs_linear_bn_relu_bwd_impl(int64_t M, int K, int N, const float *gy, const float *w, const float *u,
-                                      const float *x, const float *gamma, const float *mean, const float *invstd,
-                                      const float *dx_add, float *gx, float *gw, float *gb, float *dgamma,
-                                      float *dbeta, hipStream_t st) {
-    if (M <= 0 || K <= 0) return hipSuccess;
-    if (M > 32 * FS_GEMM_SPLIT || N <= 0 || ((uintptr_t)gy & 15) != 0 || N % 4 != 0) return hipErrorNotSupported;
-    LinBnBwdArgs a{};
-    a.gdx = GemmArgs{M, K, N, gy, N, 1, w, K, 1, nullptr, nullptr, 0, nullptr, K, nullptr};
-    a.gdw = GemmArgs{N, K, M, gy, 1, N, u, K, 1, nullptr, nullptr, 0, gw, K, gb};
-    if (gemm_split(a.gdw) != FS_GEMM_SPLIT) return hipErrorNotSupported;
-    a.x = x;
-    a.u = u;
-    a.gamma = gamma;
-    a.mean = mean;
-    a.invstd = invstd;
-    a.dx_add = dx_add;
-    a.dx = gx;
-    a.dgamma = dgamma;
-    a.dbeta = dbeta;
-    a.ns = (unsigned)((K + 31) / 32);
-    const unsigned tw = (unsigned)(((N + 31) / 32) * ((K + 31) / 32));
-    hipLaunchKernelGGL(linear_bn_bwd_kernel<FS_GEMM_SPLIT>, dim3(a.ns + tw), dim3(64 * FS_GEMM_SPLIT), 0, st, a);
     return hipGetLastError();
 }
 

@@ -431,18 +431,16 @@ class _BnReluLinear(torch.autograd.Function):
         gx = torch.empty_like(x)
         gg = torch.empty_like(gamma)
         gbeta = torch.empty_like(gamma)
-        # one launch: input / weight gradients and the BatchNorm + ReLU backward (batch <= 256)
-        rc = L.fs_linear_bn_relu_bwd(M, K, N, p(gy), p(w), p(u), p(x), p(gamma), p(mean), p(invstd), p(add), p(gx),
-                                     p(gw), p(gb), p(gg), p(gbeta), _lib.stream_ptr())
-        if rc == _lib.FS_EUNSUPPORTED:
-            gu = torch.empty_like(u)
-            g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
-            g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
-            _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
-            _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
-                                              p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
-        else:
-            _lib.check(rc, "fs_linear_bn_relu_bwd")
+        # the input / weight gradient pair over 48 workgroups, then the BatchNorm + ReLU
+        # backward: 10.9 us per layer in a graph, against 18.1 us for one launch whose
+        # column strips own the BatchNorm sums (4 workgroups carry the whole input gradient;
+        # tools/linbn_probe.py, profiles/r03/r03k_linbn_probe.log)
+        gu = torch.empty_like(u)
+        g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
+        g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
+        _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
+        _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
+                                          p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
         gr = None
         if ctx.has_r and ctx.needs_input_grad[7]:
             if ctx.res is not None:

@@ -390,17 +390,6 @@ int fs_bn_relu_train_fwd(int64_t Bn, int32_t H, const float *x, const float *gam
 
 /* Gradients of the above: dx [Bn][H], dgamma, dbeta [H] (nullable) from dy = dL/dy and
  * the forward's x, y, mean, invstd. */
-/* Backward of y = Linear(relu(BatchNorm1d_train(x))) (+ r) in one launch, batch M <= 256
- * (_BnReluLinear's backward; resnet.py:35-51): gu = gy W, gw = gy^T u, gb = column sums of
- * gy, then the BatchNorm + ReLU backward of gu (u = the saved relu output, x the saved
- * pre-BatchNorm input, mean / invstd the batch statistics): gx (+ dx_add, nullable),
- * dgamma, dbeta (nullable).  x, u, gx: [M][K]; gy: [M][N]; w: [N][K].  FS_EUNSUPPORTED
- * for M > 256 (then fs_linear_f32_pair + fs_bn_relu_train_bwd). */
-int fs_linear_bn_relu_bwd(int64_t M, int32_t K, int32_t N, const float *gy, const float *w, const float *u,
-                          const float *x, const float *gamma, const float *mean, const float *invstd,
-                          const float *dx_add, float *gx, float *gw, float *gb, float *dgamma, float *dbeta,
-                          void *stream);
-
 /* fs_bn_relu_train_bwd: dx = the input gradient (+ dx_add [Bn][H], nullable: the block
  * input's residual-branch gradient, resnet.py:51, added in the same launch instead of by
  * autograd); dgamma, dbeta nullable. */

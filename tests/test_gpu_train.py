@@ -147,51 +147,3 @@ def test_linear_group_launch_matches_single_launches():
         torch.testing.assert_close(outs[0][3], gu.sum(0), rtol=1e-5, atol=1e-3)
 
 
-@pytest.mark.parametrize("M", [256, 232, 37])
-def test_linear_bn_relu_bwd_matches_pair_and_bn_backward(M):
-    """fs_linear_bn_relu_bwd (one launch) against fs_linear_f32_pair + fs_bn_relu_train_bwd:
-    dW and db identical (same tiles), dx / dgamma / dbeta equal to rounding (the column
-    sums are taken over the strip's row tiles instead of the BatchNorm kernel's row groups)."""
-    from flowstate import _lib
-
-    L, p = _lib.load(), _lib.ptr
-    g = torch.Generator().manual_seed(M)
-    K, N = 128, 128
-    x = torch.randn((M, K), generator=g).cuda()
-    gamma = (torch.rand(K, generator=g) + 0.5).cuda()
-    beta = torch.randn(K, generator=g).cuda() * 0.1
-    mean, var = x.mean(0), x.var(0, unbiased=False)
-    invstd = 1.0 / torch.sqrt(var + 1e-3)
-    u = torch.relu(gamma * ((x - mean) * invstd) + beta)
-    w = torch.randn((N, K), generator=g).cuda() * 0.1
-    gy = torch.randn((M, N), generator=g).cuda()
-    add = torch.randn((M, K), generator=g).cuda()
-    outs = []
-    for fused in (True, False):
-        gx, gw, gb = torch.empty_like(x), torch.empty_like(w), torch.empty(N, device="cuda")
-        gg, gbt = torch.empty(K, device="cuda"), torch.empty(K, device="cuda")
-        if fused:
-            _lib.check(L.fs_linear_bn_relu_bwd(M, K, N, p(gy), p(w), p(u), p(x), p(gamma), p(mean), p(invstd), p(add),
-                                               p(gx), p(gw), p(gb), p(gg), p(gbt), _lib.stream_ptr()))
-        else:
-            gu = torch.empty_like(u)
-            g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
-            g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
-            _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()))
-            _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
-                                              p(gg), p(gbt), _lib.stream_ptr()))
-        outs.append((gx, gw, gb, gg, gbt))
-    (fx, fw, fb, fg, fbt), (sx, sw, sb, sg, sbt) = outs
-    assert torch.equal(fw, sw) and torch.equal(fb, sb)
-    torch.testing.assert_close(fx, sx, rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(fg, sg, rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(fbt, sbt, rtol=1e-4, atol=1e-3)
-    # against autograd in float64
-    xd = x.double().requires_grad_(True)
-    gd, bd, wd = gamma.double().requires_grad_(True), beta.double().requires_grad_(True), w.double()
-    m_, v_ = xd.mean(0), xd.var(0, unbiased=False)
-    ud = torch.relu(gd * ((xd - m_) / torch.sqrt(v_ + 1e-3)) + bd)
-    (ud @ wd.t()).backward(gy.double())
-    torch.testing.assert_close(fx - add, xd.grad.float(), rtol=1e-3, atol=1e-3)
-    torch.testing.assert_close(fg, gd.grad.float(), rtol=1e-3, atol=1e-2)
-    torch.testing.assert_close(fbt, bd.grad.float(), rtol=1e-3, atol=1e-2)
