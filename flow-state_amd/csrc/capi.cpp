@@ -440,6 +440,19 @@ int fs_rqs_backward(int64_t M, int32_t K, int32_t inverse, const float *x, const
 
 int64_t fs_set_wide_rows(int64_t rows) { return fs_set_wide_rows_impl(rows); }
 
+int fs_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float *step,
+                 const float *loss, double lr, double beta1, double beta2, double eps, double weight_decay,
+                 void *stream) {
+    REQUIRE(n >= 0 && step && (n == 0 || (param && grad && exp_avg && exp_avg_sq)) && lr > 0.0 && beta1 >= 0.0 &&
+                beta1 < 1.0 && beta2 >= 0.0 && beta2 < 1.0 && eps >= 0.0 && weight_decay >= 0.0,
+            "fs_adam_step: invalid arguments");
+    REQUIRE((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) == 0,
+            "fs_adam_step: buffers must be 16-byte aligned");
+    return hip_rc(fs_adam_step_impl(param, grad, exp_avg, exp_avg_sq, n, step, loss, lr, beta1, beta2, eps,
+                                    weight_decay, (hipStream_t)stream),
+                  "fs_adam_step");
+}
+
 int fs_target_energy(const float *x, int64_t B, int32_t N, double bound, double temperature, int32_t num_wells,
                      double V0_0, double V0_1, double r0, double k, float *E, float *grad_x, void *stream) {
     REQUIRE(B >= 0 && N >= 1 && N <= 1024 && bound > 0.0 && temperature > 0.0 && num_wells >= 0 && num_wells <= 2 &&

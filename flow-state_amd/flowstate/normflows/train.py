@@ -16,9 +16,12 @@ torch.cuda.graph (fused spline kernels and HIP GEMMs included) and replays it:
   * the batch is copied into a static input buffer before each replay;
   * the base draws of reverse_kld come from the default generator inside the graph
     (fresh draws every replay, as the reference's q0 sampling);
-  * Adam runs with capturable=True; the reference's "skip the step when the loss is
-    NaN / inf" is a device-side select: parameters and optimizer state are snapshotted
-    before the update and restored where the loss was not finite;
+  * Adam is one fused HIP pass over the flat parameter / gradient / moment buffers
+    (fs_adam_step, csrc/optim_kernels.hip: torch's capturable Adam arithmetic, ~16
+    launches in torch), and the reference's "skip the step when the loss is NaN / inf"
+    happens inside it: the kernel reads the loss and writes nothing when it is not
+    finite.  Options it does not cover (amsgrad, maximize, tensor lr) keep torch's
+    capturable Adam with a device-side snapshot / restore around it;
   * the spline's NaN-discriminant flags are reduced inside the graph and checked after
     the replay (the reference raises ValueError; here it is raised after the step).
 """
@@ -131,7 +134,8 @@ class GraphedTrainStep:
             self.opt.param_groups[0]["params"] = used
             self.params = used
             self._state_tensors = self._flatten()
-            self._backup = [t.detach().clone() for t in self._state_tensors]
+            # the snapshot buffers of torch's Adam path only (fs_adam_step skips by itself)
+            self._backup = None if self._fused_adam_ok() else [t.detach().clone() for t in self._state_tensors]
         graph = torch.cuda.CUDAGraph()
         self._zero_grad()
         AF._defer_nan = True
@@ -141,17 +145,49 @@ class GraphedTrainStep:
                 loss = step_loss(model, x, self.batch_size, self.alpha, self.flat_bn)
                 loss.backward()
                 self._gather_grads()
-                finite = ~(torch.isnan(loss) | torch.isinf(loss))
-                for b, t in zip(self._backup, self._state_tensors):
-                    b.copy_(t.detach())
-                self.opt.step()
-                with torch.no_grad():
+                if self._fused_adam_ok():
+                    self._adam_step(loss.detach())  # skips itself on a non-finite loss
+                else:
+                    finite = ~(torch.isnan(loss) | torch.isinf(loss))
                     for b, t in zip(self._backup, self._state_tensors):
-                        t.copy_(torch.where(finite, t, b))
+                        b.copy_(t.detach())
+                    self.opt.step()
+                    with torch.no_grad():
+                        for b, t in zip(self._backup, self._state_tensors):
+                            t.copy_(torch.where(finite, t, b))
                 nan_flag = AF.reduce_nan_flags(dev)
         finally:
             AF._defer_nan = False
         return _Captured(graph, x, loss.detach(), nan_flag)  # keep no autograd graph alive
+
+    def _fused_adam_ok(self):
+        """fs_adam_step covers the reference's Adam: flat buffers, float lr, L2 weight decay,
+        no amsgrad / maximize / differentiable, a float32 step count on the device."""
+        if getattr(self, "_flat_grad", None) is None:
+            return False
+        g = self.opt.param_groups[0]
+        st = self.opt.state.get(self._flat_param, {})
+        step = st.get("step")
+        return (not g.get("amsgrad") and not g.get("maximize") and not g.get("differentiable")
+                and not g.get("decoupled_weight_decay") and not torch.is_tensor(g["lr"])
+                and not any(torch.is_tensor(b) for b in g["betas"]) and torch.is_tensor(step)
+                and step.is_cuda and step.dtype == torch.float32 and "exp_avg" in st and "exp_avg_sq" in st)
+
+    def _adam_step(self, loss=None):
+        """One Adam step over the flat buffers (fs_adam_step); loss (device scalar,
+        nullable): nothing is written when it is NaN / inf."""
+        from .. import _lib
+
+        g = self.opt.param_groups[0]
+        st = self.opt.state[self._flat_param]
+        p = _lib.ptr
+        b1, b2 = g["betas"]
+        if loss is not None:
+            loss = loss.reshape(1).to(torch.float32).contiguous()
+        _lib.check(_lib.load().fs_adam_step(p(self._flat_param), p(self._flat_grad), p(st["exp_avg"]),
+                                            p(st["exp_avg_sq"]), self._flat_param.numel(), p(st["step"]),
+                                            p(loss), float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                            float(g["weight_decay"]), _lib.stream_ptr()), "fs_adam_step")
 
     def _opt_tensors(self):
         return [v for st in self.opt.state.values() for v in st.values() if torch.is_tensor(v)]
@@ -233,7 +269,10 @@ class GraphedTrainStep:
         if bool(~(torch.isnan(loss) | torch.isinf(loss))):
             loss.backward()
             self._gather_grads()
-            self.opt.step()
+            if self._fused_adam_ok():
+                self._adam_step()
+            else:
+                self.opt.step()
         return loss.detach()
 
     def step(self, batch):

@@ -277,6 +277,16 @@ int64_t fs_set_wide_rows(int64_t rows);
 int fs_target_energy(const float *x, int64_t B, int32_t N, double bound, double temperature, int32_t num_wells,
                      double V0_0, double V0_1, double r0, double k, float *E, float *grad_x, void *stream);
 
+/* One Adam step (torch.optim.Adam, L2 weight decay added to the gradient; the Algorithm-2
+ * optimizer, main_algorithm_2.py:310,440) over n float32 parameters param [n] with their
+ * gradient grad and moments exp_avg / exp_avg_sq [n], in torch's capturable multi-tensor
+ * arithmetic; step [1] is the float32 step count (incremented).  loss (nullable) [1]: when
+ * it is NaN or inf nothing is written (main_algorithm_2.py:324-326 skips the step).  All
+ * buffers 16-byte aligned. */
+int fs_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float *step,
+                 const float *loss, double lr, double beta1, double beta2, double eps, double weight_decay,
+                 void *stream);
+
 /* unconstrained_rational_quadratic_spline, circular tails (NF/normflows/utils/
  * splines.py:16-222) for M independent elements: x [M], unnormalised widths /
  * heights uw, uh [M][K], derivatives ud [M][K+1] (row-major, contiguous).

@@ -147,3 +147,39 @@ def test_linear_group_launch_matches_single_launches():
         torch.testing.assert_close(outs[0][3], gu.sum(0), rtol=1e-5, atol=1e-3)
 
 
+
+
+@pytest.mark.parametrize("n", [4096 + 3, 1000])
+def test_fused_adam_matches_torch_capturable_adam(n):
+    """fs_adam_step (csrc/optim_kernels.hip) against torch.optim.Adam(capturable=True) with
+    L2 weight decay (main_algorithm_2.py:310) over several steps, including a step whose
+    loss is NaN (nothing written, the step count kept: main_algorithm_2.py:324-326)."""
+    from flowstate import _lib
+
+    L, p = _lib.load(), _lib.ptr
+    g = torch.Generator(device="cuda").manual_seed(n)
+    lr, betas, eps, wd = 5.4351e-4, (0.9, 0.999), 1e-8, 9.5857e-5
+    ref = torch.nn.Parameter(torch.randn(n, device="cuda", generator=g))
+    opt = torch.optim.Adam([ref], lr=lr, betas=betas, eps=eps, weight_decay=wd, capturable=True)
+    par = ref.detach().clone()
+    m, v = torch.zeros_like(par), torch.zeros_like(par)
+    step = torch.zeros((), device="cuda")
+    for it in range(6):
+        grad = torch.randn(n, device="cuda", generator=g) * (10.0 ** (it % 3 - 1))
+        loss = torch.tensor([float("nan") if it == 3 else 1.0], device="cuda")
+        if it != 3:
+            ref.grad = grad.clone()
+            opt.step()
+        before = (par.clone(), m.clone(), v.clone(), step.clone())
+        _lib.check(L.fs_adam_step(p(par), p(grad), p(m), p(v), n, p(step), p(loss), lr, betas[0], betas[1], eps, wd,
+                                  _lib.stream_ptr()))
+        torch.cuda.synchronize()
+        if it == 3:
+            for a, b in zip((par, m, v, step), before):
+                assert torch.equal(a, b)
+            continue
+        st = opt.state[ref]
+        assert float(step) == float(st["step"])
+        torch.testing.assert_close(m, st["exp_avg"], rtol=1e-6, atol=1e-9)
+        torch.testing.assert_close(v, st["exp_avg_sq"], rtol=1e-6, atol=1e-12)
+        torch.testing.assert_close(par, ref.detach(), rtol=1e-6, atol=1e-8)
