@@ -729,6 +729,44 @@ int fs_coupling_pair_pre(const fs_coupling *s, const float *z, const float *uw, 
                   "fs_coupling_pair_pre");
 }
 
+int fs_coupling_bwd_step(const fs_coupling *f, const float *x_f, const float *g_t, float *gx_f, const float *gx_add,
+                         const fs_coupling *c, const float *x, const float *params, const float *uw, const float *uh,
+                         const float *ud, const float *g_lq, float *gx, float *g_params, float *g_u, void *stream) {
+    int rc = check_coupling(f, "fs_coupling_bwd_step");
+    if (rc || (rc = check_coupling(c, "fs_coupling_bwd_step"))) return rc;
+    REQUIRE(f->rows == c->rows && f->D == c->D && c->D <= 256, "fs_coupling_bwd_step: the layers differ in rows or D");
+    REQUIRE(c->rows == 0 || (x_f && g_t && gx_f && x && params && uw && uh && ud && gx && g_params && g_u),
+            "fs_coupling_bwd_step: invalid arguments");
+    return hip_rc(fs_coupling_bwd_step_impl(f, x_f, g_t, gx_f, gx_add, c, x, params, uw, uh, ud, g_lq, gx, g_params,
+                                            g_u, (hipStream_t)stream),
+                  "fs_coupling_bwd_step");
+}
+
+int fs_coupling_pair_step(const fs_coupling *s, const float *params, const float *lad_u, const float *lq_in,
+                          float *out, float *lq_out, int32_t *nan_flag, const fs_coupling *s_next, const float *uw_next,
+                          const float *uh_next, const float *ud_next, float *t_next, float *out_next,
+                          float *lad_u_next, const fs_coupling *d, const float *x, const float *params_d,
+                          const float *uw, const float *uh, const float *ud, const float *lq_in_d, float *out_d,
+                          float *lq_out_d, const fs_coupling *d_next, float *t_density_next, void *stream) {
+    int rc = check_coupling(s, "fs_coupling_pair_step");
+    if (rc || (rc = check_coupling(d, "fs_coupling_pair_step")) || (rc = check_coupling(s_next, "fs_coupling_pair_step")) ||
+        (rc = check_coupling(d_next, "fs_coupling_pair_step")))
+        return rc;
+    REQUIRE(s->K == d->K && s->D == d->D && s_next->K == s->K && s_next->D == s->D && d_next->D == d->D &&
+                s_next->rows == s->rows && d_next->rows == d->rows && s->D <= 256,
+            "fs_coupling_pair_step: the layers differ in K, D or rows (D <= 256)");
+    REQUIRE(s->rows == 0 || (params && lad_u && out && lq_out && uw_next && uh_next && ud_next && t_next && out_next &&
+                             lad_u_next),
+            "fs_coupling_pair_step: invalid sampling arguments");
+    REQUIRE(d->rows == 0 || (x && params_d && uw && uh && ud && out_d && lq_out_d && t_density_next),
+            "fs_coupling_pair_step: invalid density arguments");
+    REQUIRE(x != out_d && out != out_next, "fs_coupling_pair_step: outputs must not alias inputs");
+    return hip_rc(fs_coupling_pair_step_impl(s, params, lad_u, lq_in, out, lq_out, nan_flag, s_next, uw_next, uh_next,
+                                             ud_next, t_next, out_next, lad_u_next, d, x, params_d, uw, uh, ud, lq_in_d,
+                                             out_d, lq_out_d, d_next, t_density_next, (hipStream_t)stream),
+                  "fs_coupling_pair_step");
+}
+
 int fs_coupling_pair_post(const fs_coupling *s, const float *params, const float *lad_u, const float *lq_in,
                           float *out, float *lq_out, int32_t *nan_flag, const fs_coupling *d, const float *x,
                           const float *params_d, const float *uw, const float *uh, const float *ud,

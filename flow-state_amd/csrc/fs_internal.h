@@ -143,6 +143,17 @@ hipError_t fs_coupling_features_fwd_impl(const fs_coupling *cp, const float *x, 
 hipError_t fs_coupling_pair_pre_impl(const fs_coupling *sp, const float *z, const float *uw, const float *uh,
                                      const float *ud, float *t, float *out, float *lad_u, int32_t *nan_flag,
                                      const fs_coupling *dp, const float *x, float *td, hipStream_t st);
+hipError_t fs_coupling_pair_step_impl(const fs_coupling *sp, const float *params, const float *lad_u,
+                                      const float *lq_in, float *out, float *lq_out, int32_t *nan_flag,
+                                      const fs_coupling *sp2, const float *uw2, const float *uh2, const float *ud2,
+                                      float *t2, float *out2, float *lad_u2, const fs_coupling *dp, const float *x,
+                                      const float *params_d, const float *uw, const float *uh, const float *ud,
+                                      const float *lq_in_d, float *out_d, float *lq_out_d, const fs_coupling *dp2,
+                                      float *t_d2, hipStream_t st);
+hipError_t fs_coupling_bwd_step_impl(const fs_coupling *fp, const float *xf, const float *g_t, float *gxf,
+                                     const float *gx_add, const fs_coupling *cp, const float *x, const float *params,
+                                     const float *uw, const float *uh, const float *ud, const float *g_lq, float *gx,
+                                     float *g_params, float *g_u, hipStream_t st);
 hipError_t fs_coupling_pair_post_impl(const fs_coupling *sp, const float *params, const float *lad_u,
                                       const float *lq_in, float *out, float *lq_out, int32_t *nan_flag,
                                       const fs_coupling *dp, const float *x, const float *params_d, const float *uw,

@@ -351,7 +351,8 @@ struct DensityFwdArgs {
 };
 
 template <int K>
-__device__ __forceinline__ void density_fwd_row(const CouplingArgs &c, const DensityFwdArgs &d, int64_t row) {
+__device__ __forceinline__ void density_fwd_row(const CouplingArgs &c, const DensityFwdArgs &d, int64_t row,
+                                                float *rb = nullptr) {
     const int lane = threadIdx.x & 63;
     const float *xr = d.x + row * c.D;
     float sc = 0.f, su = 0.f;
@@ -370,6 +371,10 @@ __device__ __forceinline__ void density_fwd_row(const CouplingArgs &c, const Den
             rqs_point<K, false>(xi, d.uw + j * K, d.uh + j * K, d.ud + j * (K + 1), c.bound, yi, li, nullptr);
         d.out[row * c.D + (pt + c.D - c.split) % c.D] = yt;
         d.out[row * c.D + (pi + c.D - c.split) % c.D] = yi;
+        if (rb) {  // the row for the next layer's features in the same launch
+            rb[(pt + c.D - c.split) % c.D] = yt;
+            rb[(pi + c.D - c.split) % c.D] = yi;
+        }
         sc += lt;
         su += li;
     }
@@ -386,25 +391,24 @@ __global__ __launch_bounds__(256) void coupling_density_fwd_kernel(CouplingArgs 
 
 // its adjoints: gx (both halves, spline part), g_params [rows][n][3K+1], g_u the per-row
 // unconditional adjoints [rows][n][3K+1] (summed over rows by the caller)
+// two waves per row: wave part 0 takes the conditional spline's adjoints, part 1 the
+// unconditional one's (each lane one feature), so the row's work is spread twice as wide.
+// gor: the row of g_out (nullable: no output gradient)
 template <int K>
-__global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
-    CouplingArgs c, const float *__restrict__ x, const float *__restrict__ params, const float *__restrict__ uw,
-    const float *__restrict__ uh, const float *__restrict__ ud, const float *__restrict__ g_out,
-    const float *__restrict__ g_lq, float *gx, float *g_params, float *g_u) {
-    // two waves per row: wave part 0 takes the conditional spline's adjoints, part 1 the
-    // unconditional one's (each lane one feature), so the row's work is spread twice as wide
+__device__ __forceinline__ void density_bwd_row(const CouplingArgs &c, const float *__restrict__ x,
+                                                const float *__restrict__ params, const float *__restrict__ uw,
+                                                const float *__restrict__ uh, const float *__restrict__ ud,
+                                                const float *gor, const float *__restrict__ g_lq, float *gx,
+                                                float *g_params, float *g_u, int64_t row, int part) {
     const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6, part = wv & 1;
-    const int64_t row = (int64_t)blockIdx.x * kCplRows + (wv >> 1);
-    if (row >= c.rows) return;
     const float *xr = x + row * c.D;
     const float gl = g_lq ? g_lq[row] : 0.f;
     constexpr int P = 3 * K + 1;
     for (int j = lane; j < c.n; j += 64) {
         const int pi = (int)c.id[j], pt = (int)c.tr[j];
         const float xi = xr[pi], xt = xr[pt];
-        const float got = g_out ? g_out[row * c.D + (pt + c.D - c.split) % c.D] : 0.f;
-        const float goi = g_out ? g_out[row * c.D + (pi + c.D - c.split) % c.D] : 0.f;
+        const float got = gor ? gor[(pt + c.D - c.split) % c.D] : 0.f;
+        const float goi = gor ? gor[(pi + c.D - c.split) % c.D] : 0.f;
         float *gp = g_params + (row * c.n + j) * P;
         // g_u row: [uw n*K | uh n*K | ud n*(K+1)], the parameters' own layouts back to back
         float *guw = g_u + row * c.n * P + j * K;
@@ -456,11 +460,25 @@ __global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
     }
 }
 
+template <int K>
+__global__ __launch_bounds__(256) void coupling_density_bwd_kernel(
+    CouplingArgs c, const float *__restrict__ x, const float *__restrict__ params, const float *__restrict__ uw,
+    const float *__restrict__ uh, const float *__restrict__ ud, const float *__restrict__ g_out,
+    const float *__restrict__ g_lq, float *gx, float *g_params, float *g_u) {
+    const int wv = threadIdx.x >> 6;
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (wv >> 1);
+    if (row >= c.rows) return;
+    density_bwd_row<K>(c, x, params, uw, uh, ud, g_out ? g_out + row * c.D : nullptr, g_lq, gx, g_params, g_u, row,
+                       wv & 1);
+}
+
 // density direction, before the conditioner: t = [cos(s x_id), sin(s x_id)]
-__device__ __forceinline__ void features_row(const CouplingArgs &c, const float *__restrict__ x, float *t, int64_t row) {
+__device__ __forceinline__ void features_row(const CouplingArgs &c, const float *__restrict__ x, float *t, int64_t row,
+                                             const float *xr = nullptr) {
     const int lane = threadIdx.x & 63;
+    if (!xr) xr = x + row * c.D;
     for (int j = lane; j < c.n; j += 64) {
-        const float v = c.scale * x[row * c.D + c.id[j]];
+        const float v = c.scale * xr[c.id[j]];
         t[row * 2 * c.n + j] = cosf(v);
         t[row * 2 * c.n + c.n + j] = sinf(v);
     }
@@ -474,20 +492,59 @@ __global__ __launch_bounds__(256) void coupling_features_fwd_kernel(CouplingArgs
 
 // adjoint of the periodic features t = [cos(s x_id), sin(s x_id)]: gx at the identity
 // positions, 0 at the transform positions (+ gx_add, the splines' gradient of the same x)
-__global__ __launch_bounds__(256) void coupling_features_bwd_kernel(CouplingArgs c, const float *__restrict__ x,
-                                                                    const float *__restrict__ g_t, float *gx,
-                                                                    const float *__restrict__ gx_add) {
+__device__ __forceinline__ void features_bwd_row(const CouplingArgs &c, const float *__restrict__ x,
+                                                 const float *__restrict__ g_t, float *gx,
+                                                 const float *__restrict__ gx_add, int64_t row, float *rb = nullptr) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
-    if (row >= c.rows) return;
     for (int j = lane; j < c.n; j += 64) {
         const int pi = (int)c.id[j], pt = (int)c.tr[j];
         const float v = c.scale * x[row * c.D + pi];
         const float gc = g_t[row * 2 * c.n + j] * -sinf(v), gs = g_t[row * 2 * c.n + c.n + j] * cosf(v);
         const float ai = gx_add ? gx_add[row * c.D + pi] : 0.f, at = gx_add ? gx_add[row * c.D + pt] : 0.f;
-        gx[row * c.D + pi] = (gc * c.scale + gs * c.scale) + ai;
+        const float gi = (gc * c.scale + gs * c.scale) + ai;
+        gx[row * c.D + pi] = gi;
         gx[row * c.D + pt] = at;
+        if (rb) {
+            rb[pi] = gi;
+            rb[pt] = at;
+        }
     }
+}
+
+__global__ __launch_bounds__(256) void coupling_features_bwd_kernel(CouplingArgs c, const float *__restrict__ x,
+                                                                    const float *__restrict__ g_t, float *gx,
+                                                                    const float *__restrict__ gx_add) {
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (threadIdx.x >> 6);
+    if (row >= c.rows) return;
+    features_bwd_row(c, x, g_t, gx, gx_add, row);
+}
+
+// The backward between two layers of the density pass in one launch (fs_coupling_bwd_step):
+// layer l's features adjoint (its input gradient, = the output gradient of layer l - 1,
+// kept in LDS and also written to gx) and then layer l - 1's spline adjoints on that row,
+// each exactly as fs_coupling_features_bwd then fs_coupling_density_bwd compute them.
+constexpr int kCplMaxDB = 256;
+
+template <int K>
+__global__ __launch_bounds__(256) void coupling_bwd_step_kernel(CouplingArgs cf, const float *__restrict__ xf,
+                                                                const float *__restrict__ g_t, float *gxf,
+                                                                const float *__restrict__ gx_add, CouplingArgs c,
+                                                                const float *__restrict__ x,
+                                                                const float *__restrict__ params,
+                                                                const float *__restrict__ uw,
+                                                                const float *__restrict__ uh,
+                                                                const float *__restrict__ ud,
+                                                                const float *__restrict__ g_lq, float *gx,
+                                                                float *g_params, float *g_u) {
+    __shared__ float rbuf[kCplRows][kCplMaxDB];
+    const int wv = threadIdx.x >> 6;
+    float *rb = rbuf[wv >> 1];
+    const int64_t row = (int64_t)blockIdx.x * kCplRows + (wv >> 1);
+    const bool live = row < c.rows;
+    if (live && (wv & 1) == 0) features_bwd_row(cf, xf, g_t, gxf, gx_add, row, rb);
+    __syncthreads();
+    if (!live) return;
+    density_bwd_row<K>(c, x, params, uw, uh, ud, rb, g_lq, gx, g_params, g_u, row, wv & 1);
 }
 
 // sampling direction (Coupling.inverse), forward only: roll, unconditional inverse spline
@@ -500,9 +557,10 @@ struct SamplePreArgs {
 };
 
 template <int K>
-__device__ __forceinline__ void sample_pre_row(const CouplingArgs &c, const SamplePreArgs &s, int64_t row) {
+__device__ __forceinline__ void sample_pre_row(const CouplingArgs &c, const SamplePreArgs &s, int64_t row,
+                                               const float *zr = nullptr) {
     const int lane = threadIdx.x & 63;
-    const float *zr = s.z + row * c.D;
+    if (!zr) zr = s.z + row * c.D;
     float su = 0.f;
     for (int j = lane; j < c.n; j += 64) {
         const int pi = (int)c.id[j], pt = (int)c.tr[j];
@@ -536,11 +594,16 @@ struct SamplePostArgs {
 };
 
 template <int K>
-__device__ __forceinline__ void sample_post_row(const CouplingArgs &c, const SamplePostArgs &s, int64_t row) {
+__device__ __forceinline__ void sample_post_row(const CouplingArgs &c, const SamplePostArgs &s, int64_t row,
+                                                float *rb = nullptr) {
     const int lane = threadIdx.x & 63;
     float sc = 0.f;
     for (int j = lane; j < c.n; j += 64) {
         const int pt = (int)c.tr[j];
+        if (rb) {
+            const int pi = (int)c.id[j];
+            rb[pi] = s.out[row * c.D + pi];  // written by this layer's pre launch
+        }
         const float xt = s.out[row * c.D + pt];
         float yt = xt, lt = 0.f;
         if (xt >= -c.bound && xt <= c.bound) {
@@ -550,6 +613,7 @@ __device__ __forceinline__ void sample_post_row(const CouplingArgs &c, const Sam
             rqs_point<K, true>(xt, w, h, p + 2 * K, c.bound, yt, lt, s.nan_flag);
         }
         s.out[row * c.D + pt] = yt;
+        if (rb) rb[pt] = yt;
         sc += lt;
     }
     sc = wave_sum(sc);
@@ -587,6 +651,37 @@ __global__ __launch_bounds__(256) void coupling_pair_post_kernel(CouplingArgs cs
     } else if (row < cd.rows) {
         density_fwd_row<K>(cd, d, row);
     }
+}
+
+// One launch between two layers of the training step's passes (fs_coupling_pair_step):
+// the post launch of layer l (sampling: conditional inverse spline; density: both splines,
+// roll, log-det) and, on the row it just produced (kept in LDS), the pre launch of the
+// next layer (sampling: roll + unconditional inverse spline + features; density: the
+// features).  Each row exactly as fs_coupling_pair_post then fs_coupling_pair_pre compute
+// it; one launch and one HBM round trip of the rows fewer per layer.
+constexpr int kCplMaxD = 256;
+
+template <int K>
+__global__ __launch_bounds__(256) void coupling_pair_step_kernel(CouplingArgs cs, SamplePostArgs s, CouplingArgs cs2,
+                                                                 SamplePreArgs s2, CouplingArgs cd, DensityFwdArgs d,
+                                                                 CouplingArgs cd2, float *t_d2, unsigned nb0) {
+    __shared__ float rbuf[kCplRows][kCplMaxD];
+    float *rb = rbuf[threadIdx.x >> 6];
+    const bool dens = blockIdx.x >= nb0;
+    const int64_t row = (int64_t)(dens ? blockIdx.x - nb0 : blockIdx.x) * kCplRows + (threadIdx.x >> 6);
+    const bool live = dens ? row < cd.rows : row < cs.rows;
+    if (live) {
+        if (!dens)
+            sample_post_row<K>(cs, s, row, rb);
+        else
+            density_fwd_row<K>(cd, d, row, rb);
+    }
+    __syncthreads();  // the row's LDS copy, written by every lane of its wave
+    if (!live) return;
+    if (!dens)
+        sample_pre_row<K>(cs2, s2, row, rb);
+    else
+        features_row(cd2, d.out, t_d2, row, rb);
 }
 
 }  // namespace fs
@@ -687,6 +782,25 @@ hipError_t fs_coupling_density_bwd_impl(const fs_coupling *cp, const float *x, c
     return hipErrorInvalidValue;
 }
 
+hipError_t fs_coupling_bwd_step_impl(const fs_coupling *fp, const float *xf, const float *g_t, float *gxf,
+                                     const float *gx_add, const fs_coupling *cp, const float *x, const float *params,
+                                     const float *uw, const float *uh, const float *ud, const float *g_lq, float *gx,
+                                     float *g_params, float *g_u, hipStream_t st) {
+    const fs::CouplingArgs af = coupling_args(fp), a = coupling_args(cp);
+    if (af.rows != a.rows || af.D != a.D || a.D > kCplMaxDB) return hipErrorInvalidValue;
+    if (a.rows <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((a.rows + kCplRows - 1) / kCplRows);
+#define FS_DB(KK)                                                                                                  \
+    if (cp->K == KK) {                                                                                             \
+        hipLaunchKernelGGL(coupling_bwd_step_kernel<KK>, dim3(grid), dim3(128 * kCplRows), 0, st, af, xf, g_t, gxf, \
+                           gx_add, a, x, params, uw, uh, ud, g_lq, gx, g_params, g_u);                            \
+        return hipGetLastError();                                                                                  \
+    }
+    FS_DB(5) FS_DB(8) FS_DB(15) FS_DB(32)
+#undef FS_DB
+    return hipErrorInvalidValue;
+}
+
 hipError_t fs_coupling_sample_pre_impl(const fs_coupling *cp, const float *z, const float *uw, const float *uh,
                                        const float *ud, float *t, float *out, float *lad_u, int32_t *nan_flag,
                                        hipStream_t st) {
@@ -735,6 +849,39 @@ hipError_t fs_coupling_pair_post_impl(const fs_coupling *sp, const float *params
     FS_PAIR_LAUNCH(coupling_pair_post_kernel, as, s, ad, d)
 }
 #undef FS_PAIR_LAUNCH
+
+hipError_t fs_coupling_pair_step_impl(const fs_coupling *sp, const float *params, const float *lad_u,
+                                      const float *lq_in, float *out, float *lq_out, int32_t *nan_flag,
+                                      const fs_coupling *sp2, const float *uw2, const float *uh2, const float *ud2,
+                                      float *t2, float *out2, float *lad_u2, const fs_coupling *dp, const float *x,
+                                      const float *params_d, const float *uw, const float *uh, const float *ud,
+                                      const float *lq_in_d, float *out_d, float *lq_out_d, const fs_coupling *dp2,
+                                      float *t_d2, hipStream_t st) {
+    const SamplePostArgs s{params, lad_u, lq_in, out, lq_out, nan_flag};
+    const SamplePreArgs s2{out, uw2, uh2, ud2, t2, out2, lad_u2, nan_flag};
+    const DensityFwdArgs d{x, params_d, uw, uh, ud, lq_in_d, out_d, lq_out_d};
+    const fs::CouplingArgs as2 = coupling_args(sp2), ad2 = coupling_args(dp2);
+    if (sp2->K != sp->K || as2.rows != sp->rows || ad2.rows != dp->rows || sp->D > kCplMaxD || dp->D > kCplMaxD ||
+        sp2->D != sp->D || dp2->D != dp->D)
+        return hipErrorInvalidValue;
+#define FS_PAIR_LAUNCH(KERNEL, ...)                                                                     \
+    const fs::CouplingArgs as = coupling_args(sp), ad = coupling_args(dp);                              \
+    if (sp->K != dp->K || as.rows < 0 || ad.rows < 0) return hipErrorInvalidValue;                     \
+    const unsigned nb0 = (unsigned)((as.rows + kCplRows - 1) / kCplRows);                              \
+    const unsigned nb = nb0 + (unsigned)((ad.rows + kCplRows - 1) / kCplRows);                         \
+    if (nb == 0) return hipSuccess;                                                                     \
+    const dim3 block(64 * kCplRows);                                                                    \
+    switch (sp->K) {                                                                                    \
+    case 5: hipLaunchKernelGGL((KERNEL<5>), dim3(nb), block, 0, st, __VA_ARGS__, nb0); break;           \
+    case 8: hipLaunchKernelGGL((KERNEL<8>), dim3(nb), block, 0, st, __VA_ARGS__, nb0); break;           \
+    case 15: hipLaunchKernelGGL((KERNEL<15>), dim3(nb), block, 0, st, __VA_ARGS__, nb0); break;         \
+    case 32: hipLaunchKernelGGL((KERNEL<32>), dim3(nb), block, 0, st, __VA_ARGS__, nb0); break;         \
+    default: return hipErrorInvalidValue;                                                               \
+    }                                                                                                   \
+    return hipGetLastError();
+    FS_PAIR_LAUNCH(coupling_pair_step_kernel, as, s, as2, s2, ad, d, ad2, t_d2)
+#undef FS_PAIR_LAUNCH
+}
 
 hipError_t fs_coupling_features_fwd_impl(const fs_coupling *cp, const float *x, float *t, hipStream_t st) {
     const fs::CouplingArgs a = coupling_args(cp);

@@ -123,6 +123,8 @@ _SIGS = {
     "fs_coupling_sample_pre": (ctypes.c_int, [_CP] + [_P] * 9),
     "fs_coupling_sample_post": (ctypes.c_int, [_CP] + [_P] * 7),
     "fs_coupling_pair_pre": (ctypes.c_int, [_CP] + [_P] * 8 + [_CP, _P, _P, _P]),
+    "fs_coupling_bwd_step": (ctypes.c_int, [_CP] + [_P] * 4 + [_CP] + [_P] * 9 + [_P]),
+    "fs_coupling_pair_step": (ctypes.c_int, [_CP] + [_P] * 6 + [_CP] + [_P] * 6 + [_CP] + [_P] * 8 + [_CP, _P, _P]),
     "fs_coupling_pair_post": (ctypes.c_int, [_CP] + [_P] * 6 + [_CP] + [_P] * 9),
     "fs_set_wide_rows": (_I64, [_I64]),
     "fs_adam_step": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P] + [ctypes.c_double] * 5 + [_P]),

@@ -656,6 +656,12 @@ class _Features(torch.autograd.Function):
         ctx.save_for_backward(x)
         ctx.layer = layer
         ctx.res = res
+        # x is the previous layer's output (the training step's density pass): the backward
+        # leaves its launch to that layer's spline backward, which carries it
+        # (fs_coupling_bwd_step); the previous layer passed x's spline gradient through the
+        # res stash, so autograd hands the placeholder gradient on unchanged
+        ctx.defer = (pair is not None and res is not None and x.grad_fn is not None
+                     and type(x.grad_fn).__name__ in ("_FinalSplinesBackward", "_DensitySplinesBackward"))
         return t
 
     @staticmethod
@@ -670,10 +676,54 @@ class _Features(torch.autograd.Function):
             add, ctx.res.g = ctx.res.g, None
             if add.shape != x.shape:
                 raise RuntimeError("spline gradient does not match the layer input")
+        if ctx.defer:
+            _pending_features_bwd[gx.data_ptr()] = (ctx.layer, x, gt, add, gx)
+            return gx, None, None, None
         c = _coupling_desc(ctx.layer, x.shape[0])
         _lib.check(_lib.load().fs_coupling_features_bwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(gt), _lib.ptr(gx),
                                                         _lib.ptr(add), _lib.stream_ptr()), "fs_coupling_features_bwd")
         return gx, None, None, None
+
+
+# Features backward launches left to the next spline backward (the previous layer's):
+# {placeholder gradient's data_ptr: (layer, x, g_t, gx_add, placeholder)}.  Each entry holds
+# its placeholder, so no other tensor can take its address meanwhile.
+_pending_features_bwd = {}
+
+
+def _density_bwd(c, x, params, uw, uh, ud, g_out, g_lq, gx, gp, gu):
+    """fs_coupling_density_bwd, or, when g_out is a features backward's pending placeholder,
+    fs_coupling_bwd_step (that backward and this one in one launch)."""
+    from .. import _lib
+
+    L, p = _lib.load(), _lib.ptr
+    q = _pending_features_bwd.pop(g_out.data_ptr(), None) if g_out is not None else None
+    if q is not None and q[4].shape == g_out.shape:
+        layer_f, xf, gt, add, gxf = q
+        cf = _coupling_desc(layer_f, xf.shape[0])
+        _lib.check(L.fs_coupling_bwd_step(ctypes.byref(cf), p(xf), p(gt), p(gxf), p(add), ctypes.byref(c), p(x),
+                                          p(params), p(uw), p(uh), p(ud), p(g_lq), p(gx), p(gp), p(gu),
+                                          _lib.stream_ptr()), "fs_coupling_bwd_step")
+        return
+    if q is not None:  # not this layer's: launch it on its own first
+        layer_f, xf, gt, add, gxf = q
+        cf = _coupling_desc(layer_f, xf.shape[0])
+        _lib.check(L.fs_coupling_features_bwd(ctypes.byref(cf), p(xf), p(gt), p(gxf), p(add), _lib.stream_ptr()),
+                   "fs_coupling_features_bwd")
+    _lib.check(L.fs_coupling_density_bwd(ctypes.byref(c), p(x), p(params), p(uw), p(uh), p(ud), p(g_out), p(g_lq),
+                                         p(gx), p(gp), p(gu), _lib.stream_ptr()), "fs_coupling_density_bwd")
+
+
+def flush_features_bwd():
+    """Launch every features backward still pending (none after a complete backward)."""
+    from .. import _lib
+
+    L, p = _lib.load(), _lib.ptr
+    while _pending_features_bwd:
+        _, (layer_f, xf, gt, add, gxf) = _pending_features_bwd.popitem()
+        cf = _coupling_desc(layer_f, xf.shape[0])
+        _lib.check(L.fs_coupling_features_bwd(ctypes.byref(cf), p(xf), p(gt), p(gxf), p(add), _lib.stream_ptr()),
+                   "fs_coupling_features_bwd")
 
 
 class _DensitySplines(torch.autograd.Function):
@@ -722,10 +772,7 @@ class _DensitySplines(torch.autograd.Function):
         n = x.shape[1] // 2
         gu = torch.empty((x.shape[0], n * (3 * K + 1)), dtype=torch.float32, device=x.device)
         c = _coupling_desc(layer, x.shape[0])
-        _lib.check(_lib.load().fs_coupling_density_bwd(ctypes.byref(c), _lib.ptr(x), _lib.ptr(params), _lib.ptr(uw),
-                                                       _lib.ptr(uh), _lib.ptr(ud), _lib.ptr(g_out), _lib.ptr(g_lq),
-                                                       _lib.ptr(gx), _lib.ptr(gp), _lib.ptr(gu), _lib.stream_ptr()),
-                   "fs_coupling_density_bwd")
+        _density_bwd(c, x, params, uw, uh, ud, g_out, g_lq, gx, gp, gu)
         # the unconditional parameters are shared by every row: their gradient is the column
         # sum of gu, taken as fs_linear_f32's row sum of gu^T (N = 0: no product), which
         # spreads it over (n(3K+1))/32 workgroups (torch's reduction took 16 us at batch 256)
@@ -808,9 +855,7 @@ class _FinalSplines(torch.autograd.Function):
         gp = torch.empty_like(params)
         gu = torch.empty((M, P), dtype=torch.float32, device=x.device)
         c = _coupling_desc(layer, M)
-        _lib.check(L.fs_coupling_density_bwd(ctypes.byref(c), p(x), p(params), p(uw), p(uh), p(ud), p(g_out),
-                                             p(g_lq), p(gx), p(gp), p(gu), _lib.stream_ptr()),
-                   "fs_coupling_density_bwd")
+        _density_bwd(c, x, params, uw, uh, ud, g_out, g_lq, gx, gp, gu)
         gh, gw = torch.empty_like(h), torch.empty_like(w)
         gb = torch.empty((P,), dtype=torch.float32, device=x.device)
         gs = torch.empty((P,), dtype=torch.float32, device=x.device)
@@ -975,6 +1020,7 @@ class _SamplingRider:
         # [pass][BatchNorm][mean | biased variance][H]; pass 0 sampling, 1 density
         self.bnstats = torch.empty((2, len(flat_bn.bns), 2, flat_bn.H), dtype=torch.float32, device=z.device)
         self.layer = None
+        self._post = None  # the last layers' post launch, carried by the next pre launch
 
     def bn_slots(self, bn, p):
         i = self.fbn.index[id(bn)]
@@ -988,7 +1034,9 @@ class _SamplingRider:
         _check_shapes(layer, self.z.shape[0], None, *self.u)
 
     def pre(self, c_density, x, t_density):
-        """fs_coupling_sample_pre of this layer + fs_coupling_features_fwd of the density's."""
+        """fs_coupling_sample_pre of this layer + fs_coupling_features_fwd of the density's;
+        with the previous layers' post launch still pending, both in one launch
+        (fs_coupling_pair_step)."""
         from .. import _lib
 
         z = self.z
@@ -997,10 +1045,22 @@ class _SamplingRider:
         self.lad_u = torch.empty((z.shape[0],), dtype=torch.float32, device=z.device)
         self.cs = _coupling_desc(self.layer, z.shape[0])
         p = _lib.ptr
-        _lib.check(_lib.load().fs_coupling_pair_pre(ctypes.byref(self.cs), p(z), p(self.u[0]), p(self.u[1]),
-                                                    p(self.u[2]), p(self.t), p(self.out), p(self.lad_u),
-                                                    p(self.nan_flag), ctypes.byref(c_density), p(x), p(t_density),
-                                                    _lib.stream_ptr()), "fs_coupling_pair_pre")
+        q, self._post = self._post, None
+        if (q is not None and q["out_d"].data_ptr() == x.data_ptr() and q["out"].data_ptr() == z.data_ptr()
+                and x.is_contiguous() and z.is_contiguous()):
+            _lib.check(_lib.load().fs_coupling_pair_step(
+                ctypes.byref(q["cs"]), p(q["params"]), p(q["lad_u"]), p(q["lq_in"]), p(q["out"]), p(q["lq_out"]),
+                p(self.nan_flag), ctypes.byref(self.cs), p(self.u[0]), p(self.u[1]), p(self.u[2]), p(self.t),
+                p(self.out), p(self.lad_u), ctypes.byref(q["cd"]), p(q["x"]), p(q["params_d"]), p(q["uw"]),
+                p(q["uh"]), p(q["ud"]), p(q["lq_in_d"]), p(q["out_d"]), p(q["lq_out_d"]), ctypes.byref(c_density),
+                p(t_density), _lib.stream_ptr()), "fs_coupling_pair_step")
+        else:
+            if q is not None:
+                self._launch_post(q)
+            _lib.check(_lib.load().fs_coupling_pair_pre(ctypes.byref(self.cs), p(z), p(self.u[0]), p(self.u[1]),
+                                                        p(self.u[2]), p(self.t), p(self.out), p(self.lad_u),
+                                                        p(self.nan_flag), ctypes.byref(c_density), p(x), p(t_density),
+                                                        _lib.stream_ptr()), "fs_coupling_pair_pre")
         self.h, self.hst = self.t, None
 
     def gemm(self, op):
@@ -1052,19 +1112,35 @@ class _SamplingRider:
         self.commit()
 
     def post(self, c_density, x, params, uw, uh, ud, lq_in, out, lq):
-        """fs_coupling_sample_post of this layer + fs_coupling_density_fwd of the density's."""
-        from .. import _lib
-
+        """fs_coupling_sample_post of this layer + fs_coupling_density_fwd of the density's:
+        left pending, so that the next layers' pre launch carries it (fs_coupling_pair_step);
+        flush() launches it alone after the last layer.  The outputs are allocated here."""
         params_s = self.params.contiguous()
         _check_shapes(self.layer, self.z.shape[0], params_s, *self.u)
         lq_s = torch.empty_like(self.lad_u)
-        p = _lib.ptr
-        _lib.check(_lib.load().fs_coupling_pair_post(ctypes.byref(self.cs), p(params_s), p(self.lad_u), p(self.lq),
-                                                     p(self.out), p(lq_s), p(self.nan_flag), ctypes.byref(c_density),
-                                                     p(x), p(params), p(uw), p(uh), p(ud), p(lq_in), p(out), p(lq),
-                                                     _lib.stream_ptr()), "fs_coupling_pair_post")
+        self.flush()
+        # every operand referenced until the launch
+        self._post = dict(cs=self.cs, params=params_s, lad_u=self.lad_u, lq_in=self.lq, out=self.out, lq_out=lq_s,
+                          cd=c_density, x=x, params_d=params, uw=uw, uh=uh, ud=ud, lq_in_d=lq_in, out_d=out,
+                          lq_out_d=lq)
         self.z, self.lq = self.out, lq_s
         self.t = self.out = self.h = self.hst = self.u0 = self.u0st = self.params = None
+
+    def _launch_post(self, q):
+        from .. import _lib
+
+        p = _lib.ptr
+        _lib.check(_lib.load().fs_coupling_pair_post(ctypes.byref(q["cs"]), p(q["params"]), p(q["lad_u"]),
+                                                     p(q["lq_in"]), p(q["out"]), p(q["lq_out"]), p(self.nan_flag),
+                                                     ctypes.byref(q["cd"]), p(q["x"]), p(q["params_d"]), p(q["uw"]),
+                                                     p(q["uh"]), p(q["ud"]), p(q["lq_in_d"]), p(q["out_d"]),
+                                                     p(q["lq_out_d"]), _lib.stream_ptr()), "fs_coupling_pair_post")
+
+    def flush(self):
+        """Launch a pending post launch on its own (after the last layers)."""
+        q, self._post = self._post, None
+        if q is not None:
+            self._launch_post(q)
 
 
 def paired_ok(model, x, z, flat_bn):
@@ -1099,12 +1175,14 @@ def paired_kld(model, x, z, flat_bn):
     flows = model.flows
     L = len(flows)
     rider = _SamplingRider(z, flat_bn)
+    flush_features_bwd()  # nothing may be pending from an interrupted backward
     log_q = None
     xd = x
     with _lib.on_device(x):
         for s in range(L):
             rider.begin(flows[s])
             xd, log_q = density_step(flows[L - 1 - s], xd, log_q, pair=rider)
+        rider.flush()
         flat_bn.update(rider.bnstats, z.shape[0], x.shape[0])
     _nan_flags.append(rider.nan_flag[0] != 0)
     check_nan_flags()

@@ -463,6 +463,25 @@ int fs_coupling_pair_post(const fs_coupling *s, const float *params, const float
                           const float *params_d, const float *uw, const float *uh, const float *ud,
                           const float *lq_in_d, float *out_d, float *lq_out_d, void *stream);
 
+/* fs_coupling_features_bwd of layer f (x_f, g_t, gx_add nullable -> gx_f, the input
+ * gradient of layer f = the output gradient of layer c) and fs_coupling_density_bwd of layer
+ * c on that gradient (g_out = gx_f) in one launch, each row exactly as the two launches
+ * compute it.  D <= 256. */
+int fs_coupling_bwd_step(const fs_coupling *f, const float *x_f, const float *g_t, float *gx_f, const float *gx_add,
+                         const fs_coupling *c, const float *x, const float *params, const float *uw, const float *uh,
+                         const float *ud, const float *g_lq, float *gx, float *g_params, float *g_u, void *stream);
+
+/* fs_coupling_pair_post of layers (s, d) and fs_coupling_pair_pre of the next layers
+ * (s_next, d_next: the sampling pass's next layer reads z = out, the density pass's next
+ * features read x = out_d) in one launch, each row exactly as the two launches compute it.
+ * D <= 256. */
+int fs_coupling_pair_step(const fs_coupling *s, const float *params, const float *lad_u, const float *lq_in,
+                          float *out, float *lq_out, int32_t *nan_flag, const fs_coupling *s_next, const float *uw_next,
+                          const float *uh_next, const float *ud_next, float *t_next, float *out_next,
+                          float *lad_u_next, const fs_coupling *d, const float *x, const float *params_d,
+                          const float *uw, const float *uh, const float *ud, const float *lq_in_d, float *out_d,
+                          float *lq_out_d, const fs_coupling *d_next, float *t_density_next, void *stream);
+
 /* ------------------------------------------------------------------ */
 /* Local moves (MCMC/monte_carlo.py)                                   */
 /* ------------------------------------------------------------------ */

@@ -87,8 +87,10 @@ def test_paired_graphed_steps_match_separate():
 
 
 def test_paired_launch_count():
-    """The paired step's forward half: per layer step 8 launches carry both passes
-    (2 coupling + 6 conditioner), against 16 when the passes run one after the other."""
+    """The paired step's forward half: per layer step 7 launches carry both passes
+    (6 conditioner + one coupling launch that holds this layer's post and the next layer's
+    pre, fs_coupling_pair_step; one more after the last layer), against 16 when the passes
+    run one after the other."""
     from torch.profiler import ProfilerActivity, profile
 
     N, rows = 16, 64
@@ -107,5 +109,5 @@ def test_paired_launch_count():
         counts[mode] = sum(1 for n in names if "gemm" in n or "coupling" in n)
         del loss
     L = kw["L"]
-    assert counts["paired"] == 8 * L, counts
+    assert counts["paired"] == 7 * L + 1, counts
     assert counts["separate"] == 16 * L, counts

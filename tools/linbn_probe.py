@@ -83,6 +83,20 @@ def main(M=256, H=128, NF=2944):
                                                                    gpl.sbk, gpl.sbn, gpl.bias, gpl.R, gpl.ldr, gpl.C,
                                                                    gpl.ldc, gpl.rowsum_a, st()), "plain"))
 
+    # final layer's forward (736 tiles) and weight gradient (dW = dY^T h over the batch)
+    hf, wff, bff = rn(M, H), rn(NF, H) * 0.05, rn(NF)
+    yf = torch.empty(M, NF, device=dev)
+    gff = _lib.GemmF32(M, NF, H, p(hf), H, 1, p(wff), 1, H, p(bff), None, 0, p(yf), NF, None)
+    out["final_fwd"] = timed(lambda: _lib.check(L.fs_linear_f32(gff.M, gff.N, gff.K, gff.A, gff.sam, gff.sak, gff.B,
+                                                                gff.sbk, gff.sbn, gff.bias, None, 0, gff.C, gff.ldc,
+                                                                None, st()), "ffwd"))
+    gpf = rn(M, NF)
+    gwf, gbf = torch.empty(NF, H, device=dev), torch.empty(NF, device=dev)
+    gdw = _lib.GemmF32(NF, H, M, p(gpf), 1, NF, p(hf), H, 1, None, None, 0, p(gwf), H, p(gbf))
+    out["final_dw"] = timed(lambda: _lib.check(L.fs_linear_f32(gdw.M, gdw.N, gdw.K, gdw.A, gdw.sam, gdw.sak, gdw.B,
+                                                               gdw.sbk, gdw.sbn, None, None, 0, gdw.C, gdw.ldc,
+                                                               gdw.rowsum_a, st()), "fdw"))
+
     # final layer's input gradient: dX = dY W over K = NF
     dyf, wf = rn(M, NF), rn(NF, H) * 0.05
     gxf = torch.empty(M, H, device=dev)
