@@ -163,6 +163,22 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
         a[s] = load4<AK>(Ap, g.sak, k + 4 * h, g.K, aok && k < g.K);
         b[s] = load4<BK>(Bp, g.sbk, k + 4 * h, g.K, bok && k < g.K);
     }
+    // the epilogue's bias and residual operands (wave 0 writes the tile) loaded with the
+    // first operands, so that their round trip is not left for after the reduction
+    const int64_t col = n0 + r;
+    float ep_bias = 0.f, ep_r[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ep_r[i] = 0.f;
+    if (SPLIT == 1 || w == 0) {
+        ep_bias = (g.bias && bok) ? g.bias[col] : 0.f;
+        if (g.R) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
+                if (row < g.M && bok) ep_r[i] = g.R[row * g.ldr + col];
+            }
+        }
+    }
     pro();
     if constexpr (BNA) {
 #pragma unroll
@@ -202,15 +218,14 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
         rs += __shfl_xor(rs, 32);
         if (h == 0 && aok) g.rowsum_a[m0 + r] = rs;
     }
-    const int64_t col = n0 + r;
-    const float bias = (g.bias && bok) ? g.bias[col] : 0.f;
+    const float bias = ep_bias;
     float sv = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
         float v = acc[i] + bias;
         if (row < g.M && bok) {
-            if (g.R) v = v + g.R[row * g.ldr + col];
+            if (g.R) v = v + ep_r[i];
             g.C[row * g.ldc + col] = v;
         }
         acc[i] = v;
