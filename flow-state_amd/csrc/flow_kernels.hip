@@ -1021,9 +1021,14 @@ __global__ void __launch_bounds__(kThreads) wide_output_kernel(WideArgs w) {
 // ---------------------------------------------------------------------------
 // Packing kernels
 // ---------------------------------------------------------------------------
+// Every packing kernel covers all layers (blockIdx.y, raw / packed strides sl / dl) and,
+// for the residual blocks, all blocks (blockIdx.z, strides sz / dz) in one launch.
 // kind 0: plain linear W[nout][kin];  kind 1: final layer widths / heights (2 tiles per feature)
 __global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restrict__ src, int kin, int kg,
-                                   int ntiles, int nout, int kind, int K, float wh_scale) {
+                                   int ntiles, int nout, int kind, int K, float wh_scale, int64_t sl, int64_t dl,
+                                   int64_t sz, int64_t dz) {
+    src += blockIdx.y * sl + blockIdx.z * sz;
+    dst += blockIdx.y * dl + blockIdx.z * dz;
     const int64_t total = (int64_t)ntiles * kg * 256;
     const int P = 3 * K + 1;
     for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
@@ -1055,7 +1060,10 @@ __global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restr
 
 // derivative rows d_0..d_K of every feature (final-layer rows 2K..3K, unscaled) as
 // [N][H/4][K+1][4]: cond_spline's per-lane gathers
-__global__ void pack_deriv_kernel(float *__restrict__ dst, const float *__restrict__ src, int N, int H, int K) {
+__global__ void pack_deriv_kernel(float *__restrict__ dst, const float *__restrict__ src, int N, int H, int K,
+                                  int64_t sl, int64_t dl) {
+    src += blockIdx.y * sl;
+    dst += blockIdx.y * dl;
     const int K1 = K + 1, P = 3 * K + 1;
     const int64_t total = (int64_t)N * H * K1;
     for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
@@ -1074,7 +1082,9 @@ __global__ void pack_deriv_kernel(float *__restrict__ dst, const float *__restri
 // vectors: biases, folded eval BatchNorm (alpha = w / sqrt(var + eps), beta = b - mean*alpha),
 // final-layer biases in packed column order, unconditional-spline knots.
 __global__ void pack_vec_kernel(float *__restrict__ dst, const float *__restrict__ src, int N, int H, int nb,
-                                int K, double tail_bound) {
+                                int K, double tail_bound, int64_t sl, int64_t dl) {
+    src += blockIdx.y * sl;
+    dst += blockIdx.y * dl;
     const RawLayout R = raw_layout(N, H, nb, K);
     const PackLayout PL = pack_layout(N, H, nb, K);
     float *V = dst + PL.vec;
@@ -1479,7 +1489,7 @@ int64_t fs_flow_packed_bytes_impl(const fs_flow_dims *d) {
 
 hipError_t fs_flow_pack_vec(float *dst, const float *raw_layer, const fs_flow_dims *d, hipStream_t st) {
     hipLaunchKernelGGL(pack_vec_kernel, dim3(16), dim3(256), 0, st, dst, raw_layer, d->N, d->H, d->nb, d->K,
-                       d->tail_bound);
+                       d->tail_bound, (int64_t)0, (int64_t)0);
     return hipGetLastError();
 }
 
@@ -1490,35 +1500,37 @@ hipError_t fs_flow_pack_impl(const fs_flow_dims *d, const float *raw, float *pac
     const PackLayout PL = pack_layout(N, H, nb, K);
     hipError_t e = hipMemsetAsync(packed, 0, (size_t)PL.stride * d->L * 4, st);
     if (e != hipSuccess) return e;
-    for (int l = 0; l < d->L; ++l) {
-        const float *src = raw + (int64_t)l * R.stride;
-        float *dst = packed + (int64_t)l * PL.stride;
-        auto lin = [&](float *o, const float *w, int kin, int kg, int ntiles, int nout, int kind) {
-            int64_t tot = (int64_t)ntiles * kg * 256;
-            int blocks = (int)((tot + 255) / 256);
-            if (blocks > 4096) blocks = 4096;
-            hipLaunchKernelGGL(pack_linear_kernel, dim3(blocks), dim3(256), 0, st, o, w, kin, kg, ntiles, nout,
-                               kind, K, (float)(1.4426950408889634 / sqrt((double)H)));
-        };
-        lin(dst + PL.win, src + R.win, 2 * N, PL.kg_in, H / 32, H, 0);
-        for (int jb = 0; jb < nb; ++jb) {
-            const float *B = src + R.blocks + (int64_t)jb * R.block_stride;
-            float *o = dst + PL.blocks + (int64_t)jb * PL.block_stride;
-            lin(o, B + RawLayout::w0(H), H, PL.kg_h, H / 32, H, 0);
-            lin(o + PL.block_stride / 2, B + RawLayout::w1(H), H, PL.kg_h, H / 32, H, 0);
-        }
-        if (K <= 16)
-            lin(dst + PL.wf, src + R.wf, H, PL.kg_h, 2 * ((N + 1) / 2), N, 2);  // feature pairs
-        else
-            lin(dst + PL.wf, src + R.wf, H, PL.kg_h, 2 * N, 0, 1);
-        {
-            const int64_t tot = (int64_t)N * H * (K + 1);
-            int blocks = (int)((tot + 255) / 256);
-            if (blocks > 4096) blocks = 4096;
-            hipLaunchKernelGGL(pack_deriv_kernel, dim3(blocks), dim3(256), 0, st, dst + PL.wd, src + R.wf, N, H, K);
-        }
-        hipLaunchKernelGGL(pack_vec_kernel, dim3(16), dim3(256), 0, st, dst, src, N, H, nb, K, d->tail_bound);
+    // one launch per kind of matrix for all layers (and blocks): 6 launches, not ~8 per layer
+    const unsigned NL = (unsigned)d->L;
+    const int64_t sl = R.stride, dl = PL.stride;
+    auto lin = [&](float *o, const float *w, int kin, int kg, int ntiles, int nout, int kind, unsigned nz, int64_t sz,
+                   int64_t dz) {
+        int64_t tot = (int64_t)ntiles * kg * 256;
+        int blocks = (int)((tot + 255) / 256);
+        if (blocks > 1024) blocks = 1024;
+        hipLaunchKernelGGL(pack_linear_kernel, dim3(blocks, NL, nz), dim3(256), 0, st, o, w, kin, kg, ntiles, nout,
+                           kind, K, (float)(1.4426950408889634 / sqrt((double)H)), sl, dl, sz, dz);
+    };
+    lin(packed + PL.win, raw + R.win, 2 * N, PL.kg_in, H / 32, H, 0, 1, 0, 0);
+    if (nb > 0) {
+        lin(packed + PL.blocks, raw + R.blocks + RawLayout::w0(H), H, PL.kg_h, H / 32, H, 0, (unsigned)nb,
+            R.block_stride, PL.block_stride);
+        lin(packed + PL.blocks + PL.block_stride / 2, raw + R.blocks + RawLayout::w1(H), H, PL.kg_h, H / 32, H, 0,
+            (unsigned)nb, R.block_stride, PL.block_stride);
     }
+    if (K <= 16)
+        lin(packed + PL.wf, raw + R.wf, H, PL.kg_h, 2 * ((N + 1) / 2), N, 2, 1, 0, 0);  // feature pairs
+    else
+        lin(packed + PL.wf, raw + R.wf, H, PL.kg_h, 2 * N, 0, 1, 1, 0, 0);
+    {
+        const int64_t tot = (int64_t)N * H * (K + 1);
+        int blocks = (int)((tot + 255) / 256);
+        if (blocks > 1024) blocks = 1024;
+        hipLaunchKernelGGL(pack_deriv_kernel, dim3(blocks, NL), dim3(256), 0, st, packed + PL.wd, raw + R.wf, N, H, K,
+                           sl, dl);
+    }
+    hipLaunchKernelGGL(pack_vec_kernel, dim3(16, NL), dim3(256), 0, st, packed, raw, N, H, nb, K, d->tail_bound, sl,
+                       dl);
     return hipGetLastError();
 }
 
