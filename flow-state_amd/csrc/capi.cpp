@@ -57,6 +57,11 @@ int64_t fs_flow_raw_floats(const fs_flow_dims *d) {
     return fs_flow_raw_floats_impl(d);
 }
 
+int fs_gather_chunks(const int64_t *tab, int64_t n, float *dst, void *stream) {
+    REQUIRE(n >= 0 && (n == 0 || (tab && dst)), "fs_gather_chunks: invalid arguments");
+    return hip_rc(fs_gather_chunks_impl(tab, n, dst, (hipStream_t)stream), "fs_gather_chunks");
+}
+
 int64_t fs_flow_packed_bytes(const fs_flow_dims *d) {
     if (check_dims(d) != FS_OK) return -1;
     return fs_flow_packed_bytes_impl(d);

@@ -1487,6 +1487,24 @@ int64_t fs_flow_packed_bytes_impl(const fs_flow_dims *d) {
     return pack_layout(d->N, d->H, d->nb, d->K).stride * d->L * 4;
 }
 
+// The raw parameter image gathered from the layers' own tensors in one launch: chunk c of
+// tab [n][3] = (source address, destination offset, length <= 8192 floats), one workgroup
+// per chunk (the host builds the table once per set of tensor addresses).
+__global__ void __launch_bounds__(256) gather_chunks_kernel(const int64_t *__restrict__ tab, float *__restrict__ dst) {
+    const int64_t *t = tab + 3 * (int64_t)blockIdx.x;
+    const float *src = (const float *)(uintptr_t)t[0];
+    float *d = dst + t[1];
+    const int64_t len = t[2];
+    for (int64_t i = threadIdx.x; i < len; i += blockDim.x) d[i] = src[i];
+}
+
+hipError_t fs_gather_chunks_impl(const int64_t *tab, int64_t n, float *dst, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if (n > 0x7fffffff) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gather_chunks_kernel, dim3((unsigned)n), dim3(256), 0, st, tab, dst);
+    return hipGetLastError();
+}
+
 hipError_t fs_flow_pack_vec(float *dst, const float *raw_layer, const fs_flow_dims *d, hipStream_t st) {
     hipLaunchKernelGGL(pack_vec_kernel, dim3(16), dim3(256), 0, st, dst, raw_layer, d->N, d->H, d->nb, d->K,
                        d->tail_bound, (int64_t)0, (int64_t)0);

@@ -28,6 +28,7 @@ hipError_t fs_flow_split_pack(const fs_flow_dims *d, const float *raw, float *pa
 hipError_t fs_flow_split_pass(const fs::FlowArgs &a, int mode, int precision, int N, int H, int K, hipStream_t st);
 // pack_vec_kernel of the f32 image (biases, folded BatchNorm, unconditional knots), launched
 // with dst shifted so that its vector section lands where the caller's image keeps it
+hipError_t fs_gather_chunks_impl(const int64_t *tab, int64_t n, float *dst, hipStream_t st);
 hipError_t fs_flow_pack_vec(float *dst, const float *raw_layer, const fs_flow_dims *d, hipStream_t st);
 
 hipError_t fs_energy_impl(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int N, double *E,

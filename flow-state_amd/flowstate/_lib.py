@@ -69,6 +69,7 @@ _SIGS = {
     "fs_last_error": (ctypes.c_char_p, []),
     "fs_version": (ctypes.c_int, []),
     "fs_flow_raw_floats": (_I64, [_D]),
+    "fs_gather_chunks": (ctypes.c_int, [_P, _I64, _P, _P]),
     "fs_flow_packed_bytes": (_I64, [_D]),
     "fs_flow_pack": (ctypes.c_int, [_D, _P, _P, _P]),
     "fs_flow_log_prob": (ctypes.c_int, [_D, _P, _P, _I64, _P, _P, _P, _P]),

@@ -69,6 +69,31 @@ class _PackCache:
         with _lib.on_device(dev):
             return self._pack(tensors, dims, key, dev)
 
+    _CHUNK = 8192
+
+    def _gather(self, tensors, ptrs, nraw, dev):
+        """The raw image in one fs_gather_chunks launch, its chunk table rebuilt only when a
+        tensor moved (ptrs: the key's data pointers); None (torch.cat instead) unless every
+        tensor is contiguous float32 and they add up to nraw."""
+        if getattr(self, "_tab_ptrs", None) != ptrs:
+            self._tab, self._tab_ptrs = None, ptrs
+            if all(t.dtype == torch.float32 and t.is_contiguous() for t in tensors) and \
+                    sum(t.numel() for t in tensors) == nraw:
+                rows, off = [], 0
+                for t in tensors:
+                    n, a = t.numel(), t.data_ptr()
+                    for s in range(0, n, self._CHUNK):
+                        rows.append((a + 4 * s, off + s, min(self._CHUNK, n - s)))
+                    off += n
+                self._tab = torch.tensor(rows, dtype=torch.int64).to(dev)
+        if self._tab is None:
+            return None
+        raw = torch.empty(nraw, dtype=torch.float32, device=dev)
+        L = _lib.load()
+        _lib.check(L.fs_gather_chunks(_lib.ptr(self._tab), self._tab.shape[0], _lib.ptr(raw), _lib.stream_ptr()),
+                   "fs_gather_chunks")
+        return raw
+
     def _pack(self, tensors, dims, key, dev):
         _lib.require_device(*tensors)
         L = _lib.load()
@@ -76,8 +101,10 @@ class _PackCache:
         nbytes = L.fs_flow_packed_bytes(dims)
         if nraw < 0 or nbytes < 0:
             _lib.check(-1, "flow dims")
-        with torch.no_grad():
-            raw = torch.cat([t.detach().reshape(-1).to(torch.float32) for t in tensors])
+        raw = self._gather(tensors, key[0][1], nraw, dev)
+        if raw is None:
+            with torch.no_grad():
+                raw = torch.cat([t.detach().reshape(-1).to(torch.float32) for t in tensors])
         if raw.numel() != nraw:
             raise _lib.FlowStateError(f"raw parameter count {raw.numel()} != expected {nraw}")
         packed = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)

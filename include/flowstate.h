@@ -84,6 +84,11 @@ int64_t fs_flow_raw_floats(const fs_flow_dims *d);
 
 /* Bytes of the packed (MFMA-fragment-ordered, BatchNorm-folded, unconditional
  * spline knots precomputed) parameter image. */
+/* Gather float32 device buffers into one: tab [n][3] (device) holds per chunk the source
+ * address, the destination offset (floats) and the length (<= 8192 floats); one launch.
+ * The raw parameter image of fs_flow_pack from the layers' own tensors
+ * (fs_flow_raw_floats). */
+int fs_gather_chunks(const int64_t *tab, int64_t n, float *dst, void *stream);
 int64_t fs_flow_packed_bytes(const fs_flow_dims *d);
 
 /* Pack raw -> packed on the device.  Must be re-run after any weight update
