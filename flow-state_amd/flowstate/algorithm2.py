@@ -95,8 +95,19 @@ class Algorithm2:
             if tail:
                 self._step.add_batch_size(tail)  # cumulative training sets change the tail
             self._step.reset_optimizer()
+            # the epoch's batches gathered once (one index upload, one gather) and the
+            # steps replayed back to back: no host synchronisation until the epoch's end,
+            # where the spline NaN flags of all steps are checked together (the reference
+            # raises inside the failing step; here the epoch's later steps have run by then)
+            shuffled = data[torch.cat(batches).to(data.device)] if batches else data[:0]
+            flags, off = [], 0
             for b in batches:
-                losses.append(self._step.step(data[b.to(data.device)]).detach().reshape(()).clone())
+                loss, flag = self._step.step(shuffled[off:off + b.numel()], check=False)
+                off += b.numel()
+                losses.append(loss.detach().reshape(()))
+                flags.append(flag.reshape(()))
+            if flags and bool(torch.stack(flags).any()):
+                raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
         else:
             opt = torch.optim.Adam(m.parameters(), lr=self.lr, weight_decay=self.wd)
             for b in batches:

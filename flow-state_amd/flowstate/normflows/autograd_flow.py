@@ -191,6 +191,20 @@ def _gemm_desc(x, w, b, r, y):
     return _lib.GemmF32(M, N, K, p(x), K, 1, p(w), 1, K, p(b), p(r), N, p(y), N, None)
 
 
+_TILE_COUNTERS = {}
+
+
+def _tile_counters(device):
+    """Split-K tile arrival counters of fs_linear_f32_group_ex, one zeroed buffer per
+    device (allocated by the first backward, normally an eager warm-up step): every call
+    leaves them zero, and the training step's backward runs its group launches in order."""
+    key = torch.device(device)
+    c = _TILE_COUNTERS.get(key)
+    if c is None:
+        c = _TILE_COUNTERS[key] = torch.zeros(4096, dtype=torch.int32, device=device)
+    return c
+
+
 def _gemm(g, device):
     """One fs_linear_f32 product; long reductions over few tiles take the split-K path with
     a torch-allocated partial-tile workspace (graph-capture safe: the caching allocator)."""
@@ -431,16 +445,17 @@ class _BnReluLinear(torch.autograd.Function):
         gx = torch.empty_like(x)
         gg = torch.empty_like(gamma)
         gbeta = torch.empty_like(gamma)
-        # the input / weight gradient pair over 48 workgroups, then the BatchNorm + ReLU
-        # backward: 10.9 us per layer in a graph, against 18.1 us for one launch whose
-        # column strips own the BatchNorm sums (4 workgroups carry the whole input gradient;
-        # tools/linbn_probe.py, profiles/r03/r03k_linbn_probe.log)
+        # the input / weight gradient pair over 48 workgroups; the last tile of each
+        # 32-column strip of the input gradient then runs the BatchNorm + ReLU backward of
+        # its columns in the same launch (fs_linear_f32_pair_bn, bit-identical to
+        # fs_bn_relu_train_bwd after the pair; a launch whose column strips own the whole
+        # product was slower: 18.1 vs 10.9 us, tools/linbn_probe.py, profiles/r03/r03k_linbn_probe.log)
         gu = torch.empty_like(u)
         g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
         g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
-        _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
-        _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
-                                          p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
+        cnt = _tile_counters(x.device)
+        _lib.check(L.fs_linear_f32_pair_bn(g0, g1, p(x), p(u), p(gamma), p(mean), p(invstd), p(gx), p(add), p(gg),
+                                           p(gbeta), p(cnt), cnt.numel(), _lib.stream_ptr()), "fs_linear_f32_pair_bn")
         gr = None
         if ctx.has_r and ctx.needs_input_grad[7]:
             if ctx.res is not None:
@@ -865,7 +880,9 @@ class _FinalSplines(torch.autograd.Function):
         nws = sum(max(0, L.fs_linear_f32_splitk_floats(d)) for d in descs)
         ws = torch.empty((max(nws, 1),), dtype=torch.float32, device=x.device)
         arr = (ctypes.POINTER(_lib.GemmF32) * 3)(*[ctypes.pointer(d) for d in descs])
-        _lib.check(L.fs_linear_f32_group(arr, 3, p(ws), nws, _lib.stream_ptr()), "fs_linear_f32_group")
+        cnt = _tile_counters(x.device)
+        _lib.check(L.fs_linear_f32_group_ex(arr, 3, p(ws), nws, p(cnt), cnt.numel(), _lib.stream_ptr()),
+                   "fs_linear_f32_group_ex")
         guw = gs[:n * K].view(n, K)
         guh = gs[n * K:2 * n * K].view(n, K)
         gud = gs[2 * n * K:].view(n, K + 1)

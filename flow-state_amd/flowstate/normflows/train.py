@@ -275,15 +275,21 @@ class GraphedTrainStep:
                 self.opt.step()
         return loss.detach()
 
-    def step(self, batch):
+    def step(self, batch, check=True):
         """One training step on `batch` (B, D); returns the loss tensor (device scalar).
-        A batch size without a captured graph runs eagerly with the same optimizer."""
+        A batch size without a captured graph runs eagerly with the same optimizer.
+        check=False: no host synchronisation for the spline's NaN flag; the step returns
+        (loss, nan_flag) instead, both device tensors owned by the caller, and the caller
+        raises (an epoch checks all its steps' flags at once, Algorithm2.train)."""
         c = self.graphs.get(int(batch.shape[0]))
         if c is None:
-            return self.eager_step(batch)
+            loss = self.eager_step(batch)
+            return loss if check else (loss, torch.zeros((), dtype=torch.bool, device=loss.device))
         c.x.copy_(batch)
         c.graph.replay()
         self.model.invalidate_packed()  # replayed writes do not bump tensor versions
+        if not check:
+            return c.loss.clone(), c.nan_flag.clone()
         if bool(c.nan_flag):
             raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
         return c.loss
