@@ -547,100 +547,6 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
 }
 
 
-// nn.Linear's backward pair followed by the backward of the BatchNorm + ReLU that produced
-// its input (_BnReluLinear): the input gradient g0 (dU = dY W, [B][H]) is the BatchNorm
-// backward's dy.  Each column strip of g0 (32 columns, all row tiles) counts its tiles in;
-// the tile that arrives last runs bn_relu_train_bwd_kernel<kBnR>'s arithmetic for the strip
-// (same per-thread row sets, same sum order: rows rg + 64 q over q, then row groups in
-// order), so dx / dgamma / dbeta are bit-identical to the separate launch.  Release /
-// acquire at device scope around the counter (partial strips from other XCDs); nobody
-// waits on anybody.
-template <int SPLIT>
-__device__ __forceinline__ void bn_bwd_strip_tail(const GemmArgs &g0, const BnBwd &bb, unsigned mt0, unsigned by) {
-    static_assert(64 * SPLIT == 512, "the strip tail maps 512 threads onto 32 columns x 16 row groups");
-    __shared__ int last;
-    __shared__ float red_d[kBnRg][32], red_x[kBnRg][32];
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned old = atomicAdd(bb.cnt + by, 1u);
-        last = old == mt0 - 1;
-        if (last) atomicExch(bb.cnt + by, 0u);
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    const int64_t B = g0.M;
-    const int H = (int)g0.N;
-    const float *dy = g0.C;
-    const int c = threadIdx.x & 31, rgb = threadIdx.x >> 5;
-    const int col = 32 * (int)by + c;
-    const bool ok = col < H;
-    const int64_t o = ok ? col : 0;
-    const float mu = bb.mean[o], is = bb.invstd[o];
-    constexpr int J = kBnRg / 16;  // row groups per thread
-    float dzv[J][kBnR], xhv[J][kBnR];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const int rg = rgb + 16 * j;
-#pragma unroll
-        for (int q = 0; q < kBnR; ++q) {
-            const int64_t i = rg + (int64_t)q * kBnRg;
-            const bool in = ok && i < B;
-            const float yv = in ? bb.y[i * H + o] : 0.f, gv = in ? dy[i * g0.ldc + o] : 0.f,
-                        xv = in ? bb.x[i * H + o] : mu;
-            dzv[j][q] = yv > 0.f ? gv : 0.f;
-            xhv[j][q] = (xv - mu) * is;
-        }
-        float sd = 0.f, sdx = 0.f;
-#pragma unroll
-        for (int q = 0; q < kBnR; ++q) {
-            sd += dzv[j][q];
-            sdx += dzv[j][q] * xhv[j][q];
-        }
-        red_d[rg][c] = sd;
-        red_x[rg][c] = sdx;
-    }
-    __syncthreads();
-    float db = 0.f, dg = 0.f;
-#pragma unroll 8
-    for (int q = 0; q < kBnRg; ++q) db += red_d[q][c];
-#pragma unroll 8
-    for (int q = 0; q < kBnRg; ++q) dg += red_x[q][c];
-    if (!ok) return;
-    const float gm = bb.gamma[col];
-    const float mdb = db / (float)B, mdg = dg / (float)B;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const int rg = rgb + 16 * j;
-#pragma unroll
-        for (int q = 0; q < kBnR; ++q) {
-            const int64_t i = rg + (int64_t)q * kBnRg;
-            if (i < B)
-                bb.dx[i * H + col] =
-                    (dzv[j][q] - mdb - xhv[j][q] * mdg) * (is * gm) + (bb.dx_add ? bb.dx_add[i * H + col] : 0.f);
-        }
-    }
-    if (rgb == 0) {
-        if (bb.dgamma) bb.dgamma[col] = dg;
-        if (bb.dbeta) bb.dbeta[col] = db;
-    }
-}
-
-template <int SPLIT>
-__global__ __launch_bounds__(64 * SPLIT) void gemm2_bn_f32_kernel(GemmArgs g0, GemmArgs g1, unsigned t0, unsigned mt0,
-                                                                 unsigned mt1, BnBwd bb) {
-    __shared__ GemmLds<SPLIT> L;
-    const unsigned b = blockIdx.x;
-    if (b < t0) {
-        gemm_tile<SPLIT, true, false>(g0, b % mt0, b / mt0, L);
-        bn_bwd_strip_tail<SPLIT>(g0, bb, mt0, b / mt0);
-    } else {
-        gemm_tile<SPLIT, false, false>(g1, (b - t0) % mt1, (b - t0) / mt1, L);
-    }
-}
-
-
 // Long-reduction products with few output tiles (the input gradient of the 2944-wide final
 // layer: 256 x 128 over K = 2944, 32 tiles): the reduction is cut into S chunks, each a
 // grid slice computing its partial tile exactly as gemm_f32_kernel does over its k range,
@@ -682,7 +588,6 @@ constexpr int kGroupMax = 4;
 struct GroupProblem {
     GemmArgs g;
     float *part;  // split-K partial tiles (S > 1)
-    unsigned *cnt;  // per-tile arrival counters (S > 1, nullable: reduce in a separate launch)
     int64_t kchunk;
     unsigned S, mt, nt, begin;
     int ak, bk;
@@ -691,40 +596,6 @@ struct GroupArgs {
     GroupProblem p[kGroupMax];
     int n;
 };
-
-// In-launch end of a split-K tile: every chunk's workgroup publishes its partial tile and
-// counts itself in; the workgroup that arrives last adds the S partials of the tile in chunk
-// order (+ bias, + R), splitk_reduce_kernel's arithmetic, and re-arms the counter to 0.
-// Release / acquire at device scope (__threadfence) around the counter, so the partials of
-// workgroups on other XCDs are visible to the last one; nobody waits, so no residency
-// assumption.
-template <int SPLIT>
-__device__ __forceinline__ void splitk_tile_end(const GroupProblem &P, unsigned bx, unsigned by) {
-    __shared__ int last;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned t = bx + by * P.mt;
-        const unsigned old = atomicAdd(P.cnt + t, 1u);
-        last = old == P.S - 1;
-        if (last) atomicExch(P.cnt + t, 0u);
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    const GemmArgs &g = P.g;
-    const int64_t m0 = (int64_t)bx * 32, n0 = (int64_t)by * 32, MN = g.M * g.N;
-    for (int e = threadIdx.x; e < 32 * 32; e += 64 * SPLIT) {
-        const int64_t m = m0 + (e >> 5), n = n0 + (e & 31);
-        if (m >= g.M || n >= g.N) continue;
-        const int64_t i = m * g.N + n;
-        float v = P.part[i];
-        for (unsigned z = 1; z < P.S; ++z) v += P.part[z * MN + i];
-        v = v + (g.bias ? g.bias[n] : 0.f);
-        if (g.R) v = v + g.R[m * g.ldr + n];
-        g.C[m * g.ldc + n] = v;
-    }
-}
 
 template <int SPLIT>
 __global__ __launch_bounds__(64 * SPLIT) void gemm_group_kernel(GroupArgs ga) {
@@ -760,7 +631,6 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_group_kernel(GroupArgs ga) {
         else
             gemm_tile<SPLIT, false, false>(c, bx, by, L);
     }
-    if (P.S > 1 && P.cnt) splitk_tile_end<SPLIT>(P, bx, by);
 }
 
 }  // namespace fs
@@ -816,10 +686,8 @@ hipError_t fs_linear_f32_splitk_impl(const GemmArgs &g, float *part, int64_t par
 // whose partials fit the workspace take it, the others run whole; every product must take
 // FS_GEMM_SPLIT waves per tile (K <= 512 or split).  hipErrorNotSupported: run them one
 // by one (the caller's fallback).
-hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_t ws_floats, hipStream_t st,
-                                    unsigned *counters, int64_t n_counters) {
+hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_t ws_floats, hipStream_t st) {
     if (n < 0 || n > kGroupMax) return hipErrorInvalidValue;
-    int64_t cused = 0;
     GroupArgs ga{};
     unsigned wg = 0;
     int64_t used = 0;
@@ -829,7 +697,6 @@ hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_
         GroupProblem &P = ga.p[ga.n];
         P.g = g;
         P.part = nullptr;
-        P.cnt = nullptr;
         P.S = 1;
         P.kchunk = g.K;
         int S = 0;
@@ -840,11 +707,6 @@ hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_
             used += need;
             P.S = (unsigned)S;
             P.kchunk = kchunk;
-            const int64_t tiles = ((g.M + 31) / 32) * ((g.N + 31) / 32);
-            if (counters && n_counters - cused >= tiles) {  // reduced in-launch by the last chunk
-                P.cnt = counters + cused;
-                cused += tiles;
-            }
         } else if (gemm_split(g) != FS_GEMM_SPLIT) {
             return hipErrorNotSupported;
         }
@@ -861,7 +723,7 @@ hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     for (int i = 0; i < ga.n; ++i) {
         const GroupProblem &P = ga.p[i];
-        if (P.S <= 1 || P.cnt) continue;
+        if (P.S <= 1) continue;
         const int64_t m = P.g.M * P.g.N;
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, P.g,
                            (const float *)P.part, (int)P.S);
@@ -910,31 +772,6 @@ hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g
     }
     if (hipError_t e = fs_linear_f32_impl(g0, st); e != hipSuccess) return e;
     return fs_linear_f32_impl(g1, st);
-}
-
-// The pair + the BatchNorm + ReLU backward of its input in one launch when the pair takes
-// the instantiated layout, the batch fits the register path (B <= 256) and the strip
-// counters fit; otherwise the pair and fs_bn_relu_train_bwd one after the other (the same
-// values either way).  dy of the BatchNorm backward is g0.C.
-hipError_t fs_linear_f32_pair_bn_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, const BnBwd &bb,
-                                      int64_t n_counters, hipStream_t st) {
-    const bool a0 = g0.sak == 1 && ((uintptr_t)g0.A & 15) == 0 && g0.sam % 4 == 0;
-    const bool b0 = g0.sbk == 1 && ((uintptr_t)g0.B & 15) == 0 && g0.sbn % 4 == 0;
-    const bool a1 = g1.sak == 1 && ((uintptr_t)g1.A & 15) == 0 && g1.sam % 4 == 0;
-    const bool b1 = g1.sbk == 1 && ((uintptr_t)g1.B & 15) == 0 && g1.sbn % 4 == 0;
-    const unsigned mt0 = (unsigned)((g0.M + 31) / 32), nt0 = (unsigned)((g0.N + 31) / 32);
-    if (g0.M > 0 && g0.N > 0 && g1.M > 0 && g1.N > 0 && gemm_split(g0) == FS_GEMM_SPLIT &&
-        gemm_split(g1) == FS_GEMM_SPLIT && a0 && !b0 && !a1 && !b1 && !g0.bias && !g0.R && !g0.rowsum_a &&
-        g0.ldc == g0.N && g0.M <= (int64_t)kBnR * kBnRg && bb.cnt && n_counters >= nt0) {
-        const unsigned mt1 = (unsigned)((g1.M + 31) / 32);
-        const unsigned t0 = mt0 * nt0, t1 = mt1 * (unsigned)((g1.N + 31) / 32);
-        hipLaunchKernelGGL(gemm2_bn_f32_kernel<FS_GEMM_SPLIT>, dim3(t0 + t1), dim3(64 * FS_GEMM_SPLIT), 0, st, g0, g1,
-                           t0, mt0, mt1, bb);
-        return hipGetLastError();
-    }
-    if (hipError_t e = fs_linear_f32_pair_impl(g0, g1, st); e != hipSuccess) return e;
-    return fs_bn_relu_train_bwd_impl(g0.M, (int)g0.N, bb.x, bb.y, g0.C, bb.gamma, bb.mean, bb.invstd, bb.dx,
-                                     bb.dx_add, bb.dgamma, bb.dbeta, st);
 }
 
 // u's write-back stores 4 floats at once where A is contiguous along k

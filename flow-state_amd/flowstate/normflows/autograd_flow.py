@@ -191,18 +191,47 @@ def _gemm_desc(x, w, b, r, y):
     return _lib.GemmF32(M, N, K, p(x), K, 1, p(w), 1, K, p(b), p(r), N, p(y), N, None)
 
 
-_TILE_COUNTERS = {}
+_GRAD_HOMES = {}
 
 
-def _tile_counters(device):
-    """Split-K tile arrival counters of fs_linear_f32_group_ex, one zeroed buffer per
-    device (allocated by the first backward, normally an eager warm-up step): every call
-    leaves them zero, and the training step's backward runs its group launches in order."""
-    key = torch.device(device)
-    c = _TILE_COUNTERS.get(key)
-    if c is None:
-        c = _TILE_COUNTERS[key] = torch.zeros(4096, dtype=torch.int32, device=device)
-    return c
+def register_grad_home(flat, flat_grad):
+    """Parameters that are views of `flat` (train.GraphedTrainStep re-homes them so) get
+    their gradients written straight into the same offsets of `flat_grad` by the backward
+    kernels; autograd hands such a view to p.grad as is, so no gather copies them."""
+    import weakref
+
+    _GRAD_HOMES[flat.untyped_storage().data_ptr()] = (weakref.ref(flat), flat.data_ptr(), flat_grad)
+
+
+_direct_grads = False  # set by paired_kld around its forward: one gradient contribution per parameter
+
+
+def _grad_out(*ps, direct=False):
+    """The gradient buffer of parameters ps (consecutive in memory when several): their
+    slice of a registered flat gradient buffer when the Function was built by paired_kld
+    (direct: each parameter enters that graph once, ALPHA = 1) and none of them holds a
+    gradient yet, else a new tensor.  autograd makes the slice p.grad as is.  A parameter
+    with two contributions in one backward (ALPHA != 1: the sampling pass is
+    differentiable too) must not share a slice, since the second Function's backward may
+    run before autograd has stored the first; those get new tensors."""
+    n = sum(q.numel() for q in ps)
+    home = _GRAD_HOMES.get(ps[0].untyped_storage().data_ptr()) if (_GRAD_HOMES and direct) else None
+    if home is not None and all(q.grad is None for q in ps):
+        flat = home[0]()
+        if flat is not None and flat.untyped_storage().data_ptr() == ps[0].untyped_storage().data_ptr():
+            off = (ps[0].data_ptr() - home[1]) // 4
+            end = off
+            for q in ps:  # every piece where the flat layout puts it
+                if q.untyped_storage().data_ptr() != flat.untyped_storage().data_ptr() or \
+                        (q.data_ptr() - home[1]) // 4 != end or not q.is_contiguous():
+                    break
+                end += q.numel()
+            else:
+                g = home[2][off:end]
+                return g.view_as(ps[0]) if len(ps) == 1 else g
+    if len(ps) == 1:
+        return torch.empty_like(ps[0])
+    return torch.empty((n,), dtype=ps[0].dtype, device=ps[0].device)
 
 
 def _gemm(g, device):
@@ -233,6 +262,8 @@ class _Linear(torch.autograd.Function):
         x = x.contiguous()
         M, K = x.shape
         ctx.save_for_backward(x, w)
+        ctx.bias = b
+        ctx.direct = _direct_grads
         ctx.has_r = r is not None
         ctx.res = res
         y = torch.empty((M, w.shape[0]), dtype=torch.float32, device=x.device)
@@ -266,8 +297,8 @@ class _Linear(torch.autograd.Function):
             gx = torch.empty_like(x)
             g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
         if need_w:
-            gw = torch.empty_like(w)
-            gb = torch.empty((N,), dtype=torch.float32, device=x.device)
+            gw = _grad_out(w, direct=ctx.direct)
+            gb = _grad_out(ctx.bias, direct=ctx.direct) if ctx.bias is not None else torch.empty((N,), dtype=torch.float32, device=x.device)
             g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
         if need_x and need_w and L.fs_linear_f32_splitk_floats(g0) == 0:
             _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
@@ -308,6 +339,8 @@ class _BnRelu(torch.autograd.Function):
                                           _lib.ptr(y), _lib.ptr(mean), _lib.ptr(invstd), _lib.stream_ptr()),
                    "fs_bn_relu_train_fwd")
         ctx.save_for_backward(x, y, gamma, mean, invstd)
+        ctx.beta = beta
+        ctx.direct = _direct_grads
         ctx.res = res
         return y
 
@@ -319,8 +352,8 @@ class _BnRelu(torch.autograd.Function):
         gy = gy.contiguous()
         M, H = x.shape
         gx = torch.empty_like(x)
-        gg = torch.empty_like(gamma)
-        gb = torch.empty_like(gamma)
+        gg = _grad_out(gamma, direct=ctx.direct)
+        gb = _grad_out(ctx.beta, direct=ctx.direct)
         add = None
         if ctx.res is not None and ctx.res.g is not None:
             add, ctx.res.g = ctx.res.g, None
@@ -356,6 +389,8 @@ class _LinearStats(torch.autograd.Function):
                                                      _lib.ptr(sts), _lib.stream_ptr()), "fs_linear_f32_ex2")
             pair.commit()
         ctx.save_for_backward(x, w)
+        ctx.bias = b
+        ctx.direct = _direct_grads
         ctx.mark_non_differentiable(st)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for st (a fill kernel per call)
         return y, st
@@ -370,8 +405,8 @@ class _LinearStats(torch.autograd.Function):
         gy = gy.contiguous()
         M, K = x.shape
         N = w.shape[0]
-        gx, gw = torch.empty_like(x), torch.empty_like(w)
-        gb = torch.empty((N,), dtype=torch.float32, device=x.device)
+        gx, gw = torch.empty_like(x), _grad_out(w, direct=ctx.direct)
+        gb = _grad_out(ctx.bias, direct=ctx.direct)
         p = _lib.ptr
         g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
         g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
@@ -419,6 +454,8 @@ class _BnReluLinear(torch.autograd.Function):
                                                      _lib.stream_ptr()), "fs_linear_f32_ex2")
             pair.commit()
         ctx.save_for_backward(x, u, gamma, mean, invstd, w)
+        ctx.gparams = (beta, b)
+        ctx.direct = _direct_grads
         ctx.has_r = r is not None
         ctx.res = res
         ctx.mark_non_differentiable(st)
@@ -437,25 +474,26 @@ class _BnReluLinear(torch.autograd.Function):
         N = w.shape[0]
         L = _lib.load()
         p = _lib.ptr
-        gw = torch.empty_like(w)
-        gb = torch.empty((N,), dtype=torch.float32, device=x.device)
+        gw = _grad_out(w, direct=ctx.direct)
+        gb = _grad_out(ctx.gparams[1], direct=ctx.direct)
         add = None
         if ctx.res is not None and ctx.res.g is not None:
             add, ctx.res.g = ctx.res.g, None
         gx = torch.empty_like(x)
-        gg = torch.empty_like(gamma)
-        gbeta = torch.empty_like(gamma)
-        # the input / weight gradient pair over 48 workgroups; the last tile of each
-        # 32-column strip of the input gradient then runs the BatchNorm + ReLU backward of
-        # its columns in the same launch (fs_linear_f32_pair_bn, bit-identical to
-        # fs_bn_relu_train_bwd after the pair; a launch whose column strips own the whole
-        # product was slower: 18.1 vs 10.9 us, tools/linbn_probe.py, profiles/r03/r03k_linbn_probe.log)
+        gg = _grad_out(gamma, direct=ctx.direct)
+        gbeta = _grad_out(ctx.gparams[0], direct=ctx.direct)
+        # the input / weight gradient pair over 48 workgroups, then the BatchNorm + ReLU
+        # backward: 10.9 us per layer in a graph, against 18.1 us for one launch whose
+        # column strips own the BatchNorm sums (4 workgroups carry the whole input gradient;
+        # tools/linbn_probe.py, profiles/r03/r03k_linbn_probe.log), and 148 against 239
+        # steps/s for the BatchNorm backward run by each strip's last tile in the pair's
+        # launch (device-scope fences; DESIGN "Training", profiles/r03/r03v_*)
         gu = torch.empty_like(u)
         g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
         g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
-        cnt = _tile_counters(x.device)
-        _lib.check(L.fs_linear_f32_pair_bn(g0, g1, p(x), p(u), p(gamma), p(mean), p(invstd), p(gx), p(add), p(gg),
-                                           p(gbeta), p(cnt), cnt.numel(), _lib.stream_ptr()), "fs_linear_f32_pair_bn")
+        _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
+        _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
+                                          p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
         gr = None
         if ctx.has_r and ctx.needs_input_grad[7]:
             if ctx.res is not None:
@@ -768,6 +806,7 @@ class _DensitySplines(torch.autograd.Function):
         else:
             pair.post(c, x, params, uw, uh, ud, lq_in, out, lq)
         ctx.save_for_backward(x, params, uw, uh, ud)
+        ctx.direct = _direct_grads
         ctx.layer = layer
         ctx.has_lq = lq_in is not None
         ctx.res = res
@@ -792,7 +831,7 @@ class _DensitySplines(torch.autograd.Function):
         # sum of gu, taken as fs_linear_f32's row sum of gu^T (N = 0: no product), which
         # spreads it over (n(3K+1))/32 workgroups (torch's reduction took 16 us at batch 256)
         P = n * (3 * K + 1)
-        gs = torch.empty((P,), dtype=torch.float32, device=x.device)
+        gs = _grad_out(uw, uh, ud, direct=ctx.direct)  # [uw | uh | ud] gradients, one row sum
         _lib.check(_lib.load().fs_linear_f32(P, 0, x.shape[0], _lib.ptr(gu), 1, P, None, 0, 0, None, None, 0, None, 0,
                                              _lib.ptr(gs), _lib.stream_ptr()), "fs_linear_f32")
         # [uw | uh | ud] back to back: contiguous views, no copies when the gradients are gathered
@@ -847,6 +886,8 @@ class _FinalSplines(torch.autograd.Function):
         else:
             pair.post(c, x, params, uw, uh, ud, lq_in, out, lq)
         ctx.save_for_backward(h, w, x, params, uw, uh, ud)
+        ctx.bias = b
+        ctx.direct = _direct_grads
         ctx.layer = layer
         ctx.has_lq = lq_in is not None
         ctx.res = res
@@ -871,18 +912,16 @@ class _FinalSplines(torch.autograd.Function):
         gu = torch.empty((M, P), dtype=torch.float32, device=x.device)
         c = _coupling_desc(layer, M)
         _density_bwd(c, x, params, uw, uh, ud, g_out, g_lq, gx, gp, gu)
-        gh, gw = torch.empty_like(h), torch.empty_like(w)
-        gb = torch.empty((P,), dtype=torch.float32, device=x.device)
-        gs = torch.empty((P,), dtype=torch.float32, device=x.device)
+        gh, gw = torch.empty_like(h), _grad_out(w, direct=ctx.direct)
+        gb = _grad_out(ctx.bias, direct=ctx.direct)
+        gs = _grad_out(uw, uh, ud, direct=ctx.direct)  # [uw | uh | ud] gradients, one row sum
         descs = [_lib.GemmF32(M, H, P, p(gp), P, 1, p(w), H, 1, None, None, 0, p(gh), H, None),  # dh = dparams W
                  _lib.GemmF32(P, H, M, p(gp), 1, P, p(h), H, 1, None, None, 0, p(gw), H, p(gb)),  # dW, db
                  _lib.GemmF32(P, 0, M, p(gu), 1, P, None, 0, 0, None, None, 0, None, 0, p(gs))]  # row sum of gu
         nws = sum(max(0, L.fs_linear_f32_splitk_floats(d)) for d in descs)
         ws = torch.empty((max(nws, 1),), dtype=torch.float32, device=x.device)
         arr = (ctypes.POINTER(_lib.GemmF32) * 3)(*[ctypes.pointer(d) for d in descs])
-        cnt = _tile_counters(x.device)
-        _lib.check(L.fs_linear_f32_group_ex(arr, 3, p(ws), nws, p(cnt), cnt.numel(), _lib.stream_ptr()),
-                   "fs_linear_f32_group_ex")
+        _lib.check(L.fs_linear_f32_group(arr, 3, p(ws), nws, _lib.stream_ptr()), "fs_linear_f32_group")
         guw = gs[:n * K].view(n, K)
         guh = gs[n * K:2 * n * K].view(n, K)
         gud = gs[2 * n * K:].view(n, K + 1)
@@ -1195,10 +1234,15 @@ def paired_kld(model, x, z, flat_bn):
     flush_features_bwd()  # nothing may be pending from an interrupted backward
     log_q = None
     xd = x
+    global _direct_grads
     with _lib.on_device(x):
-        for s in range(L):
-            rider.begin(flows[s])
-            xd, log_q = density_step(flows[L - 1 - s], xd, log_q, pair=rider)
+        _direct_grads = True  # the density pass is the only differentiable one here
+        try:
+            for s in range(L):
+                rider.begin(flows[s])
+                xd, log_q = density_step(flows[L - 1 - s], xd, log_q, pair=rider)
+        finally:
+            _direct_grads = False
         rider.flush()
         flat_bn.update(rider.bnstats, z.shape[0], x.shape[0])
     _nan_flags.append(rider.nan_flag[0] != 0)

@@ -200,9 +200,14 @@ class GraphedTrainStep:
             self.opt.zero_grad(set_to_none=False)
 
     def _gather_grads(self):
-        """The parameters' gradients into the flat buffer Adam reads: one concatenation
-        instead of one accumulate-add per parameter tensor."""
+        """The parameters' gradients into the flat buffer Adam reads.  The backward kernels
+        write them there directly (autograd_flow.register_grad_home: each p.grad is then a
+        view of its own slice), so nothing is copied; otherwise one concatenation instead
+        of one accumulate-add per parameter tensor."""
         if getattr(self, "_flat_grad", None) is None:
+            return
+        base = self._flat_grad.data_ptr()
+        if all(p.grad is not None and p.grad.data_ptr() == base + 4 * o for p, o in zip(self.params, self._goffs)):
             return
         gs = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=p.device)
               for p in self.params]
@@ -220,8 +225,11 @@ class GraphedTrainStep:
         flat = torch.cat([p.detach().reshape(-1) for p in ps])
         for p, o, n in zip(ps, offs, sizes):
             p.data = flat[o:o + n].view_as(p)
-        # gradients: gathered into one flat buffer after each backward (_gather_grads)
+        # gradients: written into one flat buffer by the backward kernels, or gathered
+        # there after each backward (_gather_grads)
         self._flat_grad = torch.zeros_like(flat)
+        self._goffs = offs[:-1]
+        AF.register_grad_home(flat, self._flat_grad)
         # Adam is elementwise, so one optimizer over the flat buffer is the same update as one
         # per parameter, in a handful of launches instead of a per-tensor fallback of
         # ~2 x (number of parameters) kernels: its state is the per-parameter state

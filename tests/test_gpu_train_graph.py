@@ -34,6 +34,11 @@ def test_graphed_step_matches_eager(alpha):
     p0 = {k: v.clone() for k, v in m1.state_dict().items()}
     for sd1, sd2 in zip(m1.state_dict().values(), m2.state_dict().values()):
         assert torch.equal(sd1, sd2)  # capture left the model untouched
+    if alpha == 1.0:
+        # the backward kernels wrote every parameter's gradient into its slice of the flat
+        # buffer Adam reads (no gather copies): p.grad is that slice
+        base = g._flat_grad.data_ptr()
+        assert all(p.grad is not None and p.grad.data_ptr() == base + 4 * o for p, o in zip(g.params, g._goffs))
     for i in range(4):
         xb = x.roll(i, 0)
         l1 = _eager(m1, opt, xb, alpha)
