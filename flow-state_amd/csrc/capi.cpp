@@ -605,31 +605,9 @@ int fs_linear_f32_splitk(const fs_gemm_f32 *d, float *workspace, int64_t workspa
                   "fs_linear_f32_splitk");
 }
 
-int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const float *x, const float *y,
-                          const float *gamma, const float *mean, const float *invstd, float *dx, const float *dx_add,
-                          float *dgamma, float *dbeta, uint32_t *strip_counters, int64_t n_counters, void *stream) {
-    REQUIRE(g0 && g1 && gemm_desc_ok(*g0) && gemm_desc_ok(*g1), "fs_linear_f32_pair_bn: invalid products");
-    REQUIRE(g0->M >= 2 && g0->N >= 1 && g0->C && x && y && gamma && mean && invstd && dx && n_counters >= 0 &&
-                (n_counters == 0 || strip_counters),
-            "fs_linear_f32_pair_bn: invalid BatchNorm backward arguments");
-    REQUIRE(g0->ldc == g0->N, "fs_linear_f32_pair_bn: the input gradient must be contiguous [B][H]");
-    fs::GemmArgs a0{g0->M, g0->N, g0->K, g0->A, g0->sam, g0->sak, g0->B, g0->sbk, g0->sbn, g0->bias, g0->R,
-                    g0->ldr, g0->C, g0->ldc, g0->rowsum_a};
-    fs::GemmArgs a1{g1->M, g1->N, g1->K, g1->A, g1->sam, g1->sak, g1->B, g1->sbk, g1->sbn, g1->bias, g1->R,
-                    g1->ldr, g1->C, g1->ldc, g1->rowsum_a};
-    const fs::BnBwd bb{x, y, gamma, mean, invstd, dx_add, dx, dgamma, dbeta, (unsigned *)strip_counters};
-    return hip_rc(fs_linear_f32_pair_bn_impl(a0, a1, bb, n_counters, (hipStream_t)stream), "fs_linear_f32_pair_bn");
-}
-
 int fs_linear_f32_group(const fs_gemm_f32 *const *gs, int32_t n, float *workspace, int64_t workspace_floats,
                         void *stream) {
-    return fs_linear_f32_group_ex(gs, n, workspace, workspace_floats, nullptr, 0, stream);
-}
-
-int fs_linear_f32_group_ex(const fs_gemm_f32 *const *gs, int32_t n, float *workspace, int64_t workspace_floats,
-                           uint32_t *tile_counters, int64_t n_counters, void *stream) {
     REQUIRE(gs && n >= 0 && n <= 4, "fs_linear_f32_group: 0..4 products");
-    REQUIRE(n_counters >= 0 && (n_counters == 0 || tile_counters), "fs_linear_f32_group_ex: invalid counters");
     fs::GemmArgs a[4];
     for (int i = 0; i < n; ++i) {
         REQUIRE(gs[i] && gemm_desc_ok(*gs[i]), "fs_linear_f32_group: invalid product %d", i);
@@ -637,8 +615,7 @@ int fs_linear_f32_group_ex(const fs_gemm_f32 *const *gs, int32_t n, float *works
         a[i] = fs::GemmArgs{g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C, g.ldc,
                             g.rowsum_a};
     }
-    hipError_t e = fs_linear_f32_group_impl(a, n, workspace, workspace_floats, (hipStream_t)stream,
-                                            (unsigned *)tile_counters, n_counters);
+    hipError_t e = fs_linear_f32_group_impl(a, n, workspace, workspace_floats, (hipStream_t)stream);
     if (e == hipErrorNotSupported) {  // one by one
         int64_t off = 0;
         for (int i = 0; i < n; ++i) {

@@ -117,16 +117,7 @@ struct BnIn {
     float *a_out;
     float *var_out;  // nullable: the biased batch variance [K] (deferred running-statistics updates)
 };
-// The BatchNorm + ReLU backward riding on a backward pair (fs_linear_f32_pair_bn): its dy is
-// the pair's input gradient g0.C; cnt: one arrival counter per 32-column strip of g0.
-struct BnBwd {
-    const float *x, *y, *gamma, *mean, *invstd, *dx_add;
-    float *dx, *dgamma, *dbeta;
-    unsigned *cnt;
-};
 }  // namespace fs
-hipError_t fs_linear_f32_pair_bn_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, const fs::BnBwd &bb,
-                                      int64_t n_counters, hipStream_t st);
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st);
 hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, hipStream_t st);
 hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipStream_t st);
@@ -139,8 +130,7 @@ int64_t fs_linear_f32_splitk_floats_impl(const fs::GemmArgs &g);
 hipError_t fs_linear_f32_splitk_impl(const fs::GemmArgs &g, float *part, int64_t part_floats, hipStream_t st);
 hipError_t fs_adam_step_impl(float *p, const float *g, float *m, float *v, int64_t n, float *step, const float *loss,
                              double lr, double beta1, double beta2, double eps, double weight_decay, hipStream_t st);
-hipError_t fs_linear_f32_group_impl(const fs::GemmArgs *gs, int n, float *ws, int64_t ws_floats, hipStream_t st,
-                                    unsigned *counters = nullptr, int64_t n_counters = 0);
+hipError_t fs_linear_f32_group_impl(const fs::GemmArgs *gs, int n, float *ws, int64_t ws_floats, hipStream_t st);
 hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,
                                      float *rm, float *rv, int64_t *nbt, float momentum, float eps, float *y,
                                      float *mean, float *invstd, hipStream_t st);

@@ -108,7 +108,7 @@ struct NoPrologue {
 // One 32 x 32 output tile (bx, by) of g by the workgroup's SPLIT waves.  pro() runs after
 // the first PF k-blocks of operand loads are issued and before they are used (the
 // BatchNorm-in-load statistics prologue, whose own loads then share their round trip).
-template <int SPLIT, bool AK, bool BK, bool BNA = false, int PF = FS_GEMM_PF, class Pro = NoPrologue, bool CS = false>
+template <int SPLIT, bool AK, bool BK, bool BNA = false, int PF = FS_GEMM_PF, class Pro = NoPrologue>
 __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t by, GemmLds<SPLIT> &L,
                                           const BnLoad *bnl = nullptr, Pro pro = {}) {
     auto &part = L.part;
@@ -226,10 +226,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
         float v = acc[i] + bias;
         if (row < g.M && bok) {
             if (g.R) v = v + ep_r[i];
-            if constexpr (CS)  // device-coherent store: read by another workgroup of this launch
-                __hip_atomic_store(g.C + row * g.ldc + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-                g.C[row * g.ldc + col] = v;
+            g.C[row * g.ldc + col] = v;
         }
         acc[i] = v;
         if (row < g.M) sv += v;
@@ -491,21 +488,6 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_fwd_kernel(
 
 // dz = dy * (y > 0); dbeta = sum dz; dgamma = sum dz xhat;
 // dx = gamma invstd (dz - dbeta / B - xhat dgamma / B)   (torch's batch_norm_backward_elemt)
-// The per-element arithmetic, rounded per operation (no contraction into FMAs, which the
-// compiler would otherwise choose per call site): the separate launch and the pair's strip
-// tail (gemm2_bn_f32_kernel) agree bit for bit.
-__device__ __forceinline__ float bn_xhat(float x, float mu, float is) {
-#pragma clang fp contract(off)
-    return (x - mu) * is;
-}
-__device__ __forceinline__ float bn_acc_prod(float s, float a, float b) {
-#pragma clang fp contract(off)
-    return s + a * b;
-}
-__device__ __forceinline__ float bn_dx(float dz, float mdb, float xh, float mdg, float is, float gm, float add) {
-#pragma clang fp contract(off)
-    return (dz - mdb - xh * mdg) * (is * gm) + add;
-}
 template <int R>
 __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
     int64_t B, int H, const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ dy,
@@ -526,18 +508,18 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
             const bool in = ok && i < B;
             const float yv = in ? y[i * H + o] : 0.f, g = in ? dy[i * H + o] : 0.f, xv = in ? x[i * H + o] : mu;
             dzv[q] = yv > 0.f ? g : 0.f;
-            xhv[q] = bn_xhat(xv, mu, is);
+            xhv[q] = (xv - mu) * is;
         }
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             sd += dzv[q];
-            sdx = bn_acc_prod(sdx, dzv[q], xhv[q]);
+            sdx += dzv[q] * xhv[q];
         }
     } else if (ok) {
         for (int64_t i = rg; i < B; i += kBnRg) {
             const float dz = y[i * H + o] > 0.f ? dy[i * H + o] : 0.f;
             sd += dz;
-            sdx = bn_acc_prod(sdx, dz, bn_xhat(x[i * H + o], mu, is));
+            sdx += dz * ((x[i * H + o] - mu) * is);
         }
     }
     const float db = wg_colsum(sd, red, c, rg);
@@ -549,122 +531,18 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int64_t i = rg + (int64_t)q * kBnRg;
-            if (i < B) dx[i * H + col] = bn_dx(dzv[q], mdb, xhv[q], mdg, is, gm, dx_add ? dx_add[i * H + col] : 0.f);
+            if (i < B) dx[i * H + col] = (dzv[q] - mdb - xhv[q] * mdg) * (is * gm) + (dx_add ? dx_add[i * H + col] : 0.f);
         }
     } else {
         for (int64_t i = rg; i < B; i += kBnRg) {
             const float dz = y[i * H + col] > 0.f ? dy[i * H + col] : 0.f;
-            const float xh = bn_xhat(x[i * H + col], mu, is);
-            dx[i * H + col] = bn_dx(dz, mdb, xh, mdg, is, gm, dx_add ? dx_add[i * H + col] : 0.f);
+            const float xh = (x[i * H + col] - mu) * is;
+            dx[i * H + col] = (dz - mdb - xh * mdg) * (is * gm) + (dx_add ? dx_add[i * H + col] : 0.f);
         }
     }
     if (rg == 0) {
         if (dgamma) dgamma[col] = dg;
         if (dbeta) dbeta[col] = db;
-    }
-}
-
-
-// nn.Linear's backward pair followed by the backward of the BatchNorm + ReLU that produced
-// its input (_BnReluLinear): the input gradient g0 (dU = dY W, [B][H]) is the BatchNorm
-// backward's dy.  Each column strip of g0 (32 columns, all row tiles) counts its tiles in;
-// the tile that arrives last runs bn_relu_train_bwd_kernel<kBnR>'s arithmetic for the strip
-// (same per-thread row sets, same sum order: rows rg + 64 q over q, then row groups in
-// order), so dx / dgamma / dbeta are bit-identical to the separate launch.  Release /
-// acquire at device scope around the counter (partial strips from other XCDs); nobody
-// waits on anybody.
-// Arrival of a workgroup whose tile was written with device-coherent stores (gemm_tile CS):
-// every wave waits for its stores' completion (s_waitcnt), then one thread counts the tile in
-// with a device-scope atomic; the last of `total` arrivals re-arms the counter and returns
-// true.  Its reads of the other tiles are device-coherent loads too, so no L2 write-back /
-// invalidate (__threadfence, which costs more than the launch this saves) is needed.
-__device__ __forceinline__ float coherent_load(const float *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool arrive_last(unsigned *cnt, unsigned total) {
-    __shared__ int last;
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = old == total - 1;
-        if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    return last != 0;
-}
-
-template <int SPLIT>
-__device__ __forceinline__ void bn_bwd_strip_tail(const GemmArgs &g0, const BnBwd &bb, unsigned mt0, unsigned by) {
-    static_assert(64 * SPLIT == 512, "the strip tail maps 512 threads onto 32 columns x 16 row groups");
-    __shared__ float red_d[kBnRg][32], red_x[kBnRg][32];
-    if (!arrive_last(bb.cnt + by, mt0)) return;
-    const int64_t B = g0.M;
-    const int H = (int)g0.N;
-    const float *dy = g0.C;
-    const int c = threadIdx.x & 31, rgb = threadIdx.x >> 5;
-    const int col = 32 * (int)by + c;
-    const bool ok = col < H;
-    const int64_t o = ok ? col : 0;
-    const float mu = bb.mean[o], is = bb.invstd[o];
-    constexpr int J = kBnRg / 16;  // row groups per thread
-    float dzv[J][kBnR], xhv[J][kBnR];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const int rg = rgb + 16 * j;
-#pragma unroll
-        for (int q = 0; q < kBnR; ++q) {
-            const int64_t i = rg + (int64_t)q * kBnRg;
-            const bool in = ok && i < B;
-            const float yv = in ? bb.y[i * H + o] : 0.f, gv = in ? coherent_load(dy + i * g0.ldc + o) : 0.f,
-                        xv = in ? bb.x[i * H + o] : mu;
-            dzv[j][q] = yv > 0.f ? gv : 0.f;
-            xhv[j][q] = bn_xhat(xv, mu, is);
-        }
-        float sd = 0.f, sdx = 0.f;
-#pragma unroll
-        for (int q = 0; q < kBnR; ++q) {
-            sd += dzv[j][q];
-            sdx = bn_acc_prod(sdx, dzv[j][q], xhv[j][q]);
-        }
-        red_d[rg][c] = sd;
-        red_x[rg][c] = sdx;
-    }
-    __syncthreads();
-    float db = 0.f, dg = 0.f;
-#pragma unroll 8
-    for (int q = 0; q < kBnRg; ++q) db += red_d[q][c];
-#pragma unroll 8
-    for (int q = 0; q < kBnRg; ++q) dg += red_x[q][c];
-    if (!ok) return;
-    const float gm = bb.gamma[col];
-    const float mdb = db / (float)B, mdg = dg / (float)B;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const int rg = rgb + 16 * j;
-#pragma unroll
-        for (int q = 0; q < kBnR; ++q) {
-            const int64_t i = rg + (int64_t)q * kBnRg;
-            if (i < B)
-                bb.dx[i * H + col] = bn_dx(dzv[j][q], mdb, xhv[j][q], mdg, is, gm, bb.dx_add ? bb.dx_add[i * H + col] : 0.f);
-        }
-    }
-    if (rgb == 0) {
-        if (bb.dgamma) bb.dgamma[col] = dg;
-        if (bb.dbeta) bb.dbeta[col] = db;
-    }
-}
-
-template <int SPLIT>
-__global__ __launch_bounds__(64 * SPLIT) void gemm2_bn_f32_kernel(GemmArgs g0, GemmArgs g1, unsigned t0, unsigned mt0,
-                                                                 unsigned mt1, BnBwd bb) {
-    __shared__ GemmLds<SPLIT> L;
-    const unsigned b = blockIdx.x;
-    if (b < t0) {
-        gemm_tile<SPLIT, true, false, false, FS_GEMM_PF, NoPrologue, true>(g0, b % mt0, b / mt0, L);
-        bn_bwd_strip_tail<SPLIT>(g0, bb, mt0, b / mt0);
-    } else {
-        gemm_tile<SPLIT, false, false>(g1, (b - t0) % mt1, (b - t0) / mt1, L);
     }
 }
 
@@ -710,7 +588,6 @@ constexpr int kGroupMax = 4;
 struct GroupProblem {
     GemmArgs g;
     float *part;  // split-K partial tiles (S > 1)
-    unsigned *cnt;  // per-tile arrival counters (S > 1, nullable: reduce in a separate launch)
     int64_t kchunk;
     unsigned S, mt, nt, begin;
     int ak, bk;
@@ -719,29 +596,6 @@ struct GroupArgs {
     GroupProblem p[kGroupMax];
     int n;
 };
-
-// In-launch end of a split-K tile: every chunk's workgroup publishes its partial tile and
-// counts itself in; the workgroup that arrives last adds the S partials of the tile in chunk
-// order (+ bias, + R), splitk_reduce_kernel's arithmetic, and re-arms the counter to 0.
-// Release / acquire at device scope (__threadfence) around the counter, so the partials of
-// workgroups on other XCDs are visible to the last one; nobody waits, so no residency
-// assumption.
-template <int SPLIT>
-__device__ __forceinline__ void splitk_tile_end(const GroupProblem &P, unsigned bx, unsigned by) {
-    if (!arrive_last(P.cnt + bx + by * P.mt, P.S)) return;
-    const GemmArgs &g = P.g;
-    const int64_t m0 = (int64_t)bx * 32, n0 = (int64_t)by * 32, MN = g.M * g.N;
-    for (int e = threadIdx.x; e < 32 * 32; e += 64 * SPLIT) {
-        const int64_t m = m0 + (e >> 5), n = n0 + (e & 31);
-        if (m >= g.M || n >= g.N) continue;
-        const int64_t i = m * g.N + n;
-        float v = coherent_load(P.part + i);
-        for (unsigned z = 1; z < P.S; ++z) v += coherent_load(P.part + z * MN + i);
-        v = v + (g.bias ? g.bias[n] : 0.f);
-        if (g.R) v = v + g.R[m * g.ldr + n];
-        g.C[m * g.ldc + n] = v;
-    }
-}
 
 template <int SPLIT>
 __global__ __launch_bounds__(64 * SPLIT) void gemm_group_kernel(GroupArgs ga) {
@@ -766,19 +620,7 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_group_kernel(GroupArgs ga) {
         c.C = P.part + (int64_t)z * P.g.M * P.g.N;
         c.ldc = P.g.N;
     }
-    if (P.S > 1 && P.cnt) {  // partial tiles read by the tile's last chunk: device-coherent stores
-        if (P.ak) {
-            if (P.bk)
-                gemm_tile<SPLIT, true, true, false, FS_GEMM_PF, NoPrologue, true>(c, bx, by, L);
-            else
-                gemm_tile<SPLIT, true, false, false, FS_GEMM_PF, NoPrologue, true>(c, bx, by, L);
-        } else {
-            if (P.bk)
-                gemm_tile<SPLIT, false, true, false, FS_GEMM_PF, NoPrologue, true>(c, bx, by, L);
-            else
-                gemm_tile<SPLIT, false, false, false, FS_GEMM_PF, NoPrologue, true>(c, bx, by, L);
-        }
-    } else if (P.ak) {
+    if (P.ak) {
         if (P.bk)
             gemm_tile<SPLIT, true, true>(c, bx, by, L);
         else
@@ -789,7 +631,6 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_group_kernel(GroupArgs ga) {
         else
             gemm_tile<SPLIT, false, false>(c, bx, by, L);
     }
-    if (P.S > 1 && P.cnt) splitk_tile_end<SPLIT>(P, bx, by);
 }
 
 }  // namespace fs
@@ -845,10 +686,8 @@ hipError_t fs_linear_f32_splitk_impl(const GemmArgs &g, float *part, int64_t par
 // whose partials fit the workspace take it, the others run whole; every product must take
 // FS_GEMM_SPLIT waves per tile (K <= 512 or split).  hipErrorNotSupported: run them one
 // by one (the caller's fallback).
-hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_t ws_floats, hipStream_t st,
-                                    unsigned *counters, int64_t n_counters) {
+hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_t ws_floats, hipStream_t st) {
     if (n < 0 || n > kGroupMax) return hipErrorInvalidValue;
-    int64_t cused = 0;
     GroupArgs ga{};
     unsigned wg = 0;
     int64_t used = 0;
@@ -858,7 +697,6 @@ hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_
         GroupProblem &P = ga.p[ga.n];
         P.g = g;
         P.part = nullptr;
-        P.cnt = nullptr;
         P.S = 1;
         P.kchunk = g.K;
         int S = 0;
@@ -869,11 +707,6 @@ hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_
             used += need;
             P.S = (unsigned)S;
             P.kchunk = kchunk;
-            const int64_t tiles = ((g.M + 31) / 32) * ((g.N + 31) / 32);
-            if (counters && n_counters - cused >= tiles) {  // reduced in-launch by the last chunk
-                P.cnt = counters + cused;
-                cused += tiles;
-            }
         } else if (gemm_split(g) != FS_GEMM_SPLIT) {
             return hipErrorNotSupported;
         }
@@ -890,7 +723,7 @@ hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     for (int i = 0; i < ga.n; ++i) {
         const GroupProblem &P = ga.p[i];
-        if (P.S <= 1 || P.cnt) continue;
+        if (P.S <= 1) continue;
         const int64_t m = P.g.M * P.g.N;
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, P.g,
                            (const float *)P.part, (int)P.S);
@@ -939,31 +772,6 @@ hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g
     }
     if (hipError_t e = fs_linear_f32_impl(g0, st); e != hipSuccess) return e;
     return fs_linear_f32_impl(g1, st);
-}
-
-// The pair + the BatchNorm + ReLU backward of its input in one launch when the pair takes
-// the instantiated layout, the batch fits the register path (B <= 256) and the strip
-// counters fit; otherwise the pair and fs_bn_relu_train_bwd one after the other (the same
-// values either way).  dy of the BatchNorm backward is g0.C.
-hipError_t fs_linear_f32_pair_bn_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, const BnBwd &bb,
-                                      int64_t n_counters, hipStream_t st) {
-    const bool a0 = g0.sak == 1 && ((uintptr_t)g0.A & 15) == 0 && g0.sam % 4 == 0;
-    const bool b0 = g0.sbk == 1 && ((uintptr_t)g0.B & 15) == 0 && g0.sbn % 4 == 0;
-    const bool a1 = g1.sak == 1 && ((uintptr_t)g1.A & 15) == 0 && g1.sam % 4 == 0;
-    const bool b1 = g1.sbk == 1 && ((uintptr_t)g1.B & 15) == 0 && g1.sbn % 4 == 0;
-    const unsigned mt0 = (unsigned)((g0.M + 31) / 32), nt0 = (unsigned)((g0.N + 31) / 32);
-    if (g0.M > 0 && g0.N > 0 && g1.M > 0 && g1.N > 0 && gemm_split(g0) == FS_GEMM_SPLIT &&
-        gemm_split(g1) == FS_GEMM_SPLIT && a0 && !b0 && !a1 && !b1 && !g0.bias && !g0.R && !g0.rowsum_a &&
-        g0.ldc == g0.N && g0.M <= (int64_t)kBnR * kBnRg && bb.cnt && n_counters >= nt0) {
-        const unsigned mt1 = (unsigned)((g1.M + 31) / 32);
-        const unsigned t0 = mt0 * nt0, t1 = mt1 * (unsigned)((g1.N + 31) / 32);
-        hipLaunchKernelGGL(gemm2_bn_f32_kernel<FS_GEMM_SPLIT>, dim3(t0 + t1), dim3(64 * FS_GEMM_SPLIT), 0, st, g0, g1,
-                           t0, mt0, mt1, bb);
-        return hipGetLastError();
-    }
-    if (hipError_t e = fs_linear_f32_pair_impl(g0, g1, st); e != hipSuccess) return e;
-    return fs_bn_relu_train_bwd_impl(g0.M, (int)g0.N, bb.x, bb.y, g0.C, bb.gamma, bb.mean, bb.invstd, bb.dx,
-                                     bb.dx_add, bb.dgamma, bb.dbeta, st);
 }
 
 // u's write-back stores 4 floats at once where A is contiguous along k

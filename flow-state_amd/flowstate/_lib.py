@@ -112,10 +112,6 @@ _SIGS = {
     "fs_linear_f32_ex2": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(BnIn), _P, ctypes.POINTER(GemmF32),
                                          ctypes.POINTER(BnIn), _P, _P]),
     "fs_linear_f32_group": (ctypes.c_int, [ctypes.POINTER(ctypes.POINTER(GemmF32)), ctypes.c_int32, _P, _I64, _P]),
-    "fs_linear_f32_pair_bn": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(GemmF32), _P, _P, _P, _P, _P,
-                                             _P, _P, _P, _P, _P, _I64, _P]),
-    "fs_linear_f32_group_ex": (ctypes.c_int, [ctypes.POINTER(ctypes.POINTER(GemmF32)), ctypes.c_int32, _P, _I64, _P,
-                                              _I64, _P]),
     "fs_bn_running_update": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, ctypes.c_int32, _I64, _I64,
                                             ctypes.c_double, _P]),
     "fs_bn_relu_train_fwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 6 + [ctypes.c_double, ctypes.c_double]

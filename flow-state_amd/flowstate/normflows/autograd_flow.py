@@ -234,26 +234,6 @@ def _grad_out(*ps, direct=False):
     return torch.empty((n,), dtype=ps[0].dtype, device=ps[0].device)
 
 
-_TILE_COUNTERS = {}
-# A/B switches (tools/gpu_ab_fuse.sh): "1" = the in-launch end off (separate reduction /
-# BatchNorm backward launch); off unless the environment turns it on
-import os as _os
-
-_AB_NO_GROUP_EX = _os.environ.get("FS_AB_NO_GROUP_EX", "1") == "1"
-_AB_NO_PAIR_BN = _os.environ.get("FS_AB_NO_PAIR_BN", "1") == "1"
-
-
-def _tile_counters(device):
-    """Arrival counters of the in-launch ends (fs_linear_f32_group_ex, fs_linear_f32_pair_bn),
-    one zeroed buffer per device (allocated by the first backward, normally an eager warm-up
-    step): every call leaves them zero, and the step's launches run in stream order."""
-    key = torch.device(device)
-    c = _TILE_COUNTERS.get(key)
-    if c is None:
-        c = _TILE_COUNTERS[key] = torch.zeros(4096, dtype=torch.int32, device=device)
-    return c
-
-
 def _gemm(g, device):
     """One fs_linear_f32 product; long reductions over few tiles take the split-K path with
     a torch-allocated partial-tile workspace (graph-capture safe: the caching allocator)."""
@@ -511,10 +491,9 @@ class _BnReluLinear(torch.autograd.Function):
         gu = torch.empty_like(u)
         g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
         g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
-        cnt = _tile_counters(x.device)
-        _lib.check(L.fs_linear_f32_pair_bn(g0, g1, p(x), p(u), p(gamma), p(mean), p(invstd), p(gx), p(add), p(gg),
-                                           p(gbeta), p(cnt), 0 if _AB_NO_PAIR_BN else cnt.numel(),
-                                           _lib.stream_ptr()), "fs_linear_f32_pair_bn")
+        _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
+        _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
+                                          p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
         gr = None
         if ctx.has_r and ctx.needs_input_grad[7]:
             if ctx.res is not None:
@@ -942,9 +921,7 @@ class _FinalSplines(torch.autograd.Function):
         nws = sum(max(0, L.fs_linear_f32_splitk_floats(d)) for d in descs)
         ws = torch.empty((max(nws, 1),), dtype=torch.float32, device=x.device)
         arr = (ctypes.POINTER(_lib.GemmF32) * 3)(*[ctypes.pointer(d) for d in descs])
-        cnt = _tile_counters(x.device)
-        _lib.check(L.fs_linear_f32_group_ex(arr, 3, p(ws), nws, p(cnt), 0 if _AB_NO_GROUP_EX else cnt.numel(),
-                                            _lib.stream_ptr()), "fs_linear_f32_group_ex")
+        _lib.check(L.fs_linear_f32_group(arr, 3, p(ws), nws, _lib.stream_ptr()), "fs_linear_f32_group")
         guw = gs[:n * K].view(n, K)
         guh = gs[n * K:2 * n * K].view(n, K)
         gud = gs[2 * n * K:].view(n, K + 1)

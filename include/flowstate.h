@@ -386,18 +386,6 @@ int fs_bn_running_update(int32_t nbn, int32_t H, float *running_mean, float *run
 int64_t fs_linear_f32_splitk_floats(const fs_gemm_f32 *g);
 int fs_linear_f32_splitk(const fs_gemm_f32 *g, float *workspace, int64_t workspace_floats, void *stream);
 
-/* nn.Linear's backward pair (g0 = the input gradient dU = dY W [B][H], contiguous;
- * g1 = the weight gradient, as fs_linear_f32_pair) followed by the backward of the
- * BatchNorm1d (train) + ReLU that produced the Linear's input u = y (fs_bn_relu_train_bwd
- * with dy = g0's output): the last of each 32-column strip's tiles to finish runs the
- * BatchNorm backward of its columns in the same launch, bit-identical to the separate
- * launch.  strip_counters: caller-owned, ceil(H / 32), all 0 before the first call and
- * left 0 by every call; when they do not fit (or B > 256, or the pair's layout is not the
- * instantiated one) the call runs the pair and fs_bn_relu_train_bwd one after the other. */
-int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const float *x, const float *y,
-                          const float *gamma, const float *mean, const float *invstd, float *dx, const float *dx_add,
-                          float *dgamma, float *dbeta, uint32_t *strip_counters, int64_t n_counters, void *stream);
-
 /* Up to 4 independent fs_linear_f32 products in one launch (a coupling layer's final
  * Linear backward: input gradient, weight + bias gradient, and the unconditional spline
  * parameters' row sum).  Products with a split-K plan take it while the workspace
@@ -405,16 +393,6 @@ int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fl
  * reductions; each product's values are those of fs_linear_f32 / fs_linear_f32_splitk. */
 int fs_linear_f32_group(const fs_gemm_f32 *const *gs, int32_t n, float *workspace, int64_t workspace_floats,
                         void *stream);
-
-/* fs_linear_f32_group whose split-K products end inside the launch: each chunk's workgroup
- * counts itself in on its tile's counter and the last one adds the partials in chunk order
- * (+ bias, + R), the same values as the separate reduction launch, one launch fewer per
- * split product.  tile_counters: caller-owned, ceil(M/32) * ceil(N/32) per split product in
- * order, all 0 before the first call; every call leaves them 0 (so one zeroed buffer serves
- * any number of calls on one stream).  Products whose counters do not fit n_counters take
- * the separate reduction. */
-int fs_linear_f32_group_ex(const fs_gemm_f32 *const *gs, int32_t n, float *workspace, int64_t workspace_floats,
-                           uint32_t *tile_counters, int64_t n_counters, void *stream);
 
 /* BatchNorm1d (training mode) followed by ReLU over x [Bn][H] (row-major):
  * batch mean / biased variance, y = relu(gamma (x - mean) invstd + beta),

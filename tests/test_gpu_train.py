@@ -104,66 +104,9 @@ def test_linear_pair_launch_matches_two_launches():
         torch.testing.assert_close(outs[0][2], gy.sum(0), rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("B,K,N,add", [(256, 128, 128, True), (256, 128, 128, False), (100, 40, 72, True),
-                                         (37, 24, 33, False), (300, 64, 64, True)])
-def test_linear_pair_bn_launch_matches_pair_then_batchnorm(B, K, N, add):
-    """fs_linear_f32_pair_bn (the backward pair of Linear(relu(BN(x))) whose last tile per
-    column strip runs the BatchNorm + ReLU backward) is bit-identical to fs_linear_f32_pair
-    followed by fs_bn_relu_train_bwd, on the in-launch path (B <= 256) and the fallback
-    (B = 300); called three times on one counter buffer, which every call leaves at 0."""
-    from flowstate import _lib
-
-    L, p = _lib.load(), _lib.ptr
-    g = torch.Generator().manual_seed(B + K)
-    x = torch.randn((B, K), generator=g).cuda()
-    gamma = (torch.rand(K, generator=g) + 0.5).cuda()
-    beta = (torch.randn(K, generator=g) * 0.3).cuda()
-    mean, var = x.mean(0), x.var(0, unbiased=False)
-    invstd = 1.0 / torch.sqrt(var + 1e-5)
-    u = torch.relu(gamma * ((x - mean) * invstd) + beta)
-    w = torch.randn((N, K), generator=g).cuda() * 0.1
-    gy = torch.randn((B, N), generator=g).cuda()
-    dx_add = torch.randn((B, K), generator=g).cuda() if add else None
-    cnt = torch.zeros(64, dtype=torch.int32, device="cuda")
-    # 12 rounds of new output gradients through the same buffers (a stale or early read of
-    # another workgroup's strip would show as a mismatch in some round)
-    bufs = [(torch.empty_like(u), torch.empty((N, K), device="cuda"), torch.empty(N, device="cuda"),
-             torch.empty_like(x), torch.empty(K, device="cuda"), torch.empty(K, device="cuda")) for _ in range(2)]
-    for rnd in range(12):
-        gy = torch.randn((B, N), generator=g).cuda() if rnd else gy
-        outs = []
-        for fused in (False, True):
-            gu, gw, gb, gx, gg, gbt = bufs[int(fused)]
-            g0 = _lib.GemmF32(B, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
-            g1 = _lib.GemmF32(N, K, B, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
-            if fused:
-                _lib.check(L.fs_linear_f32_pair_bn(g0, g1, p(x), p(u), p(gamma), p(mean), p(invstd), p(gx),
-                                                   p(dx_add), p(gg), p(gbt), p(cnt), cnt.numel(), _lib.stream_ptr()))
-            else:
-                _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()))
-                _lib.check(L.fs_bn_relu_train_bwd(B, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx),
-                                                  p(dx_add), p(gg), p(gbt), _lib.stream_ptr()))
-            outs.append(tuple(t.clone() for t in bufs[int(fused)]))
-        torch.cuda.synchronize()
-        assert int(cnt.abs().sum()) == 0
-        for name, a, b in zip(("gu", "gw", "gb", "gx", "dgamma", "dbeta"), outs[0], outs[1]):
-            assert torch.equal(a, b), (rnd, name, (a - b).abs().max().item())
-    # and the values are BatchNorm + ReLU's backward (torch autograd, float32)
-    xr = x.clone().requires_grad_(True)
-    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
-    ur = torch.relu(torch.nn.functional.batch_norm(xr, None, None, gr, br, training=True, eps=1e-5))
-    ur.backward(gy @ w)
-    ref_dx = xr.grad + (dx_add if add else 0.0)
-    torch.testing.assert_close(outs[1][3], ref_dx, rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(outs[1][4], gr.grad, rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(outs[1][5], br.grad, rtol=1e-4, atol=1e-3)
-
-
 def test_linear_group_launch_matches_single_launches():
     """fs_linear_f32_group (the final Linear's backward + the unconditional row sum in one
-    launch, split-K included) gives exactly what the products give one by one; so does
-    fs_linear_f32_group_ex, whose split-K tiles are added by their last chunk inside the
-    launch (called three times on one counter buffer: the counters re-arm to 0)."""
+    launch, split-K included) gives exactly what the products give one by one."""
     import ctypes
 
     from flowstate import _lib
@@ -176,8 +119,7 @@ def test_linear_group_launch_matches_single_launches():
         gp = torch.randn((M, P), generator=g).cuda()
         gu = torch.randn((M, P), generator=g).cuda()
         outs = []
-        cnt = torch.zeros(4096, dtype=torch.int32, device="cuda")
-        for grouped in (True, "ex", "ex", "ex", False):
+        for grouped in (True, False):
             gh, gw = torch.empty_like(h), torch.empty_like(w)
             gb, gs = torch.empty(P, device="cuda"), torch.empty(P, device="cuda")
             descs = [_lib.GemmF32(M, H, P, p(gp), P, 1, p(w), H, 1, None, None, 0, p(gh), H, None),
@@ -185,13 +127,8 @@ def test_linear_group_launch_matches_single_launches():
                      _lib.GemmF32(P, 0, M, p(gu), 1, P, None, 0, 0, None, None, 0, None, 0, p(gs))]
             nws = sum(max(0, L.fs_linear_f32_splitk_floats(d)) for d in descs)
             ws = torch.empty((max(nws, 1),), device="cuda")
-            arr = (ctypes.POINTER(_lib.GemmF32) * 3)(*[ctypes.pointer(d) for d in descs])
-            if grouped == "ex":
-                ws.fill_(float("nan"))  # nothing of an earlier call's partials may leak in
-                _lib.check(L.fs_linear_f32_group_ex(arr, 3, p(ws), nws, p(cnt), cnt.numel(), _lib.stream_ptr()))
-                torch.cuda.synchronize()
-                assert int(cnt.abs().sum()) == 0
-            elif grouped:
+            if grouped:
+                arr = (ctypes.POINTER(_lib.GemmF32) * 3)(*[ctypes.pointer(d) for d in descs])
                 _lib.check(L.fs_linear_f32_group(arr, 3, p(ws), nws, _lib.stream_ptr()))
             else:
                 for d in descs:
@@ -202,9 +139,8 @@ def test_linear_group_launch_matches_single_launches():
                         _lib.check(L.fs_linear_f32(d.M, d.N, d.K, d.A, d.sam, d.sak, d.B, d.sbk, d.sbn, None, None, 0,
                                                    d.C, d.ldc, d.rowsum_a, _lib.stream_ptr()))
             outs.append((gh, gw, gb, gs))
-        for o in outs[1:]:
-            for a, b in zip(outs[0], o):
-                assert torch.equal(a, b)
+        for a, b in zip(*outs):
+            assert torch.equal(a, b)
         torch.testing.assert_close(outs[0][0], gp @ w, rtol=1e-5, atol=2e-3)
         torch.testing.assert_close(outs[0][1], gp.t() @ h, rtol=1e-5, atol=2e-3)
         torch.testing.assert_close(outs[0][2], gp.sum(0), rtol=1e-5, atol=1e-3)
