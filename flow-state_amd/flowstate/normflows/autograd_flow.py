@@ -206,6 +206,12 @@ def register_grad_home(flat, flat_grad):
 _direct_grads = False  # set by paired_kld around its forward: one gradient contribution per parameter
 
 
+def _in_grad_home(t):
+    """t lives in a registered flat gradient buffer (memory that outlives the backward)."""
+    sp = t.untyped_storage().data_ptr()
+    return any(h[2].untyped_storage().data_ptr() == sp for h in _GRAD_HOMES.values())
+
+
 def _grad_out(*ps, direct=False):
     """The gradient buffer of parameters ps (consecutive in memory when several): their
     slice of a registered flat gradient buffer when the Function was built by paired_kld
@@ -495,11 +501,14 @@ class _BnReluLinear(torch.autograd.Function):
         g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
         if fused_in:
             _lib.check(L.fs_linear_f32_pair_bnin(g0, g1, p(bnb["u"]), p(bnb["x"]), p(bnb["mean"]), p(bnb["invstd"]),
-                                                 p(bnb["gamma"]), p(bnb["bstats"]), p(bnb["gg"]), p(bnb["gbeta"]),
+                                                 p(bnb["gamma"]), p(bnb["bstats"]), bnb["gg"], bnb["gbeta"],
                                                  _lib.stream_ptr()), "fs_linear_f32_pair_bnin")
+        # (dgamma / dbeta must be flat-buffer slices: autograd keeps them as p.grad without
+        # reading them, and the stash holds only their addresses, so that nothing but the
+        # returned tensors references them and autograd takes them as they are)
         defer = (ctx.direct and res is not None and ctx.op is not None and ctx.op[1] == 1 and res.bnb is None
                  and not fused_in and K <= 256 and gamma.grad is None and ctx.gparams[0].grad is None
-                 and x.is_contiguous() and u.is_contiguous())
+                 and x.is_contiguous() and u.is_contiguous() and _in_grad_home(gg) and _in_grad_home(gbeta))
         add = None
         if res is not None and res.g is not None:
             add, res.g = res.g, None
@@ -515,7 +524,7 @@ class _BnReluLinear(torch.autograd.Function):
             _lib.check(L.fs_linear_f32_pair_bnstat(g0, g1, p(u), p(x), p(mean), p(invstd), p(bst), _lib.stream_ptr()),
                        "fs_linear_f32_pair_bnstat")
             res.bnb = {"dy": gu, "u": u, "x": x, "mean": mean, "invstd": invstd, "gamma": gamma, "bstats": bst,
-                       "gg": gg, "gbeta": gbeta}
+                       "gg": gg.data_ptr(), "gbeta": gbeta.data_ptr()}
             gx = gu
         else:
             # the input / weight gradient pair over 48 workgroups, then the BatchNorm + ReLU
