@@ -671,42 +671,71 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_fwd_kernel(
 
 // dz = dy * (y > 0); dbeta = sum dz; dgamma = sum dz xhat;
 // dx = gamma invstd (dz - dbeta / B - xhat dgamma / B)   (torch's batch_norm_backward_elemt)
+// R > 0 (B <= 256): the batch sums in the order of the pairs' deferred BatchNorm backward
+// (fs_linear_f32_pair_bnstat / _bnin): per 32-row tile the two 16-row halves of its MFMA
+// accumulator layout (rows 8 (i >> 2) + 4 h + (i & 3), i = 0..15 in order), half 0 + half 1,
+// then the tiles in order, with the same uncontracted arithmetic, so both paths agree bit
+// for bit.
 template <int R>
 __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
     int64_t B, int H, const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ dy,
     const float *__restrict__ gamma, const float *__restrict__ mean, const float *__restrict__ invstd,
     float *__restrict__ dx, const float *__restrict__ dx_add, float *__restrict__ dgamma, float *__restrict__ dbeta) {
     __shared__ float red[kBnRg][kBnCols];
+    __shared__ float dz_s[R > 0 ? R * kBnRg : 1][kBnCols], xh_s[R > 0 ? R * kBnRg : 1][kBnCols];
+    __shared__ float hs_d[R > 0 ? 2 * R * kBnRg / 32 : 1][kBnCols], hs_x[R > 0 ? 2 * R * kBnRg / 32 : 1][kBnCols];
     const int c = threadIdx.x % kBnCols, rg = threadIdx.x / kBnCols;
     const int col = blockIdx.x * kBnCols + c;
     const bool ok = col < H;
     const int64_t o = ok ? col : 0;
     const float mu = mean[o], is = invstd[o];
     float dzv[R > 0 ? R : 1], xhv[R > 0 ? R : 1];
-    float sd = 0.f, sdx = 0.f;
-    if (R > 0) {
+    float db = 0.f, dg = 0.f;
+    if constexpr (R > 0) {
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int64_t i = rg + (int64_t)q * kBnRg;
             const bool in = ok && i < B;
             const float yv = in ? y[i * H + o] : 0.f, g = in ? dy[i * H + o] : 0.f, xv = in ? x[i * H + o] : mu;
             dzv[q] = yv > 0.f ? g : 0.f;
-            xhv[q] = (xv - mu) * is;
+            xhv[q] = bn_xhat(xv, mu, is);
+            dz_s[i][c] = dzv[q];
+            xh_s[i][c] = xhv[q];
         }
+        __syncthreads();
+        constexpr int NH = 2 * R * kBnRg / 32;  // 16-row halves of the 32-row tiles
+        if (rg < NH) {
+            const int t = rg >> 1, hh = rg & 1;
+            float sd = 0.f, sdx = 0.f;
 #pragma unroll
-        for (int q = 0; q < R; ++q) {
-            sd += dzv[q];
-            sdx += dzv[q] * xhv[q];
+            for (int e = 0; e < 16; ++e) {
+                const int64_t row = 32 * t + 8 * (e >> 2) + 4 * hh + (e & 3);
+                if (row < B) {
+                    sd += dz_s[row][c];
+                    sdx = bn_acc_prod(sdx, dz_s[row][c], xh_s[row][c]);
+                }
+            }
+            hs_d[rg][c] = sd;
+            hs_x[rg][c] = sdx;
         }
-    } else if (ok) {
-        for (int64_t i = rg; i < B; i += kBnRg) {
-            const float dz = y[i * H + o] > 0.f ? dy[i * H + o] : 0.f;
-            sd += dz;
-            sdx += dz * ((x[i * H + o] - mu) * is);
+        __syncthreads();
+        const int nt = (int)((B + 31) / 32);
+        for (int t = 0; t < nt; ++t) {
+            db += hs_d[2 * t][c] + hs_d[2 * t + 1][c];
+            dg += hs_x[2 * t][c] + hs_x[2 * t + 1][c];
         }
+    } else {
+        float sd = 0.f, sdx = 0.f;
+        if (ok) {
+            for (int64_t i = rg; i < B; i += kBnRg) {
+                const float dz = y[i * H + o] > 0.f ? dy[i * H + o] : 0.f;
+                sd += dz;
+                sdx = bn_acc_prod(sdx, dz, bn_xhat(x[i * H + o], mu, is));
+            }
+        }
+        db = wg_colsum(sd, red, c, rg);
+        dg = wg_colsum(sdx, red, c, rg);
     }
-    const float db = wg_colsum(sd, red, c, rg);
-    const float dg = wg_colsum(sdx, red, c, rg);
     if (!ok) return;
     const float gm = gamma[col];
     const float mdb = db / (float)B, mdg = dg / (float)B;
@@ -714,13 +743,13 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int64_t i = rg + (int64_t)q * kBnRg;
-            if (i < B) dx[i * H + col] = (dzv[q] - mdb - xhv[q] * mdg) * (is * gm) + (dx_add ? dx_add[i * H + col] : 0.f);
+            if (i < B) dx[i * H + col] = bn_dx(dzv[q], mdb, xhv[q], mdg, is, gm, dx_add ? dx_add[i * H + col] : 0.f);
         }
     } else {
         for (int64_t i = rg; i < B; i += kBnRg) {
             const float dz = y[i * H + col] > 0.f ? dy[i * H + col] : 0.f;
-            const float xh = (x[i * H + col] - mu) * is;
-            dx[i * H + col] = (dz - mdb - xh * mdg) * (is * gm) + (dx_add ? dx_add[i * H + col] : 0.f);
+            const float xh = bn_xhat(x[i * H + col], mu, is);
+            dx[i * H + col] = bn_dx(dz, mdb, xh, mdg, is, gm, dx_add ? dx_add[i * H + col] : 0.f);
         }
     }
     if (rg == 0) {
