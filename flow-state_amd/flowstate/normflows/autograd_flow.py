@@ -428,7 +428,10 @@ class _BnReluLinear(torch.autograd.Function):
     for the next BatchNorm (fs_linear_f32_ex).  u = relu(BN(x)) is written once for the
     backward, which is the weight / input gradient pair on u and then the BatchNorm + ReLU
     backward (fs_bn_relu_train_bwd, with the block's residual gradient added there as in
-    _BnRelu)."""
+    _BnRelu).  Inside paired_kld the block's second BatchNorm backward has no launch of its
+    own: the second Linear's pair writes its tile partial sums (fs_linear_f32_pair_bnstat)
+    and hands the raw dy on, and the first Linear's pair forms dX as it loads its operands
+    (fs_linear_f32_pair_bnin); bit-identical to the separate launches."""
 
     @staticmethod
     def forward(ctx, x, x_stats, gamma, beta, bn, w, b, r, res=None, pair=None, op=None):
