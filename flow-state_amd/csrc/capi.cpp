@@ -605,29 +605,6 @@ int fs_linear_f32_splitk(const fs_gemm_f32 *d, float *workspace, int64_t workspa
                   "fs_linear_f32_splitk");
 }
 
-static fs::GemmArgs gemm_args(const fs_gemm_f32 &g) {
-    return fs::GemmArgs{g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C, g.ldc, g.rowsum_a};
-}
-
-int fs_linear_f32_pair_bnstat(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const float *u, const float *x,
-                              const float *mean, const float *invstd, float *bstats, void *stream) {
-    REQUIRE(g0 && g1 && gemm_desc_ok(*g0) && gemm_desc_ok(*g1), "fs_linear_f32_pair_bnstat: invalid products");
-    REQUIRE(u && x && mean && invstd && bstats, "fs_linear_f32_pair_bnstat: invalid BatchNorm operands");
-    return hip_rc(fs_linear_f32_pair_bnstat_impl(gemm_args(*g0), gemm_args(*g1), u, x, mean, invstd, bstats,
-                                                 (hipStream_t)stream),
-                  "fs_linear_f32_pair_bnstat");
-}
-
-int fs_linear_f32_pair_bnin(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const float *u, const float *x,
-                            const float *mean, const float *invstd, const float *gamma, const float *bstats,
-                            float *dgamma, float *dbeta, void *stream) {
-    REQUIRE(g0 && g1 && gemm_desc_ok(*g0) && gemm_desc_ok(*g1), "fs_linear_f32_pair_bnin: invalid products");
-    REQUIRE(u && x && mean && invstd && gamma && bstats && g0->M >= 2, "fs_linear_f32_pair_bnin: invalid BatchNorm operands");
-    return hip_rc(fs_linear_f32_pair_bnin_impl(gemm_args(*g0), gemm_args(*g1), u, x, mean, invstd, gamma, bstats,
-                                               g0->M, dgamma, dbeta, (hipStream_t)stream),
-                  "fs_linear_f32_pair_bnin");
-}
-
 int fs_linear_f32_group(const fs_gemm_f32 *const *gs, int32_t n, float *workspace, int64_t workspace_floats,
                         void *stream) {
     REQUIRE(gs && n >= 0 && n <= 4, "fs_linear_f32_group: 0..4 products");

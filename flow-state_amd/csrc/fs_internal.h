@@ -119,13 +119,6 @@ struct BnIn {
 };
 }  // namespace fs
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st);
-hipError_t fs_linear_f32_pair_bnstat_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, const float *u,
-                                          const float *x, const float *mean, const float *invstd, float *bstats,
-                                          hipStream_t st);
-hipError_t fs_linear_f32_pair_bnin_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, const float *u, const float *x,
-                                        const float *mean, const float *invstd, const float *gamma,
-                                        const float *bstats, int64_t rows, float *dgamma, float *dbeta,
-                                        hipStream_t st);
 hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, hipStream_t st);
 hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipStream_t st);
 bool fs_linear_ex2_ok(const fs::GemmArgs &g0, const fs::BnIn *b0, const fs::GemmArgs &g1, const fs::BnIn *b1);

@@ -101,53 +101,16 @@ struct BnLoad {
     int64_t by, nt;
 };
 
-// A operand = the backward of BatchNorm1d (train) + ReLU applied on load (BN-backward-in-load):
-// the raw A is dy of that BatchNorm (the gradient of u = relu(BN(x))), and each element
-// becomes dx = gamma invstd (dz - sum dz / B - xhat sum(dz xhat) / B) with dz = dy (u > 0),
-// xhat = (x - mean) invstd; u and x are read at A's own positions (same layout as A); the
-// column sums come from the producer's per-tile partials (BnBwdIn.bstats).  COLK: the
-// BatchNorm column of A[m][k] is k (A = dX, row-major) or m (A = dX^T).
-struct BnbLoad {
-    const float *mu, *is, *mdb, *mdg, *gm;  // LDS, per BatchNorm column
-    const float *u, *x;                     // [rows][H] like A
-};
-
 struct NoPrologue {
     __device__ void operator()() const {}
-};
-
-// bn_xhat / bn_acc_prod / bn_dx: the BatchNorm backward's per-element arithmetic, rounded per
-// operation (no contraction into FMAs, which the compiler would otherwise choose per call
-// site), shared by bn_relu_train_bwd_kernel, the partial sums of a pair's epilogue and the
-// BN-backward-in-load of the next pair.
-__device__ __forceinline__ float bn_xhat(float x, float mu, float is) {
-#pragma clang fp contract(off)
-    return (x - mu) * is;
-}
-__device__ __forceinline__ float bn_acc_prod(float s, float a, float b) {
-#pragma clang fp contract(off)
-    return s + a * b;
-}
-__device__ __forceinline__ float bn_dx(float dz, float mdb, float xh, float mdg, float is, float gm, float add) {
-#pragma clang fp contract(off)
-    return (dz - mdb - xh * mdg) * (is * gm) + add;
-}
-
-// g0's epilogue of a pair whose input gradient dU (g0.C) is the dy of a BatchNorm + ReLU
-// backward: per 32-row tile and column, sum dz and sum dz xhat -> bstats[tile][col][2].
-struct BnBwdEpi {
-    const float *u, *x, *mean, *invstd;
-    float *bstats;
 };
 
 // One 32 x 32 output tile (bx, by) of g by the workgroup's SPLIT waves.  pro() runs after
 // the first PF k-blocks of operand loads are issued and before they are used (the
 // BatchNorm-in-load statistics prologue, whose own loads then share their round trip).
-template <int SPLIT, bool AK, bool BK, bool BNA = false, int PF = FS_GEMM_PF, class Pro = NoPrologue, int BNB = 0>
+template <int SPLIT, bool AK, bool BK, bool BNA = false, int PF = FS_GEMM_PF, class Pro = NoPrologue>
 __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t by, GemmLds<SPLIT> &L,
-                                          const BnLoad *bnl = nullptr, Pro pro = {}, const BnbLoad *bbl = nullptr,
-                                          const BnBwdEpi *epi = nullptr) {
-    // BNB: 0 = plain A, 1 = BN-backward-in-load with the column along k, 2 = along m
+                                          const BnLoad *bnl = nullptr, Pro pro = {}) {
     auto &part = L.part;
     auto &rs_part = L.rs_part;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -194,33 +157,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
         }
         return v;
     };
-    const int64_t aoff = aok ? (m0 + r) * g.sam : 0;
-    t4 ua[PF], xa[PF];
-    auto bnb = [&](t4 v, t4 uu, t4 xx, int64_t k0, bool ok) {
-        if constexpr (BNB != 0) {
-            if (!ok) return v;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t k = k0 + j;
-                if (k < g.K) {
-                    const int c = BNB == 1 ? (int)k : (int)(m0 + r);
-                    const float is = bbl->is[c];
-                    const float dz = uu[j] > 0.f ? v[j] : 0.f;
-                    v[j] = bn_dx(dz, bbl->mdb[c], bn_xhat(xx[j], bbl->mu[c], is), bbl->mdg[c], is, bbl->gm[c], 0.f);
-                }
-            }
-        }
-        return v;
-    };
 #pragma unroll
     for (int s = 0; s < PF; ++s) {
         const int64_t k = kb0 + s * step;
         a[s] = load4<AK>(Ap, g.sak, k + 4 * h, g.K, aok && k < g.K);
         b[s] = load4<BK>(Bp, g.sbk, k + 4 * h, g.K, bok && k < g.K);
-        if constexpr (BNB != 0) {
-            ua[s] = load4<AK>(bbl->u + aoff, g.sak, k + 4 * h, g.K, aok && k < g.K);
-            xa[s] = load4<AK>(bbl->x + aoff, g.sak, k + 4 * h, g.K, aok && k < g.K);
-        }
     }
     // the epilogue's bias and residual operands (wave 0 writes the tile) loaded with the
     // first operands, so that their round trip is not left for after the reduction
@@ -228,18 +169,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
     float ep_bias = 0.f, ep_r[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) ep_r[i] = 0.f;
-    float ep_u[16], ep_x[16], ep_mu = 0.f, ep_is = 0.f;
-    if (epi && (SPLIT == 1 || w == 0)) {
-        ep_mu = bok ? epi->mean[col] : 0.f;
-        ep_is = bok ? epi->invstd[col] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
-            const bool in = row < g.M && bok;
-            ep_u[i] = in ? epi->u[row * g.ldc + col] : 0.f;
-            ep_x[i] = in ? epi->x[row * g.ldc + col] : 0.f;
-        }
-    }
     if (SPLIT == 1 || w == 0) {
         ep_bias = (g.bias && bok) ? g.bias[col] : 0.f;
         if (g.R) {
@@ -258,13 +187,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
             a[s] = bn(a[s], k + 4 * h, aok && k < g.K);
         }
     }
-    if constexpr (BNB != 0) {
-#pragma unroll
-        for (int s = 0; s < PF; ++s) {
-            const int64_t k = kb0 + s * step;
-            a[s] = bnb(a[s], ua[s], xa[s], k + 4 * h, aok && k < g.K);
-        }
-    }
     for (int64_t kb = kb0; kb < g.K; kb += PF * step) {
 #pragma unroll
         for (int s = 0; s < PF; ++s) {
@@ -275,17 +197,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][j], b[s][j], acc, 0, 0, 0);
                 if (rows) rs += ((a[s][0] + a[s][1]) + a[s][2]) + a[s][3];
                 const int64_t kn = k + PF * step;
-                if constexpr (BNB != 0) {
-                    const bool okn = aok && kn < g.K;
-                    const t4 an = load4<AK>(Ap, g.sak, kn + 4 * h, g.K, okn);
-                    const t4 un = load4<AK>(bbl->u + aoff, g.sak, kn + 4 * h, g.K, okn);
-                    const t4 xn = load4<AK>(bbl->x + aoff, g.sak, kn + 4 * h, g.K, okn);
-                    b[s] = load4<BK>(Bp, g.sbk, kn + 4 * h, g.K, bok && kn < g.K);
-                    a[s] = bnb(an, un, xn, kn + 4 * h, okn);
-                } else {
-                    a[s] = bn(load4<AK>(Ap, g.sak, kn + 4 * h, g.K, aok && kn < g.K), kn + 4 * h, aok && kn < g.K);
-                    b[s] = load4<BK>(Bp, g.sbk, kn + 4 * h, g.K, bok && kn < g.K);
-                }
+                a[s] = bn(load4<AK>(Ap, g.sak, kn + 4 * h, g.K, aok && kn < g.K), kn + 4 * h, aok && kn < g.K);
+                b[s] = load4<BK>(Bp, g.sbk, kn + 4 * h, g.K, bok && kn < g.K);
             }
         }
     }
@@ -317,24 +230,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
         }
         acc[i] = v;
         if (row < g.M) sv += v;
-    }
-    if (epi) {  // this tile's BatchNorm-backward partial sums per column: sum dz, sum dz xhat
-        float sd = 0.f, sdx = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int64_t row = m0 + 8 * (i >> 2) + 4 * h + (i & 3);
-            if (row < g.M) {
-                const float dz = ep_u[i] > 0.f ? acc[i] : 0.f;
-                sd += dz;
-                sdx = bn_acc_prod(sdx, dz, bn_xhat(ep_x[i], ep_mu, ep_is));
-            }
-        }
-        sd += __shfl_xor(sd, 32);
-        sdx += __shfl_xor(sdx, 32);
-        if (h == 0 && bok) {
-            epi->bstats[(bx * g.N + col) * 2] = sd;
-            epi->bstats[(bx * g.N + col) * 2 + 1] = sdx;
-        }
     }
     if (g.stats) {  // this tile's column mean and sum of squared deviations (the consumer's BatchNorm)
         const int64_t nr = g.M - m0 < 32 ? g.M - m0 : 32;
@@ -498,84 +393,6 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm2_f32_kernel(GemmArgs g0, Gemm
         gemm_tile<SPLIT, A1K, B1K>(g1, (b - t0) % mt1, (b - t0) / mt1, L);
 }
 
-// nn.Linear's backward pair when the Linear's output feeds a BatchNorm1d (train) + ReLU
-// whose backward is left to the next pair (fs_linear_f32_pair_bnstat): g0 = dU (its dy) is
-// written as usual and its epilogue adds each 32-row tile's per-column partial sums of
-// dz = dy (u > 0) and dz xhat (BnBwdEpi.bstats).
-template <int SPLIT>
-__global__ __launch_bounds__(64 * SPLIT) void gemm2_bnstat_kernel(GemmArgs g0, GemmArgs g1, unsigned t0, unsigned mt0,
-                                                                 unsigned mt1, BnBwdEpi e) {
-    __shared__ GemmLds<SPLIT> L;
-    const unsigned b = blockIdx.x;
-    if (b < t0)
-        gemm_tile<SPLIT, true, false>(g0, b % mt0, b / mt0, L, nullptr, NoPrologue{}, nullptr, &e);
-    else
-        gemm_tile<SPLIT, false, false>(g1, (b - t0) % mt1, (b - t0) / mt1, L);
-}
-
-// The next pair (fs_linear_f32_pair_bnin): nn.Linear's backward whose output gradient dX is
-// that BatchNorm + ReLU backward of the raw dy (g0.A = dy [rows][H], g1.A = dy^T), applied
-// to the A operands as they are loaded.  Every workgroup first adds the producer's tile
-// partials per column in tile order (db = sum dz, dg = sum dz xhat) into LDS with mean,
-// invstd and gamma; workgroup 0 writes dgamma = dg and dbeta = db.
-struct BnBwdIn {
-    const float *u, *x, *mean, *invstd, *gamma, *bstats;
-    int64_t tiles, rows;
-    int H;
-    float *dgamma, *dbeta;
-};
-struct BnbLds {
-    float mu[kBnMaxK], is[kBnMaxK], mdb[kBnMaxK], mdg[kBnMaxK], gm[kBnMaxK];
-};
-
-__device__ __forceinline__ void bnb_prologue(const BnBwdIn &bi, bool lead, BnbLds &S) {
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    const int c = threadIdx.x;
-    if (c < bi.H) {
-        const float mu = bi.mean[c], is = bi.invstd[c], gm = bi.gamma[c];
-        float db = 0.f, dg = 0.f;
-        for (int64_t t0 = 0; t0 < bi.tiles; t0 += kBnStTiles) {
-            const int nt = (int)(bi.tiles - t0 < kBnStTiles ? bi.tiles - t0 : kBnStTiles);
-            const f2 *src = (const f2 *)bi.bstats + t0 * bi.H + c;  // [tile][H] pairs
-            f2 v[kBnStTiles];
-#pragma unroll
-            for (int t = 0; t < kBnStTiles; ++t) v[t] = t < nt ? src[t * bi.H] : f2{0.f, 0.f};
-#pragma unroll
-            for (int t = 0; t < kBnStTiles; ++t) {
-                if (t < nt) {
-                    db += v[t][0];
-                    dg += v[t][1];
-                }
-            }
-        }
-        S.mu[c] = mu;
-        S.is[c] = is;
-        S.gm[c] = gm;
-        S.mdb[c] = db / (float)bi.rows;
-        S.mdg[c] = dg / (float)bi.rows;
-        if (lead) {
-            if (bi.dgamma) bi.dgamma[c] = dg;
-            if (bi.dbeta) bi.dbeta[c] = db;
-        }
-    }
-    __syncthreads();
-}
-
-template <int SPLIT>
-__global__ __launch_bounds__(64 * SPLIT) void gemm2_bnin_kernel(GemmArgs g0, GemmArgs g1, unsigned t0, unsigned mt0,
-                                                               unsigned mt1, BnBwdIn bi) {
-    __shared__ GemmLds<SPLIT> L;
-    __shared__ BnbLds S;
-    const BnbLoad bl{S.mu, S.is, S.mdb, S.mdg, S.gm, bi.u, bi.x};
-    const unsigned b = blockIdx.x;
-    auto pro = [&] { bnb_prologue(bi, b == 0, S); };
-    if (b < t0)
-        gemm_tile<SPLIT, true, false, false, 2, decltype(pro), 1>(g0, b % mt0, b / mt0, L, nullptr, pro, &bl);
-    else
-        gemm_tile<SPLIT, false, false, false, 2, decltype(pro), 2>(g1, (b - t0) % mt1, (b - t0) / mt1, L, nullptr, pro,
-                                                                  &bl);
-}
-
 // ---------------------------------------------------------------------------
 // BatchNorm1d (train) + ReLU.  Workgroup = kBnCols columns x kBnRg row groups.
 // 4 columns x 64 row groups (32 workgroups at H = 128, 4 register-cached rows per thread):
@@ -671,71 +488,42 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_fwd_kernel(
 
 // dz = dy * (y > 0); dbeta = sum dz; dgamma = sum dz xhat;
 // dx = gamma invstd (dz - dbeta / B - xhat dgamma / B)   (torch's batch_norm_backward_elemt)
-// R > 0 (B <= 256): the batch sums in the order of the pairs' deferred BatchNorm backward
-// (fs_linear_f32_pair_bnstat / _bnin): per 32-row tile the two 16-row halves of its MFMA
-// accumulator layout (rows 8 (i >> 2) + 4 h + (i & 3), i = 0..15 in order), half 0 + half 1,
-// then the tiles in order, with the same uncontracted arithmetic, so both paths agree bit
-// for bit.
 template <int R>
 __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
     int64_t B, int H, const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ dy,
     const float *__restrict__ gamma, const float *__restrict__ mean, const float *__restrict__ invstd,
     float *__restrict__ dx, const float *__restrict__ dx_add, float *__restrict__ dgamma, float *__restrict__ dbeta) {
     __shared__ float red[kBnRg][kBnCols];
-    __shared__ float dz_s[R > 0 ? R * kBnRg : 1][kBnCols], xh_s[R > 0 ? R * kBnRg : 1][kBnCols];
-    __shared__ float hs_d[R > 0 ? 2 * R * kBnRg / 32 : 1][kBnCols], hs_x[R > 0 ? 2 * R * kBnRg / 32 : 1][kBnCols];
     const int c = threadIdx.x % kBnCols, rg = threadIdx.x / kBnCols;
     const int col = blockIdx.x * kBnCols + c;
     const bool ok = col < H;
     const int64_t o = ok ? col : 0;
     const float mu = mean[o], is = invstd[o];
     float dzv[R > 0 ? R : 1], xhv[R > 0 ? R : 1];
-    float db = 0.f, dg = 0.f;
-    if constexpr (R > 0) {
+    float sd = 0.f, sdx = 0.f;
+    if (R > 0) {
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int64_t i = rg + (int64_t)q * kBnRg;
             const bool in = ok && i < B;
             const float yv = in ? y[i * H + o] : 0.f, g = in ? dy[i * H + o] : 0.f, xv = in ? x[i * H + o] : mu;
             dzv[q] = yv > 0.f ? g : 0.f;
-            xhv[q] = bn_xhat(xv, mu, is);
-            dz_s[i][c] = dzv[q];
-            xh_s[i][c] = xhv[q];
+            xhv[q] = (xv - mu) * is;
         }
-        __syncthreads();
-        constexpr int NH = 2 * R * kBnRg / 32;  // 16-row halves of the 32-row tiles
-        if (rg < NH) {
-            const int t = rg >> 1, hh = rg & 1;
-            float sd = 0.f, sdx = 0.f;
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int64_t row = 32 * t + 8 * (e >> 2) + 4 * hh + (e & 3);
-                if (row < B) {
-                    sd += dz_s[row][c];
-                    sdx = bn_acc_prod(sdx, dz_s[row][c], xh_s[row][c]);
-                }
-            }
-            hs_d[rg][c] = sd;
-            hs_x[rg][c] = sdx;
+        for (int q = 0; q < R; ++q) {
+            sd += dzv[q];
+            sdx += dzv[q] * xhv[q];
         }
-        __syncthreads();
-        const int nt = (int)((B + 31) / 32);
-        for (int t = 0; t < nt; ++t) {
-            db += hs_d[2 * t][c] + hs_d[2 * t + 1][c];
-            dg += hs_x[2 * t][c] + hs_x[2 * t + 1][c];
+    } else if (ok) {
+        for (int64_t i = rg; i < B; i += kBnRg) {
+            const float dz = y[i * H + o] > 0.f ? dy[i * H + o] : 0.f;
+            sd += dz;
+            sdx += dz * ((x[i * H + o] - mu) * is);
         }
-    } else {
-        float sd = 0.f, sdx = 0.f;
-        if (ok) {
-            for (int64_t i = rg; i < B; i += kBnRg) {
-                const float dz = y[i * H + o] > 0.f ? dy[i * H + o] : 0.f;
-                sd += dz;
-                sdx = bn_acc_prod(sdx, dz, bn_xhat(x[i * H + o], mu, is));
-            }
-        }
-        db = wg_colsum(sd, red, c, rg);
-        dg = wg_colsum(sdx, red, c, rg);
     }
+    const float db = wg_colsum(sd, red, c, rg);
+    const float dg = wg_colsum(sdx, red, c, rg);
     if (!ok) return;
     const float gm = gamma[col];
     const float mdb = db / (float)B, mdg = dg / (float)B;
@@ -743,13 +531,13 @@ __global__ __launch_bounds__(kBnCols *kBnRg) void bn_relu_train_bwd_kernel(
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int64_t i = rg + (int64_t)q * kBnRg;
-            if (i < B) dx[i * H + col] = bn_dx(dzv[q], mdb, xhv[q], mdg, is, gm, dx_add ? dx_add[i * H + col] : 0.f);
+            if (i < B) dx[i * H + col] = (dzv[q] - mdb - xhv[q] * mdg) * (is * gm) + (dx_add ? dx_add[i * H + col] : 0.f);
         }
     } else {
         for (int64_t i = rg; i < B; i += kBnRg) {
             const float dz = y[i * H + col] > 0.f ? dy[i * H + col] : 0.f;
-            const float xh = bn_xhat(x[i * H + col], mu, is);
-            dx[i * H + col] = bn_dx(dz, mdb, xh, mdg, is, gm, dx_add ? dx_add[i * H + col] : 0.f);
+            const float xh = (x[i * H + col] - mu) * is;
+            dx[i * H + col] = (dz - mdb - xh * mdg) * (is * gm) + (dx_add ? dx_add[i * H + col] : 0.f);
         }
     }
     if (rg == 0) {
@@ -984,44 +772,6 @@ hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g
     }
     if (hipError_t e = fs_linear_f32_impl(g0, st); e != hipSuccess) return e;
     return fs_linear_f32_impl(g1, st);
-}
-
-static bool pair_layout_ok(const GemmArgs &g0, const GemmArgs &g1) {
-    const bool a0 = g0.sak == 1 && ((uintptr_t)g0.A & 15) == 0 && g0.sam % 4 == 0;
-    const bool b0 = g0.sbk == 1 && ((uintptr_t)g0.B & 15) == 0 && g0.sbn % 4 == 0;
-    const bool a1 = g1.sak == 1 && ((uintptr_t)g1.A & 15) == 0 && g1.sam % 4 == 0;
-    const bool b1 = g1.sbk == 1 && ((uintptr_t)g1.B & 15) == 0 && g1.sbn % 4 == 0;
-    return g0.M > 0 && g0.N > 0 && g1.M > 0 && g1.N > 0 && gemm_split(g0) == FS_GEMM_SPLIT &&
-           gemm_split(g1) == FS_GEMM_SPLIT && a0 && !b0 && !a1 && !b1;
-}
-
-hipError_t fs_linear_f32_pair_bnstat_impl(const GemmArgs &g0, const GemmArgs &g1, const float *u, const float *x,
-                                          const float *mean, const float *invstd, float *bstats, hipStream_t st) {
-    if (!pair_layout_ok(g0, g1) || g0.ldc != g0.N || g0.stats || !u || !x || !mean || !invstd || !bstats)
-        return hipErrorNotSupported;
-    const unsigned mt0 = (unsigned)((g0.M + 31) / 32), mt1 = (unsigned)((g1.M + 31) / 32);
-    const unsigned t0 = mt0 * (unsigned)((g0.N + 31) / 32), t1 = mt1 * (unsigned)((g1.N + 31) / 32);
-    hipLaunchKernelGGL(gemm2_bnstat_kernel<FS_GEMM_SPLIT>, dim3(t0 + t1), dim3(64 * FS_GEMM_SPLIT), 0, st, g0, g1, t0,
-                       mt0, mt1, BnBwdEpi{u, x, mean, invstd, bstats});
-    return hipGetLastError();
-}
-
-hipError_t fs_linear_f32_pair_bnin_impl(const GemmArgs &g0, const GemmArgs &g1, const float *u, const float *x,
-                                        const float *mean, const float *invstd, const float *gamma,
-                                        const float *bstats, int64_t rows, float *dgamma, float *dbeta,
-                                        hipStream_t st) {
-    // g0 = dX W over K = H with A = dy [rows][H]; g1 = dX^T Y over K = rows with A = dy^T
-    const int64_t H = g0.K;
-    if (!pair_layout_ok(g0, g1) || H > kBnMaxK || H > 64 * FS_GEMM_SPLIT || g1.M != H || g0.M != rows ||
-        g1.K != rows || g0.sam != H || g1.sak != H || g1.sam != 1 || g0.A != g1.A || !u || !x || !mean || !invstd ||
-        !gamma || !bstats)
-        return hipErrorNotSupported;
-    const unsigned mt0 = (unsigned)((g0.M + 31) / 32), mt1 = (unsigned)((g1.M + 31) / 32);
-    const unsigned t0 = mt0 * (unsigned)((g0.N + 31) / 32), t1 = mt1 * (unsigned)((g1.N + 31) / 32);
-    const BnBwdIn bi{u, x, mean, invstd, gamma, bstats, (rows + 31) / 32, rows, (int)H, dgamma, dbeta};
-    hipLaunchKernelGGL(gemm2_bnin_kernel<FS_GEMM_SPLIT>, dim3(t0 + t1), dim3(64 * FS_GEMM_SPLIT), 0, st, g0, g1, t0,
-                       mt0, mt1, bi);
-    return hipGetLastError();
 }
 
 // u's write-back stores 4 floats at once where A is contiguous along k

@@ -106,10 +106,6 @@ _SIGS = {
     "fs_linear_f32": (ctypes.c_int, [_I64, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _P, _I64, _P, _I64,
                                      _P, _P]),
     "fs_linear_f32_pair": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(GemmF32), _P]),
-    "fs_linear_f32_pair_bnstat": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(GemmF32), _P, _P, _P, _P, _P,
-                                                 _P]),
-    "fs_linear_f32_pair_bnin": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(GemmF32), _P, _P, _P, _P, _P,
-                                               _P, _P, _P, _P]),
     "fs_linear_f32_splitk_floats": (_I64, [ctypes.POINTER(GemmF32)]),
     "fs_linear_f32_splitk": (ctypes.c_int, [ctypes.POINTER(GemmF32), _P, _I64, _P]),
     "fs_linear_f32_ex": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(BnIn), _P, _P]),

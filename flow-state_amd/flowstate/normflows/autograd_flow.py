@@ -206,12 +206,6 @@ def register_grad_home(flat, flat_grad):
 _direct_grads = False  # set by paired_kld around its forward: one gradient contribution per parameter
 
 
-def _in_grad_home(t):
-    """t lives in a registered flat gradient buffer (memory that outlives the backward)."""
-    sp = t.untyped_storage().data_ptr()
-    return any(h[2].untyped_storage().data_ptr() == sp for h in _GRAD_HOMES.values())
-
-
 def _grad_out(*ps, direct=False):
     """The gradient buffer of parameters ps (consecutive in memory when several): their
     slice of a registered flat gradient buffer when the Function was built by paired_kld
@@ -428,10 +422,7 @@ class _BnReluLinear(torch.autograd.Function):
     for the next BatchNorm (fs_linear_f32_ex).  u = relu(BN(x)) is written once for the
     backward, which is the weight / input gradient pair on u and then the BatchNorm + ReLU
     backward (fs_bn_relu_train_bwd, with the block's residual gradient added there as in
-    _BnRelu).  Inside paired_kld the block's second BatchNorm backward has no launch of its
-    own: the second Linear's pair writes its tile partial sums (fs_linear_f32_pair_bnstat)
-    and hands the raw dy on, and the first Linear's pair forms dX as it loads its operands
-    (fs_linear_f32_pair_bnin); bit-identical to the separate launches."""
+    _BnRelu)."""
 
     @staticmethod
     def forward(ctx, x, x_stats, gamma, beta, bn, w, b, r, res=None, pair=None, op=None):
@@ -465,7 +456,6 @@ class _BnReluLinear(torch.autograd.Function):
         ctx.save_for_backward(x, u, gamma, mean, invstd, w)
         ctx.gparams = (beta, b)
         ctx.direct = _direct_grads
-        ctx.op = op
         ctx.has_r = r is not None
         ctx.res = res
         ctx.mark_non_differentiable(st)
@@ -484,63 +474,26 @@ class _BnReluLinear(torch.autograd.Function):
         N = w.shape[0]
         L = _lib.load()
         p = _lib.ptr
-        res = ctx.res
         gw = _grad_out(w, direct=ctx.direct)
         gb = _grad_out(ctx.gparams[1], direct=ctx.direct)
+        add = None
+        if ctx.res is not None and ctx.res.g is not None:
+            add, ctx.res.g = ctx.res.g, None
+        gx = torch.empty_like(x)
         gg = _grad_out(gamma, direct=ctx.direct)
         gbeta = _grad_out(ctx.gparams[0], direct=ctx.direct)
-        g0 = g1 = None
-        bnb, fused_in = None, False
-        if res is not None and res.bnb is not None and ctx.op is not None and ctx.op[1] == 0:
-            # this Linear's output feeds the block's second BatchNorm, whose backward the
-            # second Linear's pair left to this one: gy is that BatchNorm's raw dy, and
-            # dX = BN+ReLU backward(gy) is formed as this pair loads its A operands
-            bnb, res.bnb = res.bnb, None
-            if gy.data_ptr() != bnb["dy"].data_ptr():
-                raise RuntimeError("the deferred BatchNorm backward lost its dy")
-            fused_in = True
+        # the input / weight gradient pair over 48 workgroups, then the BatchNorm + ReLU
+        # backward: 10.9 us per layer in a graph, against 18.1 us for one launch whose
+        # column strips own the BatchNorm sums (4 workgroups carry the whole input gradient;
+        # tools/linbn_probe.py, profiles/r03/r03k_linbn_probe.log), and 148 against 239
+        # steps/s for the BatchNorm backward run by each strip's last tile in the pair's
+        # launch (device-scope fences; DESIGN "Training", profiles/r03/r03v_*)
         gu = torch.empty_like(u)
         g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
         g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
-        if fused_in:
-            _lib.check(L.fs_linear_f32_pair_bnin(g0, g1, p(bnb["u"]), p(bnb["x"]), p(bnb["mean"]), p(bnb["invstd"]),
-                                                 p(bnb["gamma"]), p(bnb["bstats"]), bnb["gg"], bnb["gbeta"],
-                                                 _lib.stream_ptr()), "fs_linear_f32_pair_bnin")
-        # (dgamma / dbeta must be flat-buffer slices: autograd keeps them as p.grad without
-        # reading them, and the stash holds only their addresses, so that nothing but the
-        # returned tensors references them and autograd takes them as they are)
-        defer = (ctx.direct and res is not None and ctx.op is not None and ctx.op[1] == 1 and res.bnb is None
-                 and not fused_in and K <= 256 and gamma.grad is None and ctx.gparams[0].grad is None
-                 and x.is_contiguous() and u.is_contiguous() and _in_grad_home(gg) and _in_grad_home(gbeta))
-        add = None
-        if res is not None and res.g is not None:
-            add, res.g = res.g, None
-        if defer:
-            # this is the block's second Linear: its BatchNorm + ReLU backward goes to the
-            # first Linear's pair (fs_linear_f32_pair_bnin), this pair only adds the tile
-            # partial sums (fs_linear_f32_pair_bnstat); x's gradient handed on is the raw dy
-            # (gu), and dgamma / dbeta land in their flat-buffer slices when that pair runs
-            # (nothing reads them before: autograd stores the slices as p.grad as they are)
-            if add is not None:
-                raise RuntimeError("a residual gradient reached the block's second BatchNorm")
-            bst = torch.empty(((M + 31) // 32, K, 2), dtype=torch.float32, device=x.device)
-            _lib.check(L.fs_linear_f32_pair_bnstat(g0, g1, p(u), p(x), p(mean), p(invstd), p(bst), _lib.stream_ptr()),
-                       "fs_linear_f32_pair_bnstat")
-            res.bnb = {"dy": gu, "u": u, "x": x, "mean": mean, "invstd": invstd, "gamma": gamma, "bstats": bst,
-                       "gg": gg.data_ptr(), "gbeta": gbeta.data_ptr()}
-            gx = gu
-        else:
-            # the input / weight gradient pair over 48 workgroups, then the BatchNorm + ReLU
-            # backward: 10.9 us per layer in a graph, against 18.1 us for one launch whose
-            # column strips own the BatchNorm sums (4 workgroups carry the whole input gradient;
-            # tools/linbn_probe.py, profiles/r03/r03k_linbn_probe.log), and 148 against 239
-            # steps/s for the BatchNorm backward run by each strip's last tile in the pair's
-            # launch (device-scope fences; DESIGN "Training", profiles/r03/r03v_*)
-            gx = torch.empty_like(x)
-            if not fused_in:
-                _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
-            _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
-                                              p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
+        _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
+        _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
+                                          p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
         gr = None
         if ctx.has_r and ctx.needs_input_grad[7]:
             if ctx.res is not None:
@@ -577,11 +530,10 @@ class _ResidualGrad:
     must construct them with res=None, which returns the residual gradient normally.
     A stash still unconsumed when the next one is written raises."""
 
-    __slots__ = ("g", "bnb")
+    __slots__ = ("g",)
 
     def __init__(self):
         self.g = None
-        self.bnb = None  # the block's second BatchNorm backward, left to the first Linear's pair
 
 
 def _conditioner_fused(net, t, pair=None, final=True):

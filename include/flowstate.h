@@ -386,23 +386,6 @@ int fs_bn_running_update(int32_t nbn, int32_t H, float *running_mean, float *run
 int64_t fs_linear_f32_splitk_floats(const fs_gemm_f32 *g);
 int fs_linear_f32_splitk(const fs_gemm_f32 *g, float *workspace, int64_t workspace_floats, void *stream);
 
-/* BatchNorm + ReLU backward between two backward pairs (the A2 conditioner's
- * Linear -> BatchNorm1d(train) + ReLU -> Linear), without a launch of its own:
- * fs_linear_f32_pair_bnstat is fs_linear_f32_pair (g0 = dU = dY W, the BatchNorm's dy,
- * contiguous [B][H]) whose g0 epilogue also writes per 32-row tile and column the partial
- * sums of dz = dU (u > 0) and dz (x - mean) invstd to bstats [ceil(B/32)][H][2] (u =
- * relu(BN(x)) and x contiguous [B][H]).  fs_linear_f32_pair_bnin is the next pair (the
- * Linear that produced x: g0 = dX W', g1 = dX^T Y with A = the raw dU [B][H] and its
- * transpose) with dX = gamma invstd (dz - db / B - xhat dg / B) formed as its A operands
- * are loaded, db / dg the tile partials added in tile order; dgamma = dg and dbeta = db
- * written by its first workgroup.  Both return an error (hipErrorNotSupported) for shapes
- * or layouts other than those (then use fs_linear_f32_pair + fs_bn_relu_train_bwd). */
-int fs_linear_f32_pair_bnstat(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const float *u, const float *x,
-                              const float *mean, const float *invstd, float *bstats, void *stream);
-int fs_linear_f32_pair_bnin(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const float *u, const float *x,
-                            const float *mean, const float *invstd, const float *gamma, const float *bstats,
-                            float *dgamma, float *dbeta, void *stream);
-
 /* Up to 4 independent fs_linear_f32 products in one launch (a coupling layer's final
  * Linear backward: input gradient, weight + bias gradient, and the unconditional spline
  * parameters' row sum).  Products with a split-K plan take it while the workspace

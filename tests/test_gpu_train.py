@@ -104,60 +104,6 @@ def test_linear_pair_launch_matches_two_launches():
         torch.testing.assert_close(outs[0][2], gy.sum(0), rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("B,H,K0,N1", [(256, 128, 128, 128), (100, 40, 72, 36)])
-def test_batchnorm_backward_between_pairs(B, H, K0, N1):
-    """Linear1(relu(BN(Linear0(t)))) backward with the BatchNorm + ReLU backward carried by
-    the pairs (fs_linear_f32_pair_bnstat's tile partial sums, fs_linear_f32_pair_bnin's
-    operand loads) against the separate path (fs_linear_f32_pair, fs_bn_relu_train_bwd,
-    fs_linear_f32_pair): bit-identical (the same batch-sum order and arithmetic)."""
-    from flowstate import _lib
-
-    L, p = _lib.load(), _lib.ptr
-    g = torch.Generator().manual_seed(B + H)
-    x = torch.randn((B, H), generator=g).cuda()  # Linear0's output = the BatchNorm input
-    gamma = (torch.rand(H, generator=g) + 0.5).cuda()
-    beta = (torch.randn(H, generator=g) * 0.3).cuda()
-    mean, var = x.mean(0), x.var(0, unbiased=False)
-    invstd = 1.0 / torch.sqrt(var + 1e-5)
-    u = torch.relu(gamma * ((x - mean) * invstd) + beta)
-    w1 = torch.randn((N1, H), generator=g).cuda() * 0.1  # Linear1: H -> N1
-    w0 = torch.randn((H, K0), generator=g).cuda() * 0.1  # Linear0: K0 -> H
-    t = torch.randn((B, K0), generator=g).cuda()  # Linear0's input
-    gy = torch.randn((B, N1), generator=g).cuda()
-
-    def pair1(gu, gw1, gb1):
-        return (_lib.GemmF32(B, H, N1, p(gy), N1, 1, p(w1), H, 1, None, None, 0, p(gu), H, None),
-                _lib.GemmF32(N1, H, B, p(gy), 1, N1, p(u), H, 1, None, None, 0, p(gw1), H, p(gb1)))
-
-    def pair0(dx, gt, gw0, gb0):
-        return (_lib.GemmF32(B, K0, H, p(dx), H, 1, p(w0), K0, 1, None, None, 0, p(gt), K0, None),
-                _lib.GemmF32(H, K0, B, p(dx), 1, H, p(t), K0, 1, None, None, 0, p(gw0), K0, p(gb0)))
-
-    outs = []
-    for fused in (False, True):
-        gu, gw1, gb1 = torch.empty((B, H), device="cuda"), torch.empty((N1, H), device="cuda"), torch.empty(N1, device="cuda")
-        gt, gw0, gb0 = torch.empty((B, K0), device="cuda"), torch.empty((H, K0), device="cuda"), torch.empty(H, device="cuda")
-        dg, db = torch.full((H,), float("nan"), device="cuda"), torch.full((H,), float("nan"), device="cuda")
-        a, b = pair1(gu, gw1, gb1)
-        if fused:
-            bst = torch.full(((B + 31) // 32, H, 2), float("nan"), device="cuda")
-            _lib.check(L.fs_linear_f32_pair_bnstat(a, b, p(u), p(x), p(mean), p(invstd), p(bst), _lib.stream_ptr()))
-            c, d = pair0(gu, gt, gw0, gb0)
-            _lib.check(L.fs_linear_f32_pair_bnin(c, d, p(u), p(x), p(mean), p(invstd), p(gamma), p(bst), p(dg), p(db),
-                                                 _lib.stream_ptr()))
-        else:
-            _lib.check(L.fs_linear_f32_pair(a, b, _lib.stream_ptr()))
-            dx = torch.empty_like(x)
-            _lib.check(L.fs_bn_relu_train_bwd(B, H, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(dx), None,
-                                              p(dg), p(db), _lib.stream_ptr()))
-            c, d = pair0(dx, gt, gw0, gb0)
-            _lib.check(L.fs_linear_f32_pair(c, d, _lib.stream_ptr()))
-        outs.append((gw1, gb1, gt, gw0, gb0, dg, db))
-    torch.cuda.synchronize()
-    for name, a, b in zip(("gw1", "gb1", "gt", "gw0", "gb0", "dgamma", "dbeta"), *outs):
-        assert torch.equal(a, b), (name, (a - b).abs().max().item())
-
-
 def test_linear_group_launch_matches_single_launches():
     """fs_linear_f32_group (the final Linear's backward + the unconditional row sum in one
     launch, split-K included) gives exactly what the products give one by one."""
