@@ -74,6 +74,7 @@ class Algorithm2:
         self.mcmc_steps_history = []
         self.graphed = bool(graphed) and next(model.parameters()).is_cuda
         self._step = None
+        self._mods = None  # (model, its modules) for the mode switches (_set_training)
 
     # ------------------------------------------------------------------
     def production(self):
@@ -97,11 +98,27 @@ class Algorithm2:
 
         return list(DataLoader(_Indices(n), batch_size=self.batch_size, shuffle=True, collate_fn=_first))
 
+    def _set_training(self, mode):
+        """model.train(mode) as a flag write per module: nn.Module.train walks the ~500
+        modules of an A2 flow through Module.__setattr__ (~2 ms per call on the host, twice
+        per cycle while the GPU waits); the same flags are set when no module overrides
+        train(), else model.train(mode) itself."""
+        m = self.model
+        if self._mods is None or self._mods[0] is not m:
+            mods = list(m.modules())
+            self._mods = (m, mods if all(type(x).train is torch.nn.Module.train for x in mods) else None)
+        mods = self._mods[1]
+        if mods is None:
+            m.train(mode)
+        else:
+            for x in mods:
+                x.__dict__["training"] = mode
+
     def train(self):
         """:430-452 — one epoch with a fresh Adam; returns the mean loss (reference:
         cycle_loss / len(dataloader), NaN / inf losses included)."""
         m = self.model
-        m.train()
+        self._set_training(True)
         data = self.training_data.to(next(m.parameters()).device)
         batches = self._batches(data.shape[0])
         losses = []
@@ -153,7 +170,7 @@ class Algorithm2:
     def refeed(self):
         """:476-540 — model.eval(), one NF-proposed MH step per run (fused HIP step);
         returns (accepted runs on this rank (C,) u8, global acceptance p_acc_update)."""
-        self.model.eval()
+        self._set_training(False)  # model.eval()
         if self.bmc.model is not self.model:
             self.bmc.set_model(self.model)
         self.bmc.invalidate_nll()  # nf_big_move re-derives the old NLL with the current weights (:251-261)
