@@ -732,7 +732,9 @@ struct WideArgs {
     float *XB;     // [R][XS] the final layer's input (the trunk's output)
     float *LDW;    // [R][8] log-det partial of virtual wave w (the fused kernel's wave w)
     float *LDC;    // [R][N] the last final phase's conditional log-det of transform feature j
-    float *LDU;    // [R][N] (density) its unconditional log-det of identity feature f
+    float *LDU;    // [R][N] (density) its unconditional log-det of identity feature f;
+                   // (sampling) the unconditional log-dets of the even layers' start
+    float *LDU2;   // [R][N] (sampling) ... of the odd layers' start
     int pending;   // the start / output launch first folds the previous final phase into LDW
     int64_t R;     // rows padded to 64
     int off;       // physical index of logical coordinate 0 in this phase
@@ -909,6 +911,50 @@ __device__ __forceinline__ float uncond_one(const float *__restrict__ U, float *
     return 0.f;
 }
 
+// (sampling modes) the start spread over features: workgroup (block, j) runs feature
+// f = wid + 8 j of virtual wave wid (one feature per wave instead of its 8): the
+// unconditional inverse spline (CO updated in place, the log-det to this layer's LDU /
+// LDU2 slot) and the periodic features of f.  The virtual wave's log-det sum over its
+// features (uncond_spline_w's order) is added to LDW by the next start / output launch,
+// before that layer's conditional terms, so LDW sees the fused kernel's additions in its
+// order: ..., su(l - 1), cond(l - 1), su(l), ...  Workgroups j = 0 do that fold for the
+// previous layer (its slot is the other buffer) and the feature padding.
+template <int H, int K, int MODE>
+__global__ void __launch_bounds__(kThreads) wide_start_s_kernel(WideArgs w) {
+    constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
+    const FlowArgs &a = w.a;
+    const int N = a.N, D = 2 * N;
+    const PackLayout PL = pack_layout(N, H, a.nb, a.K);
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int j = (int)blockIdx.y;
+    const int64_t row0 = (int64_t)blockIdx.x * kRows, row = row0 + lane;
+    float *CO = w.CO + row0 * D;
+    float *X = w.XA + row0 * XS;
+    const float *P = a.packed + (int64_t)w.layer * PL.stride;
+    float *lu_cur = (w.layer & 1) ? w.LDU2 : w.LDU;
+    if (j == 0 && w.pending) {
+        const float *lu_prev = (w.layer & 1) ? w.LDU : w.LDU2;
+        float ld = w.LDW[row * kWaves + wid];
+        float su = 0.f;
+        for (int f = wid; f < N; f += kWaves) su += lu_prev[row * N + f];
+        ld += su;
+        w.LDW[row * kWaves + wid] = wide_fold<K, MODE>(w, row, wid, ld);
+    }
+    const int f = wid + kWaves * j;
+    if (f < N) {
+        bool nan_any = false;
+        lu_cur[row * N + f] = uncond_one<K, true>(P + PL.unc, CO, D, D, w.off, a, nan_any, f);
+        if (nan_any && row < a.nrows && a.err) atomicOr(a.err, 1);
+        const float v = CO[lane * D + (2 * f + w.off) % D];
+        const float sv = a.scale_pf * v;
+        X[lane * XS + f] = cosf(sv);
+        X[lane * XS + N + f] = sinf(sv);
+    }
+    if (j == 0)
+        for (int c = D + wid; c < 8 * PL.kg_in; c += kWaves) X[lane * XS + c] = 0.f;
+}
+
 // Final layer + conditional spline of one feature unit (a transform feature, or a pair of
 // them for K <= 16) per wave, for one 64-row block; (density) also the unconditional
 // spline of the same-index identity feature(s).  WPB waves per workgroup share the
@@ -984,7 +1030,14 @@ __global__ void __launch_bounds__(kThreads) wide_output_kernel(WideArgs w) {
     {
         const int vw = threadIdx.x >> 6;
         const int64_t row = row0 + (threadIdx.x & 63);
-        w.LDW[row * kWaves + vw] = wide_fold<K, MODE>(w, row, vw, w.LDW[row * kWaves + vw]);
+        float ld = w.LDW[row * kWaves + vw];
+        if (MODE != MODE_DENSITY) {  // the last layer's unconditional log-dets (wide_start_s_kernel)
+            const float *lu = (w.layer & 1) ? w.LDU2 : w.LDU;
+            float su = 0.f;
+            for (int f = vw; f < N; f += kWaves) su += lu[row * N + f];
+            ld += su;
+        }
+        w.LDW[row * kWaves + vw] = wide_fold<K, MODE>(w, row, vw, ld);
     }
     __syncthreads();
     if (threadIdx.x < kRows) {
@@ -1232,7 +1285,7 @@ constexpr int64_t kWideMaxRows = 65536;  // the workspace never grows beyond thi
 static size_t wide_bytes(int64_t R, int N, int H) {
     const int64_t XS = flow_xw(H) + 4;
     return (size_t)(rup(R * 2 * N * 4, 256) + 2 * rup(R * XS * 4, 256) + rup(R * kWaves * 4, 256) +
-                    2 * rup(R * N * 4, 256));
+                    3 * rup(R * N * 4, 256));
 }
 
 struct WideLaunch {
@@ -1382,6 +1435,8 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     w.LDC = (float *)p;
     p += rup(R * N * 4, 256);
     w.LDU = (float *)p;
+    p += rup(R * N * 4, 256);
+    w.LDU2 = (float *)p;
     w.pending = 0;
     const unsigned nblk = (unsigned)(R / kRows);
     constexpr int WPW = 4;  // feature units (waves) per final-phase workgroup
@@ -1400,7 +1455,10 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
         w.layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
         if (MODE != MODE_DENSITY) w.off = (w.off + N) % D;
         w.pending = s > 0;
-        add((const void *)wide_start_kernel<H, K, MODE>, dim3(nblk), dim3(kThreads), 0);
+        if (MODE == MODE_DENSITY)
+            add((const void *)wide_start_kernel<H, K, MODE>, dim3(nblk), dim3(kThreads), 0);
+        else
+            add((const void *)wide_start_s_kernel<H, K, MODE>, dim3(nblk, kWaves), dim3(kThreads), 0);
         add((const void *)wide_trunk_kernel<H>, dim3((unsigned)(R / 32)), dim3(64 * (H / 32)), 0);
         add((const void *)wide_final_kernel<H, K, MODE, WPW>, dim3(nblk, (units + WPW - 1) / WPW), dim3(64 * WPW),
             fin_lds);
