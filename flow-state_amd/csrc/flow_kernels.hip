@@ -1439,7 +1439,10 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     w.LDU2 = (float *)p;
     w.pending = 0;
     const unsigned nblk = (unsigned)(R / kRows);
-    constexpr int WPW = 4;  // feature units (waves) per final-phase workgroup
+#ifndef FS_WIDE_WPW
+#define FS_WIDE_WPW 4
+#endif
+    constexpr int WPW = FS_WIDE_WPW;  // feature units (waves) per final-phase workgroup
     const int units = K <= 16 ? (N + 1) / 2 : N;
     const unsigned fin_lds = (unsigned)(kRows * XS * 4);
     {
