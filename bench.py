@@ -539,8 +539,10 @@ def acceptance_match(bmc, stepper, n_chains=2048, steps=10):
     PCG64 stream (draw only when ratio < 1, :284-287).  Reported: both acceptance
     counts per step, the decisions that differ (a flip makes that chain's later inputs
     differ: `chains_diverged`), and log q against the reference-order float32 value
-    (max, median, fraction beyond the north star's 1e-5) and, on a subset, both
-    float32 evaluations against the exact (float64) value."""
+    (max, median, fraction beyond the north star's 1e-5) and, on the last step's
+    proposals of all n_chains chains, both float32 evaluations (the GPU's and the
+    reference-order one) against the exact value (the oracle in float64): max, p99,
+    median and the fraction beyond 1e-5 for each."""
     from oracle import flow as OF
     from oracle import physics as OP
 
@@ -581,17 +583,24 @@ def acceptance_match(bmc, stepper, n_chains=2048, steps=10):
         nll = np.where(acc_o, -lq, nll)
         fin = np.isfinite(lq)
         rels.append(np.abs(lq_gpu[fin] - lq[fin]) / np.abs(lq[fin]))
+        lq_last = lq
     rel = np.concatenate(rels)
-    # both float32 evaluations against the exact value (the oracle in float64) on a subset
-    S64 = min(256, S)
+    # both float32 evaluations against the exact value (the oracle in float64) on the last
+    # step's proposals of every replayed chain (the same rows as the last step's f32 column)
     cen, lq_gpu = rec[-1][1], rec[-1][2]
-    lq = OF.log_prob(sd, cen[:S64].clone(), dims).numpy().astype(np.float64)
+    lq = lq_last
     sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
-    lq64 = OF.log_prob(sd64, cen[:S64].double(), dims).numpy()
+    t64 = time.perf_counter()
+    lq64 = OF.log_prob(sd64, cen.double(), dims).numpy()
+    t64 = time.perf_counter() - t64
 
-    def max_rel(a, b):
-        fin = np.isfinite(b)
-        return float((np.abs(a[fin] - b[fin]) / np.abs(b[fin])).max()) if fin.any() else 0.0
+    def vs64(a, b):
+        fin = np.isfinite(b) & np.isfinite(a)
+        r = np.abs(a[fin] - b[fin]) / np.abs(b[fin])
+        if not r.size:
+            return {"rows": 0}
+        return {"rows": int(r.size), "max_rel": float(r.max()), "p99_rel": float(np.percentile(r, 99)),
+                "median_rel": float(np.median(r)), "frac_beyond_1e-5": float((r > 1e-5).mean())}
 
     n = S * steps
     ga = sum(p["gpu_accepts"] for p in per_step)
@@ -606,8 +615,11 @@ def acceptance_match(bmc, stepper, n_chains=2048, steps=10):
                                     "median_rel": float(np.median(rel)) if rel.size else 0.0,
                                     "frac_beyond_1e-5": float((rel > 1e-5).mean()) if rel.size else 0.0},
             "max_rel_log_q_gpu_vs_oracle_f32": float(rel.max()) if rel.size else 0.0,
-            "max_rel_log_q_vs_f64": {"chains": S64, "gpu_f32": max_rel(lq_gpu[:S64], lq64),
-                                     "oracle_f32": max_rel(lq, lq64)},
+            # which float32 evaluation is closer to the exact value, on all S rows
+            "log_q_vs_f64": {"what": "last step's proposals of every replayed chain; relative to the oracle's "
+                                     "float64 evaluation of the same weights and inputs",
+                             "gpu_f32": vs64(lq_gpu, lq64), "reference_order_f32": vs64(lq, lq64),
+                             "f64_s": t64},
             "oracle_s": time.perf_counter() - t0}
 
 
@@ -695,8 +707,11 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         stepper.step(timed=True)
+    torch.cuda.synchronize()  # this rank's steps done: the rest is the end reduction
+    t_steps = time.perf_counter() - t0
     hist, wells, table = final_reduction(bmc)
     torch.cuda.synchronize()
+    t_red = time.perf_counter() - t0 - t_steps
     stepper.harvest()
     if dist:
         dist.barrier()
@@ -705,10 +720,22 @@ def main():
     bmc.check_errors()
     n_acc = torch.tensor([int(bmc.n_accept.item()) - acc0], dtype=torch.int64, device=dev)
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    # per-rank attribution of the timed region (gathered to rank 0): its own wall time,
+    # its steps alone, the end reduction's RCCL calls (which also absorb the wait for the
+    # slowest rank) and its kernels' HIP-event times
+    mine = torch.tensor([elapsed, t_steps, t_red] + list(stepper.t / args.steps), dtype=torch.float64,
+                        device=dev if args.backend == "nccl" else "cpu")
+    per_rank = [mine]
     if dist:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
         dist.all_reduce(n_acc)
+        per_rank = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
     elapsed = float(t_max.item())
+    per_rank = [r.cpu().tolist() for r in per_rank]
+    ranks = [{"rank": i, "elapsed_s": r[0], "steps_s": r[1], "final_reduction_ms": r[2] * 1e3,
+              "kernel_ms": {"flow_propose": r[3], "flow_log_prob": r[4], "energy": r[5], "mh_accept": r[6]}}
+             for i, r in enumerate(per_rank)]
 
     total_steps = C * world * args.steps
     value = total_steps / elapsed
@@ -742,6 +769,12 @@ def main():
                         "gathered_chain_rows": int(table.shape[0]),
                         "deltaF_mean_sem": parallel.free_energy_stats(table)[:2]},
         "kernel_ms": {"flow_propose": t_prop, "flow_log_prob": t_lp, "energy": t_en, "mh_accept": t_acc},
+        # where a multi-GPU run loses time: each rank's timed region, its steps alone, the
+        # end reduction (RCCL all-reduce + all-gather), and the spread over ranks
+        "ranks": ranks,
+        "timed_region_skew_ms": (max(r["elapsed_s"] for r in ranks) - min(r["elapsed_s"] for r in ranks)) * 1e3,
+        "steps_skew_ms": (max(r["steps_s"] for r in ranks) - min(r["steps_s"] for r in ranks)) * 1e3,
+        "final_reduction_ms_max": max(r["final_reduction_ms"] for r in ranks),
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic,
                      "traffic_source": traffic_src, "algorithmic_bytes_per_launch": alg_bytes,
@@ -770,8 +803,13 @@ def main():
             out[name] = {"error": f"{type(e).__name__}: {e}"}
             print(f"bench.py: {name} failed: {e!r}", file=sys.stderr, flush=True)
 
+    out["parity_checked"] = None  # the acceptance-rate match runs on rank 0 at N=1 only
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         leg("acceptance_match", acceptance_match, bmc, stepper)
+        am = out["acceptance_match"]
+        # the metric's qualifier: true only when the replay ran and matched every decision
+        # made on identical inputs (an errored check is false, never a clean run)
+        out["parity_checked"] = "error" not in am and am["mismatched_on_identical_inputs"] == 0
     if world == 1 and not args.no_alt_precision and args.precision == "f32":
         leg("alt_precision", alt_precisions, bmc, stepper)
     if world == 1 and not args.no_single_pass and args.precision == "f32":

@@ -446,14 +446,14 @@ int fs_rqs_backward(int64_t M, int32_t K, int32_t inverse, const float *x, const
 int64_t fs_set_wide_rows(int64_t rows) { return fs_set_wide_rows_impl(rows); }
 
 int fs_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float *step,
-                 const float *loss, double lr, double beta1, double beta2, double eps, double weight_decay,
-                 void *stream) {
+                 const float *loss, const int32_t *skip, double lr, double beta1, double beta2, double eps,
+                 double weight_decay, void *stream) {
     REQUIRE(n >= 0 && step && (n == 0 || (param && grad && exp_avg && exp_avg_sq)) && lr > 0.0 && beta1 >= 0.0 &&
                 beta1 < 1.0 && beta2 >= 0.0 && beta2 < 1.0 && eps >= 0.0 && weight_decay >= 0.0,
             "fs_adam_step: invalid arguments");
     REQUIRE((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) == 0,
             "fs_adam_step: buffers must be 16-byte aligned");
-    return hip_rc(fs_adam_step_impl(param, grad, exp_avg, exp_avg_sq, n, step, loss, lr, beta1, beta2, eps,
+    return hip_rc(fs_adam_step_impl(param, grad, exp_avg, exp_avg_sq, n, step, loss, skip, lr, beta1, beta2, eps,
                                     weight_decay, (hipStream_t)stream),
                   "fs_adam_step");
 }
@@ -575,13 +575,13 @@ int fs_linear_f32_ex2(const fs_gemm_f32 *d0, const fs_bn_in *bn0, float *stats0,
 
 int fs_bn_running_update(int32_t nbn, int32_t H, float *running_mean, float *running_var, int64_t *num_batches,
                          const float *stats, int32_t passes, int64_t rows0, int64_t rows1, double momentum,
-                         void *stream) {
+                         const int32_t *skip, void *stream) {
     REQUIRE(nbn >= 0 && H >= 0 && passes >= 1 && passes <= 2 && rows0 >= 2 && (passes < 2 || rows1 >= 2),
             "fs_bn_running_update: invalid arguments");
     REQUIRE(nbn == 0 || H == 0 || (running_mean && running_var && num_batches && stats),
             "fs_bn_running_update: NULL buffer");
     return hip_rc(fs_bn_running_update_impl(nbn, H, running_mean, running_var, num_batches, stats, passes, rows0,
-                                            rows1, (float)momentum, (hipStream_t)stream),
+                                            rows1, (float)momentum, skip, (hipStream_t)stream),
                   "fs_bn_running_update");
 }
 

@@ -125,11 +125,12 @@ bool fs_linear_ex2_ok(const fs::GemmArgs &g0, const fs::BnIn *b0, const fs::Gemm
 hipError_t fs_linear_ex2_impl(const fs::GemmArgs &g0, const fs::BnIn *b0, const fs::GemmArgs &g1, const fs::BnIn *b1,
                               hipStream_t st);
 hipError_t fs_bn_running_update_impl(int nbn, int H, float *rm, float *rv, int64_t *nbt, const float *stats,
-                                     int passes, int64_t rows0, int64_t rows1, float momentum, hipStream_t st);
+                                     int passes, int64_t rows0, int64_t rows1, float momentum, const int32_t *skip,
+                                     hipStream_t st);
 int64_t fs_linear_f32_splitk_floats_impl(const fs::GemmArgs &g);
 hipError_t fs_linear_f32_splitk_impl(const fs::GemmArgs &g, float *part, int64_t part_floats, hipStream_t st);
 hipError_t fs_adam_step_impl(float *p, const float *g, float *m, float *v, int64_t n, float *step, const float *loss,
-                             double lr, double beta1, double beta2, double eps, double weight_decay, hipStream_t st);
+                             const int32_t *skip, double lr, double beta1, double beta2, double eps, double weight_decay, hipStream_t st);
 hipError_t fs_linear_f32_group_impl(const fs::GemmArgs *gs, int n, float *ws, int64_t ws_floats, hipStream_t st);
 hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,
                                      float *rm, float *rv, int64_t *nbt, float momentum, float eps, float *y,

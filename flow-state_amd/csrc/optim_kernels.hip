@@ -5,7 +5,7 @@
 // capturable multi-tensor Adam takes ~16 launches for the same update, and the step's
 // "skip on a non-finite loss" rule (main_algorithm_2.py:324-326) cost a snapshot and a
 // select of every buffer around it; here the kernel reads the loss and writes nothing when
-// it is NaN / inf.
+// it is NaN / inf, or when the caller's skip word is set.
 //
 // The per-element arithmetic is torch's capturable _multi_tensor_adam (torch/optim/adam.py)
 // op by op in float32: g' = g + wd p; m = lerp(m, g', 1 - beta1); v = v beta2 + (1 - beta2)
@@ -30,6 +30,12 @@ __device__ __forceinline__ bool loss_finite(const float *loss) {
     return !(isnan(l) || isinf(l));
 }
 
+// The step writes nothing when the loss is not finite or the caller's skip word is set (a
+// graphed epoch's sticky NaN flag: no update after a failed step).
+__device__ __forceinline__ bool skip_step(const float *loss, const int32_t *skip) {
+    return (loss && !loss_finite(loss)) || (skip && *skip != 0);
+}
+
 __device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v, float wd, float w1, float b2,
                                           float w2, float bc2s, float eps, float step_size) {
     const float gd = g + wd * p;
@@ -47,8 +53,8 @@ __device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v,
 __global__ void __launch_bounds__(256) adam_kernel(float *__restrict__ p, const float *__restrict__ g,
                                                    float *__restrict__ m, float *__restrict__ v, int64_t n,
                                                    const float *__restrict__ step, const float *__restrict__ loss,
-                                                   AdamScalars s) {
-    if (loss && !loss_finite(loss)) return;
+                                                   const int32_t *__restrict__ skip, AdamScalars s) {
+    if (skip_step(loss, skip)) return;
     const float t = *step + 1.f;
     float bc1 = powf(s.beta1, t), bc2 = powf(s.beta2, t);
     bc1 = bc1 - 1.f;
@@ -79,8 +85,8 @@ __global__ void __launch_bounds__(256) adam_kernel(float *__restrict__ p, const 
         adam_elem(p[i], g[i], m[i], v[i], s.wd, s.one_m_beta1, s.beta2, s.one_m_beta2, bc2s, s.eps, step_size);
 }
 
-__global__ void adam_count_kernel(float *step, const float *loss) {
-    if (loss && !loss_finite(loss)) return;
+__global__ void adam_count_kernel(float *step, const float *loss, const int32_t *skip) {
+    if (skip_step(loss, skip)) return;
     *step = *step + 1.f;
 }
 
@@ -89,7 +95,7 @@ __global__ void adam_count_kernel(float *step, const float *loss) {
 using namespace fs;
 
 hipError_t fs_adam_step_impl(float *p, const float *g, float *m, float *v, int64_t n, float *step, const float *loss,
-                             double lr, double beta1, double beta2, double eps, double weight_decay, hipStream_t st) {
+                             const int32_t *skip, double lr, double beta1, double beta2, double eps, double weight_decay, hipStream_t st) {
     if (n < 0) return hipErrorInvalidValue;
     // 16-byte aligned buffers (the flat torch buffers are): the vector loop reads 4 at a time
     if ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) != 0) return hipErrorInvalidValue;
@@ -101,9 +107,9 @@ hipError_t fs_adam_step_impl(float *p, const float *g, float *m, float *v, int64
         if (blocks > 4096) blocks = 4096;  // grid-stride beyond ~16 workgroups per CU
         if (blocks < 1) blocks = 1;
         hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, g, m, v, n, (const float *)step,
-                           loss, s);
+                           loss, skip, s);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(adam_count_kernel, dim3(1), dim3(1), 0, st, step, loss);
+    hipLaunchKernelGGL(adam_count_kernel, dim3(1), dim3(1), 0, st, step, loss, skip);
     return hipGetLastError();
 }

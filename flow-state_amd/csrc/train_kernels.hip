@@ -361,11 +361,12 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_ex2_kernel(GemmArgs g0, BnIn 
 // running buffers rm / rv [nbn][H], counters nbt [nbn]) the momentum updates of `passes`
 // passes in pass order, from stats [passes][nbn][2][H] (batch mean, biased variance;
 // rows of the pass), exactly as the in-launch update computes them; nbt += passes.
+// Nothing is written when the skip word (nullable) is set.
 __global__ void __launch_bounds__(256) bn_running_update_kernel(int nbn, int H, float *rm, float *rv, int64_t *nbt,
                                                                 const float *stats, int passes, int64_t rows0,
-                                                                int64_t rows1, float m) {
+                                                                int64_t rows1, float m, const int32_t *skip) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)nbn * H) return;
+    if (i >= (int64_t)nbn * H || (skip && *skip != 0)) return;
     const int64_t bnx = i / H, h = i - bnx * H;
     float a = rm[i], v = rv[i];
     for (int p = 0; p < passes; ++p) {
@@ -822,11 +823,12 @@ hipError_t fs_linear_ex2_impl(const GemmArgs &g0, const BnIn *b0, const GemmArgs
 }
 
 hipError_t fs_bn_running_update_impl(int nbn, int H, float *rm, float *rv, int64_t *nbt, const float *stats,
-                                     int passes, int64_t rows0, int64_t rows1, float momentum, hipStream_t st) {
+                                     int passes, int64_t rows0, int64_t rows1, float momentum, const int32_t *skip,
+                                     hipStream_t st) {
     if (nbn <= 0 || H <= 0 || passes <= 0) return hipSuccess;
     const int64_t n = (int64_t)nbn * H;
     hipLaunchKernelGGL(bn_running_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nbn, H, rm, rv,
-                       nbt, stats, passes, rows0, rows1, momentum);
+                       nbt, stats, passes, rows0, rows1, momentum, skip);
     return hipGetLastError();
 }
 

@@ -113,7 +113,7 @@ _SIGS = {
                                          ctypes.POINTER(BnIn), _P, _P]),
     "fs_linear_f32_group": (ctypes.c_int, [ctypes.POINTER(ctypes.POINTER(GemmF32)), ctypes.c_int32, _P, _I64, _P]),
     "fs_bn_running_update": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, ctypes.c_int32, _I64, _I64,
-                                            ctypes.c_double, _P]),
+                                            ctypes.c_double, _P, _P]),
     "fs_bn_relu_train_fwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 6 + [ctypes.c_double, ctypes.c_double]
                              + [_P] * 4),
     "fs_bn_relu_train_bwd": (ctypes.c_int, [_I64, ctypes.c_int32] + [_P] * 11),
@@ -128,7 +128,7 @@ _SIGS = {
     "fs_coupling_pair_step": (ctypes.c_int, [_CP] + [_P] * 6 + [_CP] + [_P] * 6 + [_CP] + [_P] * 8 + [_CP, _P, _P]),
     "fs_coupling_pair_post": (ctypes.c_int, [_CP] + [_P] * 6 + [_CP] + [_P] * 9),
     "fs_set_wide_rows": (_I64, [_I64]),
-    "fs_adam_step": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P] + [ctypes.c_double] * 5 + [_P]),
+    "fs_adam_step": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P, _P] + [ctypes.c_double] * 5 + [_P]),
     "fs_target_energy": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_int32]
                          + [ctypes.c_double] * 4 + [_P, _P, _P]),
     "fs_classify_wells": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double,

@@ -133,10 +133,13 @@ class Algorithm2:
             if tail:
                 self._step.add_batch_size(tail)  # cumulative training sets change the tail
             self._step.reset_optimizer()
+            self._step.reset_nan()
             # the epoch's batches gathered once (one index upload, one gather) and the
             # steps replayed back to back: no host synchronisation until the epoch's end,
             # where the spline NaN flags of all steps are checked together (the reference
-            # raises inside the failing step; here the epoch's later steps have run by then)
+            # raises inside the failing step; here the later steps have replayed by then,
+            # but the sticky NaN word kept them from writing: parameters, Adam state and
+            # BatchNorm statistics are those after the last good step, train.py)
             shuffled = data[torch.cat(batches).to(data.device)] if batches else data[:0]
             flags, off = [], 0
             for b in batches:

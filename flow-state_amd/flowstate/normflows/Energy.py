@@ -90,7 +90,9 @@ class _TargetEnergy(torch.autograd.Function):
         return E
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gE):
+        # dE/dx is a saved constant: a second derivative raises instead of returning zeros
         (g,) = ctx.saved_tensors
         return gE[:, None].to(g.dtype) * g, None
 

@@ -82,6 +82,11 @@ def rational_quadratic_spline(x, uw, uh, ud, inverse, left, right, bottom, top):
 
 _nan_flags = []
 _defer_nan = False  # set while a training step is captured in a graph (train.py)
+# While a training step is captured (train.py): the graph's sticky NaN word (int32 [1] on the
+# device, never cleared inside the graph).  The shared-launch sampling pass ORs its spline
+# flags straight into it and the deferred running-statistics update skips on it, so a step
+# after (and including) the first NaN writes no BatchNorm statistics.
+_sticky_nan = None
 
 
 def reduce_nan_flags(device):
@@ -1055,12 +1060,17 @@ class FlatBatchNorm:
                    bn.running_var.data_ptr() == self.rv[i].data_ptr() and
                    bn.num_batches_tracked.data_ptr() == self.nbt[i].data_ptr() for i, bn in enumerate(self.bns))
 
-    def update(self, stats, rows0, rows1):
+    def update(self, stats, rows0, rows1, skip=None):
+        """skip (int32 [1] device word, nullable): nothing is written when it is non-zero."""
         from .. import _lib
 
         _lib.check(_lib.load().fs_bn_running_update(len(self.bns), self.H, _lib.ptr(self.rm), _lib.ptr(self.rv),
                                                     _lib.ptr(self.nbt), _lib.ptr(stats), 2, int(rows0), int(rows1),
-                                                    self.momentum, _lib.stream_ptr()), "fs_bn_running_update")
+                                                    self.momentum, _lib.ptr(skip), _lib.stream_ptr()),
+                   "fs_bn_running_update")
+
+    def buffers(self):
+        return [self.rm, self.rv, self.nbt]
 
 
 class _SamplingRider:
@@ -1071,7 +1081,8 @@ class _SamplingRider:
     def __init__(self, z, flat_bn):
         self.z = z.contiguous()
         self.lq = None
-        self.nan_flag = torch.zeros(1, dtype=torch.int32, device=z.device)
+        # inside a captured training step: the graph's sticky word (train.py), never cleared
+        self.nan_flag = _sticky_nan if _sticky_nan is not None else torch.zeros(1, dtype=torch.int32, device=z.device)
         self.fbn = flat_bn
         # [pass][BatchNorm][mean | biased variance][H]; pass 0 sampling, 1 density
         self.bnstats = torch.empty((2, len(flat_bn.bns), 2, flat_bn.H), dtype=torch.float32, device=z.device)
@@ -1199,6 +1210,9 @@ class _SamplingRider:
             self._launch_post(q)
 
 
+_last_paired = False  # set by paired_kld (train.py reads it after a warm-up step)
+
+
 def paired_ok(model, x, z, flat_bn):
     """The shared-launch passes apply: device f32 rows, every layer on the fused coupling
     kernels with the BatchNorm-in-load conditioner, one layer shape throughout, the flat
@@ -1244,7 +1258,11 @@ def paired_kld(model, x, z, flat_bn):
         finally:
             _direct_grads = False
         rider.flush()
-        flat_bn.update(rider.bnstats, z.shape[0], x.shape[0])
+        # the sampling pass's spline flags are in the sticky word already when captured:
+        # the failing step and every later one leave the running statistics alone
+        flat_bn.update(rider.bnstats, z.shape[0], x.shape[0], skip=_sticky_nan)
+    global _last_paired
+    _last_paired = True
     _nan_flags.append(rider.nan_flag[0] != 0)
     check_nan_flags()
     return -torch.mean(log_q), rider.z, rider.lq

@@ -23,7 +23,14 @@ torch.cuda.graph (fused spline kernels and HIP GEMMs included) and replays it:
     finite.  Options it does not cover (amsgrad, maximize, tensor lr) keep torch's
     capturable Adam with a device-side snapshot / restore around it;
   * the spline's NaN-discriminant flags are reduced inside the graph and checked after
-    the replay (the reference raises ValueError; here it is raised after the step).
+    the replay (the reference raises ValueError; here it is raised after the step).  They
+    are also ORed into a sticky device word that Adam and the BatchNorm running-statistics
+    update skip on, so when an epoch replays its steps back to back and checks the flags
+    only at its end (Algorithm2.train), the failing step and every later one write no
+    parameters, moments or running statistics: the state is the one after the last good
+    step.  (The reference stops inside the failing step's sampling pass, after that pass
+    has updated the running statistics of the layers up to the failing one; here that
+    step's updates are dropped as a whole.)
 """
 import inspect
 
@@ -97,6 +104,8 @@ class GraphedTrainStep:
         # BatchNorm running buffers re-homed flat: the step's two passes share launches
         # (step_loss, autograd_flow.paired_kld); None keeps them separate
         self.flat_bn = AF.FlatBatchNorm.try_build(model) if paired else None
+        # sticky spline-NaN word of the replays since the last reset_nan() (see the module doc)
+        self._sticky = torch.zeros(1, dtype=torch.int32, device=dev)
         model.train()
         self.graphs = {}
         for bs in [self.batch_size] + [int(b) for b in extra_batch_sizes if int(b) != self.batch_size]:
@@ -115,10 +124,17 @@ class GraphedTrainStep:
         saved_opt = [v.detach().clone() for v in self._opt_tensors()] if self.opt.state else None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
+        AF._last_paired = False
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._eager_step(x)
         torch.cuda.current_stream().wait_stream(s)
+        # the shared-launch passes skip their deferred running-statistics update on the
+        # sticky word themselves; any other path updates the BatchNorm buffers inside the
+        # forward, so the graph snapshots them and puts them back after a NaN step
+        paired = AF._last_paired and warmup > 0
+        bn_bufs = [] if paired else self._bn_buffers()
+        bn_backup = [b.detach().clone() for b in bn_bufs]
         with torch.no_grad():
             for t, v in zip(list(model.parameters()) + list(model.buffers()), saved):
                 t.copy_(v)
@@ -139,26 +155,53 @@ class GraphedTrainStep:
         graph = torch.cuda.CUDAGraph()
         self._zero_grad()
         AF._defer_nan = True
+        AF._sticky_nan = self._sticky
         try:
             with torch.cuda.graph(graph):  # own pool: graphs replay in any order
+                with torch.no_grad():
+                    for b, t in zip(bn_backup, bn_bufs):
+                        b.copy_(t)
                 self._zero_grad()
                 loss = step_loss(model, x, self.batch_size, self.alpha, self.flat_bn)
                 loss.backward()
                 self._gather_grads()
+                nan_flag = AF.reduce_nan_flags(dev)
+                with torch.no_grad():
+                    self._sticky.bitwise_or_(nan_flag.to(torch.int32))
                 if self._fused_adam_ok():
-                    self._adam_step(loss.detach())  # skips itself on a non-finite loss
+                    # skips itself on a non-finite loss or a set sticky word
+                    self._adam_step(loss.detach(), skip=self._sticky)
                 else:
-                    finite = ~(torch.isnan(loss) | torch.isinf(loss))
+                    keep = ~(torch.isnan(loss) | torch.isinf(loss)) & (self._sticky[0] == 0)
                     for b, t in zip(self._backup, self._state_tensors):
                         b.copy_(t.detach())
                     self.opt.step()
                     with torch.no_grad():
                         for b, t in zip(self._backup, self._state_tensors):
-                            t.copy_(torch.where(finite, t, b))
-                nan_flag = AF.reduce_nan_flags(dev)
+                            t.copy_(torch.where(keep, t, b))
+                with torch.no_grad():
+                    failed = self._sticky[0] != 0
+                    for b, t in zip(bn_backup, bn_bufs):
+                        t.copy_(torch.where(failed, b, t))
         finally:
             AF._defer_nan = False
+            AF._sticky_nan = None
         return _Captured(graph, x, loss.detach(), nan_flag)  # keep no autograd graph alive
+
+    def _bn_buffers(self):
+        """The running-statistics buffers a training step updates."""
+        if self.flat_bn is not None and self.flat_bn.intact():
+            return self.flat_bn.buffers()
+        return [t for m in self.model.modules() if isinstance(m, torch.nn.BatchNorm1d)
+                for t in (m.running_mean, m.running_var, m.num_batches_tracked) if t is not None]
+
+    def reset_nan(self):
+        """Clear the sticky spline-NaN word (an epoch starts with it clear)."""
+        self._sticky.zero_()
+
+    def nan_state(self):
+        """The sticky word as a device bool: some replay since reset_nan() hit a NaN."""
+        return self._sticky[0] != 0
 
     def _fused_adam_ok(self):
         """fs_adam_step covers the reference's Adam: flat buffers, float lr, L2 weight decay,
@@ -168,14 +211,20 @@ class GraphedTrainStep:
         g = self.opt.param_groups[0]
         st = self.opt.state.get(self._flat_param, {})
         step = st.get("step")
-        return (not g.get("amsgrad") and not g.get("maximize") and not g.get("differentiable")
-                and not g.get("decoupled_weight_decay") and not torch.is_tensor(g["lr"])
-                and not any(torch.is_tensor(b) for b in g["betas"]) and torch.is_tensor(step)
-                and step.is_cuda and step.dtype == torch.float32 and "exp_avg" in st and "exp_avg_sq" in st)
+        if (g.get("amsgrad") or g.get("maximize") or g.get("differentiable") or g.get("decoupled_weight_decay")
+                or torch.is_tensor(g["lr"]) or any(torch.is_tensor(b) for b in g["betas"])):
+            return False
+        # fs_adam_step's preconditions (capi.cpp); lr = 0 etc. keep torch's Adam
+        b1, b2 = g["betas"]
+        if not (g["lr"] > 0 and 0 <= b1 < 1 and 0 <= b2 < 1 and g["eps"] >= 0 and g["weight_decay"] >= 0):
+            return False
+        return (torch.is_tensor(step) and step.is_cuda and step.dtype == torch.float32 and "exp_avg" in st
+                and "exp_avg_sq" in st)
 
-    def _adam_step(self, loss=None):
+    def _adam_step(self, loss=None, skip=None):
         """One Adam step over the flat buffers (fs_adam_step); loss (device scalar,
-        nullable): nothing is written when it is NaN / inf."""
+        nullable): nothing is written when it is NaN / inf; skip (int32 [1], nullable):
+        nothing is written when it is non-zero."""
         from .. import _lib
 
         g = self.opt.param_groups[0]
@@ -186,7 +235,7 @@ class GraphedTrainStep:
             loss = loss.reshape(1).to(torch.float32).contiguous()
         _lib.check(_lib.load().fs_adam_step(p(self._flat_param), p(self._flat_grad), p(st["exp_avg"]),
                                             p(st["exp_avg_sq"]), self._flat_param.numel(), p(st["step"]),
-                                            p(loss), float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                            p(loss), p(skip), float(g["lr"]), float(b1), float(b2), float(g["eps"]),
                                             float(g["weight_decay"]), _lib.stream_ptr()), "fs_adam_step")
 
     def _opt_tensors(self):
@@ -207,11 +256,24 @@ class GraphedTrainStep:
         if getattr(self, "_flat_grad", None) is None:
             return
         base = self._flat_grad.data_ptr()
-        if all(p.grad is not None and p.grad.data_ptr() == base + 4 * o for p, o in zip(self.params, self._goffs)):
+        home = [p.grad is not None and p.grad.data_ptr() == base + 4 * o for p, o in zip(self.params, self._goffs)]
+        if all(home):
             return
-        gs = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=p.device)
-              for p in self.params]
-        torch.cat(gs, out=self._flat_grad)
+        if not any(home):
+            gs = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=p.device)
+                  for p in self.params]
+            torch.cat(gs, out=self._flat_grad)
+            return
+        # some gradients are their home slices already (torch.cat may not read its output):
+        # copy only the others
+        for p, o, h in zip(self.params, self._goffs, home):
+            if h:
+                continue
+            dst = self._flat_grad[o:o + p.numel()]
+            if p.grad is None:
+                dst.zero_()
+            else:
+                dst.copy_(p.grad.reshape(-1))
 
     @torch.no_grad()
     def _flatten(self):
@@ -288,11 +350,15 @@ class GraphedTrainStep:
         A batch size without a captured graph runs eagerly with the same optimizer.
         check=False: no host synchronisation for the spline's NaN flag; the step returns
         (loss, nan_flag) instead, both device tensors owned by the caller, and the caller
-        raises (an epoch checks all its steps' flags at once, Algorithm2.train)."""
+        raises (an epoch checks all its steps' flags at once, Algorithm2.train).  The
+        sticky word is not cleared then: after a NaN step every later replay writes nothing
+        until reset_nan()."""
         c = self.graphs.get(int(batch.shape[0]))
         if c is None:
             loss = self.eager_step(batch)
             return loss if check else (loss, torch.zeros((), dtype=torch.bool, device=loss.device))
+        if check:
+            self.reset_nan()  # a NaN of an earlier checked step has raised already
         c.x.copy_(batch)
         c.graph.replay()
         self.model.invalidate_packed()  # replayed writes do not bump tensor versions

@@ -286,11 +286,13 @@ int fs_target_energy(const float *x, int64_t B, int32_t N, double bound, double 
  * optimizer, main_algorithm_2.py:310,440) over n float32 parameters param [n] with their
  * gradient grad and moments exp_avg / exp_avg_sq [n], in torch's capturable multi-tensor
  * arithmetic; step [1] is the float32 step count (incremented).  loss (nullable) [1]: when
- * it is NaN or inf nothing is written (main_algorithm_2.py:324-326 skips the step).  All
+ * it is NaN or inf nothing is written (main_algorithm_2.py:324-326 skips the step); skip
+ * (nullable) [1]: when non-zero nothing is written either (a graphed epoch's sticky
+ * spline-NaN flag: no update after the step that raised, splines.py:176-183).  All
  * buffers 16-byte aligned. */
 int fs_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float *step,
-                 const float *loss, double lr, double beta1, double beta2, double eps, double weight_decay,
-                 void *stream);
+                 const float *loss, const int32_t *skip, double lr, double beta1, double beta2, double eps,
+                 double weight_decay, void *stream);
 
 /* unconstrained_rational_quadratic_spline, circular tails (NF/normflows/utils/
  * splines.py:16-222) for M independent elements: x [M], unnormalised widths /
@@ -372,10 +374,11 @@ int fs_linear_f32_ex2(const fs_gemm_f32 *g0, const fs_bn_in *bn0, float *stats0,
  * biased variance (fs_bn_in mean_out / var_out of launches that left running_mean NULL);
  * the passes' updates are applied in pass order (rows0 / rows1 = their batch sizes) and
  * num_batches += passes.  With passes = 2 this is the reference's order when pass 0 is
- * reverse_kld's sampling pass and pass 1 forward_kld's density pass. */
+ * reverse_kld's sampling pass and pass 1 forward_kld's density pass.  skip (nullable) [1]:
+ * when non-zero nothing is written (as fs_adam_step's). */
 int fs_bn_running_update(int32_t nbn, int32_t H, float *running_mean, float *running_var, int64_t *num_batches,
                          const float *stats, int32_t passes, int64_t rows0, int64_t rows1, double momentum,
-                         void *stream);
+                         const int32_t *skip, void *stream);
 
 /* Long reductions over few output tiles (K >= 2048, <= 128 tiles of 32 x 32, no rowsum:
  * the input gradient of the 2944-wide final layer, 256 x 128 over K = 2944): the reduction

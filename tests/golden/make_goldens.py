@@ -28,6 +28,11 @@ Fixtures:
                     only), on uniform rows and flow samples prepared as nf_big_move does
   box_trace.npz     reference SimulationBox.minimum_image / compute_distance(s) and
                     EnergyCalculator.calculate_particle_energy_virial outputs
+  train_a2.npz      one Algorithm-2 training step at config 5's own size (A2 flow L=23,
+                    H=128, 2 blocks, K=15, N=64, batch 256, ALPHA=1; weights by seed +
+                    checksum): losses, every parameter gradient's norm plus a few whole
+                    gradients, the BatchNorm running statistics after the step, and the
+                    Adam update (per-tensor norms plus a few whole tensors)
 """
 import contextlib
 import hashlib
@@ -795,6 +800,115 @@ def train_cycle_case(NF):
     print("train_cycle: ok", out["a10_losses"], out["a5_losses"])
 
 
+TRAIN_A2_FULL = ("flows.0.prqct.transform_net.initial_layer.weight",
+                 "flows.0.prqct.transform_net.final_layer.bias",
+                 "flows.0.prqct.unconditional_transform.unnormalized_heights",
+                 "flows.11.prqct.transform_net.blocks.0.batch_norm_layers.1.weight",
+                 "flows.11.prqct.transform_net.blocks.1.linear_layers.0.weight",
+                 "flows.22.prqct.transform_net.blocks.1.linear_layers.1.bias",
+                 "flows.22.prqct.transform_net.initial_layer.bias")
+
+
+def train_a2_case(NF):
+    """One step of the Algorithm-2 training loop (main_algorithm_2.py:437-452) at config
+    5's own size: the A2 flow (L=23, H=128, nb=2, K=15; main_algorithm_2.py:43-51,287-294)
+    at N=64 in train mode, seeded weights (oracle.flow.random_state_dict, seed 41, final
+    layers N(0, 0.05); only the checksum is stored), a fresh Adam (LR / WEIGHT_DECAY of
+    main_algorithm_2.py), one batch of 256 training rows, reverse_kld(256) with supplied
+    base draws (q0 patched, so the GPU replays the same z), loss = ALPHA * forward_kld +
+    (1 - ALPHA) * reverse_kld at ALPHA = 1 (core.py:88-142).  Stored: both losses, each
+    parameter gradient's norm (and a few whole gradients), every BatchNorm running
+    statistic after the step (both passes updated them, reverse_kld first), and the Adam
+    update p_after - p_before (norms, and the same few tensors whole).  The same step's
+    gradients by the reference model in float64 give the exact values the float32
+    gradients are measured against: per tensor |g32 - g64|, and g64 of the few tensors."""
+    from oracle import flow as OF
+    from oracle import physics as OP
+    N = 64
+    dims = OF.FlowDims(N=N, L=23, H=128, nb=2, K=15, B=OF.half_box(N))
+    sd = OF.random_state_dict(dims, seed=41, final_std=0.05)
+    B, bs = dims.B, 256
+    rng = np.random.default_rng(43)
+    # training rows as the driver feeds them (sampled box configurations - HALF_BOX): an
+    # FCC lattice with thermal jitter for half the batch, uniform rows for the other half
+    lat = OP.fcc_lattice(N)[None] + rng.normal(0, 0.35, (bs // 2, N, 2))
+    lat = np.mod(lat, 2 * B) - B
+    uni = (rng.random((bs - bs // 2, N, 2)) * 2 - 1) * B * 0.95
+    x = torch.from_numpy(np.concatenate([lat, uni]).reshape(bs, -1).astype(np.float32))
+    z0 = (torch.rand((bs, dims.D), generator=torch.Generator().manual_seed(44)) * 2 - 1) * B
+    real_zeros = torch.zeros
+
+    def zeros_cpu(*a, **k):
+        if k.get("device") == "cuda":
+            k["device"] = "cpu"
+        return real_zeros(*a, **k)
+
+    model = build_ref_model(NF, dims)
+    model.load_state_dict(sd, strict=True)
+    model.p = NF.Energy.DoubleWellLJ(dims.D, dims.N, 1.0, dims.B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+    model.q0.forward = lambda n: z0[:n].clone()
+    model.train()
+    names = [n for n, _ in model.named_parameters()]
+    before = {n: p.detach().clone() for n, p in model.named_parameters()}
+    out = {"x": x.numpy(), "z0": z0.numpy(), "seed": np.int64(41), "names": np.array(names),
+           "checksum": np.frombuffer(bytes.fromhex(sd_checksum(sd)), dtype=np.uint8)}
+    torch.zeros = zeros_cpu
+    try:
+        opt = torch.optim.Adam(model.parameters(), lr=0.000543510751759681, weight_decay=9.5857178422352e-05)
+        opt.zero_grad()
+        energy_loss, _ = model.reverse_kld(bs)
+        sample_loss = model.forward_kld(x)
+        loss = 1.0 * sample_loss + (1 - 1.0) * energy_loss
+        out["rkld"] = energy_loss.detach().numpy()
+        out["fkld"] = sample_loss.detach().numpy()
+        out["step_loss"] = loss.detach().numpy()
+        assert bool(~(torch.isnan(loss) | torch.isinf(loss)))
+        loss.backward()
+        gnorm, dnorm = [], []
+        for n, p in model.named_parameters():
+            g = p.grad
+            gnorm.append(float(g.double().norm()) if g is not None else -1.0)
+            if n in TRAIN_A2_FULL:
+                out["grad/" + n] = g.numpy().copy()
+        opt.step()
+        for n, p in model.named_parameters():
+            d = (p.detach() - before[n]).double()
+            dnorm.append(float(d.norm()))
+            if n in TRAIN_A2_FULL:
+                out["update/" + n] = (p.detach() - before[n]).numpy()
+        out["grad_norm"] = np.array(gnorm)
+        out["update_norm"] = np.array(dnorm)
+        for k, v in model.state_dict().items():
+            if "running" in k or "num_batches" in k:
+                out["bn/" + k] = v.numpy()
+        # the reference's own float32 error: the same step's gradients in float64
+        g32 = {n: p.grad.detach().double().clone() for n, p in model.named_parameters() if p.grad is not None}
+        m64 = build_ref_model(NF, dims)
+        m64.load_state_dict(sd, strict=True)
+        m64 = m64.double()
+        m64.p = NF.Energy.DoubleWellLJ(dims.D, dims.N, 1.0, dims.B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+        z64 = z0.double()
+        m64.q0.forward = lambda n: z64[:n].clone()
+        m64.train()
+        m64.reverse_kld(bs)  # its BatchNorm updates, as the float32 step (values unused)
+        l64 = m64.forward_kld(x.double())
+        l64.backward()
+        err = []
+        for n, p in m64.named_parameters():
+            if n in g32:
+                err.append(float((g32[n] - p.grad.detach()).norm()))
+                if n in TRAIN_A2_FULL:
+                    out["grad64/" + n] = p.grad.detach().numpy().copy()
+            else:
+                err.append(-1.0)
+        out["grad_err32_norm"] = np.array(err)
+        out["fkld64"] = l64.detach().numpy()
+    finally:
+        torch.zeros = real_zeros
+    np.savez_compressed(os.path.join(HERE, "train_a2.npz"), **out)
+    print("train_a2: ok", float(out["fkld"]), float(out["rkld"]), float(out["step_loss"]))
+
+
 def judge_case(NF, MC):
     """Reference judge_normalizing_flow / bulk_judge_normalizing_flow /
     metropolis_acceptance_particle_move (monte_carlo.py:191-223, 305-370) on a scripted
@@ -971,6 +1085,10 @@ def main(only=None):
         torch.set_num_threads(8)
         a1_case(NF)
         return
+    if only == "train_a2":
+        torch.set_num_threads(8)
+        train_a2_case(NF)
+        return
     flow_case(NF, "tiny", OF.FlowDims(N=4, L=2, H=32, nb=1, K=5, B=OF.half_box(4)), 1, 64, True)
     flow_case(NF, "n16", OF.FlowDims(N=16, L=3, H=64, nb=2, K=8, B=OF.half_box(16)), 2, 48, False)
     flow_case(NF, "n64", OF.FlowDims(N=64, L=2, H=128, nb=2, K=32, B=OF.half_box(64)), 3, 16, False)
@@ -989,6 +1107,7 @@ def main(only=None):
     target_energy_case(NF)
     torch.set_num_threads(8)
     a1_case(NF)
+    train_a2_case(NF)
 
 
 if __name__ == "__main__":

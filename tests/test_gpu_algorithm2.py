@@ -179,3 +179,70 @@ def test_config5_cycle_at_reference_sizes():
     want_nll = np.where(acc, -lq, nll_old)
     np.testing.assert_allclose(nll_after, want_nll, rtol=1e-5, atol=1e-4)
     assert p == acc.mean()
+
+
+def test_graphed_step_matches_reference_at_config5_size():
+    """The graphed HIP training step (GraphedTrainStep: shared-launch reverse_kld sampling
+    pass + forward_kld density pass, their backward, the deferred BatchNorm running
+    statistics, fs_adam_step) on config 5's own shapes (A2 flow, N=64, batch 256, ALPHA = 1)
+    against the reference's own step (tests/golden/train_a2.npz, made by importing the
+    reference): the loss, every parameter gradient, every running statistic, the Adam
+    update.  Tolerances: test_train_cpu.A2_TOL (written out there)."""
+    from flowstate.normflows import autograd_flow as AF
+    from flowstate.normflows.train import GraphedTrainStep
+    from test_train_cpu import A2_LR, A2_WD, build_a2, check_a2_step
+
+    m, f = build_a2("cuda")
+    before = {n: p.detach().clone() for n, p in m.named_parameters()}
+    step = GraphedTrainStep(m, 256, A2_LR, A2_WD, alpha=1.0)
+    assert step.flat_bn is not None and step._fused_adam_ok()
+    x = torch.from_numpy(f["x"]).cuda()
+    loss = step.step(x)
+    torch.cuda.synchronize()
+    assert AF._last_paired  # the shared-launch passes ran (captured after warm-up)
+    names = {id(p): n for n, p in m.named_parameters()}
+    grads = {names[id(p)]: step._flat_grad[o:o + p.numel()].view_as(p).clone()
+             for p, o in zip(step.params, step._goffs)}
+    check_a2_step(m, f, loss.item(), grads, before)
+
+
+def test_graphed_epoch_writes_nothing_after_a_nan_step():
+    """A graphed epoch checks the spline's NaN flags only at its end (Algorithm2.train).
+    The sticky NaN word stops every step from the failing one on: parameters, Adam state
+    and BatchNorm running statistics after an epoch whose 2nd of 4 steps hits a NaN
+    discriminant equal those after its 1st step, and the epoch raises the reference's
+    error (splines.py:176-183)."""
+    from flowstate.normflows.train import GraphedTrainStep
+    from test_train_cpu import A2_LR, A2_WD, build_a2
+
+    m, f = build_a2("cuda")
+    z0 = torch.from_numpy(f["z0"]).cuda()
+    zs = z0.clone()
+    m.q0.forward = lambda n: zs[:n].clone()
+    step = GraphedTrainStep(m, 256, A2_LR, A2_WD, alpha=1.0)
+    x = torch.from_numpy(f["x"]).cuda()
+    step.reset_nan()
+    loss, flag = step.step(x, check=False)
+    torch.cuda.synchronize()
+    assert not bool(flag)
+    after1 = [t.detach().clone() for t in step._state_tensors] + [b.clone() for b in step.flat_bn.buffers()]
+    # step 2: a NaN identity feature makes every conditioner output NaN, so the first
+    # layer's inverse splines of the finite transform features see NaN discriminants (a
+    # NaN input itself is outside the tail bound: identity, no error, as in the reference)
+    bad = z0.clone()
+    bad[:, 0] = float("nan")
+    flags = []
+    for i in range(3):
+        zs.copy_(bad if i == 0 else z0)
+        _, fl = step.step(x, check=False)
+        flags.append(fl)
+    torch.cuda.synchronize()
+    assert bool(flags[0]) and bool(step.nan_state())
+    now = [t.detach() for t in step._state_tensors] + step.flat_bn.buffers()
+    for a, b in zip(now, after1):
+        assert torch.equal(a, b)
+    # a checked step clears the word first and trains again
+    zs.copy_(z0)
+    step.step(x)
+    assert not bool(step.nan_state())
+    assert not torch.equal(step._state_tensors[0], after1[0])

@@ -153,7 +153,8 @@ def test_linear_group_launch_matches_single_launches():
 def test_fused_adam_matches_torch_capturable_adam(n):
     """fs_adam_step (csrc/optim_kernels.hip) against torch.optim.Adam(capturable=True) with
     L2 weight decay (main_algorithm_2.py:310) over several steps, including a step whose
-    loss is NaN (nothing written, the step count kept: main_algorithm_2.py:324-326)."""
+    loss is NaN (nothing written, the step count kept: main_algorithm_2.py:324-326) and one
+    whose skip word is set (a graphed epoch's sticky spline-NaN flag)."""
     from flowstate import _lib
 
     L, p = _lib.load(), _lib.ptr
@@ -167,14 +168,15 @@ def test_fused_adam_matches_torch_capturable_adam(n):
     for it in range(6):
         grad = torch.randn(n, device="cuda", generator=g) * (10.0 ** (it % 3 - 1))
         loss = torch.tensor([float("nan") if it == 3 else 1.0], device="cuda")
-        if it != 3:
+        skip = torch.tensor([1 if it == 4 else 0], dtype=torch.int32, device="cuda")
+        if it not in (3, 4):
             ref.grad = grad.clone()
             opt.step()
         before = (par.clone(), m.clone(), v.clone(), step.clone())
-        _lib.check(L.fs_adam_step(p(par), p(grad), p(m), p(v), n, p(step), p(loss), lr, betas[0], betas[1], eps, wd,
-                                  _lib.stream_ptr()))
+        _lib.check(L.fs_adam_step(p(par), p(grad), p(m), p(v), n, p(step), p(loss), p(skip), lr, betas[0], betas[1],
+                                  eps, wd, _lib.stream_ptr()))
         torch.cuda.synchronize()
-        if it == 3:
+        if it in (3, 4):
             for a, b in zip((par, m, v, step), before):
                 assert torch.equal(a, b)
             continue

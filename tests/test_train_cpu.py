@@ -124,3 +124,114 @@ def test_target_energy_restatement_matches_reference(N):
     E = mod._energy(x)
     (gx,) = torch.autograd.grad(E.sum(), x)
     check_target_energy(mod, f, N, x, E, gx)
+
+
+# --- one training step at config 5's own size (tests/golden/train_a2.npz) -----------------
+A2_LR, A2_WD = 0.000543510751759681, 9.5857178422352e-05  # main_algorithm_2.py LR / WEIGHT_DECAY
+
+
+def build_a2(device):
+    """The golden's A2 flow (L=23, H=128, nb=2, K=15) at N=64 from its seed (checksum
+    checked), DoubleWellLJ target, q0 replaying the stored base draws, train mode."""
+    import hashlib
+
+    from flowstate.models import A2, flow_from_state_dict
+    from flowstate.normflows.Energy import DoubleWellLJ
+    from oracle import flow as OF
+
+    f = np.load(os.path.join(G, "train_a2.npz"))
+    N = 64
+    dims = OF.FlowDims(N=N, B=OF.half_box(N), **A2)
+    sd = OF.random_state_dict(dims, seed=int(f["seed"]), final_std=0.05)
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(sd[k].contiguous().numpy().tobytes())
+    assert h.digest() == f["checksum"].tobytes(), "weights differ from the golden's"
+    m = flow_from_state_dict(sd, N, bound=dims.B, device="cpu", **A2)
+    m.p = DoubleWellLJ(dims.D, N, 1.0, dims.B, V0_list=[-10.0, -10.5], r0=1.2, k=15)
+    m = m.to(device)
+    z0 = torch.from_numpy(f["z0"]).to(device)
+    m.q0.forward = lambda n: z0[:n].clone()
+    m.train()
+    return m, f
+
+
+# The float32 envelope of the comparison, measured rather than guessed: the golden holds
+# the same step's gradients by the reference model in float64 (the exact values), so each
+# gradient is held to a multiple of the REFERENCE'S OWN float32 error against them
+# (|g_ref32 - g64| is ~7e-4 of |g| at the median tensor and ~2e-3 on some BatchNorm
+# weights: 23 coupling layers of 256 rows).  This path sums in other orders (MFMA tiles on
+# the GPU), so it may not match the reference's rounding, only its accuracy.  The biases
+# in front of a train-mode BatchNorm have an exactly-zero true gradient (the batch mean
+# removes them); both sides compute rounding noise of ~1e-9 there, covered by grad_abs
+# (weight decay dominates their Adam update).
+A2_TOL = dict(loss_rtol=1e-5,           # the step's loss (forward_kld at ALPHA = 1) vs the reference's
+              grad_vs_f32_err=4.0,      # per tensor: |g - g64| <= 4 |g_ref32 - g64| + grad_abs (2-norm)
+              grad_max_vs_f32_err=4.0,  # whole tensors: max|g - g64| <= 4 max|g_ref32 - g64| + grad_abs
+              grad_abs=1e-7,
+              bn_rtol=1e-4, bn_atol=1e-6,  # running statistics after the step
+              update_rel=3e-2)          # Adam update: |d - d_ref| <= update_rel * |d_ref| per tensor
+
+
+def check_a2_step(m, f, loss, grads, before):
+    """loss (float), grads {name: tensor or None}, before {name: parameter before the step};
+    m holds the parameters and running statistics after the step."""
+    t = A2_TOL
+    np.testing.assert_allclose(loss, float(f["step_loss"]), rtol=t["loss_rtol"])
+    names = [str(n) for n in f["names"]]
+    params = dict(m.named_parameters())
+    assert names == list(params)
+    worst = 0.0
+    for n, gn, e32 in zip(names, f["grad_norm"], f["grad_err32_norm"]):
+        g = grads.get(n)
+        if gn < 0:  # no gradient in the reference (unused preprocessing weights)
+            assert g is None or not g.abs().max().item(), n
+            continue
+        # every tensor: its gradient norm within a multiple of the reference's own float32
+        # error (only g32's norm and |g32 - g64| are stored for all of them)
+        d32 = abs(float(g.double().norm()) - gn)
+        assert d32 <= t["grad_vs_f32_err"] * e32 + t["grad_abs"], (n, d32, e32)
+        if "grad/" + n in f:
+            g64 = torch.from_numpy(f["grad64/" + n]).double()
+            ref32 = torch.from_numpy(f["grad/" + n]).double()
+            gg = g.double().cpu()
+            e = float((gg - g64).norm())
+            e_ref = float((ref32 - g64).norm())
+            mx = float((gg - g64).abs().max())
+            mx_ref = float((ref32 - g64).abs().max())
+            assert e <= t["grad_vs_f32_err"] * e_ref + t["grad_abs"], (n, e, e_ref)
+            assert mx <= t["grad_max_vs_f32_err"] * mx_ref + t["grad_abs"], (n, mx, mx_ref)
+            worst = max(worst, e / max(e_ref, 1e-30))
+    print(f"A2 step: worst whole-tensor gradient error vs float64 = {worst:.2f} x the reference's float32 error")
+    for k, v in m.state_dict().items():
+        if "bn/" + k in f:
+            ref = f["bn/" + k]
+            if "num_batches" in k:
+                assert int(v) == int(ref), k
+            else:
+                np.testing.assert_allclose(v.cpu().numpy(), ref, rtol=t["bn_rtol"], atol=t["bn_atol"], err_msg=k)
+    for n, dn in zip(names, f["update_norm"]):
+        d = (params[n].detach() - before[n]).double()
+        assert float((d.norm() - dn).abs()) <= t["update_rel"] * dn + 1e-9, (n, float(d.norm()), dn)
+        if "update/" + n in f:
+            ref = torch.from_numpy(f["update/" + n]).double().to(d.device)
+            assert float((d - ref).norm()) <= t["update_rel"] * float(ref.norm()) + 1e-9, n
+
+
+def test_training_step_matches_reference_at_config5_size_cpu():
+    """One Algorithm-2 step at config 5's own size (A2, N=64, batch 256, ALPHA = 1) through
+    the host-side torch restatement (CPU tensors) against the reference's own step."""
+    torch.set_num_threads(8)
+    m, f = build_a2("cpu")
+    before = {n: p.detach().clone() for n, p in m.named_parameters()}
+    x = torch.from_numpy(f["x"])
+    opt = torch.optim.Adam(m.parameters(), lr=A2_LR, weight_decay=A2_WD)
+    opt.zero_grad()
+    energy_loss, _ = m.reverse_kld(256)
+    np.testing.assert_allclose(energy_loss.item(), float(f["rkld"]), rtol=1e-5)
+    loss = 1.0 * m.forward_kld(x) + 0.0 * energy_loss
+    loss.backward()
+    grads = {n: (p.grad.detach().clone() if p.grad is not None else None) for n, p in m.named_parameters()}
+    opt.step()
+    check_a2_step(m, f, loss.item(), grads, before)
