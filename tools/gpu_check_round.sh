@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-3 GPU check: the named tests first, then the whole GPU suite, smoke and the
+# GPU check of a round: the named tests first, then the whole GPU suite, smoke and the
 # driver's bench command; $1 = tag, $2 = "quick" to stop after the named tests
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

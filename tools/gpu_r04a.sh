@@ -5,6 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r04a}
 mkdir -p gpurun_out
+timeout -k 10 60 ./tools/probes/mfma_order > gpurun_out/${T}_mfma_order.log 2>&1; echo "mfma order rc=$?"; cat gpurun_out/${T}_mfma_order.log
 timeout -k 10 900 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_algorithm2.py \
   tests/test_gpu_train.py tests/test_gpu_train_graph.py tests/test_gpu_paired.py \
   "tests/test_gpu_flow.py::test_a1_flow_samples_closer_to_float64_than_reference_f32" -s > gpurun_out/${T}_pytest.log 2>&1
