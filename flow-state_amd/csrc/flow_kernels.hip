@@ -882,6 +882,150 @@ __global__ void __launch_bounds__(64 * (H / 32)) wide_trunk_kernel(WideArgs w) {
     for (int i = 0; i < 16; ++i) w.XB[(rowt + acc_row(0, i, h)) * XS + col] = hr[0][0][i] + sh;
 }
 
+// The same trunk on 16-row tiles, so that a batch fills twice as many CUs (4096 rows: 256
+// workgroups instead of 128).  v_mfma_f32_16x16x4_f32 is the same exact fmaf chain as
+// v_mfma_f32_32x32x2_f32 (tools/probes/mfma_order.hip: bit-identical on every output), so
+// feeding it the k order of the 32-row tiles keeps the results bit-identical: per 8-wide
+// k-group g the 32x32x2 chain takes k = 8g + (0, 4), (1, 5), (2, 6), (3, 7); here MFMA 0
+// takes the k-slots (0, 4, 1, 5) and MFMA 1 (2, 6, 3, 7), i.e. lane (q, r) of a 16x16x4
+// supplies k = 8g + 4 (q & 1) + (q >> 1) and then + 2.  Its weight values are the 32-row
+// image's fragment: lane 32 (q & 1) + 16 c + r, elements (q >> 1) and 2 + (q >> 1), two
+// dword loads (c = this wave's 16-column half).  The activation pair is one ds_read_b64 of
+// a tile image whose quads are stored as columns (0, 2, 1, 3), bit 1 of the position
+// flipped in rows 8-15, at a row stride of 8 mod 64 dwords (no bank conflicts).
+__device__ __forceinline__ int t16_pos(int row, int col, int xs) {
+    const int p = (col & ~3) | ((col & 1) << 1) | ((col >> 1) & 1);
+    return row * xs + (p ^ (((row >> 3) & 1) << 1));
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 ldb_pair(__amdgpu_buffer_rsrc_t W, int voff, int soff) {
+    f32x2 v;
+    v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(W, voff, soff, 0));
+    v[1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(W, voff + 8, soff, 0));
+    return v;
+}
+
+// acc[c] (16 x 16, columns 32 tile + 16 c ..) = X[16 x 8 kg] . B[tile], ACC: onto acc
+template <int XS16, int PD, bool ACC>
+__device__ __forceinline__ void gemm16(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
+                                       int tile, f32x4 (&acc)[2]) {
+    const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15, h = lane >> 5, qo = q & 1;
+    if (!ACC)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[c][i] = 0.f;
+    const float *xa = X + r * XS16 + 4 * qo + ((2 * h) ^ (((r >> 3) & 1) << 1));
+    const int vb = (32 * qo + r) * 16 + 4 * h;  // + 256 c: the second 16-column half
+    const int fb = sec + tile * kg * 1024;
+    f32x2 rb[PD][2];
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+        if (s < kg)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) rb[s][c] = ldb_pair(W, vb + 256 * c, fb + s * 1024);
+    for (int g0 = 0; g0 < kg; g0 += PD) {
+#pragma unroll
+        for (int s = 0; s < PD; ++s) {
+            const int g = g0 + s;
+            if (g < kg) {
+                const f32x2 a = *(const f32x2 *)(xa + 8 * g);
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+                        acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], rb[s][c][m], acc[c], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                const int gn = g + PD;
+                if (gn < kg)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) rb[s][c] = ldb_pair(W, vb + 256 * c, fb + gn * 1024);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+}
+
+#ifndef FS_WIDE16_PD
+#define FS_WIDE16_PD 8
+#endif
+
+// wide_trunk_kernel on a 16-row tile: one wave per 32-column tile (two 16x16 halves), the
+// same GEMMs, epilogues (FS_EPI), deferred biases and residual stream, bit for bit
+template <int H>
+__global__ void __launch_bounds__(64 * (H / 32)) wide_trunk16_kernel(WideArgs w) {
+    constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;  // XA / XB row stride
+    constexpr int XS16 = XS + 4;                             // the LDS image's (== 8 mod 64)
+    static_assert(XS16 % 64 == 8, "trunk16 LDS row stride");
+    __shared__ __attribute__((aligned(16))) float X[16 * XS16];
+    const FlowArgs &a = w.a;
+    const int N = a.N;
+    const PackLayout PL = pack_layout(N, H, a.nb, a.K);
+    const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15;
+    const int tile = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t rowt = (int64_t)blockIdx.x * 16;
+    const int nq = 2 * PL.kg_in;  // 16-byte quads of the used feature columns
+    for (int e = threadIdx.x; e < 16 * nq; e += blockDim.x) {
+        const int rr = e / nq, qq = e - rr * nq;
+        const f32x4 v = *(const f32x4 *)(w.XA + (rowt + rr) * XS + 4 * qq);
+        f32x4 o;  // positions of columns (0, 1, 2, 3): (0, 2, 1, 3), bit 1 flipped in rows 8-15
+        if (rr < 8) {
+            o[0] = v[0]; o[1] = v[2]; o[2] = v[1]; o[3] = v[3];
+        } else {
+            o[0] = v[1]; o[1] = v[3]; o[2] = v[0]; o[3] = v[2];
+        }
+        *(f32x4 *)(X + rr * XS16 + 4 * qq) = o;
+    }
+    __syncthreads();
+    const float *P = a.packed + (int64_t)w.layer * PL.stride;
+    const float *V = P + PL.vec;
+    const __amdgpu_buffer_rsrc_t W =
+        __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
+    int col[2], pos[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        col[c] = 32 * tile + 16 * c + r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pos[c][i] = t16_pos(4 * q + i, col[c], XS16);
+    }
+    f32x4 hr[2], acc[2];
+    gemm16<XS16, FS_WIDE16_PD, false>(X, W, (int)(PL.win * 4), PL.kg_in, tile, hr);  // initial_layer
+    for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
+        const float *VB = V + PL.v_blocks + (int64_t)4 * H * jb;
+        float e0[2], e1[2], e2[2], e3[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            e0[c] = VB[col[c]];
+            e1[c] = VB[H + col[c]];
+            e2[c] = VB[2 * H + col[c]];
+            e3[c] = VB[3 * H + col[c]];
+        }
+        const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4);
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) X[pos[c][i]] = FS_EPI(hr[c][i], e0[c], e1[c]);
+        __syncthreads();
+        gemm16<XS16, FS_WIDE16_PD, false>(X, W, w0, PL.kg_h, tile, acc);
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) X[pos[c][i]] = FS_EPI(acc[c][i], e2[c], e3[c]);
+        __syncthreads();
+        gemm16<XS16, FS_WIDE16_PD, true>(X, W, w0 + (int)(PL.block_stride * 2), PL.kg_h, tile, hr);  // h += Lin1(t)
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const float sh = V[col[c]];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w.XB[(rowt + 4 * q + i) * XS + col[c]] = hr[c][i] + sh;
+    }
+}
+
 // One feature of uncond_spline_w: the same arithmetic, its log-det returned (0 outside).
 template <int K, bool INV>
 __device__ __forceinline__ float uncond_one(const float *__restrict__ U, float *CO, int cs, int D, int off,
@@ -1282,6 +1426,20 @@ static void *wide_workspace(size_t bytes, hipStream_t st) {
 
 constexpr int64_t kWideMaxRows = 65536;  // the workspace never grows beyond this many rows
 
+// the trunk on 16-row tiles (wide_trunk16_kernel, default) or 32-row ones (FS_WIDE_TRUNK16=0,
+// fs_set_wide_trunk16); bit-identical either way
+static std::atomic<int> g_trunk16{-1};
+static bool wide_trunk16() {
+    int v = g_trunk16.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char *e = getenv("FS_WIDE_TRUNK16");
+        int expect = -1;
+        g_trunk16.compare_exchange_strong(expect, (e && e[0] == '0') ? 0 : 1);
+        v = g_trunk16.load(std::memory_order_relaxed);
+    }
+    return v != 0;
+}
+
 static size_t wide_bytes(int64_t R, int N, int H) {
     const int64_t XS = flow_xw(H) + 4;
     return (size_t)(rup(R * 2 * N * 4, 256) + 2 * rup(R * XS * 4, 256) + rup(R * kWaves * 4, 256) +
@@ -1462,7 +1620,10 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
             add((const void *)wide_start_kernel<H, K, MODE>, dim3(nblk), dim3(kThreads), 0);
         else
             add((const void *)wide_start_s_kernel<H, K, MODE>, dim3(nblk, kWaves), dim3(kThreads), 0);
-        add((const void *)wide_trunk_kernel<H>, dim3((unsigned)(R / 32)), dim3(64 * (H / 32)), 0);
+        if (wide_trunk16())
+            add((const void *)wide_trunk16_kernel<H>, dim3((unsigned)(R / 16)), dim3(64 * (H / 32)), 0);
+        else
+            add((const void *)wide_trunk_kernel<H>, dim3((unsigned)(R / 32)), dim3(64 * (H / 32)), 0);
         add((const void *)wide_final_kernel<H, K, MODE, WPW>, dim3(nblk, (units + WPW - 1) / WPW), dim3(64 * WPW),
             fin_lds);
         if (MODE == MODE_DENSITY) w.off = (w.off + N) % D;
@@ -1488,6 +1649,12 @@ static hipError_t wide_pass_mode(const FlowArgs &a, int N, int H, int K, hipStre
 }  // namespace fs
 
 using namespace fs;
+
+int32_t fs_set_wide_trunk16_impl(int32_t on) {
+    const int32_t prev = wide_trunk16() ? 1 : 0;
+    if (on >= 0) g_trunk16.store(on ? 1 : 0, std::memory_order_relaxed);
+    return prev;
+}
 
 int64_t fs_set_wide_rows_impl(int64_t rows) {
     const int64_t prev = wide_rows_limit();

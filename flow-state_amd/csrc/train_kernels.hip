@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <atomic>
 
 #include "fs_internal.h"
 
@@ -354,6 +357,331 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_ex2_kernel(GemmArgs g0, BnIn 
         gemm_tile<SPLIT, true, true, true, kBnPF>(g, bx, by, L, &bl, [&] { bn_prologue<64 * SPLIT>(g, bn, bx == 0 && by == 0, S); });
     } else {
         gemm_tile<SPLIT, true, true, false, kBnPF>(g, bx, by, L);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Lean forward products.  nn.Linear's forward at the training shapes (A = x row-major
+// [M][K], B = W row-major [N][K], K a multiple of 64 up to 256, N a multiple of 32) is
+// every product of gemm_ex2_kernel / gemm_bn_f32_kernel and the contiguous ones of
+// gemm_f32_kernel.  Those generic kernels carry 64-bit strided addressing, bounds tests per
+// element and, for two problems per launch, more kernel arguments than SGPRs (spilled to
+// VGPR lanes): 5.5 k instructions for gemm_ex2_kernel, a few thousand executed per wave
+// around its 8 MFMAs.  gemm_lin_kernel computes the same tile with the same k order,
+// partial-sum order, BatchNorm-in-load and epilogue arithmetic (bit-identical results,
+// tests/test_gpu_train_fused.py), with 32-bit buffer offsets (rows past M read as zero
+// through the buffer descriptor's range) and each problem's arguments read only by the
+// workgroups that compute it.
+struct LinP {
+    const float *A, *W, *bias, *R;
+    float *C, *stats;
+    int M, N, ldr, ldc;
+};
+struct LinBn {
+    const float *st, *gamma, *beta;
+    float *mean_out, *invstd_out, *var_out, *a_out, *rm, *rv;
+    int64_t *nbt;
+    float eps, momentum;
+    int tiles, on;
+};
+struct Lin2 {
+    LinP p[2];
+    LinBn b[2];
+    unsigned t0, mt0, mt1;
+};
+struct LinLds {
+    t16 part[7][64];
+    BnLds S;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t lin_rsrc(const float *p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)p, (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ t4 lin_ld(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_bit_cast(t4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// bn_prologue's arithmetic (column k = thread k, Chan's update over the producer's tiles
+// in order, biased variance, invstd; the lead workgroup's outputs and running statistics)
+template <int K>
+__device__ __forceinline__ void lin_bn_prologue(const LinBn &bn, int rows, bool lead, BnLds &S) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const int k = threadIdx.x;
+    if (k < K) {
+        const float gk = bn.gamma[k], bk = bn.beta[k];
+        float n = 0.f, mean = 0.f, m2 = 0.f;
+        for (int t0 = 0; t0 < bn.tiles; t0 += kBnStTiles) {
+            const int nt = bn.tiles - t0 < kBnStTiles ? bn.tiles - t0 : kBnStTiles;
+            const f2 *src = (const f2 *)bn.st + t0 * K + k;
+            f2 v[kBnStTiles];
+#pragma unroll
+            for (int t = 0; t < kBnStTiles; ++t) v[t] = t < nt ? src[t * K] : f2{0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < kBnStTiles; ++t) {
+                if (t < nt) {
+                    const int row0 = 32 * (t0 + t);
+                    const float nb = (float)(rows - row0 < 32 ? rows - row0 : 32);
+                    const float nn = n + nb, d = v[t][0] - mean;
+                    mean = mean + d * (nb / nn);
+                    m2 = m2 + v[t][1] + d * d * (n * nb / nn);
+                    n = nn;
+                }
+            }
+        }
+        const float var = m2 / (float)rows;
+        const float invstd = 1.f / sqrtf(var + bn.eps);
+        S.mu[k] = mean;
+        S.is[k] = invstd;
+        S.gm[k] = gk;
+        S.bt[k] = bk;
+        if (lead) {
+            if (bn.mean_out) bn.mean_out[k] = mean;
+            if (bn.invstd_out) bn.invstd_out[k] = invstd;
+            if (bn.var_out) bn.var_out[k] = var;
+            if (bn.rm) {
+                bn.rm[k] = running_update(bn.rm[k], mean, bn.momentum);
+                bn.rv[k] = running_update(bn.rv[k], unbiased(var, rows), bn.momentum);
+            }
+        }
+    }
+    if (lead && threadIdx.x == 0 && bn.nbt) *bn.nbt += 1;
+    __syncthreads();
+}
+
+// One 32 x 32 tile (bx, by) of P by 8 waves: wave w reduces the k-blocks 8w + 64s
+template <int KBW>
+__device__ __forceinline__ void lin_tile(const LinP &P, const LinBn &bn, unsigned bx, unsigned by, LinLds &L) {
+    constexpr int K = 64 * KBW;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int M = P.M;
+    const int m = (int)bx * 32 + r, col = (int)by * 32 + r;
+    const bool aok = m < M;
+    const __amdgpu_buffer_rsrc_t Ar = lin_rsrc(P.A, M * K * 4), Wr = lin_rsrc(P.W, P.N * K * 4);
+    const int kq = 8 * w + 4 * h;  // this lane's first k in each k-block
+    t4 a[KBW], b[KBW];
+#pragma unroll
+    for (int s = 0; s < KBW; ++s) {
+        a[s] = lin_ld(Ar, (m * K + kq + 64 * s) * 4);
+        b[s] = lin_ld(Wr, (col * K + kq + 64 * s) * 4);
+    }
+    float ep_bias = 0.f, ep_r[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ep_r[i] = 0.f;
+    if (w == 0) {
+        ep_bias = P.bias ? P.bias[col] : 0.f;
+        if (P.R) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int row = (int)bx * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+                if (row < M) ep_r[i] = P.R[row * P.ldr + col];
+            }
+        }
+    }
+    if (bn.on) {
+        lin_bn_prologue<K>(bn, M, bx == 0 && by == 0, L.S);
+        const int nt = P.N / 32;
+#pragma unroll
+        for (int s = 0; s < KBW; ++s) {
+            const int k0 = kq + 64 * s;
+            if (aok) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int k = k0 + j;
+                    const float o = L.S.gm[k] * ((a[s][j] - L.S.mu[k]) * L.S.is[k]) + L.S.bt[k];
+                    a[s][j] = o > 0.f ? o : 0.f;
+                }
+                if (bn.a_out && (k0 >> 5) % nt == (int)by) *(t4 *)(bn.a_out + m * K + k0) = a[s];
+            }
+        }
+    }
+    t16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KBW; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][j], b[s][j], acc, 0, 0, 0);
+    if (w > 0) L.part[w - 1][lane] = acc;
+    __syncthreads();
+    if (w > 0) return;
+#pragma unroll 1
+    for (int p = 0; p < 7; ++p) acc += L.part[p][lane];
+    const float bias = ep_bias;
+    float sv = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int row = (int)bx * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+        float v = acc[i] + bias;
+        if (row < M) {
+            if (P.R) v = v + ep_r[i];
+            P.C[row * P.ldc + col] = v;
+        }
+        acc[i] = v;
+        if (row < M) sv += v;
+    }
+    if (P.stats) {
+        const int nr = M - (int)bx * 32 < 32 ? M - (int)bx * 32 : 32;
+        const float mean = (sv + __shfl_xor(sv, 32)) / (float)nr;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = (int)bx * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+            const float d = acc[i] - mean;
+            if (row < M) q += d * d;
+        }
+        q += __shfl_xor(q, 32);
+        if (h == 0) {
+            P.stats[((int)bx * P.N + col) * 2] = mean;
+            P.stats[((int)bx * P.N + col) * 2 + 1] = q;
+        }
+    }
+}
+
+// workgroups [0, t0) compute problem 0 (column-major over its mt0 row tiles), the rest
+// problem 1; the branch is uniform, so each workgroup reads only its own problem's arguments
+template <int KBW>
+__global__ __launch_bounds__(512) void gemm_lin_kernel(Lin2 a) {
+    __shared__ LinLds L;
+    const unsigned b = blockIdx.x;
+    if (b < a.t0) {
+        lin_tile<KBW>(a.p[0], a.b[0], b % a.mt0, b / a.mt0, L);
+    } else {
+        const unsigned c = b - a.t0;
+        lin_tile<KBW>(a.p[1], a.b[1], c % a.mt1, c / a.mt1, L);
+    }
+}
+
+// Lean general products: any of the strided layouts gemm_tile takes (A[m][k] at
+// A[m sam + k sak], B[k][n] at B[k sbk + n sbn]; AK / BK: contiguous along k), with the
+// row sum, for K up to 512 at 8 waves per tile: nn.Linear's backward pair (the input
+// gradient dY W and the weight / bias gradient dY^T X) and the single products outside
+// the forward layout.  gemm_tile's k order, partial-sum order, row sum and epilogue (bit-
+// identical), with 32-bit buffer offsets: the descriptors' byte ranges are the operands'
+// extents, so every load past row M, column N or depth K reads zero and needs no test.
+struct LinG {
+    const float *A, *B, *bias, *R;
+    float *C, *stats, *rowsum;
+    int M, N, K, sam, sak, sbk, sbn, ldr, ldc, abytes, bbytes;
+};
+struct LinG2 {
+    LinG p[2];
+    unsigned t0, mt0, mt1;
+};
+struct LinGLds {
+    t16 part[7][64];
+    float rs_part[8][64];
+};
+
+template <bool CONTIG>
+__device__ __forceinline__ t4 ling_ld(__amdgpu_buffer_rsrc_t r, int base, int stride) {
+    if (CONTIG) return lin_ld(r, base * 4);
+    t4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (base + j * stride) * 4, 0, 0));
+    return v;
+}
+
+template <bool AK, bool BK, int KBMAX>
+__device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned by, LinGLds &L) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int M = P.M, N = P.N, K = P.K;
+    const int m = (int)bx * 32 + r, col = (int)by * 32 + r;
+    const bool rows = P.rowsum != nullptr && by == 0;
+    // rows past M / columns past N: an offset past the operand, read as zero
+    const int am = m < M ? m * P.sam : P.abytes / 4, bn = col < N ? col * P.sbn : P.bbytes / 4;
+    const __amdgpu_buffer_rsrc_t Ar = lin_rsrc(P.A, P.abytes), Br = lin_rsrc(P.B, P.bbytes);
+    t4 a[KBMAX], b[KBMAX];
+#pragma unroll
+    for (int s = 0; s < KBMAX; ++s) {
+        const int k = 8 * w + 64 * s + 4 * h;
+        if (8 * w + 64 * s < K) {  // wave-uniform
+            a[s] = k < K ? ling_ld<AK>(Ar, am + k * P.sak, P.sak) : t4{0.f, 0.f, 0.f, 0.f};
+            b[s] = k < K ? ling_ld<BK>(Br, bn + k * P.sbk, P.sbk) : t4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    float ep_bias = 0.f, ep_r[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ep_r[i] = 0.f;
+    if (w == 0 && col < N) {
+        ep_bias = P.bias ? P.bias[col] : 0.f;
+        if (P.R) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int row = (int)bx * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+                if (row < M) ep_r[i] = P.R[row * P.ldr + col];
+            }
+        }
+    }
+    t16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    float rs = 0.f;
+#pragma unroll
+    for (int s = 0; s < KBMAX; ++s) {
+        if (8 * w + 64 * s < K) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][j], b[s][j], acc, 0, 0, 0);
+            if (rows) rs += ((a[s][0] + a[s][1]) + a[s][2]) + a[s][3];
+        }
+    }
+    if (w > 0) L.part[w - 1][lane] = acc;
+    if (rows) L.rs_part[w][lane] = rs;
+    __syncthreads();
+    if (w > 0) return;
+#pragma unroll 1
+    for (int p = 0; p < 7; ++p) acc += L.part[p][lane];
+    if (rows) {
+#pragma unroll
+        for (int p = 1; p < 8; ++p) rs += L.rs_part[p][lane];
+        rs += __shfl_xor(rs, 32);
+        if (h == 0 && m < M) P.rowsum[m] = rs;
+    }
+    const bool bok = col < N;
+    const float bias = ep_bias;
+    float sv = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int row = (int)bx * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+        float v = acc[i] + bias;
+        if (row < M && bok) {
+            if (P.R) v = v + ep_r[i];
+            P.C[row * P.ldc + col] = v;
+        }
+        acc[i] = v;
+        if (row < M) sv += v;
+    }
+    if (P.stats) {
+        const int nr = M - (int)bx * 32 < 32 ? M - (int)bx * 32 : 32;
+        const float mean = (sv + __shfl_xor(sv, 32)) / (float)nr;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = (int)bx * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+            const float d = acc[i] - mean;
+            if (row < M) q += d * d;
+        }
+        q += __shfl_xor(q, 32);
+        if (h == 0 && bok) {
+            P.stats[((int)bx * N + col) * 2] = mean;
+            P.stats[((int)bx * N + col) * 2 + 1] = q;
+        }
+    }
+}
+
+// one product, or two (nn.Linear's backward pair: problem 0 the input gradient, A
+// contiguous along k; problem 1 the weight gradient, both strided), workgroups split at t0
+template <bool A0K, bool B0K, bool A1K, bool B1K, int KBMAX>
+__global__ __launch_bounds__(512) void gemm_ling_kernel(LinG2 a) {
+    __shared__ LinGLds L;
+    const unsigned b = blockIdx.x;
+    if (b < a.t0) {
+        ling_tile<A0K, B0K, KBMAX>(a.p[0], b % a.mt0, b / a.mt0, L);
+    } else {
+        const unsigned c = b - a.t0;
+        ling_tile<A1K, B1K, KBMAX>(a.p[1], c % a.mt1, c / a.mt1, L);
     }
 }
 
@@ -733,8 +1061,141 @@ hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_
     return hipSuccess;
 }
 
+// gemm_lin_kernel takes a product: nn.Linear's forward layout, K = 64, 128, 192 or 256, N a
+// multiple of 32, 16-byte aligned operands, no row sum, 32-bit offsets
+static bool lin_ok(const GemmArgs &g, const BnIn *bn) {
+    const int64_t lim = (int64_t)1 << 30;
+    return g.M > 0 && g.N > 0 && g.K > 0 && g.K % 64 == 0 && g.K <= 256 && g.N % 32 == 0 && g.sak == 1 &&
+           g.sam == g.K && g.sbk == 1 && g.sbn == g.K && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
+           !g.rowsum_a && g.M * g.K < lim && g.N * g.K < lim && g.M * g.ldc < lim && (!g.R || g.M * g.ldr < lim) &&
+           g.M <= 32LL * 65535 && (!bn || (bn->rows == g.M && (!bn->a_out || ((uintptr_t)bn->a_out & 15) == 0)));
+}
+
+static void lin_fill(LinP &p, LinBn &b, const GemmArgs &g, const BnIn *bn) {
+    p = LinP{g.A, g.B, g.bias, g.R, g.C, g.stats, (int)g.M, (int)g.N, (int)g.ldr, (int)g.ldc};
+    b = LinBn{};
+    if (bn)
+        b = LinBn{bn->stats, bn->gamma, bn->beta, bn->mean_out, bn->invstd_out, bn->var_out, bn->a_out,
+                  bn->running_mean, bn->running_var, bn->num_batches, bn->eps, bn->momentum, (int)bn->tiles, 1};
+}
+
+// the lean kernels (default) or the generic ones (FS_LEAN_GEMM=0, fs_set_lean_gemm)
+static std::atomic<int> g_lean{-1};
+static bool lean_gemm() {
+    int v = g_lean.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char *e = getenv("FS_LEAN_GEMM");
+        int expect = -1;
+        g_lean.compare_exchange_strong(expect, (e && e[0] == '0') ? 0 : 1);
+        v = g_lean.load(std::memory_order_relaxed);
+    }
+    return v != 0;
+}
+
+int32_t fs_set_lean_gemm_impl(int32_t on) {
+    const int32_t prev = lean_gemm() ? 1 : 0;
+    if (on >= 0) g_lean.store(on ? 1 : 0, std::memory_order_relaxed);
+    return prev;
+}
+
+static bool ak_of(const GemmArgs &g) { return g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0; }
+static bool bk_of(const GemmArgs &g) { return g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0; }
+
+// byte extent of a strided operand: the element past the last one addressed, (rows - 1)
+// strides along one dimension plus (depth - 1) along the other
+static int64_t extent_bytes(int64_t n0, int64_t s0, int64_t n1, int64_t s1) {
+    if (n0 <= 0 || n1 <= 0) return 0;
+    return ((n0 - 1) * s0 + (n1 - 1) * s1 + 1) * 4;
+}
+
+// gemm_ling_kernel takes a product: K <= 512 and a multiple of 4 (a lane's quad of k is
+// wholly inside or wholly past the reduction), non-negative strides, 32-bit offsets
+static bool ling_ok(const GemmArgs &g) {
+    const int64_t lim = (int64_t)1 << 30;
+    if (g.M <= 0 || g.K <= 0 || g.K > 512 || g.K % 4 != 0 || (g.N <= 0 && !g.rowsum_a) || g.N < 0) return false;
+    if (g.sam < 0 || g.sak < 0 || g.sbk < 0 || g.sbn < 0 || g.M > 32LL * 65535 || g.N > 32LL * 65535) return false;
+    const int64_t ab = extent_bytes(g.M, g.sam, g.K, g.sak), bb = extent_bytes(g.K, g.sbk, g.N, g.sbn);
+    return ab < lim && bb < lim && g.M * g.ldc < lim && (!g.R || g.M * g.ldr < lim) &&
+           g.M * g.sam < lim && g.K * g.sak < lim && g.K * g.sbk < lim && g.N * g.sbn < lim;
+}
+
+static LinG ling_fill(const GemmArgs &g) {
+    return LinG{g.A, g.B, g.bias, g.R, g.C, g.stats, g.rowsum_a, (int)g.M, (int)g.N, (int)g.K, (int)g.sam, (int)g.sak,
+                (int)g.sbk, (int)g.sbn, (int)g.ldr, (int)g.ldc, (int)extent_bytes(g.M, g.sam, g.K, g.sak),
+                (int)extent_bytes(g.K, g.sbk, g.N, g.sbn)};
+}
+
+// one or two products (g1 nullable; both ling_ok) in one gemm_ling_kernel launch: the
+// instantiated layouts are any single product and the backward pair (A0K, !B0K, !A1K, !B1K)
+static hipError_t ling_launch(const GemmArgs &g0, const GemmArgs *g1, hipStream_t st) {
+    LinG2 a{};
+    a.p[0] = ling_fill(g0);
+    a.mt0 = (unsigned)((g0.M + 31) / 32);
+    a.t0 = a.mt0 * (unsigned)(g0.N > 0 ? (g0.N + 31) / 32 : 1);
+    unsigned t1 = 0;
+    int kmax = (int)g0.K;
+    if (g1) {
+        a.p[1] = ling_fill(*g1);
+        a.mt1 = (unsigned)((g1->M + 31) / 32);
+        t1 = a.mt1 * (unsigned)(g1->N > 0 ? (g1->N + 31) / 32 : 1);
+        if (g1->K > kmax) kmax = (int)g1->K;
+    } else {
+        a.mt1 = 1;
+    }
+    const dim3 grid(a.t0 + t1), block(512);
+    const bool a0 = ak_of(g0), b0 = bk_of(g0);
+#define FS_LG(A0, B0, A1, B1)                                                                                    \
+    do {                                                                                                         \
+        if (kmax <= 128)                                                                                         \
+            hipLaunchKernelGGL((gemm_ling_kernel<A0, B0, A1, B1, 2>), grid, block, 0, st, a);                     \
+        else if (kmax <= 256)                                                                                    \
+            hipLaunchKernelGGL((gemm_ling_kernel<A0, B0, A1, B1, 4>), grid, block, 0, st, a);                     \
+        else                                                                                                     \
+            hipLaunchKernelGGL((gemm_ling_kernel<A0, B0, A1, B1, 8>), grid, block, 0, st, a);                     \
+        return hipGetLastError();                                                                                \
+    } while (0)
+    if (g1) {
+        if (a0 && !b0 && !ak_of(*g1) && !bk_of(*g1)) FS_LG(true, false, false, false);
+        return hipErrorNotSupported;
+    }
+    if (a0 && b0) FS_LG(true, true, true, true);
+    if (a0 && !b0) FS_LG(true, false, true, false);
+    if (!a0 && b0) FS_LG(false, true, false, true);
+    FS_LG(false, false, false, false);
+#undef FS_LG
+}
+
+// one or two products (g1 nullable) in one gemm_lin_kernel launch; both lin_ok, one K
+static hipError_t lin_launch(const GemmArgs &g0, const BnIn *b0, const GemmArgs *g1, const BnIn *b1, hipStream_t st) {
+    Lin2 a{};
+    lin_fill(a.p[0], a.b[0], g0, b0);
+    a.mt0 = (unsigned)((g0.M + 31) / 32);
+    a.t0 = a.mt0 * (unsigned)(g0.N / 32);
+    unsigned t1 = 0;
+    if (g1) {
+        lin_fill(a.p[1], a.b[1], *g1, b1);
+        a.mt1 = (unsigned)((g1->M + 31) / 32);
+        t1 = a.mt1 * (unsigned)(g1->N / 32);
+    } else {
+        a.mt1 = 1;
+    }
+    const dim3 grid(a.t0 + t1), block(512);
+    switch (g0.K) {
+        case 64: hipLaunchKernelGGL(gemm_lin_kernel<1>, grid, block, 0, st, a); break;
+        case 128: hipLaunchKernelGGL(gemm_lin_kernel<2>, grid, block, 0, st, a); break;
+        case 192: hipLaunchKernelGGL(gemm_lin_kernel<3>, grid, block, 0, st, a); break;
+        case 256: hipLaunchKernelGGL(gemm_lin_kernel<4>, grid, block, 0, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st) {
     if (g.M <= 0 || (g.N <= 0 && !g.rowsum_a)) return hipSuccess;
+    if (lean_gemm()) {
+        if (lin_ok(g, nullptr)) return lin_launch(g, nullptr, nullptr, nullptr, st);
+        if (ling_ok(g)) return ling_launch(g, nullptr, st);
+    }
     // one column tile even when N = 0, so that rowsum_a is still written
     const dim3 grid((unsigned)((g.M + 31) / 32), (unsigned)(g.N > 0 ? (g.N + 31) / 32 : 1));
     const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0;
@@ -762,6 +1223,8 @@ hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g
     const bool a1 = g1.sak == 1 && ((uintptr_t)g1.A & 15) == 0 && g1.sam % 4 == 0;
     const bool b1 = g1.sbk == 1 && ((uintptr_t)g1.B & 15) == 0 && g1.sbn % 4 == 0;
     const bool live0 = g0.M > 0 && g0.N > 0, live1 = g1.M > 0 && g1.N > 0;
+    if (lean_gemm() && live0 && live1 && ling_ok(g0) && ling_ok(g1) && a0 && !b0 && !a1 && !b1)
+        return ling_launch(g0, &g1, st);
     // the instantiated pair: nn.Linear's input gradient (dY W) and weight gradient (dY^T X)
     if (live0 && live1 && gemm_split(g0) == FS_GEMM_SPLIT && gemm_split(g1) == FS_GEMM_SPLIT && a0 && !b0 && !a1 &&
         !b1) {
@@ -783,6 +1246,7 @@ static bool bn_out_ok(const GemmArgs &g, const BnIn *bn) {
 hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipStream_t st) {
     if (!bn) return fs_linear_f32_impl(g, st);
     if (g.M <= 0 || g.N <= 0) return hipSuccess;
+    if (lean_gemm() && lin_ok(g, bn)) return lin_launch(g, bn, nullptr, nullptr, st);
     const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0;
     const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0;
     if (g.K > kBnMaxK || g.rowsum_a || !bn_out_ok(g, bn)) return hipErrorInvalidValue;
@@ -814,6 +1278,7 @@ bool fs_linear_ex2_ok(const GemmArgs &g0, const BnIn *b0, const GemmArgs &g1, co
 
 hipError_t fs_linear_ex2_impl(const GemmArgs &g0, const BnIn *b0, const GemmArgs &g1, const BnIn *b1, hipStream_t st) {
     if (!fs_linear_ex2_ok(g0, b0, g1, b1)) return hipErrorInvalidValue;
+    if (lean_gemm() && lin_ok(g0, b0) && lin_ok(g1, b1) && g0.K == g1.K) return lin_launch(g0, b0, &g1, b1, st);
     const unsigned mt0 = (unsigned)((g0.M + 31) / 32), mt1 = (unsigned)((g1.M + 31) / 32);
     const unsigned t0 = mt0 * (unsigned)((g0.N + 31) / 32), t1 = mt1 * (unsigned)((g1.N + 31) / 32);
     const BnIn none{};

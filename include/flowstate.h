@@ -268,6 +268,16 @@ int fs_nf_mh_step_banked(const fs_flow_dims *d, const void *packed, const fs_phy
  * previous limit.  Process-wide. */
 int64_t fs_set_wide_rows(int64_t rows);
 
+/* Kernel-variant switches for A/B measurements and bit-identity tests, process-wide; each
+ * returns the previous value (a negative argument only reads it).  The results do not
+ * depend on them.
+ * fs_set_wide_trunk16: 1 (default, or FS_WIDE_TRUNK16) = the wide path's ResidualNet on
+ *   16-row tiles (v_mfma_f32_16x16x4_f32, twice the workgroups), 0 = 32-row tiles.
+ * fs_set_lean_gemm: 1 (default, or FS_LEAN_GEMM) = the training products on the lean
+ *   kernels (32-bit buffer offsets), 0 = the generic strided kernels. */
+int32_t fs_set_wide_trunk16(int32_t on);
+int32_t fs_set_lean_gemm(int32_t on);
+
 /* ------------------------------------------------------------------ */
 /* Training (Algorithm 2): the circular RQS element-wise, with backward */
 /* ------------------------------------------------------------------ */

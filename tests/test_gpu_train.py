@@ -185,3 +185,105 @@ def test_fused_adam_matches_torch_capturable_adam(n):
         torch.testing.assert_close(m, st["exp_avg"], rtol=1e-6, atol=1e-9)
         torch.testing.assert_close(v, st["exp_avg_sq"], rtol=1e-6, atol=1e-12)
         torch.testing.assert_close(par, ref.detach(), rtol=1e-6, atol=1e-8)
+
+
+@pytest.mark.parametrize("M,K,N,bn,res", [(256, 128, 128, True, True), (232, 128, 128, True, False),
+                                          (256, 128, 2944, False, False), (100, 64, 96, False, True),
+                                          (256, 256, 128, True, False), (37, 192, 32, True, True)])
+def test_lean_forward_product_matches_generic_kernel(M, K, N, bn, res):
+    """nn.Linear's forward layout takes gemm_lin_kernel (32-bit buffer offsets, rows past M
+    read as zero); the generic gemm_bn_f32_kernel / gemm_f32_kernel take the same product
+    with W handed over transposed (strided along k), and with the lean kernels switched off
+    (fs_set_lean_gemm).  All must agree bit for bit: output, tile statistics,
+    u = relu(BN(x)) and the BatchNorm outputs.  Then fs_linear_f32_ex2 (two problems, one
+    launch) against the two products alone."""
+    from flowstate import _lib
+
+    L, p, st = _lib.load(), _lib.ptr, _lib.stream_ptr
+    g = torch.Generator().manual_seed(M + K + N)
+    x = torch.randn((M, K), generator=g).cuda()
+    w = (torch.randn((N, K), generator=g) * 0.1).cuda()
+    wt = w.t().contiguous()
+    b = torch.randn(N, generator=g).cuda()
+    r = torch.randn((M, N), generator=g).cuda() if res else None
+    gam, bet = (torch.rand(K, generator=g) + 0.5).cuda(), (torch.randn(K, generator=g) * 0.1).cuda()
+    xst = torch.empty(((M + 31) // 32, K, 2), device="cuda")
+    if bn:  # the producer's tile statistics of x
+        wi = torch.eye(K, device="cuda")
+        xx = torch.empty_like(x)
+        _lib.check(L.fs_linear_f32_ex(_lib.GemmF32(M, K, K, p(x), K, 1, p(wi), 1, K, None, None, 0, p(xx), K, None),
+                                      None, p(xst), st()))
+        x = xx
+    outs = []
+    for lean, tr in ((True, False), (False, True), (False, False)):
+        prev = L.fs_set_lean_gemm(1 if lean else 0)
+        y = torch.empty((M, N), device="cuda")
+        sto = torch.empty(((M + 31) // 32, N, 2), device="cuda")
+        u = torch.empty_like(x)
+        mo, io, vo = (torch.empty(K, device="cuda") for _ in range(3))
+        rm, rv = torch.zeros(K, device="cuda"), torch.ones(K, device="cuda")
+        nbt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        gd = (_lib.GemmF32(M, N, K, p(x), K, 1, p(wt), N, 1, p(b), p(r), N, p(y), N, None) if tr else
+              _lib.GemmF32(M, N, K, p(x), K, 1, p(w), 1, K, p(b), p(r), N, p(y), N, None))
+        bi = _lib.BnIn(p(xst), (M + 31) // 32, M, p(gam), p(bet), 1e-5, 0.1, p(rm), p(rv), p(nbt), p(mo), p(io),
+                       p(u), p(vo)) if bn else None
+        _lib.check(L.fs_linear_f32_ex(gd, bi, p(sto), st()))
+        L.fs_set_lean_gemm(prev)
+        outs.append([y, sto] + ([u, mo, io, vo, rm, rv, nbt] if bn else []))
+    torch.cuda.synchronize()
+    for a, c, d in zip(*outs):
+        assert torch.equal(a, c) and torch.equal(a, d)
+    ref = (torch.relu(torch.nn.functional.batch_norm(x, None, None, gam, bet, True, 0.1, 1e-5)) if bn else x) @ w.t() + b
+    if res:
+        ref = ref + r
+    torch.testing.assert_close(outs[0][0], ref, rtol=1e-4, atol=1e-4)
+    # two problems in one launch (the second a copy of the first on other buffers)
+    y2 = [torch.empty((M, N), device="cuda") for _ in range(2)]
+    s2 = [torch.empty(((M + 31) // 32, N, 2), device="cuda") for _ in range(2)]
+    gds = [_lib.GemmF32(M, N, K, p(x), K, 1, p(w), 1, K, p(b), p(r), N, p(y2[i]), N, None) for i in range(2)]
+    bis = [_lib.BnIn(p(xst), (M + 31) // 32, M, p(gam), p(bet), 1e-5, 0.1, None, None, None, None, None, None, None)
+           if bn else None for _ in range(2)]
+    _lib.check(L.fs_linear_f32_ex2(gds[0], bis[0], p(s2[0]), gds[1], bis[1], p(s2[1]), st()))
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert torch.equal(y2[i], outs[0][0]) and torch.equal(s2[i], outs[0][1])
+
+
+@pytest.mark.parametrize("M,K,N", [(256, 128, 128), (232, 128, 128), (256, 128, 2944), (100, 64, 96), (36, 512, 40)])
+def test_lean_backward_products_match_generic_kernel(M, K, N):
+    """nn.Linear's backward on gemm_ling_kernel (32-bit buffer offsets, loads past the
+    operands read as zero): the input / weight gradient pair in one launch
+    (fs_linear_f32_pair), the weight gradient with its bias row sum alone, and a row sum
+    without product (the unconditional spline's batch sum), each against the generic
+    kernels (fs_set_lean_gemm(0)) bit for bit, and against torch."""
+    from flowstate import _lib
+
+    L, p, st = _lib.load(), _lib.ptr, _lib.stream_ptr
+    g = torch.Generator().manual_seed(M * 7 + N)
+    x = torch.randn((M, K), generator=g).cuda()   # the layer input
+    w = (torch.randn((N, K), generator=g) * 0.1).cuda()
+    gy = torch.randn((M, N), generator=g).cuda()  # dL/dy
+    outs = []
+    for lean in (1, 0):
+        prev = L.fs_set_lean_gemm(lean)
+        gx, gw, gb = torch.empty_like(x), torch.empty_like(w), torch.empty(N, device="cuda")
+        g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
+        g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
+        if N <= 512:
+            _lib.check(L.fs_linear_f32_pair(g0, g1, st()))
+        else:  # a long input-gradient reduction takes the split-K path; the weight gradient alone
+            _lib.check(L.fs_linear_f32(g1.M, g1.N, g1.K, g1.A, g1.sam, g1.sak, g1.B, g1.sbk, g1.sbn, None, None, 0,
+                                       g1.C, g1.ldc, g1.rowsum_a, st()))
+            gx.zero_()
+        gs = torch.empty(N, device="cuda")
+        _lib.check(L.fs_linear_f32(N, 0, M, p(gy), 1, N, None, 0, 0, None, None, 0, None, 0, p(gs), st()))
+        L.fs_set_lean_gemm(prev)
+        outs.append((gx, gw, gb, gs))
+    torch.cuda.synchronize()
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+    if N <= 512:
+        torch.testing.assert_close(outs[0][0], gy @ w, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(outs[0][1], gy.t() @ x, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(outs[0][2], gy.sum(0), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(outs[0][3], gy.sum(0), rtol=1e-4, atol=1e-4)

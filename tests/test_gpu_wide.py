@@ -124,3 +124,37 @@ def test_fused_steps_bit_identical(N, kw, C):
     a, b = _both(run)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+class trunk16:
+    """The wide path's trunk on 16-row (1) or 32-row (0) tiles for a block."""
+
+    def __init__(self, on):
+        self.on = on
+
+    def __enter__(self):
+        self.prev = _lib.load().fs_set_wide_trunk16(self.on)
+
+    def __exit__(self, *exc):
+        _lib.load().fs_set_wide_trunk16(self.prev)
+
+
+@pytest.mark.parametrize("N,kw,B", [(64, A1, 1000), (16, A1, 4096), (64, A2, 200), (3, dict(L=2, H=32, nb=2, K=5), 77)],
+                         ids=["a1-n64-1000", "a1-n16-4096", "a2-n64-200", "n3-h32-77"])
+def test_trunk16_bit_identical_to_trunk32(N, kw, B):
+    """The 16-row trunk (v_mfma_f32_16x16x4_f32 fed the 32x32x2 k order) against the
+    32-row one, density and sampling, and both against the fused kernel."""
+    dims, sd, m = _model(N, kw, seed=11)
+    g = torch.Generator().manual_seed(B)
+    x = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
+    zb = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
+    outs = []
+    with wide_rows(16384):
+        for on in (1, 0):
+            with trunk16(on):
+                outs.append([m.log_prob(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)])
+    with wide_rows(0):
+        outs.append([m.log_prob(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)])
+    torch.cuda.synchronize()
+    for a, b, c in zip(*outs):
+        assert torch.equal(a, b) and torch.equal(a, c)

@@ -171,7 +171,13 @@ A2_TOL = dict(loss_rtol=1e-5,           # the step's loss (forward_kld at ALPHA 
               grad_max_vs_f32_err=4.0,  # whole tensors: max|g - g64| <= 4 max|g_ref32 - g64| + grad_abs
               grad_abs=1e-7,
               bn_rtol=1e-4, bn_atol=1e-6,  # running statistics after the step
-              update_rel=3e-2)          # Adam update: |d - d_ref| <= update_rel * |d_ref| per tensor
+              # Adam's first update is -lr g'/(|g'| + eps), g' = g + wd p: nearly -lr sign(g'),
+              # so it amplifies the float32 noise of every near-zero g' to a sizeable fraction
+              # of lr.  Checked: (i) the update is Adam's on this path's own gradients, to
+              # float32 rounding of p (every tensor); (ii) on the whole tensors, its distance
+              # to Adam's update on the exact (float64) gradients is within 4x the reference's
+              # own float32 update's distance to it
+              update_vs_f32_err=4.0)
 
 
 def check_a2_step(m, f, loss, grads, before):
@@ -211,12 +217,28 @@ def check_a2_step(m, f, loss, grads, before):
                 assert int(v) == int(ref), k
             else:
                 np.testing.assert_allclose(v.cpu().numpy(), ref, rtol=t["bn_rtol"], atol=t["bn_atol"], err_msg=k)
-    for n, dn in zip(names, f["update_norm"]):
-        d = (params[n].detach() - before[n]).double()
-        assert float((d.norm() - dn).abs()) <= t["update_rel"] * dn + 1e-9, (n, float(d.norm()), dn)
+    def adam_first(g, p0):  # torch.optim.Adam's first step (L2 weight decay), float64
+        gp = g.double() + A2_WD * p0.double()
+        return -A2_LR * gp / (gp.abs() + 1e-8)
+
+    worst_u = 0.0
+    for n, gn in zip(names, f["grad_norm"]):
+        p0, p1 = before[n], params[n].detach()
+        d = (p1 - p0).double()
+        if gn < 0:
+            assert not d.abs().max().item(), n  # no gradient: Adam leaves it alone
+            continue
+        want = adam_first(grads[n], p0)
+        ulp = 2.0 ** -23 * torch.maximum(p0.abs(), p1.abs()).double()
+        assert bool(((d - want).abs() <= 2 * ulp + 1e-6 * A2_LR).all()), (n, float((d - want).abs().max()))
         if "update/" + n in f:
+            g64 = torch.from_numpy(f["grad64/" + n]).to(p0.device)
+            d64 = adam_first(g64, p0)
             ref = torch.from_numpy(f["update/" + n]).double().to(d.device)
-            assert float((d - ref).norm()) <= t["update_rel"] * float(ref.norm()) + 1e-9, n
+            e, e_ref = float((d - d64).norm()), float((ref - d64).norm())
+            assert e <= t["update_vs_f32_err"] * e_ref + 1e-7, (n, e, e_ref)
+            worst_u = max(worst_u, e / max(e_ref, 1e-30))
+    print(f"A2 step: worst whole-tensor Adam update error vs float64 = {worst_u:.2f} x the reference's")
 
 
 def test_training_step_matches_reference_at_config5_size_cpu():
