@@ -920,28 +920,33 @@ __device__ __forceinline__ void gemm16(const float *__restrict__ X, __amdgpu_buf
     const float *xa = X + r * XS16 + 4 * qo + ((2 * h) ^ (((r >> 3) & 1) << 1));
     const int vb = (32 * qo + r) * 16 + 4 * h;  // + 256 c: the second 16-column half
     const int fb = sec + tile * kg * 1024;
-    f32x2 rb[PD][2];
+    // both operands in PD-deep rings: the weights from L2 / MALL, the activation pairs from
+    // LDS (an LDS read issued right before its MFMAs would stall every k-group)
+    f32x2 rb[PD][2], ra[PD];
 #pragma unroll
     for (int s = 0; s < PD; ++s)
-        if (s < kg)
+        if (s < kg) {
 #pragma unroll
             for (int c = 0; c < 2; ++c) rb[s][c] = ldb_pair(W, vb + 256 * c, fb + s * 1024);
+            ra[s] = *(const f32x2 *)(xa + 8 * s);
+        }
     for (int g0 = 0; g0 < kg; g0 += PD) {
 #pragma unroll
         for (int s = 0; s < PD; ++s) {
             const int g = g0 + s;
             if (g < kg) {
-                const f32x2 a = *(const f32x2 *)(xa + 8 * g);
 #pragma unroll
                 for (int m = 0; m < 2; ++m)
 #pragma unroll
                     for (int c = 0; c < 2; ++c)
-                        acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], rb[s][c][m], acc[c], 0, 0, 0);
+                        acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[s][m], rb[s][c][m], acc[c], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
                 const int gn = g + PD;
-                if (gn < kg)
+                if (gn < kg) {
+                    ra[s] = *(const f32x2 *)(xa + 8 * gn);
 #pragma unroll
                     for (int c = 0; c < 2; ++c) rb[s][c] = ldb_pair(W, vb + 256 * c, fb + gn * 1024);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }

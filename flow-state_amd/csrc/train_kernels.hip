@@ -554,24 +554,24 @@ __global__ __launch_bounds__(512) void gemm_lin_kernel(Lin2 a) {
 
 // Lean general products: any of the strided layouts gemm_tile takes (A[m][k] at
 // A[m sam + k sak], B[k][n] at B[k sbk + n sbn]; AK / BK: contiguous along k), with the
-// row sum, for K up to 512 at 8 waves per tile: nn.Linear's backward pair (the input
-// gradient dY W and the weight / bias gradient dY^T X) and the single products outside
-// the forward layout.  gemm_tile's k order, partial-sum order, row sum and epilogue (bit-
-// identical), with 32-bit buffer offsets: the descriptors' byte ranges are the operands'
-// extents, so every load past row M, column N or depth K reads zero and needs no test.
+// row sum, at 8 waves per tile: nn.Linear's backward pair (the input gradient dY W and the
+// weight / bias gradient dY^T X), the final Linear's backward group (split-K input
+// gradient, weight gradient, the unconditional spline's row sum) and the single products
+// outside the forward layout.  gemm_tile's k order (wave w: k-blocks 8w + 64s ascending),
+// partial-sum order, row sum and epilogue, so the results are bit-identical to it, with
+// 32-bit buffer offsets: the descriptors' byte ranges are the operands' extents and a lane
+// loads only quads below K, so nothing past an operand (or a split-K chunk) is read and
+// no per-element test is needed.  Loads run kLingPF k-blocks ahead of the MFMAs.
 struct LinG {
     const float *A, *B, *bias, *R;
     float *C, *stats, *rowsum;
     int M, N, K, sam, sak, sbk, sbn, ldr, ldc, abytes, bbytes;
 };
-struct LinG2 {
-    LinG p[2];
-    unsigned t0, mt0, mt1;
-};
 struct LinGLds {
     t16 part[7][64];
     float rs_part[8][64];
 };
+constexpr int kLingPF = 4;
 
 template <bool CONTIG>
 __device__ __forceinline__ t4 ling_ld(__amdgpu_buffer_rsrc_t r, int base, int stride) {
@@ -583,7 +583,7 @@ __device__ __forceinline__ t4 ling_ld(__amdgpu_buffer_rsrc_t r, int base, int st
     return v;
 }
 
-template <bool AK, bool BK, int KBMAX>
+template <bool AK, bool BK>
 __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned by, LinGLds &L) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -593,14 +593,14 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
     // rows past M / columns past N: an offset past the operand, read as zero
     const int am = m < M ? m * P.sam : P.abytes / 4, bn = col < N ? col * P.sbn : P.bbytes / 4;
     const __amdgpu_buffer_rsrc_t Ar = lin_rsrc(P.A, P.abytes), Br = lin_rsrc(P.B, P.bbytes);
-    t4 a[KBMAX], b[KBMAX];
+    const t4 zero = {0.f, 0.f, 0.f, 0.f};
+    t4 a[kLingPF], b[kLingPF];
+    const int kb0 = 8 * w;
 #pragma unroll
-    for (int s = 0; s < KBMAX; ++s) {
-        const int k = 8 * w + 64 * s + 4 * h;
-        if (8 * w + 64 * s < K) {  // wave-uniform
-            a[s] = k < K ? ling_ld<AK>(Ar, am + k * P.sak, P.sak) : t4{0.f, 0.f, 0.f, 0.f};
-            b[s] = k < K ? ling_ld<BK>(Br, bn + k * P.sbk, P.sbk) : t4{0.f, 0.f, 0.f, 0.f};
-        }
+    for (int s = 0; s < kLingPF; ++s) {
+        const int k = kb0 + 64 * s + 4 * h;
+        a[s] = k < K ? ling_ld<AK>(Ar, am + k * P.sak, P.sak) : zero;
+        b[s] = k < K ? ling_ld<BK>(Br, bn + k * P.sbk, P.sbk) : zero;
     }
     float ep_bias = 0.f, ep_r[16];
 #pragma unroll
@@ -619,12 +619,19 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     float rs = 0.f;
+    for (int kb = kb0; kb < K; kb += 64 * kLingPF) {
 #pragma unroll
-    for (int s = 0; s < KBMAX; ++s) {
-        if (8 * w + 64 * s < K) {
+        for (int s = 0; s < kLingPF; ++s) {
+            const int k = kb + 64 * s;
+            if (k < K) {  // wave-uniform
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][j], b[s][j], acc, 0, 0, 0);
-            if (rows) rs += ((a[s][0] + a[s][1]) + a[s][2]) + a[s][3];
+                for (int j = 0; j < 4; ++j)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][j], b[s][j], acc, 0, 0, 0);
+                if (rows) rs += ((a[s][0] + a[s][1]) + a[s][2]) + a[s][3];
+                const int kn = k + 64 * kLingPF + 4 * h;
+                a[s] = kn < K ? ling_ld<AK>(Ar, am + kn * P.sak, P.sak) : zero;
+                b[s] = kn < K ? ling_ld<BK>(Br, bn + kn * P.sbk, P.sbk) : zero;
+            }
         }
     }
     if (w > 0) L.part[w - 1][lane] = acc;
@@ -671,17 +678,60 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
     }
 }
 
-// one product, or two (nn.Linear's backward pair: problem 0 the input gradient, A
-// contiguous along k; problem 1 the weight gradient, both strided), workgroups split at t0
-template <bool A0K, bool B0K, bool A1K, bool B1K, int KBMAX>
-__global__ __launch_bounds__(512) void gemm_ling_kernel(LinG2 a) {
+// Up to kLingMax products in one launch, each whole or split along K into S chunks (chunk z
+// a partial tile by the same arithmetic over its k range, written to part + z M N and added
+// in chunk order by splitk_reduce_kernel after the launch).  Workgroups [begin_i,
+// begin_{i+1}) compute problem i; its layout (AK, BK) picks one of four tile bodies by a
+// uniform branch.
+constexpr int kLingMax = 4;
+struct LinGProb {
+    LinG g;
+    float *part;
+    int kchunk;
+    unsigned S, mt, nt, begin;
+    int ak, bk;
+};
+struct LinGrp {
+    LinGProb p[kLingMax];
+    int n;
+};
+
+__global__ __launch_bounds__(512) void gemm_ling_kernel(LinGrp ga) {
     __shared__ LinGLds L;
-    const unsigned b = blockIdx.x;
-    if (b < a.t0) {
-        ling_tile<A0K, B0K, KBMAX>(a.p[0], b % a.mt0, b / a.mt0, L);
+    int i = 0;
+#pragma unroll
+    for (int t = 1; t < kLingMax; ++t)
+        if (t < ga.n && blockIdx.x >= ga.p[t].begin) i = t;
+    const LinGProb &Q = ga.p[i];
+    unsigned b = blockIdx.x - Q.begin;
+    const unsigned per = Q.mt * Q.nt, z = b / per;
+    b -= z * per;
+    const unsigned bx = b % Q.mt, by = b / Q.mt;
+    LinG c = Q.g;
+    if (Q.S > 1) {  // chunk z of the reduction: its own partial tile, nothing else
+        const int k0 = (int)z * Q.kchunk;
+        c.A = Q.g.A + k0 * Q.g.sak;
+        c.B = Q.g.B + k0 * Q.g.sbk;
+        c.abytes = Q.g.abytes - k0 * Q.g.sak * 4;
+        c.bbytes = Q.g.bbytes - k0 * Q.g.sbk * 4;
+        c.K = Q.g.K - k0 < Q.kchunk ? Q.g.K - k0 : Q.kchunk;
+        c.bias = nullptr;
+        c.R = nullptr;
+        c.rowsum = nullptr;
+        c.stats = nullptr;
+        c.C = Q.part + (int64_t)z * Q.g.M * Q.g.N;
+        c.ldc = Q.g.N;
+    }
+    if (Q.ak) {
+        if (Q.bk)
+            ling_tile<true, true>(c, bx, by, L);
+        else
+            ling_tile<true, false>(c, bx, by, L);
     } else {
-        const unsigned c = b - a.t0;
-        ling_tile<A1K, B1K, KBMAX>(a.p[1], c % a.mt1, c / a.mt1, L);
+        if (Q.bk)
+            ling_tile<false, true>(c, bx, by, L);
+        else
+            ling_tile<false, false>(c, bx, by, L);
     }
 }
 
@@ -966,6 +1016,11 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_group_kernel(GroupArgs ga) {
 
 using namespace fs;
 
+static bool lean_gemm();
+static bool ling_ok(const GemmArgs &g);
+static hipError_t ling_group(const GemmArgs *gs, int n, float *const *part, const int *S, const int64_t *kchunk,
+                             hipStream_t st);
+
 static int gemm_split(const GemmArgs &g) {
     return g.K > 8 * 4 * 16 ? FS_GEMM_SPLIT_LONG : g.K >= 256 ? FS_GEMM_SPLIT_MID : FS_GEMM_SPLIT;
 }
@@ -995,6 +1050,7 @@ hipError_t fs_linear_f32_splitk_impl(const GemmArgs &g, float *part, int64_t par
     int64_t kchunk = 0;
     const int64_t need = splitk_plan(g, S, kchunk);
     if (need == 0 || !part || part_floats < need) return fs_linear_f32_impl(g, st);
+    if (lean_gemm() && ling_ok(g)) return ling_group(&g, 1, &part, &S, &kchunk, st);
     const bool ak = g.sak == 1 && ((uintptr_t)g.A & 15) == 0 && g.sam % 4 == 0 && kchunk % 4 == 0;
     const bool bk = g.sbk == 1 && ((uintptr_t)g.B & 15) == 0 && g.sbn % 4 == 0 && kchunk % 4 == 0;
     const dim3 grid((unsigned)((g.M + 31) / 32), (unsigned)((g.N + 31) / 32), (unsigned)S);
@@ -1017,6 +1073,36 @@ hipError_t fs_linear_f32_splitk_impl(const GemmArgs &g, float *part, int64_t par
 // by one (the caller's fallback).
 hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_t ws_floats, hipStream_t st) {
     if (n < 0 || n > kGroupMax) return hipErrorInvalidValue;
+    if (lean_gemm()) {  // the same split-K plans on the lean kernel
+        GemmArgs lg[kGroupMax];
+        float *part[kGroupMax];
+        int S[kGroupMax];
+        int64_t kc[kGroupMax];
+        int m = 0;
+        int64_t used = 0;
+        bool ok = true;
+        for (int i = 0; i < n && ok; ++i) {
+            const GemmArgs &g = gs[i];
+            if (g.M <= 0 || (g.N <= 0 && !g.rowsum_a)) continue;
+            ok = ling_ok(g);
+            int s = 0;
+            int64_t kchunk = 0;
+            const int64_t need = splitk_plan(g, s, kchunk);
+            lg[m] = g;
+            if (need > 0 && ws && ws_floats - used >= need) {
+                part[m] = ws + used;
+                used += need;
+                S[m] = s;
+                kc[m] = kchunk;
+            } else {
+                part[m] = nullptr;
+                S[m] = 1;
+                kc[m] = g.K;
+            }
+            ++m;
+        }
+        if (ok) return m ? ling_group(lg, m, part, S, kc, st) : hipSuccess;
+    }
     GroupArgs ga{};
     unsigned wg = 0;
     int64_t used = 0;
@@ -1108,15 +1194,15 @@ static int64_t extent_bytes(int64_t n0, int64_t s0, int64_t n1, int64_t s1) {
     return ((n0 - 1) * s0 + (n1 - 1) * s1 + 1) * 4;
 }
 
-// gemm_ling_kernel takes a product: K <= 512 and a multiple of 4 (a lane's quad of k is
-// wholly inside or wholly past the reduction), non-negative strides, 32-bit offsets
+// gemm_ling_kernel takes a product: K a multiple of 4 (a lane's quad of k is wholly inside
+// or wholly past the reduction), non-negative strides, 32-bit offsets
 static bool ling_ok(const GemmArgs &g) {
     const int64_t lim = (int64_t)1 << 30;
-    if (g.M <= 0 || g.K <= 0 || g.K > 512 || g.K % 4 != 0 || (g.N <= 0 && !g.rowsum_a) || g.N < 0) return false;
+    if (g.M <= 0 || g.K <= 0 || g.K % 4 != 0 || (g.N <= 0 && !g.rowsum_a) || g.N < 0) return false;
     if (g.sam < 0 || g.sak < 0 || g.sbk < 0 || g.sbn < 0 || g.M > 32LL * 65535 || g.N > 32LL * 65535) return false;
     const int64_t ab = extent_bytes(g.M, g.sam, g.K, g.sak), bb = extent_bytes(g.K, g.sbk, g.N, g.sbn);
-    return ab < lim && bb < lim && g.M * g.ldc < lim && (!g.R || g.M * g.ldr < lim) &&
-           g.M * g.sam < lim && g.K * g.sak < lim && g.K * g.sbk < lim && g.N * g.sbn < lim;
+    return ab < lim && bb < lim && g.M * g.ldc < lim && (!g.R || g.M * g.ldr < lim) && g.K < lim / 4 &&
+           g.M * g.sam < lim && g.K * g.sak < lim && g.K * g.sbk < lim && g.N * g.sbn < lim && g.M * g.N < lim;
 }
 
 static LinG ling_fill(const GemmArgs &g) {
@@ -1125,44 +1211,48 @@ static LinG ling_fill(const GemmArgs &g) {
                 (int)extent_bytes(g.K, g.sbk, g.N, g.sbn)};
 }
 
-// one or two products (g1 nullable; both ling_ok) in one gemm_ling_kernel launch: the
-// instantiated layouts are any single product and the backward pair (A0K, !B0K, !A1K, !B1K)
+// n products (all ling_ok) in one gemm_ling_kernel launch; part[i] / S[i] / kchunk[i]: the
+// split-K plan of product i (S = 1: whole), then one splitk_reduce_kernel per split product
+static hipError_t ling_group(const GemmArgs *gs, int n, float *const *part, const int *S, const int64_t *kchunk,
+                             hipStream_t st) {
+    if (n <= 0 || n > kLingMax) return hipErrorInvalidValue;
+    LinGrp ga{};
+    unsigned wg = 0;
+    for (int i = 0; i < n; ++i) {
+        const GemmArgs &g = gs[i];
+        LinGProb &Q = ga.p[ga.n++];
+        Q.g = ling_fill(g);
+        Q.S = (unsigned)S[i];
+        Q.part = part[i];
+        Q.kchunk = (int)kchunk[i];
+        // split chunks: contiguous loads need chunk starts on 16-byte boundaries
+        Q.ak = ak_of(g) && (Q.S == 1 || Q.kchunk % 4 == 0);
+        Q.bk = bk_of(g) && (Q.S == 1 || Q.kchunk % 4 == 0);
+        Q.mt = (unsigned)((g.M + 31) / 32);
+        Q.nt = (unsigned)(g.N > 0 ? (g.N + 31) / 32 : 1);
+        Q.begin = wg;
+        wg += Q.mt * Q.nt * Q.S;
+    }
+    hipLaunchKernelGGL(gemm_ling_kernel, dim3(wg), dim3(512), 0, st, ga);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    for (int i = 0; i < n; ++i) {
+        if (S[i] <= 1) continue;
+        const GemmArgs &g = gs[i];
+        const int64_t m = g.M * g.N;
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, g,
+                           (const float *)part[i], S[i]);
+        if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// one or two whole products (g1 nullable; both ling_ok) in one launch
 static hipError_t ling_launch(const GemmArgs &g0, const GemmArgs *g1, hipStream_t st) {
-    LinG2 a{};
-    a.p[0] = ling_fill(g0);
-    a.mt0 = (unsigned)((g0.M + 31) / 32);
-    a.t0 = a.mt0 * (unsigned)(g0.N > 0 ? (g0.N + 31) / 32 : 1);
-    unsigned t1 = 0;
-    int kmax = (int)g0.K;
-    if (g1) {
-        a.p[1] = ling_fill(*g1);
-        a.mt1 = (unsigned)((g1->M + 31) / 32);
-        t1 = a.mt1 * (unsigned)(g1->N > 0 ? (g1->N + 31) / 32 : 1);
-        if (g1->K > kmax) kmax = (int)g1->K;
-    } else {
-        a.mt1 = 1;
-    }
-    const dim3 grid(a.t0 + t1), block(512);
-    const bool a0 = ak_of(g0), b0 = bk_of(g0);
-#define FS_LG(A0, B0, A1, B1)                                                                                    \
-    do {                                                                                                         \
-        if (kmax <= 128)                                                                                         \
-            hipLaunchKernelGGL((gemm_ling_kernel<A0, B0, A1, B1, 2>), grid, block, 0, st, a);                     \
-        else if (kmax <= 256)                                                                                    \
-            hipLaunchKernelGGL((gemm_ling_kernel<A0, B0, A1, B1, 4>), grid, block, 0, st, a);                     \
-        else                                                                                                     \
-            hipLaunchKernelGGL((gemm_ling_kernel<A0, B0, A1, B1, 8>), grid, block, 0, st, a);                     \
-        return hipGetLastError();                                                                                \
-    } while (0)
-    if (g1) {
-        if (a0 && !b0 && !ak_of(*g1) && !bk_of(*g1)) FS_LG(true, false, false, false);
-        return hipErrorNotSupported;
-    }
-    if (a0 && b0) FS_LG(true, true, true, true);
-    if (a0 && !b0) FS_LG(true, false, true, false);
-    if (!a0 && b0) FS_LG(false, true, false, true);
-    FS_LG(false, false, false, false);
-#undef FS_LG
+    GemmArgs gs[2] = {g0, g1 ? *g1 : g0};
+    float *part[2] = {nullptr, nullptr};
+    const int S[2] = {1, 1};
+    const int64_t kc[2] = {g0.K, g1 ? g1->K : g0.K};
+    return ling_group(gs, g1 ? 2 : 1, part, S, kc, st);
 }
 
 // one or two products (g1 nullable) in one gemm_lin_kernel launch; both lin_ok, one K

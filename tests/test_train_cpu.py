@@ -229,16 +229,21 @@ def check_a2_step(m, f, loss, grads, before):
             assert not d.abs().max().item(), n  # no gradient: Adam leaves it alone
             continue
         want = adam_first(grads[n], p0)
+        # torch's Adam runs in float32 with beta2 = 0.999 rounded to float (its bias
+        # correction 1 - 0.999f is 1.3e-5 off 0.001): updates agree with the exact formula
+        # to ~1e-5 relative, plus the rounding of p itself
         ulp = 2.0 ** -23 * torch.maximum(p0.abs(), p1.abs()).double()
-        assert bool(((d - want).abs() <= 2 * ulp + 1e-6 * A2_LR).all()), (n, float((d - want).abs().max()))
+        assert bool(((d - want).abs() <= 2 * ulp + 5e-5 * want.abs() + 1e-6 * A2_LR).all()), \
+            (n, float((d - want).abs().max()))
         if "update/" + n in f:
             g64 = torch.from_numpy(f["grad64/" + n]).to(p0.device)
             d64 = adam_first(g64, p0)
             ref = torch.from_numpy(f["update/" + n]).double().to(d.device)
             e, e_ref = float((d - d64).norm()), float((ref - d64).norm())
             assert e <= t["update_vs_f32_err"] * e_ref + 1e-7, (n, e, e_ref)
-            worst_u = max(worst_u, e / max(e_ref, 1e-30))
-    print(f"A2 step: worst whole-tensor Adam update error vs float64 = {worst_u:.2f} x the reference's")
+            if e > 1e-7:  # above the absolute floor
+                worst_u = max(worst_u, e / max(e_ref, 1e-30))
+    print(f"A2 step: worst whole-tensor Adam update error vs float64 (above 1e-7) = {worst_u:.2f} x the reference's")
 
 
 def test_training_step_matches_reference_at_config5_size_cpu():

@@ -19,6 +19,15 @@ for v in lean nolean; do
   FS_LEAN_GEMM=$lean timeout -k 10 300 python tools/bench_train.py > gpurun_out/${T}_bench_train_$v.log 2>&1
   rc=$?; echo "bench_train $v rc=$rc"; tail -c 400 gpurun_out/${T}_bench_train_$v.log; [ $rc -eq 0 ] || exit $rc
 done
+for t in 1 0; do
+  FS_WIDE_TRUNK16=$t timeout -k 10 300 python tools/bench_wide.py 200,1024,4096,8192 > gpurun_out/${T}_bench_wide_t$t.log 2>&1
+  rc=$?; echo "bench_wide trunk16=$t rc=$rc"; cat gpurun_out/${T}_bench_wide_t$t.log | cut -c1-220; [ $rc -eq 0 ] || exit $rc
+done
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${T}_prof_refeed -o run -- python3 tools/prof_refeed.py > gpurun_out/${T}_prof_refeed.log 2>&1
+rc=$?; echo "refeed rocprof rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_prof_refeed.log; exit $rc; }
+f=$(find gpurun_out/${T}_prof_refeed -name "*kernel_trace.csv" | head -1)
+python3 tools/trace_window.py "$f" 1 > gpurun_out/${T}_refeed_window.json && head -c 1500 gpurun_out/${T}_refeed_window.json
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${T}_bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/${T}_bench.log; exit $rc; }
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
