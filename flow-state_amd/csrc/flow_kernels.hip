@@ -90,7 +90,8 @@ __device__ __forceinline__ void b_prologue(BRing<CT, PD> &br, __amdgpu_buffer_rs
             for (int ct = 0; ct < CT; ++ct) br.rb[s][ct] = ldb_frag(W, voff, sec + (ct * kg + s) * 1024);
 }
 
-// acc[rt][ct] = X[rows 32*(rt0+rt)..+31][0 : 8*kg] . B[tile ct0+ct]
+// acc[rt][ct] = X[rows 32*(rt0+rt)..+31][0 : 8*kg] . B[tile ct0+ct]  (TR = false: a ResidualNet
+// section, fragment values in kResPos order)
 // W: buffer descriptor of the layer's packed parameters; sec: byte offset of
 // this GEMM's fragment section (wave-uniform).  32-bit offsets only: no 64-bit
 // pointer per ring slot to keep live.  Operands of k-group g live in ring slot
@@ -100,6 +101,12 @@ __device__ __forceinline__ void b_prologue(BRing<CT, PD> &br, __amdgpu_buffer_rs
 // done by the matrix cores instead of 16 VALU adds per tile).  TR = true computes the
 // transposed tile, acc^T = B^T . X^T (the packed weight fragment is a valid A operand
 // as it stands): accumulator lane = chain, registers = output columns.
+// The ResidualNet sections (initial layer, blocks) store each lane's four k values of a
+// fragment in the order j = 0, 2, 1, 3 (pack kind 0): element j sits at kResPos[j].  The
+// 32x32x2 GEMMs read all four either way; the 16-row trunk's lanes need j = (h, 2 + h),
+// which this order makes one 8-byte load.  The final-layer sections keep 0, 1, 2, 3.
+__device__ constexpr int kResPos[4] = {0, 2, 1, 3};
+
 template <int XS, int RT, int CT, int PD, bool ACC = false, bool TR = false>
 __device__ __forceinline__ void gemm_run(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
                                          int rt0, int ct0, BRing<CT, PD> &br, f32x16 (&acc)[RT][CT]) {
@@ -133,7 +140,8 @@ __device__ __forceinline__ void gemm_run(const float *__restrict__ X, __amdgpu_b
                         for (int rt = 0; rt < RT; ++rt)
                             acc[rt][ct] = TR ? __builtin_amdgcn_mfma_f32_32x32x2f32(br.rb[s][ct][j], ra[s][rt][j],
                                                                                    acc[rt][ct], 0, 0, 0)
-                                             : __builtin_amdgcn_mfma_f32_32x32x2f32(ra[s][rt][j], br.rb[s][ct][j],
+                                             : __builtin_amdgcn_mfma_f32_32x32x2f32(ra[s][rt][j],
+                                                                                   br.rb[s][ct][kResPos[j]],
                                                                                    acc[rt][ct], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
                 const int gn = g + PD;
@@ -889,8 +897,9 @@ __global__ void __launch_bounds__(64 * (H / 32)) wide_trunk_kernel(WideArgs w) {
 // k-group g the 32x32x2 chain takes k = 8g + (0, 4), (1, 5), (2, 6), (3, 7); here MFMA 0
 // takes the k-slots (0, 4, 1, 5) and MFMA 1 (2, 6, 3, 7), i.e. lane (q, r) of a 16x16x4
 // supplies k = 8g + 4 (q & 1) + (q >> 1) and then + 2.  Its weight values are the 32-row
-// image's fragment: lane 32 (q & 1) + 16 c + r, elements (q >> 1) and 2 + (q >> 1), two
-// dword loads (c = this wave's 16-column half).  The activation pair is one ds_read_b64 of
+// image's fragment: lane 32 (q & 1) + 16 c + r, elements (q >> 1) and 2 + (q >> 1), one
+// 8-byte load each (c = this wave's 16-column half; kResPos puts the pair side by side in the
+// ResidualNet sections).  The activation pair is one ds_read_b64 of
 // a tile image whose quads are stored as columns (0, 2, 1, 3), bit 1 of the position
 // flipped in rows 8-15, at a row stride of 8 mod 64 dwords (no bank conflicts).
 __device__ __forceinline__ int t16_pos(int row, int col, int xs) {
@@ -901,10 +910,7 @@ __device__ __forceinline__ int t16_pos(int row, int col, int xs) {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f32x2 ldb_pair(__amdgpu_buffer_rsrc_t W, int voff, int soff) {
-    f32x2 v;
-    v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(W, voff, soff, 0));
-    v[1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(W, voff + 8, soff, 0));
-    return v;
+    return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(W, voff, soff, 0));
 }
 
 // acc[c] (16 x 16, columns 32 tile + 16 c ..) = X[16 x 8 kg] . B[tile], ACC: onto acc
@@ -918,7 +924,7 @@ __device__ __forceinline__ void gemm16(const float *__restrict__ X, __amdgpu_buf
 #pragma unroll
             for (int i = 0; i < 4; ++i) acc[c][i] = 0.f;
     const float *xa = X + r * XS16 + 4 * qo + ((2 * h) ^ (((r >> 3) & 1) << 1));
-    const int vb = (32 * qo + r) * 16 + 4 * h;  // + 256 c: the second 16-column half
+    const int vb = (32 * qo + r) * 16 + 8 * h;  // + 256 c: the second 16-column half
     const int fb = sec + tile * kg * 1024;
     // both operands in PD-deep rings: the weights from L2 / MALL, the activation pairs from
     // LDS (an LDS read issued right before its MFMAs would stall every k-group)
@@ -954,7 +960,7 @@ __device__ __forceinline__ void gemm16(const float *__restrict__ X, __amdgpu_buf
 }
 
 #ifndef FS_WIDE16_PD
-#define FS_WIDE16_PD 8
+#define FS_WIDE16_PD 24  // k-groups in flight (2 loads each): the weights stream from MALL / HBM
 #endif
 
 // wide_trunk_kernel on a 16-row tile: one wave per 32-column tile (two 16x16 halves), the
@@ -1225,7 +1231,8 @@ __global__ void __launch_bounds__(kThreads) wide_output_kernel(WideArgs w) {
 // ---------------------------------------------------------------------------
 // Every packing kernel covers all layers (blockIdx.y, raw / packed strides sl / dl) and,
 // for the residual blocks, all blocks (blockIdx.z, strides sz / dz) in one launch.
-// kind 0: plain linear W[nout][kin];  kind 1: final layer widths / heights (2 tiles per feature)
+// kind 0: plain linear W[nout][kin] (ResidualNet; lane values in kResPos order);  kind 1: final
+// layer widths / heights (2 tiles per feature)
 __global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restrict__ src, int kin, int kg,
                                    int ntiles, int nout, int kind, int K, float wh_scale, int64_t sl, int64_t dl,
                                    int64_t sz, int64_t dz) {
@@ -1235,7 +1242,9 @@ __global__ void pack_linear_kernel(float *__restrict__ dst, const float *__restr
     const int P = 3 * K + 1;
     for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
          idx += (int64_t)gridDim.x * blockDim.x) {
-        const int j = idx & 3;
+        const int pos = idx & 3;
+        // kind 0 (ResidualNet): positions 0..3 hold j = 0, 2, 1, 3 (kResPos)
+        const int j = kind == 0 ? (pos == 1 ? 2 : pos == 2 ? 1 : pos) : pos;
         const int lane = (idx >> 2) & 63;
         const int64_t tg = idx >> 8;
         const int g = (int)(tg % kg);

@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r04c}
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_wide.py tests/test_gpu_train.py tests/test_gpu_train_fused.py tests/test_gpu_paired.py tests/test_gpu_train_graph.py tests/test_gpu_algorithm2.py > gpurun_out/${T}_pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_algorithm2.py tests/test_gpu_train.py tests/test_gpu_train_fused.py tests/test_gpu_paired.py tests/test_gpu_train_graph.py tests/test_gpu_spline_grad.py tests/test_gpu_wide.py > gpurun_out/${T}_pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/${T}_pytest.log; [ $rc -eq 0 ] || exit $rc
 for t in 1 0; do
   FS_WIDE_TRUNK16=$t timeout -k 10 300 python tools/bench_wide.py 200,1024,4096,8192 > gpurun_out/${T}_bench_wide_t$t.log 2>&1
