@@ -1440,6 +1440,19 @@ static void *wide_workspace(size_t bytes, hipStream_t st) {
 
 constexpr int64_t kWideMaxRows = 65536;  // the workspace never grows beyond this many rows
 
+// compute units of the current device (cached per device)
+static int device_cus() {
+    static std::atomic<int> cus[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    int v = cus[dev].load(std::memory_order_relaxed);
+    if (v <= 0) {
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        cus[dev].store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
+
 // the trunk on 16-row tiles (wide_trunk16_kernel, default) or 32-row ones (FS_WIDE_TRUNK16=0,
 // fs_set_wide_trunk16); bit-identical either way
 static std::atomic<int> g_trunk16{-1};
@@ -1479,7 +1492,7 @@ struct WideGraph {
     hipGraphNode_t first = nullptr, last = nullptr;
 };
 
-static std::vector<char> wide_key(const WideArgs &w, const void *kfn0, int H, int K, int mode) {
+static std::vector<char> wide_key(const WideArgs &w, const void *kfn0, int H, int K, int mode, int variant) {
     WideArgs k = w;
     FlowArgs &a = k.a;  // the call-specific fields only the input / output launches read
     a.in = nullptr;
@@ -1489,12 +1502,12 @@ static std::vector<char> wide_key(const WideArgs &w, const void *kfn0, int H, in
     a.half_width = 0.0;
     a.add_base = 0;
     k.off = k.layer = k.jb = 0;
-    std::vector<char> key(sizeof(WideArgs) + sizeof(void *) + 3 * sizeof(int));
+    std::vector<char> key(sizeof(WideArgs) + sizeof(void *) + 4 * sizeof(int));
     char *p = key.data();
     memset(p, 0, key.size());
     memcpy(p, &k, sizeof(WideArgs));
     memcpy(p + sizeof(WideArgs), &kfn0, sizeof(void *));
-    const int hk[3] = {H, K, mode};
+    const int hk[4] = {H, K, mode, variant};
     memcpy(p + sizeof(WideArgs) + sizeof(void *), hk, sizeof(hk));
     return key;
 }
@@ -1622,6 +1635,10 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
         static std::atomic<unsigned long long> attr_set{0};
         if (hipError_t e = fs_set_max_lds_once((const void *)kf, attr_set); e != hipSuccess) return e;
     }
+    // 16-row trunk tiles while they fit the chip in one round (4096 rows on 256 CUs): past
+    // that the 32-row tiles' higher arithmetic intensity wins (8192 rows: 9.0 vs 11.6 ms per
+    // A1 N=16 pass, profiles/r04/)
+    const bool trunk16 = wide_trunk16() && R / 16 <= device_cus();
     std::vector<WideLaunch> seq;
     seq.reserve(4 + (size_t)a.L * 3);
     auto add = [&](const void *f, dim3 g, dim3 b, unsigned lds) { seq.push_back({f, g, b, lds, w}); };
@@ -1634,7 +1651,7 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
             add((const void *)wide_start_kernel<H, K, MODE>, dim3(nblk), dim3(kThreads), 0);
         else
             add((const void *)wide_start_s_kernel<H, K, MODE>, dim3(nblk, kWaves), dim3(kThreads), 0);
-        if (wide_trunk16())
+        if (trunk16)
             add((const void *)wide_trunk16_kernel<H>, dim3((unsigned)(R / 16)), dim3(64 * (H / 32)), 0);
         else
             add((const void *)wide_trunk_kernel<H>, dim3((unsigned)(R / 32)), dim3(64 * (H / 32)), 0);
@@ -1645,7 +1662,7 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     w.pending = 1;
     add((const void *)wide_output_kernel<K, MODE>, dim3(nblk), dim3(kThreads), 0);
     w.off = w.layer = w.jb = w.pending = 0;
-    hipError_t e = wide_run(seq, wide_key(w, seq.front().func, H, K, MODE), st);
+    hipError_t e = wide_run(seq, wide_key(w, seq.front().func, H, K, MODE, trunk16 ? 1 : 0), st);
     if (e == hipSuccess) used = true;
     return e;
 }
