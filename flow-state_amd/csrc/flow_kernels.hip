@@ -1568,7 +1568,7 @@ static hipError_t wide_run(const std::vector<WideLaunch> &seq, std::vector<char>
             (void)hipGraphDestroy(wg.graph);
             return e;
         }
-        if (lst.size() >= 8) {  // evict the least recently used (after the stream's work drains)
+        if (lst.size() >= 16) {  // evict the least recently used (after the stream's work drains)
             (void)hipStreamSynchronize(st);
             (void)hipGraphExecDestroy(lst.front().exec);
             (void)hipGraphDestroy(lst.front().graph);

@@ -43,11 +43,8 @@ __device__ __forceinline__ void build_knots(const float *u, float B, Knots<K> &k
         kn.p[k] = expf(u[k] - m);
         s += kn.p[k];
     }
-    // one reciprocal instead of K IEEE divisions (~10 instructions each, one wave per row
-    // here: the chain is the kernel's time); within 1 ulp of p / s
-    const float is = 1.f / s;
 #pragma unroll
-    for (int k = 0; k < K; ++k) kn.p[k] = kn.p[k] * is;
+    for (int k = 0; k < K; ++k) kn.p[k] = kn.p[k] / s;
     const float c1 = 1.f - kMin * (float)K;
     double cs = 0.0;
     kn.c[0] = -B;
@@ -333,11 +330,10 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 template <int K>
 __device__ __forceinline__ void cond_params(const float *p, float sq, float *w, float *h) {
-    const float isq = 1.f / sq;  // params[..., :K] / sqrt(H) (coupling.py:340-342), as a product
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        w[k] = p[k] * isq;
-        h[k] = p[K + k] * isq;
+        w[k] = p[k] / sq;  // params[..., :K] / sqrt(H) (coupling.py:340-342)
+        h[k] = p[K + k] / sq;
     }
 }
 
@@ -429,8 +425,8 @@ __device__ __forceinline__ void density_bwd_row(const CouplingArgs &c, const flo
             gx[row * c.D + pt] = g;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                gp[k] = gw[k] * (1.f / c.sq);
-                gp[K + k] = gh[k] * (1.f / c.sq);
+                gp[k] = gw[k] / c.sq;
+                gp[K + k] = gh[k] / c.sq;
             }
 #pragma unroll
             for (int k = 0; k <= K; ++k) gp[2 * K + k] = gd[k];
