@@ -1175,92 +1175,6 @@ __global__ void __launch_bounds__(64 * WPB) wide_final_kernel(WideArgs w) {
     if (nan_any && row0 + lane < a.nrows && a.err) atomicOr(a.err, 1);
 }
 
-// The K <= 16 final phase with each feature pair on TWO waves: wave 0 of the pair computes
-// the searched tile (widths when evaluating, heights when inverting), wave 1 the other, both
-// publish their lane-per-chain tile through LDS, then wave 0 runs feature 2p's spline and
-// wave 1 feature 2p+1's (and, density, one unconditional spline each).  The same device
-// functions on the same operands: bit-identical to wide_final_kernel, with each wave's
-// MFMA chain (and spline) halved, which is what bounds this phase at the refeed's sizes.
-template <int H, int K, int MODE, int WPB>
-__global__ void __launch_bounds__(128 * WPB) wide_final2_kernel(WideArgs w) {
-    static_assert(K <= 16, "feature pairs");
-    constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float *X = (float *)smem;
-    float *TB = X + kRows * XS;  // [WPB units][2 tiles][32 rows][64 lanes]
-    const FlowArgs &a = w.a;
-    const int N = a.N, D = 2 * N;
-    const PackLayout PL = pack_layout(N, H, a.nb, a.K);
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int up = wv >> 1, side = wv & 1;  // unit within the workgroup, tile / feature of the pair
-    const int u = (int)blockIdx.y * WPB + up;
-    const int64_t row0 = (int64_t)blockIdx.x * kRows;
-    const float *Xg = w.XB + row0 * XS;
-    for (int e = threadIdx.x; e < kRows * (H / 4); e += blockDim.x) {
-        const int rr = e / (H / 4), q = e - rr * (H / 4);
-        *(f32x4 *)(X + rr * XS + 4 * q) = *(const f32x4 *)(Xg + rr * XS + 4 * q);
-    }
-    __syncthreads();
-    const bool live = 2 * u < N;
-    float *CO = w.CO + row0 * D;
-    const int cs = D, off = w.off;
-    const float *P = a.packed + (int64_t)w.layer * PL.stride;
-    const float *V = P + PL.vec;
-    const __amdgpu_buffer_rsrc_t W =
-        __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
-    bool nan_any = false;
-    Prof pf;
-    constexpr bool INV = MODE != MODE_DENSITY;
-    constexpr int TS = INV ? 1 : 0;
-    const int pp = u, ja = 2 * pp, jb = 2 * pp + 1;
-    const bool hb = jb < N;
-    float *tb = TB + (size_t)up * 2 * 32 * 64;
-    f32x16 tS[2][1], tO[2][1];
-    if (live) {
-        const float *ba = V + PL.v_bf + 96 * ja;
-        const float *bb = hb ? V + PL.v_bf + 96 * jb : ba + 16;
-        // side 0: the searched tile (2 pp + TS), side 1: the other one
-        const int tsel = side == 0 ? TS : 1 - TS;
-        f32x16(&mine)[2][1] = side == 0 ? tS : tO;
-        final_tile_pair<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + tsel, ba + 32 * tsel,
-                                      bb + 32 * tsel, mine);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            tb[(side * 32 + i) * 64 + lane] = mine[0][0][i];
-            tb[(side * 32 + 16 + i) * 64 + lane] = mine[1][0][i];
-        }
-    }
-    __syncthreads();
-    if (!live) return;
-    {
-        f32x16(&other)[2][1] = side == 0 ? tO : tS;
-        const int os = 1 - side;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            other[0][0][i] = tb[(os * 32 + i) * 64 + lane];
-            other[1][0][i] = tb[(os * 32 + 16 + i) * 64 + lane];
-        }
-    }
-    float *lc = w.LDC + (row0 + lane) * N;
-    if (side == 0)
-        lc[ja] = spline_from_tiles<XS, H, K, INV>(tS, tO, 0, X, W, (int)((PL.wd + (int64_t)ja * H * (K + 1)) * 4),
-                                                  V + PL.v_bd + ja * (K + 1), CO, cs, (2 * ja + 1 + off) % D, a,
-                                                  nan_any, pf);
-    else if (hb)
-        lc[jb] = spline_from_tiles<XS, H, K, INV>(tS, tO, 16, X, W, (int)((PL.wd + (int64_t)jb * H * (K + 1)) * 4),
-                                                  V + PL.v_bd + jb * (K + 1), CO, cs, (2 * jb + 1 + off) % D, a,
-                                                  nan_any, pf);
-    if (MODE == MODE_DENSITY) {
-        const int f = 2 * u + side;
-        if (f < N) {
-            float *lu = w.LDU + (row0 + lane) * N;
-            lu[f] = uncond_one<K, false>(P + PL.unc, CO, cs, D, off, a, nan_any, f);
-        }
-    }
-    if (nan_any && row0 + lane < a.nrows && a.err) atomicOr(a.err, 1);
-}
-
 template <int K, int MODE>
 __global__ void __launch_bounds__(kThreads) wide_output_kernel(WideArgs w) {
     const FlowArgs &a = w.a;
@@ -1526,20 +1440,6 @@ static void *wide_workspace(size_t bytes, hipStream_t st) {
 
 constexpr int64_t kWideMaxRows = 65536;  // the workspace never grows beyond this many rows
 
-// K <= 16 final phase on two waves per feature pair (wide_final2_kernel, default) or one
-// (FS_WIDE_FINAL2=0, fs_set_wide_final2); bit-identical either way
-static std::atomic<int> g_final2{-1};
-static bool wide_final2() {
-    int v = g_final2.load(std::memory_order_relaxed);
-    if (v < 0) {
-        const char *e = getenv("FS_WIDE_FINAL2");
-        int expect = -1;
-        g_final2.compare_exchange_strong(expect, (e && e[0] == '0') ? 0 : 1);
-        v = g_final2.load(std::memory_order_relaxed);
-    }
-    return v != 0;
-}
-
 // compute units of the current device (cached per device)
 static int device_cus() {
     static std::atomic<int> cus[64];
@@ -1735,14 +1635,6 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
         static std::atomic<unsigned long long> attr_set{0};
         if (hipError_t e = fs_set_max_lds_once((const void *)kf, attr_set); e != hipSuccess) return e;
     }
-    // K <= 16: each feature pair on two waves (wide_final2_kernel), WPW pairs per workgroup
-    const bool final2 = K <= 16 && wide_final2();
-    const unsigned fin2_lds = fin_lds + (unsigned)(WPW * 2 * 32 * 64 * 4);
-    if (K <= 16) {
-        auto kf = wide_final2_kernel<H, (K <= 16 ? K : 16), MODE, WPW>;
-        static std::atomic<unsigned long long> attr_set2{0};
-        if (hipError_t e = fs_set_max_lds_once((const void *)kf, attr_set2); e != hipSuccess) return e;
-    }
     // 16-row trunk tiles while they fit the chip in one round (4096 rows on 256 CUs): past
     // that the 32-row tiles' higher arithmetic intensity wins (8192 rows: 9.0 vs 11.6 ms per
     // A1 N=16 pass, profiles/r04/)
@@ -1763,18 +1655,14 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
             add((const void *)wide_trunk16_kernel<H>, dim3((unsigned)(R / 16)), dim3(64 * (H / 32)), 0);
         else
             add((const void *)wide_trunk_kernel<H>, dim3((unsigned)(R / 32)), dim3(64 * (H / 32)), 0);
-        if (final2)
-            add((const void *)wide_final2_kernel<H, (K <= 16 ? K : 16), MODE, WPW>, dim3(nblk, (units + WPW - 1) / WPW),
-                dim3(128 * WPW), fin2_lds);
-        else
-            add((const void *)wide_final_kernel<H, K, MODE, WPW>, dim3(nblk, (units + WPW - 1) / WPW), dim3(64 * WPW),
-                fin_lds);
+        add((const void *)wide_final_kernel<H, K, MODE, WPW>, dim3(nblk, (units + WPW - 1) / WPW), dim3(64 * WPW),
+            fin_lds);
         if (MODE == MODE_DENSITY) w.off = (w.off + N) % D;
     }
     w.pending = 1;
     add((const void *)wide_output_kernel<K, MODE>, dim3(nblk), dim3(kThreads), 0);
     w.off = w.layer = w.jb = w.pending = 0;
-    hipError_t e = wide_run(seq, wide_key(w, seq.front().func, H, K, MODE, (trunk16 ? 1 : 0) | (final2 ? 2 : 0)), st);
+    hipError_t e = wide_run(seq, wide_key(w, seq.front().func, H, K, MODE, trunk16 ? 1 : 0), st);
     if (e == hipSuccess) used = true;
     return e;
 }
@@ -1796,12 +1684,6 @@ using namespace fs;
 int32_t fs_set_wide_trunk16_impl(int32_t on) {
     const int32_t prev = wide_trunk16() ? 1 : 0;
     if (on >= 0) g_trunk16.store(on ? 1 : 0, std::memory_order_relaxed);
-    return prev;
-}
-
-int32_t fs_set_wide_final2_impl(int32_t on) {
-    const int32_t prev = wide_final2() ? 1 : 0;
-    if (on >= 0) g_final2.store(on ? 1 : 0, std::memory_order_relaxed);
     return prev;
 }
 

@@ -273,12 +273,9 @@ int64_t fs_set_wide_rows(int64_t rows);
  * depend on them.
  * fs_set_wide_trunk16: 1 (default, or FS_WIDE_TRUNK16) = the wide path's ResidualNet on
  *   16-row tiles (v_mfma_f32_16x16x4_f32, twice the workgroups), 0 = 32-row tiles.
- * fs_set_wide_final2: 1 (default, or FS_WIDE_FINAL2) = the wide path's K <= 16 final phase
- *   with each feature pair on two waves, 0 = one wave per pair.
  * fs_set_lean_gemm: 1 (default, or FS_LEAN_GEMM) = the training products on the lean
  *   kernels (32-bit buffer offsets), 0 = the generic strided kernels. */
 int32_t fs_set_wide_trunk16(int32_t on);
-int32_t fs_set_wide_final2(int32_t on);
 int32_t fs_set_lean_gemm(int32_t on);
 
 /* ------------------------------------------------------------------ */

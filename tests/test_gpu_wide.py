@@ -158,48 +158,3 @@ def test_trunk16_bit_identical_to_trunk32(N, kw, B):
     torch.cuda.synchronize()
     for a, b, c in zip(*outs):
         assert torch.equal(a, b) and torch.equal(a, c)
-
-
-class final2:
-    """The wide path's K <= 16 final phase on two waves per feature pair (1) or one (0)."""
-
-    def __init__(self, on):
-        self.on = on
-
-    def __enter__(self):
-        self.prev = _lib.load().fs_set_wide_final2(self.on)
-
-    def __exit__(self, *exc):
-        _lib.load().fs_set_wide_final2(self.prev)
-
-
-@pytest.mark.parametrize("N,kw,B", [(64, A2, 200), (64, A2, 1000), (16, dict(L=3, H=64, nb=2, K=8), 77),
-                                    (3, dict(L=2, H=32, nb=2, K=5), 130)],
-                         ids=["a2-n64-200", "a2-n64-1000", "n16-h64-77", "n3-h32-130"])
-def test_final2_bit_identical(N, kw, B):
-    """The two-waves-per-pair final phase against the one-wave one and the fused kernel:
-    density, sampling and propose (in-kernel draws) outputs and log-dets."""
-    dims, sd, m = _model(N, kw, seed=13)
-    L = _lib.load()
-    g = torch.Generator().manual_seed(B + 1)
-    x = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B * 1.001).cuda()
-    zb = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
-
-    def run():
-        cfg = torch.empty((B, dims.D), device="cuda")
-        lq = torch.empty(B, device="cuda")
-        err = torch.zeros(1, dtype=torch.int32, device="cuda")
-        _lib.check(L.fs_flow_propose_lq(m.dims(), _lib.ptr(m.packed()), B, 7, 3, 0, float(dims.B), _lib.ptr(cfg),
-                                        None, None, _lib.ptr(lq), _lib.ptr(err), _lib.stream_ptr()))
-        return [m.log_prob(x).clone(), m.inverse(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)] + [cfg, lq]
-
-    outs = []
-    with wide_rows(16384):
-        for on in (1, 0):
-            with final2(on):
-                outs.append(run())
-    with wide_rows(0):
-        outs.append(run())
-    torch.cuda.synchronize()
-    for a, b, c in zip(*outs):
-        assert torch.equal(a, b) and torch.equal(a, c)
