@@ -200,6 +200,26 @@ __device__ __forceinline__ void final_tile_pair(const float *__restrict__ X, __a
     lanes_to_chains(t[0][0], t[1][0]);
 }
 
+// final_tile_pair for the 32 chains of X's first row tile, duplicated into both lane halves
+// (lane l and l + 32: chain l)
+template <int XS, int FPD = 4>
+__device__ __forceinline__ void final_tile_pair32(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec,
+                                                  int kg, int tile, const float *__restrict__ ba,
+                                                  const float *__restrict__ bb, f32x16 (&t)[2][1]) {
+    const int h = (threadIdx.x >> 5) & 1;
+    f32x16 t1[1][1];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *(const f32x4 *)((g < 2 ? ba + 8 * g : bb + 8 * (g - 2)) + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t1[0][0][4 * g + j] = v[j];
+    }
+    gemm64<XS, 1, 1, FPD, true, true>(X, W, sec, kg, 0, tile, t1);
+    t[0][0] = t1[0][0];
+    t[1][0] = t1[0][0];
+    lanes_to_chains(t[0][0], t[1][0]);
+}
+
 #pragma clang fp contract(off)
 
 // Derivative-row gathers of cond_spline: QB quads (16-byte pieces of rows bin and
@@ -345,14 +365,16 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
 
 // cond_spline for a feature pair (K <= 16): both tiles of the pair first, then each
 // feature's spline from its 16 columns (c0 = 0 or 16) of the lane-per-chain tiles.
-template <int XS, int H, int K, bool INV>
+// RM: lane -> chain mask (31: a 32-chain tile pair duplicated into both lane halves, whose
+// upper half only computes)
+template <int XS, int H, int K, bool INV, int RM = 63>
 __device__ __forceinline__ float spline_from_tiles(const f32x16 (&tS)[2][1], const f32x16 (&tO)[2][1], int c0,
                                                    const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int dsec,
                                                    const float *__restrict__ bd, float *CO, int cs, int p,
                                                    const FlowArgs &a, bool &nan_any, Prof &pf) {
     constexpr int NQ = H / 4;
     constexpr int QB = NQ >= 8 ? 4 : NQ / 2;
-    const int lane = threadIdx.x & 63;
+    const int lane = (int)threadIdx.x & RM;
     const float x = CO[lane * cs + p];
     const bool inside = (x >= a.negB) && (x <= a.B);
     float ks[K + 1];
@@ -411,7 +433,7 @@ __device__ __forceinline__ float spline_from_tiles(const f32x16 (&tS)[2][1], con
     rqs_eval<INV>(x, icw, cw1 - icw, ich, ch1 - ich, d0, d1, y, l, nd);
     pf.mark(PH_SPLINE);
     if (inside) {
-        CO[lane * cs + p] = y;
+        if (RM == 63 || (threadIdx.x & 32) == 0) CO[lane * cs + p] = y;
         nan_any |= nd;
         return l;
     }
@@ -966,16 +988,78 @@ __device__ __forceinline__ void gemm16(const float *__restrict__ X, __amdgpu_buf
 // wide_trunk_kernel on a 16-row tile: one wave per 32-column tile (two 16x16 halves), the
 // same GEMMs, epilogues (FS_EPI), deferred biases and residual stream, bit for bit
 template <int H>
-__global__ void __launch_bounds__(64 * (H / 32)) wide_trunk16_kernel(WideArgs w) {
-    constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;  // XA / XB row stride
-    constexpr int XS16 = XS + 4;                             // the LDS image's (== 8 mod 64)
+struct Trunk16 {
+    static constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;  // XA / XB row stride
+    static constexpr int XS16 = XS + 4;                             // the LDS image's (== 8 mod 64)
     static_assert(XS16 % 64 == 8, "trunk16 LDS row stride");
-    __shared__ __attribute__((aligned(16))) float X[16 * XS16];
+};
+
+// the trunk of one 16-row tile whose features are in the LDS image X (t16_pos layout); a
+// launch of NW > H / 32 waves leaves the extra ones to the barriers
+template <int H, int NW = H / 32>
+__device__ __forceinline__ void trunk16_run(float *X, const WideArgs &w, int64_t rowt) {
+    constexpr int XS = Trunk16<H>::XS, XS16 = Trunk16<H>::XS16;
     const FlowArgs &a = w.a;
     const int N = a.N;
     const PackLayout PL = pack_layout(N, H, a.nb, a.K);
     const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15;
     const int tile = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool act = NW == H / 32 || tile < H / 32;
+    const float *P = a.packed + (int64_t)w.layer * PL.stride;
+    const float *V = P + PL.vec;
+    const __amdgpu_buffer_rsrc_t W =
+        __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
+    int col[2], pos[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        col[c] = act ? 32 * tile + 16 * c + r : 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pos[c][i] = t16_pos(4 * q + i, col[c], XS16);
+    }
+    f32x4 hr[2], acc[2];
+    if (act) gemm16<XS16, FS_WIDE16_PD, false>(X, W, (int)(PL.win * 4), PL.kg_in, tile, hr);  // initial_layer
+    for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
+        const float *VB = V + PL.v_blocks + (int64_t)4 * H * jb;
+        float e0[2], e1[2], e2[2], e3[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            e0[c] = VB[col[c]];
+            e1[c] = VB[H + col[c]];
+            e2[c] = VB[2 * H + col[c]];
+            e3[c] = VB[3 * H + col[c]];
+        }
+        const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4);
+        __syncthreads();
+        if (act)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) X[pos[c][i]] = FS_EPI(hr[c][i], e0[c], e1[c]);
+        __syncthreads();
+        if (act) gemm16<XS16, FS_WIDE16_PD, false>(X, W, w0, PL.kg_h, tile, acc);
+        __syncthreads();
+        if (act)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) X[pos[c][i]] = FS_EPI(acc[c][i], e2[c], e3[c]);
+        __syncthreads();
+        if (act) gemm16<XS16, FS_WIDE16_PD, true>(X, W, w0 + (int)(PL.block_stride * 2), PL.kg_h, tile, hr);  // h += Lin1(t)
+    }
+    if (!act) return;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const float sh = V[col[c]];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w.XB[(rowt + 4 * q + i) * XS + col[c]] = hr[c][i] + sh;
+    }
+}
+
+template <int H>
+__global__ void __launch_bounds__(64 * (H / 32)) wide_trunk16_kernel(WideArgs w) {
+    constexpr int XS = Trunk16<H>::XS, XS16 = Trunk16<H>::XS16;
+    __shared__ __attribute__((aligned(16))) float X[16 * XS16];
+    const PackLayout PL = pack_layout(w.a.N, H, w.a.nb, w.a.K);
     const int64_t rowt = (int64_t)blockIdx.x * 16;
     const int nq = 2 * PL.kg_in;  // 16-byte quads of the used feature columns
     for (int e = threadIdx.x; e < 16 * nq; e += blockDim.x) {
@@ -990,62 +1074,16 @@ __global__ void __launch_bounds__(64 * (H / 32)) wide_trunk16_kernel(WideArgs w)
         *(f32x4 *)(X + rr * XS16 + 4 * qq) = o;
     }
     __syncthreads();
-    const float *P = a.packed + (int64_t)w.layer * PL.stride;
-    const float *V = P + PL.vec;
-    const __amdgpu_buffer_rsrc_t W =
-        __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
-    int col[2], pos[2][4];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        col[c] = 32 * tile + 16 * c + r;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pos[c][i] = t16_pos(4 * q + i, col[c], XS16);
-    }
-    f32x4 hr[2], acc[2];
-    gemm16<XS16, FS_WIDE16_PD, false>(X, W, (int)(PL.win * 4), PL.kg_in, tile, hr);  // initial_layer
-    for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
-        const float *VB = V + PL.v_blocks + (int64_t)4 * H * jb;
-        float e0[2], e1[2], e2[2], e3[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            e0[c] = VB[col[c]];
-            e1[c] = VB[H + col[c]];
-            e2[c] = VB[2 * H + col[c]];
-            e3[c] = VB[3 * H + col[c]];
-        }
-        const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4);
-        __syncthreads();
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) X[pos[c][i]] = FS_EPI(hr[c][i], e0[c], e1[c]);
-        __syncthreads();
-        gemm16<XS16, FS_WIDE16_PD, false>(X, W, w0, PL.kg_h, tile, acc);
-        __syncthreads();
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) X[pos[c][i]] = FS_EPI(acc[c][i], e2[c], e3[c]);
-        __syncthreads();
-        gemm16<XS16, FS_WIDE16_PD, true>(X, W, w0 + (int)(PL.block_stride * 2), PL.kg_h, tile, hr);  // h += Lin1(t)
-    }
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const float sh = V[col[c]];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w.XB[(rowt + 4 * q + i) * XS + col[c]] = hr[c][i] + sh;
-    }
+    trunk16_run<H>(X, w, rowt);
 }
 
-// One feature of uncond_spline_w: the same arithmetic, its log-det returned (0 outside).
+// One feature of uncond_spline_w at the value x: its log-det returned and the new value in
+// v (0 and x outside the tail bound).
 template <int K, bool INV>
-__device__ __forceinline__ float uncond_one(const float *__restrict__ U, float *CO, int cs, int D, int off,
-                                            const FlowArgs &a, bool &nan_any, int f) {
-    const int lane = threadIdx.x & 63;
+__device__ __forceinline__ float uncond_eval(const float *__restrict__ U, float x, const FlowArgs &a,
+                                             bool &nan_any, int f, float &v) {
     constexpr int K1 = K + 1;
     const float *T = U + (size_t)f * 3 * K1;
-    const int p = (2 * f + off) % D;
-    const float x = CO[lane * cs + p];
     const bool inside = (x >= a.negB) && (x <= a.B);
     const float *kn = INV ? T + K1 : T;
     int bin = -1;
@@ -1059,11 +1097,31 @@ __device__ __forceinline__ float uncond_one(const float *__restrict__ U, float *
     bool nd;
     rqs_eval<INV>(x, icw, cw1 - icw, ich, ch1 - ich, d0, d1, y, l, nd);
     if (inside) {
-        CO[lane * cs + p] = y;
+        v = y;
         nan_any |= nd;
         return l;
     }
+    v = x;
     return 0.f;
+}
+
+// ... on one row (co: its coordinates, p: the feature's physical index), updated in place
+template <int K, bool INV>
+__device__ __forceinline__ float uncond_at(const float *__restrict__ U, float *co, int p, const FlowArgs &a,
+                                           bool &nan_any, int f) {
+    const float x = co[p];
+    float v;
+    const float l = uncond_eval<K, INV>(U, x, a, nan_any, f, v);
+    if ((x >= a.negB) && (x <= a.B)) co[p] = v;
+    return l;
+}
+
+// ... on the lane's row of a 64-row block
+template <int K, bool INV>
+__device__ __forceinline__ float uncond_one(const float *__restrict__ U, float *CO, int cs, int D, int off,
+                                            const FlowArgs &a, bool &nan_any, int f) {
+    const int lane = threadIdx.x & 63;
+    return uncond_at<K, INV>(U, CO + lane * cs, (2 * f + off) % D, a, nan_any, f);
 }
 
 // (sampling modes) the start spread over features: workgroup (block, j) runs feature
@@ -1110,24 +1168,105 @@ __global__ void __launch_bounds__(kThreads) wide_start_s_kernel(WideArgs w) {
         for (int c = D + wid; c < 8 * PL.kg_in; c += kWaves) X[lane * XS + c] = 0.f;
 }
 
+// The start of a layer for the 16 rows of one trunk tile, then that tile's trunk: the
+// periodic features go straight into the trunk's LDS image, which saves the start launch
+// and the XA round trip.  Sampling modes write CO, LDU / LDU2 and LDW as
+// wide_start_s_kernel does, density LDW as wide_start_kernel: the same device code on the
+// same operands, so the pass stays bit-identical (tests/test_gpu_wide.py).
+template <int H>
+constexpr int trunk16s_waves() {  // twice the trunk's waves (the start's splines) up to 8
+    return 2 * (H / 32) < 8 ? 2 * (H / 32) : (H / 32 > 8 ? H / 32 : 8);
+}
+
+template <int H, int K, int MODE>
+__global__ void __launch_bounds__(64 * trunk16s_waves<H>()) wide_trunk16s_kernel(WideArgs w) {
+    constexpr int XS16 = Trunk16<H>::XS16;
+    __shared__ __attribute__((aligned(16))) float X[16 * XS16];
+    __shared__ float TU[MODE != MODE_DENSITY ? kMaxN * 3 * (K + 1) : 1];  // unconditional spline tables
+    const FlowArgs &a = w.a;
+    const int N = a.N, D = 2 * N;
+    const PackLayout PL = pack_layout(N, H, a.nb, a.K);
+    const int64_t rowt = (int64_t)blockIdx.x * 16;
+    if (w.pending)  // the previous final phase folded into LDW (wide_fold's order)
+        for (int e = threadIdx.x; e < 16 * kWaves; e += blockDim.x) {
+            const int64_t row = rowt + (e >> 3);
+            const int vw = e & (kWaves - 1);
+            float ld = w.LDW[row * kWaves + vw];
+            if (MODE != MODE_DENSITY) {
+                const float *lu_prev = (w.layer & 1) ? w.LDU : w.LDU2;
+                float su = 0.f;
+                for (int f = vw; f < N; f += kWaves) su += lu_prev[row * N + f];
+                ld += su;
+            }
+            w.LDW[row * kWaves + vw] = wide_fold<K, MODE>(w, row, vw, ld);
+        }
+    const float *P = a.packed + (int64_t)w.layer * PL.stride;
+    float *lu_cur = (w.layer & 1) ? w.LDU2 : w.LDU;
+    // every thread's coordinates first (independent loads in flight together), the
+    // sampling modes' spline tables staged in LDS (one coalesced pass), then the features
+    constexpr int NW = trunk16s_waves<H>(), NT = 64 * NW, IT = (16 * kMaxN + NT - 1) / NT;
+    float xv[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = (int)threadIdx.x + it * NT;
+        if (e < 16 * N) xv[it] = w.CO[(rowt + (e & 15)) * D + (2 * (e >> 4) + w.off) % D];
+    }
+    const float *U = P + PL.unc;
+    if (MODE != MODE_DENSITY) {
+        const int nu = N * 3 * (K + 1);
+        for (int e = threadIdx.x; e < nu; e += NT) TU[e] = U[e];
+        __syncthreads();
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = (int)threadIdx.x + it * NT;
+        if (e >= 16 * N) break;
+        const int rr = e & 15, f = e >> 4;
+        const int64_t row = rowt + rr;
+        float v = xv[it];
+        if (MODE != MODE_DENSITY) {
+            bool nan_any = false;
+            const float x = v;
+            lu_cur[row * N + f] = uncond_eval<K, true>(TU, x, a, nan_any, f, v);
+            if ((x >= a.negB) && (x <= a.B)) w.CO[row * D + (2 * f + w.off) % D] = v;
+            if (nan_any && row < a.nrows && a.err) atomicOr(a.err, 1);
+        }
+        const float sv = a.scale_pf * v;
+        X[t16_pos(rr, f, XS16)] = cosf(sv);
+        X[t16_pos(rr, N + f, XS16)] = sinf(sv);
+    }
+    const int npad = 8 * PL.kg_in - D;  // zero feature columns up to the k-group edge
+    for (int e = threadIdx.x; e < 16 * npad; e += blockDim.x) {
+        const int rr = e / npad;
+        X[t16_pos(rr, D + e - rr * npad, XS16)] = 0.f;
+    }
+    __syncthreads();
+    trunk16_run<H, NW>(X, w, rowt);
+}
+
 // Final layer + conditional spline of one feature unit (a transform feature, or a pair of
 // them for K <= 16) per wave, for one 64-row block; (density) also the unconditional
 // spline of the same-index identity feature(s).  WPB waves per workgroup share the
 // block's final-layer input staged in LDS.  Log-dets go to LDC / LDU per feature; the
 // next start / output launch adds them in the fused kernel's order (wide_fold).
-template <int H, int K, int MODE, int WPB>
+template <int H, int K, int MODE, int WPB, int RB = kRows>
 __global__ void __launch_bounds__(64 * WPB) wide_final_kernel(WideArgs w) {
+    // RB = 32 (K <= 16): 32-row blocks, half the MFMA chain per wave for batches that leave
+    // most of the chip idle; each chain's spline runs in both lane halves, the lower one stores
+    static_assert(RB == kRows || (RB == 32 && K <= 16), "32-row final blocks: feature pairs only");
     constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
+    constexpr int RM = RB - 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float *X = (float *)smem;
     const FlowArgs &a = w.a;
     const int N = a.N, D = 2 * N;
     const PackLayout PL = pack_layout(N, H, a.nb, a.K);
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & RM;
+    const bool store = RB == kRows || (threadIdx.x & 32) == 0;
     const int u = __builtin_amdgcn_readfirstlane((int)blockIdx.y * WPB + (int)(threadIdx.x >> 6));
-    const int64_t row0 = (int64_t)blockIdx.x * kRows;
+    const int64_t row0 = (int64_t)blockIdx.x * RB;
     const float *Xg = w.XB + row0 * XS;
-    for (int e = threadIdx.x; e < kRows * (H / 4); e += blockDim.x) {
+    for (int e = threadIdx.x; e < RB * (H / 4); e += blockDim.x) {
         const int rr = e / (H / 4), q = e - rr * (H / 4);
         *(f32x4 *)(X + rr * XS + 4 * q) = *(const f32x4 *)(Xg + rr * XS + 4 * q);
     }
@@ -1151,28 +1290,40 @@ __global__ void __launch_bounds__(64 * WPB) wide_final_kernel(WideArgs w) {
         const float *ba = V + PL.v_bf + 96 * ja;
         const float *bb = hb ? V + PL.v_bf + 96 * jb : ba + 16;
         f32x16 tS[2][1], tO[2][1];
-        final_tile_pair<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + TS, ba + 32 * TS, bb + 32 * TS, tS);
-        final_tile_pair<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + 1 - TS, ba + 32 * (1 - TS), bb + 32 * (1 - TS),
-                            tO);
-        lc[ja] = spline_from_tiles<XS, H, K, INV>(tS, tO, 0, X, W, (int)((PL.wd + (int64_t)ja * H * (K + 1)) * 4),
-                                                  V + PL.v_bd + ja * (K + 1), CO, cs, (2 * ja + 1 + off) % D, a,
-                                                  nan_any, pf);
-        if (hb)
-            lc[jb] = spline_from_tiles<XS, H, K, INV>(tS, tO, 16, X, W, (int)((PL.wd + (int64_t)jb * H * (K + 1)) * 4),
-                                                      V + PL.v_bd + jb * (K + 1), CO, cs, (2 * jb + 1 + off) % D, a,
-                                                      nan_any, pf);
+        if constexpr (RB == kRows) {
+            final_tile_pair<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + TS, ba + 32 * TS, bb + 32 * TS, tS);
+            final_tile_pair<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + 1 - TS, ba + 32 * (1 - TS),
+                                          bb + 32 * (1 - TS), tO);
+        } else {
+            final_tile_pair32<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + TS, ba + 32 * TS, bb + 32 * TS,
+                                            tS);
+            final_tile_pair32<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + 1 - TS, ba + 32 * (1 - TS),
+                                            bb + 32 * (1 - TS), tO);
+        }
+        const float la = spline_from_tiles<XS, H, K, INV, RM>(tS, tO, 0, X, W,
+                                                              (int)((PL.wd + (int64_t)ja * H * (K + 1)) * 4),
+                                                              V + PL.v_bd + ja * (K + 1), CO, cs, (2 * ja + 1 + off) % D,
+                                                              a, nan_any, pf);
+        if (store) lc[ja] = la;
+        if (hb) {
+            const float lb = spline_from_tiles<XS, H, K, INV, RM>(tS, tO, 16, X, W,
+                                                                  (int)((PL.wd + (int64_t)jb * H * (K + 1)) * 4),
+                                                                  V + PL.v_bd + jb * (K + 1), CO, cs,
+                                                                  (2 * jb + 1 + off) % D, a, nan_any, pf);
+            if (store) lc[jb] = lb;
+        }
     } else {
         const int j = u;
         lc[j] = cond_spline<XS, H, K, MODE != MODE_DENSITY, kWideFPD>(
             X, W, (int)(PL.wf * 4), PL.kg_h, V + PL.v_bf + 96 * j, (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
             V + PL.v_bd + j * (K + 1), CO, cs, (2 * j + 1 + off) % D, j, a, nan_any, pf);
     }
-    if (MODE == MODE_DENSITY) {
+    if (MODE == MODE_DENSITY && store) {
         float *lu = w.LDU + (row0 + lane) * N;
         for (int f = u * UPF; f < (u + 1) * UPF && f < N; ++f)
-            lu[f] = uncond_one<K, false>(P + PL.unc, CO, cs, D, off, a, nan_any, f);
+            lu[f] = uncond_at<K, false>(P + PL.unc, CO + lane * cs, (2 * f + off) % D, a, nan_any, f);
     }
-    if (nan_any && row0 + lane < a.nrows && a.err) atomicOr(a.err, 1);
+    if (nan_any && store && row0 + lane < a.nrows && a.err) atomicOr(a.err, 1);
 }
 
 template <int K, int MODE>
@@ -1453,16 +1604,31 @@ static int device_cus() {
     return v;
 }
 
-// the trunk on 16-row tiles (wide_trunk16_kernel, default) or 32-row ones (FS_WIDE_TRUNK16=0,
-// fs_set_wide_trunk16); bit-identical either way
+// the trunk on 16-row tiles with the layer's start merged in (wide_trunk16s_kernel, 2, the
+// default), on 16-row tiles after a start launch (1) or on 32-row ones (0); FS_WIDE_TRUNK16,
+// fs_set_wide_trunk16.  Bit-identical in every setting.
 static std::atomic<int> g_trunk16{-1};
-static bool wide_trunk16() {
+static int wide_trunk16() {
     int v = g_trunk16.load(std::memory_order_relaxed);
     if (v < 0) {
         const char *e = getenv("FS_WIDE_TRUNK16");
         int expect = -1;
-        g_trunk16.compare_exchange_strong(expect, (e && e[0] == '0') ? 0 : 1);
+        g_trunk16.compare_exchange_strong(expect, (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2);
         v = g_trunk16.load(std::memory_order_relaxed);
+    }
+    return v;
+}
+
+// the final phase on 32-row blocks for small batches (default, or FS_WIDE_FINAL32=0 /
+// fs_set_wide_final32(0) for 64-row blocks); bit-identical either way
+static std::atomic<int> g_final32{-1};
+static bool wide_final32() {
+    int v = g_final32.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char *e = getenv("FS_WIDE_FINAL32");
+        int expect = -1;
+        g_final32.compare_exchange_strong(expect, (e && e[0] == '0') ? 0 : 1);
+        v = g_final32.load(std::memory_order_relaxed);
     }
     return v != 0;
 }
@@ -1638,7 +1804,13 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     // 16-row trunk tiles while they fit the chip in one round (4096 rows on 256 CUs): past
     // that the 32-row tiles' higher arithmetic intensity wins (8192 rows: 9.0 vs 11.6 ms per
     // A1 N=16 pass, profiles/r04/)
-    const bool trunk16 = wide_trunk16() && R / 16 <= device_cus();
+    const int trunk16 = R / 16 <= device_cus() ? wide_trunk16() : 0;
+    // 32-row final-phase blocks (feature pairs) while twice the 64-row grid fits the chip
+    const int fgy = (units + WPW - 1) / WPW;
+    const bool final32 = K <= 16 && wide_final32() && (R / 32) * fgy <= device_cus();
+    const void *final_fn = (const void *)wide_final_kernel<H, K, MODE, WPW>;
+    if constexpr (K <= 16)
+        if (final32) final_fn = (const void *)wide_final_kernel<H, K, MODE, WPW, 32>;
     std::vector<WideLaunch> seq;
     seq.reserve(4 + (size_t)a.L * 3);
     auto add = [&](const void *f, dim3 g, dim3 b, unsigned lds) { seq.push_back({f, g, b, lds, w}); };
@@ -1647,22 +1819,27 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
         w.layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
         if (MODE != MODE_DENSITY) w.off = (w.off + N) % D;
         w.pending = s > 0;
-        if (MODE == MODE_DENSITY)
+        if (trunk16 == 2)
+            add((const void *)wide_trunk16s_kernel<H, K, MODE>, dim3((unsigned)(R / 16)), dim3(64 * trunk16s_waves<H>()),
+                0);
+        else if (MODE == MODE_DENSITY)
             add((const void *)wide_start_kernel<H, K, MODE>, dim3(nblk), dim3(kThreads), 0);
         else
             add((const void *)wide_start_s_kernel<H, K, MODE>, dim3(nblk, kWaves), dim3(kThreads), 0);
-        if (trunk16)
+        if (trunk16 == 1)
             add((const void *)wide_trunk16_kernel<H>, dim3((unsigned)(R / 16)), dim3(64 * (H / 32)), 0);
-        else
+        else if (trunk16 == 0)
             add((const void *)wide_trunk_kernel<H>, dim3((unsigned)(R / 32)), dim3(64 * (H / 32)), 0);
-        add((const void *)wide_final_kernel<H, K, MODE, WPW>, dim3(nblk, (units + WPW - 1) / WPW), dim3(64 * WPW),
-            fin_lds);
+        if (final32)
+            add(final_fn, dim3((unsigned)(R / 32), fgy), dim3(64 * WPW), fin_lds / 2);
+        else
+            add(final_fn, dim3(nblk, fgy), dim3(64 * WPW), fin_lds);
         if (MODE == MODE_DENSITY) w.off = (w.off + N) % D;
     }
     w.pending = 1;
     add((const void *)wide_output_kernel<K, MODE>, dim3(nblk), dim3(kThreads), 0);
     w.off = w.layer = w.jb = w.pending = 0;
-    hipError_t e = wide_run(seq, wide_key(w, seq.front().func, H, K, MODE, trunk16 ? 1 : 0), st);
+    hipError_t e = wide_run(seq, wide_key(w, seq.front().func, H, K, MODE, trunk16 | (final32 ? 4 : 0)), st);
     if (e == hipSuccess) used = true;
     return e;
 }
@@ -1682,8 +1859,14 @@ static hipError_t wide_pass_mode(const FlowArgs &a, int N, int H, int K, hipStre
 using namespace fs;
 
 int32_t fs_set_wide_trunk16_impl(int32_t on) {
-    const int32_t prev = wide_trunk16() ? 1 : 0;
-    if (on >= 0) g_trunk16.store(on ? 1 : 0, std::memory_order_relaxed);
+    const int32_t prev = wide_trunk16();
+    if (on >= 0) g_trunk16.store(on > 2 ? 2 : on, std::memory_order_relaxed);
+    return prev;
+}
+
+int32_t fs_set_wide_final32_impl(int32_t on) {
+    const int32_t prev = wide_final32() ? 1 : 0;
+    if (on >= 0) g_final32.store(on ? 1 : 0, std::memory_order_relaxed);
     return prev;
 }
 

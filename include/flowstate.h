@@ -271,11 +271,17 @@ int64_t fs_set_wide_rows(int64_t rows);
 /* Kernel-variant switches for A/B measurements and bit-identity tests, process-wide; each
  * returns the previous value (a negative argument only reads it).  The results do not
  * depend on them.
- * fs_set_wide_trunk16: 1 (default, or FS_WIDE_TRUNK16) = the wide path's ResidualNet on
- *   16-row tiles (v_mfma_f32_16x16x4_f32, twice the workgroups), 0 = 32-row tiles.
+ * fs_set_wide_trunk16: 2 (default, or FS_WIDE_TRUNK16) = the wide path's ResidualNet on
+ *   16-row tiles (v_mfma_f32_16x16x4_f32, twice the workgroups) with each layer's start
+ *   phase merged into the trunk launch, 1 = 16-row tiles after a separate start launch,
+ *   0 = 32-row tiles.
+ * fs_set_wide_final32: 1 (default, or FS_WIDE_FINAL32) = the wide path's final phase on
+ *   32-row blocks when twice the 64-row grid fits the chip (spline bins K <= 16), 0 = always
+ *   64-row blocks.
  * fs_set_lean_gemm: 1 (default, or FS_LEAN_GEMM) = the training products on the lean
  *   kernels (32-bit buffer offsets), 0 = the generic strided kernels. */
 int32_t fs_set_wide_trunk16(int32_t on);
+int32_t fs_set_wide_final32(int32_t on);
 int32_t fs_set_lean_gemm(int32_t on);
 
 /* ------------------------------------------------------------------ */

@@ -127,7 +127,8 @@ def test_fused_steps_bit_identical(N, kw, C):
 
 
 class trunk16:
-    """The wide path's trunk on 16-row (1) or 32-row (0) tiles for a block."""
+    """The wide path's trunk for a block: 16-row tiles with the layer's start merged in (2),
+    16-row tiles after a start launch (1) or 32-row tiles (0)."""
 
     def __init__(self, on):
         self.on = on
@@ -142,16 +143,53 @@ class trunk16:
 @pytest.mark.parametrize("N,kw,B", [(64, A1, 1000), (16, A1, 4096), (64, A2, 200), (3, dict(L=2, H=32, nb=2, K=5), 77)],
                          ids=["a1-n64-1000", "a1-n16-4096", "a2-n64-200", "n3-h32-77"])
 def test_trunk16_bit_identical_to_trunk32(N, kw, B):
-    """The 16-row trunk (v_mfma_f32_16x16x4_f32 fed the 32x32x2 k order) against the
-    32-row one, density and sampling, and both against the fused kernel."""
+    """The 16-row trunk (v_mfma_f32_16x16x4_f32 fed the 32x32x2 k order), with and without
+    the start merged in, against the 32-row one, density and sampling, and all against
+    the fused kernel."""
     dims, sd, m = _model(N, kw, seed=11)
     g = torch.Generator().manual_seed(B)
     x = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
     zb = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
     outs = []
     with wide_rows(16384):
-        for on in (1, 0):
+        for on in (2, 1, 0):
             with trunk16(on):
+                outs.append([m.log_prob(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)])
+    with wide_rows(0):
+        outs.append([m.log_prob(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)])
+    torch.cuda.synchronize()
+    for a, b, c, d in zip(*outs):
+        assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(a, d)
+
+
+class final32:
+    """The wide path's final phase on 32-row blocks (1, small batches) or 64-row ones (0)."""
+
+    def __init__(self, on):
+        self.on = on
+
+    def __enter__(self):
+        self.prev = _lib.load().fs_set_wide_final32(self.on)
+
+    def __exit__(self, *exc):
+        _lib.load().fs_set_wide_final32(self.prev)
+
+
+@pytest.mark.parametrize("N,kw,B", [(64, A2, 200), (64, A2, 1000), (3, dict(L=2, H=32, nb=2, K=5), 77),
+                                    (16, dict(L=3, H=64, nb=1, K=8), 333)],
+                         ids=["a2-n64-200", "a2-n64-1000", "n3-h32-77", "n16-h64-333"])
+def test_final32_bit_identical_to_final64(N, kw, B):
+    """The final phase on 32-row blocks (one row tile per wave, each chain's spline in both
+    lane halves) against 64-row blocks and the fused kernel, density and sampling, with a
+    few out-of-bound inputs among the rows."""
+    dims, sd, m = _model(N, kw, seed=12)
+    g = torch.Generator().manual_seed(B + 1)
+    x = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B * 1.001).cuda()  # a few rows outside the bound
+    zb = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
+    outs = []
+    with wide_rows(16384):
+        for on in (1, 0):
+            with final32(on):
                 outs.append([m.log_prob(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)])
     with wide_rows(0):
         outs.append([m.log_prob(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)])
