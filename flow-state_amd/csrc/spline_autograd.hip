@@ -18,6 +18,10 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
+#include <atomic>
+
 #include "fs_internal.h"
 
 #pragma clang fp contract(off)
@@ -90,18 +94,15 @@ __device__ __forceinline__ int find_bin(float x, const float *knots) {
     return b < 0 ? 0 : (b > K - 1 ? K - 1 : b);
 }
 
-// one element: x inside [-B, B] (callers route the outside identity themselves)
+// one element from its built knots (wc: width knots, hc: height knots); x inside [-B, B]
 template <int K, bool INV>
-__device__ __forceinline__ void rqs_point(float xv, const float *uw, const float *uh, const float *dd, float B,
-                                          float &out, float &lad, int32_t *nan_flag) {
-    Knots<K> W, Hh;
-    build_knots<K>(uw, B, W);
-    build_knots<K>(uh, B, Hh);
-    const int b = find_bin<K>(xv, INV ? Hh.c : W.c);
+__device__ __forceinline__ void rqs_eval_knots(float xv, const float *wc, const float *hc, const float *dd,
+                                               float &out, float &lad, int32_t *nan_flag) {
+    const int b = find_bin<K>(xv, INV ? hc : wc);
     const float d0 = kMin + softplus(dd[b]), d1 = kMin + softplus(dd[b + 1]);
     float icw, cw1, ich, ch1;
-    pick_bin<K>(W.c, b, icw, cw1);
-    pick_bin<K>(Hh.c, b, ich, ch1);
+    pick_bin<K>(wc, b, icw, cw1);
+    pick_bin<K>(hc, b, ich, ch1);
     const float ibw = cw1 - icw, ih = ch1 - ich;
     const float s = ih / ibw;
     float th;
@@ -127,6 +128,16 @@ __device__ __forceinline__ void rqs_point(float xv, const float *uw, const float
         out = ich + ih * (s * th * th + d0 * t) / den;
         lad = l;
     }
+}
+
+// one element: x inside [-B, B] (callers route the outside identity themselves)
+template <int K, bool INV>
+__device__ __forceinline__ void rqs_point(float xv, const float *uw, const float *uh, const float *dd, float B,
+                                          float &out, float &lad, int32_t *nan_flag) {
+    Knots<K> W, Hh;
+    build_knots<K>(uw, B, W);
+    build_knots<K>(uh, B, Hh);
+    rqs_eval_knots<K, INV>(xv, W.c, Hh.c, dd, out, lad, nan_flag);
 }
 
 template <int K, bool INV>
@@ -163,19 +174,17 @@ __device__ __forceinline__ void knots_backward(const Knots<K> &kn, const float *
     for (int j = 0; j < K; ++j) gu[j] = kn.p[j] * (c1 * gw[j] - dot);
 }
 
-// adjoints of one element inside [-B, B]: gx, guw[K], guh[K], gud[K+1]
+// the adjoint core of one element inside [-B, B] from its built knots: gx and the
+// adjoints of the bin's knots (gcw / gch over c[0..K]) and derivative logits (gud)
 template <int K, bool INV>
-__device__ __forceinline__ void rqs_point_bwd(float xv, const float *uw, const float *uh, const float *dd, float B,
-                                              float go, float gl, float &gx, float *guw, float *guh, float *gud) {
-    Knots<K> W, Hh;
-    build_knots<K>(uw, B, W);
-    build_knots<K>(uh, B, Hh);
-    const int b = find_bin<K>(xv, INV ? Hh.c : W.c);
+__device__ __forceinline__ void rqs_bwd_core(float xv, const float *wc, const float *hc, const float *dd, float go,
+                                             float gl, float &gx, float *gcw, float *gch, float *gud) {
+    const int b = find_bin<K>(xv, INV ? hc : wc);
     const float e0 = dd[b], e1 = dd[b + 1];
     const float d0 = kMin + softplus(e0), d1 = kMin + softplus(e1);
     float icw, cw1, ich, ch1;
-    pick_bin<K>(W.c, b, icw, cw1);
-    pick_bin<K>(Hh.c, b, ich, ch1);
+    pick_bin<K>(wc, b, icw, cw1);
+    pick_bin<K>(hc, b, ich, ch1);
     const float ibw = cw1 - icw, ih = ch1 - ich;
     const float s = ih / ibw;
     float th;
@@ -258,14 +267,11 @@ __device__ __forceinline__ void rqs_point_bwd(float xv, const float *uw, const f
     g_ih += g_s / ibw;
     g_ibw -= g_s * s / ibw;
     gx = g_x;
-    float gcw[K + 1], gch[K + 1];
 #pragma unroll
     for (int k = 0; k <= K; ++k) {
         gcw[k] = (k == b) ? (g_icw - g_ibw) : ((k == b + 1) ? g_ibw : 0.f);
         gch[k] = (k == b) ? (g_ich - g_ih) : ((k == b + 1) ? g_ih : 0.f);
     }
-    knots_backward<K>(W, gcw, B, guw);
-    knots_backward<K>(Hh, gch, B, guh);
 #pragma unroll
     for (int k = 0; k <= K; ++k) {
         float g = 0.f;
@@ -275,6 +281,18 @@ __device__ __forceinline__ void rqs_point_bwd(float xv, const float *uw, const f
     }
 }
 
+// adjoints of one element inside [-B, B]: gx, guw[K], guh[K], gud[K+1]
+template <int K, bool INV>
+__device__ __forceinline__ void rqs_point_bwd(float xv, const float *uw, const float *uh, const float *dd, float B,
+                                              float go, float gl, float &gx, float *guw, float *guh, float *gud) {
+    Knots<K> W, Hh;
+    build_knots<K>(uw, B, W);
+    build_knots<K>(uh, B, Hh);
+    float gcw[K + 1], gch[K + 1];
+    rqs_bwd_core<K, INV>(xv, W.c, Hh.c, dd, go, gl, gx, gcw, gch, gud);
+    knots_backward<K>(W, gcw, B, guw);
+    knots_backward<K>(Hh, gch, B, guh);
+}
 
 template <int K, bool INV>
 __global__ __launch_bounds__(256) void rqs_backward_kernel(int64_t M, const float *__restrict__ x, const float *__restrict__ uw,
@@ -684,6 +702,300 @@ __global__ __launch_bounds__(256) void coupling_pair_step_kernel(CouplingArgs cs
         features_row(cd2, d.out, t_d2, row, rb);
 }
 
+// ---------------------------------------------------------------------------
+// The same two launches with each row's splines spread over more waves
+// (fs_set_coupling_waves, default on).  A spline's cost is mostly building its two knot
+// sets (softmax + cumulative sum over K, each element a precise division), one lane per
+// feature in a serial chain; here wave h of a pair builds one set (h = 0 widths, h = 1
+// heights), the pair swaps the knots through LDS and finishes the element from them.
+// Every value comes from the same device functions on the same operands, so the
+// results are bit-identical to coupling_pair_step_kernel / coupling_bwd_step_kernel
+// (tests/test_gpu_train.py).
+
+// knots c[0..K] of wave slot w (lane-major in kx: conflict-free)
+template <int K>
+__device__ __forceinline__ void knots_put(float *kx, int w, const float *c) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k <= K; ++k) kx[(w * (K + 1) + k) * 64 + lane] = c[k];
+}
+
+template <int K>
+__device__ __forceinline__ void knots_get(const float *kx, int w, float *c) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k <= K; ++k) c[k] = kx[(w * (K + 1) + k) * 64 + lane];
+}
+
+// this wave's knot set (own) and its partner's (slot w ^ 1) as (width, height) knots
+template <int K>
+__device__ __forceinline__ void knots_pair(float *kx, int w, int h, const float *own, float *wc, float *hc) {
+    knots_put<K>(kx, w, own);
+    __syncthreads();
+    float oc[K + 1];
+    knots_get<K>(kx, w ^ 1, oc);
+#pragma unroll
+    for (int k = 0; k <= K; ++k) {
+        wc[k] = h == 0 ? own[k] : oc[k];
+        hc[k] = h == 0 ? oc[k] : own[k];
+    }
+}
+
+// sample_post_row on a wave pair (h: this wave's knot set); the lower wave stores
+template <int K>
+__device__ __forceinline__ void sample_post_row2(const CouplingArgs &c, const SamplePostArgs &s, int64_t row, float *rb,
+                                                 float *kx, int h) {
+    const int lane = threadIdx.x & 63;
+    float sc = 0.f;
+    for (int j0 = 0; j0 < c.n; j0 += 64) {  // uniform trip count: the pair meets at its barriers
+        const int j = j0 + lane;
+        const bool on = j < c.n;
+        const int jj = on ? j : 0;
+        const int pt = (int)c.tr[jj];
+        if (h == 0 && on) {
+            const int pi = (int)c.id[jj];
+            rb[pi] = s.out[row * c.D + pi];  // written by this layer's pre launch
+        }
+        const float xt = s.out[row * c.D + pt];
+        const float *p = s.params + (row * c.n + jj) * (3 * K + 1);
+        Knots<K> kn;
+        {
+            float u[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) u[k] = p[h * K + k] / c.sq;  // cond_params' half
+            build_knots<K>(u, c.bound, kn);
+        }
+        float wc[K + 1], hc[K + 1];
+        knots_pair<K>(kx, h, h, kn.c, wc, hc);
+        float yt = xt, lt = 0.f;
+        if (on && xt >= -c.bound && xt <= c.bound)
+            rqs_eval_knots<K, true>(xt, wc, hc, p + 2 * K, yt, lt, h == 0 ? s.nan_flag : nullptr);
+        if (h == 0 && on) {
+            s.out[row * c.D + pt] = yt;
+            rb[pt] = yt;
+        }
+        sc += on ? lt : 0.f;
+        __syncthreads();  // the partner has read this round's knots
+    }
+    sc = wave_sum(sc);
+    if (h == 0 && lane == 0) s.lq_out[row] = (s.lq_in ? s.lq_in[row] : 0.f) - (s.lad_u[row] + sc);
+}
+
+// sample_pre_row on a wave pair: the lower wave stores the cosines and the row, the upper
+// one the sines
+template <int K>
+__device__ __forceinline__ void sample_pre_row2(const CouplingArgs &c, const SamplePreArgs &s, int64_t row,
+                                                const float *zr, float *kx, int h) {
+    const int lane = threadIdx.x & 63;
+    float su = 0.f;
+    for (int j0 = 0; j0 < c.n; j0 += 64) {
+        const int j = j0 + lane;
+        const bool on = j < c.n;
+        const int jj = on ? j : 0;
+        const int pi = (int)c.id[jj], pt = (int)c.tr[jj];
+        const float xi = zr[(pi + c.split) % c.D];
+        Knots<K> kn;
+        build_knots<K>((h == 0 ? s.uw : s.uh) + jj * K, c.bound, kn);
+        float wc[K + 1], hc[K + 1];
+        knots_pair<K>(kx, h, h, kn.c, wc, hc);
+        float yi = xi, li = 0.f;
+        if (on && xi >= -c.bound && xi <= c.bound)
+            rqs_eval_knots<K, true>(xi, wc, hc, s.ud + jj * (K + 1), yi, li, h == 0 ? s.nan_flag : nullptr);
+        const float v = c.scale * yi;
+        if (on) {
+            if (h == 0) {
+                s.t[row * 2 * c.n + j] = cosf(v);
+                s.out[row * c.D + pi] = yi;
+                s.out[row * c.D + pt] = zr[(pt + c.split) % c.D];
+            } else {
+                s.t[row * 2 * c.n + c.n + j] = sinf(v);
+            }
+        }
+        su += on ? li : 0.f;
+        __syncthreads();
+    }
+    su = wave_sum(su);
+    if (h == 0 && lane == 0) s.lad_u[row] = su;
+}
+
+// density_fwd_row on a wave pair: wave 0 the conditional spline of the transform half,
+// wave 1 the unconditional one of the identity half; the log-det sums meet in red
+template <int K>
+__device__ __forceinline__ float density_fwd_row2(const CouplingArgs &c, const DensityFwdArgs &d, int64_t row, float *rb,
+                                                  float *red, int h) {
+    const int lane = threadIdx.x & 63;
+    const float *xr = d.x + row * c.D;
+    float sl = 0.f;
+    for (int j = lane; j < c.n; j += 64) {
+        if (h == 0) {
+            const int pt = (int)c.tr[j];
+            const float xt = xr[pt];
+            float yt = xt, lt = 0.f;
+            if (xt >= -c.bound && xt <= c.bound) {
+                const float *p = d.params + (row * c.n + j) * (3 * K + 1);
+                float w[K], hh[K];
+                cond_params<K>(p, c.sq, w, hh);
+                rqs_point<K, false>(xt, w, hh, p + 2 * K, c.bound, yt, lt, nullptr);
+            }
+            d.out[row * c.D + (pt + c.D - c.split) % c.D] = yt;
+            rb[(pt + c.D - c.split) % c.D] = yt;
+            sl += lt;
+        } else {
+            const int pi = (int)c.id[j];
+            const float xi = xr[pi];
+            float yi = xi, li = 0.f;
+            if (xi >= -c.bound && xi <= c.bound)
+                rqs_point<K, false>(xi, d.uw + j * K, d.uh + j * K, d.ud + j * (K + 1), c.bound, yi, li, nullptr);
+            d.out[row * c.D + (pi + c.D - c.split) % c.D] = yi;
+            rb[(pi + c.D - c.split) % c.D] = yi;
+            sl += li;
+        }
+    }
+    sl = wave_sum(sl);
+    if (h == 1 && lane == 0) red[0] = sl;
+    return sl;
+}
+
+template <int K>
+__global__ __launch_bounds__(128) void coupling_pair_step2_kernel(CouplingArgs cs, SamplePostArgs s, CouplingArgs cs2,
+                                                                  SamplePreArgs s2, CouplingArgs cd, DensityFwdArgs d,
+                                                                  CouplingArgs cd2, float *t_d2, unsigned nb0) {
+    __shared__ float rb[kCplMaxD];
+    __shared__ float kx[2 * (K + 1) * 64];
+    __shared__ float red[1];
+    const int h = (int)(threadIdx.x >> 6);
+    const bool dens = blockIdx.x >= nb0;
+    const int64_t row = (int64_t)(dens ? blockIdx.x - nb0 : blockIdx.x);
+    if (!dens) {
+        if (row >= cs.rows) return;  // whole workgroup: no barrier is left waiting
+        sample_post_row2<K>(cs, s, row, rb, kx, h);
+        __syncthreads();  // the row in LDS
+        sample_pre_row2<K>(cs2, s2, row, rb, kx, h);
+        return;
+    }
+    if (row >= cd.rows) return;
+    const float sl = density_fwd_row2<K>(cd, d, row, rb, red, h);
+    __syncthreads();  // the row in LDS, the unconditional log-det sum in red
+    const int lane = threadIdx.x & 63;
+    if (h == 0 && lane == 0) d.lq_out[row] = (d.lq_in ? d.lq_in[row] : 0.f) + (sl + red[0]);  // density_fwd_row's order
+    for (int j = lane; j < cd2.n; j += 64) {  // features_row, cosines on wave 0, sines on wave 1
+        const float v = cd2.scale * rb[cd2.id[j]];
+        if (h == 0)
+            t_d2[row * 2 * cd2.n + j] = cosf(v);
+        else
+            t_d2[row * 2 * cd2.n + cd2.n + j] = sinf(v);
+    }
+}
+
+// density_bwd_row on four waves: part = wave >> 1 (0: the conditional spline's adjoints,
+// 1: the unconditional one's, as in density_bwd_row), h = wave & 1 the knot set it builds
+// and back-propagates (0 widths, 1 heights); the core adjoints are computed by both waves
+// of a part from the swapped knots
+template <int K>
+__device__ __forceinline__ void density_bwd_row4(const CouplingArgs &c, const float *__restrict__ x,
+                                                 const float *__restrict__ params, const float *__restrict__ uw,
+                                                 const float *__restrict__ uh, const float *__restrict__ ud,
+                                                 const float *gor, const float *__restrict__ g_lq, float *gx,
+                                                 float *g_params, float *g_u, int64_t row, float *kx) {
+    const int lane = threadIdx.x & 63, wv = (int)(threadIdx.x >> 6), part = wv >> 1, h = wv & 1;
+    const float *xr = x + row * c.D;
+    const float gl = g_lq ? g_lq[row] : 0.f;
+    constexpr int P = 3 * K + 1;
+    for (int j0 = 0; j0 < c.n; j0 += 64) {
+        const int j = j0 + lane;
+        const bool on = j < c.n;
+        const int jj = on ? j : 0;
+        const int pi = (int)c.id[jj], pt = (int)c.tr[jj];
+        const int pos = part == 0 ? pt : pi;
+        const float xv = xr[pos];
+        const float go = gor ? gor[(pos + c.D - c.split) % c.D] : 0.f;
+        const float *p = params + (row * c.n + jj) * P;
+        Knots<K> kn;
+        if (part == 0) {
+            float u[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) u[k] = p[h * K + k] / c.sq;  // cond_params' half
+            build_knots<K>(u, c.bound, kn);
+        } else {
+            build_knots<K>((h == 0 ? uw : uh) + jj * K, c.bound, kn);
+        }
+        float wc[K + 1], hc[K + 1];
+        knots_pair<K>(kx, wv, h, kn.c, wc, hc);
+        const bool inside = xv >= -c.bound && xv <= c.bound;
+        float *gp = g_params + (row * c.n + jj) * P;
+        // g_u row: [uw n*K | uh n*K | ud n*(K+1)], the parameters' own layouts back to back
+        float *guw = g_u + row * c.n * P + jj * K;
+        float *guh = guw + c.n * K;
+        float *gud = g_u + row * c.n * P + 2 * c.n * K + jj * (K + 1);
+        if (on && inside) {
+            float g, gcw[K + 1], gch[K + 1], gd[K + 1];
+            rqs_bwd_core<K, false>(xv, wc, hc, part == 0 ? p + 2 * K : ud + jj * (K + 1), go, gl, g, gcw, gch, gd);
+            float gsel[K + 1], gk[K];
+#pragma unroll
+            for (int k = 0; k <= K; ++k) gsel[k] = h == 0 ? gcw[k] : gch[k];
+            knots_backward<K>(kn, gsel, c.bound, gk);
+            if (part == 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) gp[h * K + k] = gk[k] / c.sq;
+                if (h == 0) {
+                    gx[row * c.D + pt] = g;
+#pragma unroll
+                    for (int k = 0; k <= K; ++k) gp[2 * K + k] = gd[k];
+                }
+            } else {
+                float *gu = h == 0 ? guw : guh;
+#pragma unroll
+                for (int k = 0; k < K; ++k) gu[k] = gk[k];
+                if (h == 0) {
+                    gx[row * c.D + pi] = g;
+#pragma unroll
+                    for (int k = 0; k <= K; ++k) gud[k] = gd[k];
+                }
+            }
+        } else if (on) {
+            if (part == 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) gp[h * K + k] = 0.f;
+                if (h == 0) {
+                    gx[row * c.D + pt] = go;
+#pragma unroll
+                    for (int k = 0; k <= K; ++k) gp[2 * K + k] = 0.f;
+                }
+            } else {
+                float *gu = h == 0 ? guw : guh;
+#pragma unroll
+                for (int k = 0; k < K; ++k) gu[k] = 0.f;
+                if (h == 0) {
+                    gx[row * c.D + pi] = go;
+#pragma unroll
+                    for (int k = 0; k <= K; ++k) gud[k] = 0.f;
+                }
+            }
+        }
+        __syncthreads();  // the partners have read this round's knots
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void coupling_bwd_step4_kernel(CouplingArgs cf, const float *__restrict__ xf,
+                                                                 const float *__restrict__ g_t, float *gxf,
+                                                                 const float *__restrict__ gx_add, CouplingArgs c,
+                                                                 const float *__restrict__ x,
+                                                                 const float *__restrict__ params,
+                                                                 const float *__restrict__ uw,
+                                                                 const float *__restrict__ uh,
+                                                                 const float *__restrict__ ud,
+                                                                 const float *__restrict__ g_lq, float *gx,
+                                                                 float *g_params, float *g_u) {
+    __shared__ float rb[kCplMaxDB];
+    __shared__ float kx[4 * (K + 1) * 64];
+    const int64_t row = blockIdx.x;
+    if (row >= c.rows) return;  // whole workgroup
+    if (threadIdx.x < 64) features_bwd_row(cf, xf, g_t, gxf, gx_add, row, rb);
+    __syncthreads();
+    density_bwd_row4<K>(c, x, params, uw, uh, ud, rb, g_lq, gx, g_params, g_u, row, kx);
+}
+
 }  // namespace fs
 
 using namespace fs;
@@ -728,6 +1040,26 @@ hipError_t fs_rqs_backward_impl(int64_t M, int K, int inverse, const float *x, c
     FS_RQS_K(FS_B)
 #undef FS_B
     return hipErrorInvalidValue;
+}
+
+// the training step's coupling launches on two / four waves per row (1, default, or
+// FS_COUPLING_WAVES / fs_set_coupling_waves) or one / two (0); bit-identical either way
+static std::atomic<int> g_cpl_waves{-1};
+static bool coupling_waves() {
+    int v = g_cpl_waves.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char *e = getenv("FS_COUPLING_WAVES");
+        int expect = -1;
+        g_cpl_waves.compare_exchange_strong(expect, (e && e[0] == '0') ? 0 : 1);
+        v = g_cpl_waves.load(std::memory_order_relaxed);
+    }
+    return v != 0;
+}
+
+int32_t fs_set_coupling_waves_impl(int32_t on) {
+    const int32_t prev = coupling_waves() ? 1 : 0;
+    if (on >= 0) g_cpl_waves.store(on ? 1 : 0, std::memory_order_relaxed);
+    return prev;
 }
 
 static fs::CouplingArgs coupling_args(const fs_coupling *c) {
@@ -790,10 +1122,15 @@ hipError_t fs_coupling_bwd_step_impl(const fs_coupling *fp, const float *xf, con
     if (af.rows != a.rows || af.D != a.D || a.D > kCplMaxDB) return hipErrorInvalidValue;
     if (a.rows <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((a.rows + kCplRows - 1) / kCplRows);
+    const bool four = coupling_waves() && a.rows <= 0x7fffffff;
 #define FS_DB(KK)                                                                                                  \
     if (cp->K == KK) {                                                                                             \
-        hipLaunchKernelGGL(coupling_bwd_step_kernel<KK>, dim3(grid), dim3(128 * kCplRows), 0, st, af, xf, g_t, gxf, \
-                           gx_add, a, x, params, uw, uh, ud, g_lq, gx, g_params, g_u);                            \
+        if (four)                                                                                                  \
+            hipLaunchKernelGGL(coupling_bwd_step4_kernel<KK>, dim3((unsigned)a.rows), dim3(256), 0, st, af, xf, g_t, \
+                               gxf, gx_add, a, x, params, uw, uh, ud, g_lq, gx, g_params, g_u);                   \
+        else                                                                                                       \
+            hipLaunchKernelGGL(coupling_bwd_step_kernel<KK>, dim3(grid), dim3(128 * kCplRows), 0, st, af, xf, g_t,  \
+                               gxf, gx_add, a, x, params, uw, uh, ud, g_lq, gx, g_params, g_u);                   \
         return hipGetLastError();                                                                                  \
     }
     FS_DB(5) FS_DB(8) FS_DB(15) FS_DB(32)
@@ -879,6 +1216,20 @@ hipError_t fs_coupling_pair_step_impl(const fs_coupling *sp, const float *params
     default: return hipErrorInvalidValue;                                                               \
     }                                                                                                   \
     return hipGetLastError();
+    if (coupling_waves() && sp->rows + dp->rows <= 0x7fffffff) {  // one row per two-wave workgroup
+        const fs::CouplingArgs as = coupling_args(sp), ad = coupling_args(dp);
+        if (sp->K != dp->K || as.rows < 0 || ad.rows < 0) return hipErrorInvalidValue;
+        const unsigned nb0 = (unsigned)as.rows, nb = nb0 + (unsigned)ad.rows;
+        if (nb == 0) return hipSuccess;
+        switch (sp->K) {
+        case 5: hipLaunchKernelGGL(coupling_pair_step2_kernel<5>, dim3(nb), dim3(128), 0, st, as, s, as2, s2, ad, d, ad2, t_d2, nb0); break;
+        case 8: hipLaunchKernelGGL(coupling_pair_step2_kernel<8>, dim3(nb), dim3(128), 0, st, as, s, as2, s2, ad, d, ad2, t_d2, nb0); break;
+        case 15: hipLaunchKernelGGL(coupling_pair_step2_kernel<15>, dim3(nb), dim3(128), 0, st, as, s, as2, s2, ad, d, ad2, t_d2, nb0); break;
+        case 32: hipLaunchKernelGGL(coupling_pair_step2_kernel<32>, dim3(nb), dim3(128), 0, st, as, s, as2, s2, ad, d, ad2, t_d2, nb0); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     FS_PAIR_LAUNCH(coupling_pair_step_kernel, as, s, as2, s2, ad, d, ad2, t_d2)
 #undef FS_PAIR_LAUNCH
 }

@@ -278,10 +278,14 @@ int64_t fs_set_wide_rows(int64_t rows);
  * fs_set_wide_final32: 1 (default, or FS_WIDE_FINAL32) = the wide path's final phase on
  *   32-row blocks when twice the 64-row grid fits the chip (spline bins K <= 16), 0 = always
  *   64-row blocks.
+ * fs_set_coupling_waves: 1 (default, or FS_COUPLING_WAVES) = the training step's coupling
+ *   launches (fs_coupling_pair_step, fs_coupling_bwd_step) with each row's splines spread
+ *   over two / four waves (one knot set per wave), 0 = one / two waves per row.
  * fs_set_lean_gemm: 1 (default, or FS_LEAN_GEMM) = the training products on the lean
  *   kernels (32-bit buffer offsets), 0 = the generic strided kernels. */
 int32_t fs_set_wide_trunk16(int32_t on);
 int32_t fs_set_wide_final32(int32_t on);
+int32_t fs_set_coupling_waves(int32_t on);
 int32_t fs_set_lean_gemm(int32_t on);
 
 /* ------------------------------------------------------------------ */

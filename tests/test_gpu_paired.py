@@ -111,3 +111,45 @@ def test_paired_launch_count():
     L = kw["L"]
     assert counts["paired"] == 7 * L + 1, counts
     assert counts["separate"] == 16 * L, counts
+
+
+class coupling_waves:
+    """The training step's coupling launches with each row's splines on two / four waves
+    (1) or on one / two (0), for a block."""
+
+    def __init__(self, on):
+        self.on = on
+
+    def __enter__(self):
+        self.prev = _lib.load().fs_set_coupling_waves(self.on)
+
+    def __exit__(self, *exc):
+        _lib.load().fs_set_coupling_waves(self.prev)
+
+
+@pytest.mark.parametrize("N,kw,rows", [(16, dict(L=4, H=64, nb=2, K=8), 96), (64, A2, 256), (16, dict(L=3, H=32, nb=1,
+                                                                                                     K=5), 37),
+                                       (8, dict(L=3, H=32, nb=1, K=32), 50)],
+                         ids=["n16-h64", "a2-n64", "n16-ragged", "n8-k32"])
+def test_coupling_waves_bit_identical(N, kw, rows):
+    """fs_coupling_pair_step / fs_coupling_bwd_step with each row's knot sets built on
+    separate waves against one wave per spline: loss, every gradient and BatchNorm buffer
+    identical, with inputs outside the tail bound on some coordinates (identity branches)."""
+    outs = []
+    for on in (1, 0):
+        with coupling_waves(on):
+            m = _model(N, kw, seed=2)
+            fbn = AF.FlatBatchNorm(m)
+            x = _batch(N, rows, seed=6)
+            x[::7, ::5] *= 1.2  # beyond the bound: the identity branches
+            for p in m.parameters():
+                p.grad = None
+            torch.cuda.manual_seed(13)
+            loss = step_loss(m, x, rows, 1.0, fbn)
+            loss.backward()
+            torch.cuda.synchronize()
+            outs.append([loss.detach().clone()] + [p.grad.clone() for p in m.parameters() if p.grad is not None]
+                        + [b.clone() for b in m.buffers()])
+    assert len(outs[0]) == len(outs[1])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

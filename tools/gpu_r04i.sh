@@ -5,8 +5,9 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r04i}
+PYTESTS=${PYTESTS:-tests/test_gpu_wide.py tests/test_gpu_mh.py}
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_wide.py tests/test_gpu_mh.py > gpurun_out/${T}_pytest_wide.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread $PYTESTS > gpurun_out/${T}_pytest_wide.log 2>&1
 rc=$?; echo "pytest wide rc=$rc"; tail -3 gpurun_out/${T}_pytest_wide.log; [ $rc -eq 0 ] || exit $rc
 for t in ${TLIST:-2 1}; do
   FS_WIDE_TRUNK16=$t timeout -k 10 300 python tools/bench_wide.py 200,1024,4096 > gpurun_out/${T}_bench_wide_t$t.log 2>&1
