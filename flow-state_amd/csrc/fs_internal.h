@@ -121,9 +121,18 @@ struct BnIn {
     float *a_out;
     float *var_out;  // nullable: the biased batch variance [K] (deferred running-statistics updates)
 };
+// a BatchNorm1d (train) + ReLU backward folded into the backward pairs around it
+// (fs_linear_f32_pair_bn; train_kernels.hip)
+struct BnFold {
+    const float *gu, *u, *y, *mean, *invstd, *gamma;
+    float *part, *dgamma, *dbeta;
+    int B, H, tiles;
+};
 }  // namespace fs
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st);
 hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, hipStream_t st);
+hipError_t fs_linear_f32_pair_bn_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, const fs::BnFold &f, int role,
+                                      hipStream_t st);
 hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipStream_t st);
 bool fs_linear_ex2_ok(const fs::GemmArgs &g0, const fs::BnIn *b0, const fs::GemmArgs &g1, const fs::BnIn *b1);
 hipError_t fs_linear_ex2_impl(const fs::GemmArgs &g0, const fs::BnIn *b0, const fs::GemmArgs &g1, const fs::BnIn *b1,

@@ -566,10 +566,23 @@ struct LinG {
     const float *A, *B, *bias, *R;
     float *C, *stats, *rowsum;
     int M, N, K, sam, sak, sbk, sbn, ldr, ldc, abytes, bbytes;
+    int pstats;  // (fs_linear_f32_pair_bn, producer) per-tile BatchNorm-backward sums of C
 };
+// A BatchNorm1d (train) + ReLU backward folded into the backward pairs on either side of it
+// (fs_linear_f32_pair_bn): the producer pair's input gradient is the BatchNorm output's
+// gradient gu; its epilogue writes per 32-row tile the column sums of dz = gu (u > 0) and
+// dz xhat; the consumer pair loads dy = BatchNorm-input gradient on the fly from gu, u, y
+// and the combined sums (bn_relu_train_bwd_kernel's formula), so dy is never written and
+// the BatchNorm backward launch disappears.  Workgroup 0 of the consumer writes dgamma,
+// dbeta.
+// (struct BnFold: fs_internal.h)
+constexpr int kFoldMaxH = 256;
 struct LinGLds {
     t16 part[7][64];
     float rs_part[8][64];
+};
+struct LinGFLds : LinGLds {  // gemm_ling_fold_kernel: + the folded BatchNorm's column terms
+    float mdb[kFoldMaxH], mdg[kFoldMaxH], mu[kFoldMaxH], is[kFoldMaxH], sc[kFoldMaxH];
 };
 constexpr int kLingPF = 4;
 
@@ -583,8 +596,51 @@ __device__ __forceinline__ t4 ling_ld(__amdgpu_buffer_rsrc_t r, int base, int st
     return v;
 }
 
-template <bool AK, bool BK>
-__device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned by, LinGLds &L) {
+// the BatchNorm-input gradient of one element (bn_relu_train_bwd_kernel's dx, no dx_add)
+__device__ __forceinline__ float fold_dx(float g, float u, float y, const LinGFLds &L, int c) {
+    const float dz = u > 0.f ? g : 0.f;
+    const float xh = (y - L.mu[c]) * L.is[c];
+    return (dz - L.mdb[c] - xh * L.mdg[c]) * L.sc[c];
+}
+
+// V = 1: A is dy [B][H] (k = column), V = 2: A is dy^T (m = column); a quad of A from gu, u, y
+// (loaded into the ring raw, turned into dy right before its MFMAs)
+struct FoldQ {
+    t4 g, u, y;
+};
+
+template <int V>
+__device__ __forceinline__ FoldQ fold_raw(__amdgpu_buffer_rsrc_t Gr, __amdgpu_buffer_rsrc_t Ur,
+                                          __amdgpu_buffer_rsrc_t Yr, int base, int stride) {
+    FoldQ q;
+    if (V == 1) {
+        q.g = lin_ld(Gr, base * 4);
+        q.u = lin_ld(Ur, base * 4);
+        q.y = lin_ld(Yr, base * 4);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int off = (base + j * stride) * 4;
+            q.g[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(Gr, off, 0, 0));
+            q.u[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(Ur, off, 0, 0));
+            q.y[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(Yr, off, 0, 0));
+        }
+    }
+    return q;
+}
+
+template <int V>
+__device__ __forceinline__ t4 fold_apply(const FoldQ &q, int c, const LinGFLds &L) {
+    t4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = fold_dx(q.g[j], q.u[j], q.y[j], L, V == 1 ? c + j : c);
+    return o;
+}
+
+// V: (fold consumer) A loaded as dy, 1 row-major, 2 transposed; PS: (fold producer) the
+// epilogue's tile sums; both only in gemm_ling_fold_kernel (LDS = LinGFLds)
+template <bool AK, bool BK, int V = 0, bool PS = false, class LDS = LinGLds>
+__device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned by, LDS &L, const BnFold &F) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int M = P.M, N = P.N, K = P.K;
@@ -593,18 +649,61 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
     // rows past M / columns past N: an offset past the operand, read as zero
     const int am = m < M ? m * P.sam : P.abytes / 4, bn = col < N ? col * P.sbn : P.bbytes / 4;
     const __amdgpu_buffer_rsrc_t Ar = lin_rsrc(P.A, P.abytes), Br = lin_rsrc(P.B, P.bbytes);
+    __amdgpu_buffer_rsrc_t Gr = Ar, Ur = Ar, Yr = Ar;
+    if constexpr (V != 0) {
+        Gr = lin_rsrc(F.gu, P.abytes);
+        Ur = lin_rsrc(F.u, P.abytes);
+        Yr = lin_rsrc(F.y, P.abytes);
+    }
+    const int mc = m < M ? m : 0;  // (V = 2) the column of A's row m
     const t4 zero = {0.f, 0.f, 0.f, 0.f};
     t4 a[kLingPF], b[kLingPF];
+    FoldQ q[V != 0 ? kLingPF : 1];
     const int kb0 = 8 * w;
 #pragma unroll
     for (int s = 0; s < kLingPF; ++s) {
         const int k = kb0 + 64 * s + 4 * h;
-        a[s] = k < K ? ling_ld<AK>(Ar, am + k * P.sak, P.sak) : zero;
+        if constexpr (V != 0) {
+            if (k < K) q[s] = fold_raw<V>(Gr, Ur, Yr, am + k * P.sak, P.sak);
+        } else {
+            a[s] = k < K ? ling_ld<AK>(Ar, am + k * P.sak, P.sak) : zero;
+        }
         b[s] = k < K ? ling_ld<BK>(Br, bn + k * P.sbk, P.sbk) : zero;
     }
-    float ep_bias = 0.f, ep_r[16];
+    if constexpr (V != 0) {  // the folded BatchNorm's column sums (their loads under the ring's)
+        for (int t = threadIdx.x; t < F.H; t += blockDim.x) {
+            float db = 0.f, dg = 0.f;
+            for (int i0 = 0; i0 < F.tiles; i0 += 8) {  // 8 tiles' loads in flight, added in order
+                float pd[8], px[8];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) ep_r[i] = 0.f;
+                for (int j = 0; j < 8; ++j)
+                    if (i0 + j < F.tiles) {
+                        pd[j] = F.part[((int64_t)(i0 + j) * F.H + t) * 2];
+                        px[j] = F.part[((int64_t)(i0 + j) * F.H + t) * 2 + 1];
+                    }
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (i0 + j < F.tiles) {
+                        db += pd[j];
+                        dg += px[j];
+                    }
+            }
+            const float is = F.invstd[t];
+            L.mdb[t] = db / (float)F.B;
+            L.mdg[t] = dg / (float)F.B;
+            L.mu[t] = F.mean[t];
+            L.is[t] = is;
+            L.sc[t] = is * F.gamma[t];
+            if (blockIdx.x == 0) {
+                if (F.dgamma) F.dgamma[t] = dg;
+                if (F.dbeta) F.dbeta[t] = db;
+            }
+        }
+        __syncthreads();
+    }
+    float ep_bias = 0.f, ep_r[16], ps_u[16], ps_y[16], ps_mu = 0.f, ps_is = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ep_r[i] = ps_u[i] = ps_y[i] = 0.f;
     if (w == 0 && col < N) {
         ep_bias = P.bias ? P.bias[col] : 0.f;
         if (P.R) {
@@ -612,6 +711,17 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
             for (int i = 0; i < 16; ++i) {
                 const int row = (int)bx * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
                 if (row < M) ep_r[i] = P.R[row * P.ldr + col];
+            }
+        }
+        if (PS) {  // the folded BatchNorm's u, y at this lane's outputs (issued early)
+            ps_mu = F.mean[col];
+            ps_is = F.invstd[col];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {  // rows past M read row M - 1 (excluded from the sums)
+                int row = (int)bx * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+                row = row < M ? row : M - 1;
+                ps_u[i] = F.u[row * P.ldc + col];
+                ps_y[i] = F.y[row * P.ldc + col];
             }
         }
     }
@@ -624,12 +734,17 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
         for (int s = 0; s < kLingPF; ++s) {
             const int k = kb + 64 * s;
             if (k < K) {  // wave-uniform
+                if constexpr (V != 0) a[s] = fold_apply<V>(q[s], V == 1 ? k + 4 * h : mc, L);
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][j], b[s][j], acc, 0, 0, 0);
                 if (rows) rs += ((a[s][0] + a[s][1]) + a[s][2]) + a[s][3];
                 const int kn = k + 64 * kLingPF + 4 * h;
-                a[s] = kn < K ? ling_ld<AK>(Ar, am + kn * P.sak, P.sak) : zero;
+                if constexpr (V != 0) {
+                    if (kn < K) q[s] = fold_raw<V>(Gr, Ur, Yr, am + kn * P.sak, P.sak);
+                } else {
+                    a[s] = kn < K ? ling_ld<AK>(Ar, am + kn * P.sak, P.sak) : zero;
+                }
                 b[s] = kn < K ? ling_ld<BK>(Br, bn + kn * P.sbk, P.sbk) : zero;
             }
         }
@@ -676,6 +791,25 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
             P.stats[((int)bx * N + col) * 2 + 1] = q;
         }
     }
+    if (PS) {  // this tile's column sums of dz and dz xhat for the folded BatchNorm
+        float pd = 0.f, pdx = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = (int)bx * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+            const float dz = ps_u[i] > 0.f ? acc[i] : 0.f;
+            const float xh = (ps_y[i] - ps_mu) * ps_is;
+            if (row < M) {
+                pd += dz;
+                pdx += dz * xh;
+            }
+        }
+        pd += __shfl_xor(pd, 32);
+        pdx += __shfl_xor(pdx, 32);
+        if (h == 0 && bok) {
+            F.part[((int)bx * N + col) * 2] = pd;
+            F.part[((int)bx * N + col) * 2 + 1] = pdx;
+        }
+    }
 }
 
 // Up to kLingMax products in one launch, each whole or split along K into S chunks (chunk z
@@ -689,11 +823,12 @@ struct LinGProb {
     float *part;
     int kchunk;
     unsigned S, mt, nt, begin;
-    int ak, bk;
+    int ak, bk, vmode;  // vmode: (fs_linear_f32_pair_bn, consumer) 1 A = dy, 2 A = dy^T
 };
 struct LinGrp {
     LinGProb p[kLingMax];
     int n;
+    BnFold fold;
 };
 
 __global__ __launch_bounds__(512) void gemm_ling_kernel(LinGrp ga) {
@@ -709,6 +844,7 @@ __global__ __launch_bounds__(512) void gemm_ling_kernel(LinGrp ga) {
     const unsigned bx = b % Q.mt, by = b / Q.mt;
     LinG c = Q.g;
     if (Q.S > 1) {  // chunk z of the reduction: its own partial tile, nothing else
+        c.pstats = 0;
         const int k0 = (int)z * Q.kchunk;
         c.A = Q.g.A + k0 * Q.g.sak;
         c.B = Q.g.B + k0 * Q.g.sbk;
@@ -724,15 +860,33 @@ __global__ __launch_bounds__(512) void gemm_ling_kernel(LinGrp ga) {
     }
     if (Q.ak) {
         if (Q.bk)
-            ling_tile<true, true>(c, bx, by, L);
+            ling_tile<true, true>(c, bx, by, L, ga.fold);
         else
-            ling_tile<true, false>(c, bx, by, L);
+            ling_tile<true, false>(c, bx, by, L, ga.fold);
     } else {
         if (Q.bk)
-            ling_tile<false, true>(c, bx, by, L);
+            ling_tile<false, true>(c, bx, by, L, ga.fold);
         else
-            ling_tile<false, false>(c, bx, by, L);
+            ling_tile<false, false>(c, bx, by, L, ga.fold);
     }
+}
+
+// nn.Linear's backward pair around a folded BatchNorm (fs_linear_f32_pair_bn): the producer's
+// (vmode 0) input gradient with the tile sums in its epilogue (pstats) and its weight
+// gradient, or the consumer's two products with dy loaded on the fly (vmode 1, 2)
+__global__ __launch_bounds__(512) void gemm_ling_fold_kernel(LinGrp ga) {
+    __shared__ LinGFLds L;
+    const int i = (ga.n > 1 && blockIdx.x >= ga.p[1].begin) ? 1 : 0;
+    const LinGProb &Q = ga.p[i];
+    const unsigned b = blockIdx.x - Q.begin, bx = b % Q.mt, by = b / Q.mt;
+    if (Q.vmode == 1)
+        ling_tile<true, false, 1, false, LinGFLds>(Q.g, bx, by, L, ga.fold);
+    else if (Q.vmode == 2)
+        ling_tile<false, false, 2, false, LinGFLds>(Q.g, bx, by, L, ga.fold);
+    else if (Q.g.pstats)
+        ling_tile<true, false, 0, true, LinGFLds>(Q.g, bx, by, L, ga.fold);
+    else
+        ling_tile<false, false, 0, false, LinGFLds>(Q.g, bx, by, L, ga.fold);
 }
 
 // Deferred BatchNorm running statistics: for each of nbn BatchNorms of width H (flat
@@ -1208,7 +1362,7 @@ static bool ling_ok(const GemmArgs &g) {
 static LinG ling_fill(const GemmArgs &g) {
     return LinG{g.A, g.B, g.bias, g.R, g.C, g.stats, g.rowsum_a, (int)g.M, (int)g.N, (int)g.K, (int)g.sam, (int)g.sak,
                 (int)g.sbk, (int)g.sbn, (int)g.ldr, (int)g.ldc, (int)extent_bytes(g.M, g.sam, g.K, g.sak),
-                (int)extent_bytes(g.K, g.sbk, g.N, g.sbn)};
+                (int)extent_bytes(g.K, g.sbk, g.N, g.sbn), 0};
 }
 
 // n products (all ling_ok) in one gemm_ling_kernel launch; part[i] / S[i] / kchunk[i]: the
@@ -1244,6 +1398,51 @@ static hipError_t ling_group(const GemmArgs *gs, int n, float *const *part, cons
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// nn.Linear's backward pair on either side of a folded BatchNorm + ReLU (struct BnFold):
+// role 1, the producer: g0 its input gradient gu [B][H], whose epilogue writes the tile sums;
+// role 2, the consumer: g0 = dy W and g1 = dy^T X with dy loaded on the fly (A = gu as the
+// layout: g0 row-major, g1 its transpose), workgroup 0 writing dgamma / dbeta
+hipError_t fs_linear_f32_pair_bn_impl(const GemmArgs &g0, const GemmArgs &g1, const BnFold &f, int role,
+                                      hipStream_t st) {
+    if (!lean_gemm() || !ling_ok(g0) || !ling_ok(g1) || f.H <= 0 || f.H > kFoldMaxH || f.B <= 0 ||
+        f.tiles != (f.B + 31) / 32 || !f.gu || !f.u || !f.y || !f.mean || !f.invstd || !f.part)
+        return hipErrorInvalidValue;
+    LinGrp ga{};
+    ga.fold = f;
+    unsigned wg = 0;
+    const GemmArgs *gs[2] = {&g0, &g1};
+    for (int i = 0; i < 2; ++i) {
+        const GemmArgs &g = *gs[i];
+        LinGProb &Q = ga.p[ga.n++];
+        Q.g = ling_fill(g);
+        Q.S = 1;
+        Q.part = nullptr;
+        Q.kchunk = (int)g.K;
+        Q.ak = ak_of(g);
+        Q.bk = bk_of(g);
+        Q.mt = (unsigned)((g.M + 31) / 32);
+        Q.nt = (unsigned)(g.N > 0 ? (g.N + 31) / 32 : 1);
+        Q.begin = wg;
+        wg += Q.mt * Q.nt;
+    }
+    if (role == 1) {
+        if (g0.M != f.B || g0.N != f.H || g0.ldc != f.H || g0.C != f.gu || !ga.p[0].ak || ga.p[0].bk || ga.p[1].ak ||
+            ga.p[1].bk)
+            return hipErrorInvalidValue;
+        ga.p[0].g.pstats = 1;
+    } else if (role == 2) {
+        if (!f.gamma || g0.A != f.gu || g1.A != f.gu || g0.M != f.B || g0.K != f.H || g0.sam != f.H || g0.sak != 1 ||
+            !ga.p[0].ak || ga.p[0].bk || g1.M != f.H || g1.K != f.B || g1.sam != 1 || g1.sak != f.H || ga.p[1].bk)
+            return hipErrorInvalidValue;
+        ga.p[0].vmode = 1;
+        ga.p[1].vmode = 2;
+    } else {
+        return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(gemm_ling_fold_kernel, dim3(wg), dim3(512), 0, st, ga);
+    return hipGetLastError();
 }
 
 // one or two whole products (g1 nullable; both ling_ok) in one launch

@@ -56,6 +56,14 @@ class BnIn(ctypes.Structure):
                 ("a_out", ctypes.c_void_p), ("var_out", ctypes.c_void_p)]
 
 
+class BnFold(ctypes.Structure):
+    """fs_bn_fold (include/flowstate.h): a BatchNorm + ReLU backward folded into the
+    backward pairs around it (fs_linear_f32_pair_bn)."""
+    _fields_ = [("gu", ctypes.c_void_p), ("u", ctypes.c_void_p), ("y", ctypes.c_void_p), ("mean", ctypes.c_void_p),
+                ("invstd", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("part", ctypes.c_void_p),
+                ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p), ("B", ctypes.c_int64), ("H", ctypes.c_int32)]
+
+
 class FlowStateError(RuntimeError):
     pass
 
@@ -106,6 +114,8 @@ _SIGS = {
     "fs_linear_f32": (ctypes.c_int, [_I64, _I64, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _P, _I64, _P, _I64,
                                      _P, _P]),
     "fs_linear_f32_pair": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(GemmF32), _P]),
+    "fs_linear_f32_pair_bn": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(GemmF32),
+                                             ctypes.POINTER(BnFold), ctypes.c_int32, _P]),
     "fs_linear_f32_splitk_floats": (_I64, [ctypes.POINTER(GemmF32)]),
     "fs_linear_f32_splitk": (ctypes.c_int, [ctypes.POINTER(GemmF32), _P, _I64, _P]),
     "fs_linear_f32_ex": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(BnIn), _P, _P]),

@@ -21,6 +21,8 @@ Reference math (paths relative to the reference root):
 """
 import ctypes
 
+import os
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -209,6 +211,36 @@ def register_grad_home(flat, flat_grad):
 
 
 _direct_grads = False  # set by paired_kld around its forward: one gradient contribution per parameter
+# the block's second BatchNorm backward folded into the backward pairs around it
+# (fs_linear_f32_pair_bn; _BnFoldLink) in the graphs paired_kld builds; FS_FOLD_BN=0 turns it off
+_fold_bn = os.environ.get("FS_FOLD_BN", "1") != "0"
+
+
+_ZERO = {}
+
+
+def _zero_grad_placeholder(dev, M, K):
+    """A [M, K] zero view of one cached scalar: what autograd sees for dy when it is folded."""
+    z = _ZERO.get(dev)
+    if z is None:
+        z = _ZERO[dev] = torch.zeros((), dtype=torch.float32, device=dev)
+    return z.expand(M, K)
+
+
+class _BnFoldLink:
+    """Carries a residual block's second BatchNorm backward from its second Linear's
+    backward (which computes gu = dL/du and the per-tile sums, fs_linear_f32_pair_bn role 1)
+    to its first Linear's backward (whose weight / input gradient pair loads dy = dL/dy from
+    them, role 2, and writes that BatchNorm's dgamma / dbeta): the BatchNorm backward launch
+    and dy itself disappear.  A side channel like _ResidualGrad: the second Linear hands
+    autograd a zero placeholder for dy, so it is only built where the whole backward runs
+    through the block (paired_kld's graphs); the first Linear takes the BatchNorm's gamma
+    and beta as extra inputs to return their gradients."""
+
+    __slots__ = ("pending",)
+
+    def __init__(self):
+        self.pending = None
 
 
 def _grad_out(*ps, direct=False):
@@ -430,7 +462,8 @@ class _BnReluLinear(torch.autograd.Function):
     _BnRelu)."""
 
     @staticmethod
-    def forward(ctx, x, x_stats, gamma, beta, bn, w, b, r, res=None, pair=None, op=None):
+    def forward(ctx, x, x_stats, gamma, beta, bn, w, b, r, res=None, pair=None, op=None, fold=None, fold_role=0,
+                gamma2=None, beta2=None):
         from .. import _lib
 
         x = x.contiguous()
@@ -440,6 +473,13 @@ class _BnReluLinear(torch.autograd.Function):
         st = torch.empty(((M + 31) // 32, N, 2), dtype=torch.float32, device=x.device)
         invstd = torch.empty((K,), dtype=torch.float32, device=x.device)
         u = torch.empty_like(x) if any(ctx.needs_input_grad) else None
+        # fold_role 1: this Linear follows the folded BatchNorm; 2: precedes it (gamma2, beta2
+        # are that BatchNorm's, their gradients returned here)
+        # (the lean kernels' limits: the weight gradients reduce over the batch in quads)
+        ctx.fold = fold if (fold is not None and _fold_bn and _direct_grads and N <= 256 and K <= 256 and M % 4 == 0
+                            and _lib.load().fs_set_lean_gemm(-1) == 1) else None
+        ctx.fold_role = fold_role
+        ctx.gparams2 = (gamma2, beta2)
         p = _lib.ptr
         _lib.require_device(x, x_stats, gamma, beta, w, b, r)
         if pair is None:
@@ -473,20 +513,54 @@ class _BnReluLinear(torch.autograd.Function):
 
         x, u, gamma, mean, invstd, w = ctx.saved_tensors
         if gy is None:
-            return (None,) * 11
-        gy = gy.contiguous()
+            return (None,) * 15
         M, K = x.shape
         N = w.shape[0]
         L = _lib.load()
         p = _lib.ptr
+        fold = ctx.fold
+        if fold is not None and ctx.fold_role == 2 and fold.pending is None:
+            fold = None  # the following Linear did not fold (its backward ran unfolded)
+        if fold is not None and ctx.fold_role == 1 and (ctx.res is None or not ctx.has_r):
+            fold = None
         gw = _grad_out(w, direct=ctx.direct)
         gb = _grad_out(ctx.gparams[1], direct=ctx.direct)
+        if fold is not None and ctx.fold_role == 1:
+            # gu = dL/du and the folded BatchNorm's tile sums; dy is left to the preceding
+            # Linear's backward (fs_linear_f32_pair_bn, _BnFoldLink)
+            gy = gy.contiguous()
+            gu = torch.empty_like(u)
+            part = torch.empty(((M + 31) // 32, K, 2), dtype=torch.float32, device=x.device)
+            g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
+            g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
+            f = _lib.BnFold(p(gu), p(u), p(x), p(mean), p(invstd), p(gamma), p(part), None, None, M, K)
+            _lib.check(L.fs_linear_f32_pair_bn(g0, g1, f, 1, _lib.stream_ptr()), "fs_linear_f32_pair_bn")
+            fold.pending = (gu, u, x, mean, invstd, gamma, part)
+            ctx.res.g = gy  # to the block's first BatchNorm backward (its dx_add)
+            gx = _zero_grad_placeholder(x.device, M, K)  # the placeholder for dy
+            return gx, None, None, None, None, gw, gb, None, None, None, None, None, None, None, None
         add = None
         if ctx.res is not None and ctx.res.g is not None:
             add, ctx.res.g = ctx.res.g, None
         gx = torch.empty_like(x)
         gg = _grad_out(gamma, direct=ctx.direct)
         gbeta = _grad_out(ctx.gparams[0], direct=ctx.direct)
+        if fold is not None and ctx.fold_role == 2:
+            # dy = dL/dy loaded from the following Linear's gu and tile sums; that BatchNorm's
+            # dgamma / dbeta written by the same launch
+            gu2, u2, y2, mean2, invstd2, gamma2, part = fold.pending
+            fold.pending = None
+            gg2 = _grad_out(ctx.gparams2[0], direct=ctx.direct)
+            gbeta2 = _grad_out(ctx.gparams2[1], direct=ctx.direct)
+            gu = torch.empty_like(u)
+            g0 = _lib.GemmF32(M, K, N, p(gu2), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
+            g1 = _lib.GemmF32(N, K, M, p(gu2), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
+            f = _lib.BnFold(p(gu2), p(u2), p(y2), p(mean2), p(invstd2), p(gamma2), p(part), p(gg2), p(gbeta2), M, N)
+            _lib.check(L.fs_linear_f32_pair_bn(g0, g1, f, 2, _lib.stream_ptr()), "fs_linear_f32_pair_bn")
+            _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
+                                              p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
+            return gx, None, gg, gbeta, None, gw, gb, None, None, None, None, None, None, gg2, gbeta2
+        gy = gy.contiguous()
         # the input / weight gradient pair over 48 workgroups, then the BatchNorm + ReLU
         # backward: 10.9 us per layer in a graph, against 18.1 us for one launch whose
         # column strips own the BatchNorm sums (4 workgroups carry the whole input gradient;
@@ -505,7 +579,7 @@ class _BnReluLinear(torch.autograd.Function):
                 ctx.res.g = gy  # to the block's first BatchNorm backward (its dx_add)
             else:
                 gr = gy
-        return gx, None, gg, gbeta, None, gw, gb, gr, None, None, None
+        return gx, None, gg, gbeta, None, gw, gb, gr, None, None, None, None, None, None, None
 
 
 def _fused_ok(net, t):
@@ -554,8 +628,11 @@ def _conditioner_fused(net, t, pair=None, final=True):
             bn0, bn1 = blk.batch_norm_layers
             l0, l1 = blk.linear_layers
             res = _ResidualGrad()
-            u, su = _BnReluLinear.apply(t, st, bn0.weight, bn0.bias, bn0, l0.weight, l0.bias, None, res, pair, (i, 0))
-            t, st = _BnReluLinear.apply(u, su, bn1.weight, bn1.bias, bn1, l1.weight, l1.bias, t, res, pair, (i, 1))
+            fold = _BnFoldLink()
+            u, su = _BnReluLinear.apply(t, st, bn0.weight, bn0.bias, bn0, l0.weight, l0.bias, None, res, pair, (i, 0),
+                                        fold, 2, bn1.weight, bn1.bias)
+            t, st = _BnReluLinear.apply(u, su, bn1.weight, bn1.bias, bn1, l1.weight, l1.bias, t, res, pair, (i, 1),
+                                        fold, 1)
         if not final:  # the caller fuses the final Linear into its next Function (_FinalSplines)
             return t
         lf = net.final_layer

@@ -37,10 +37,20 @@ def _state(m):
     return [t.detach().clone() for t in list(m.parameters()) + list(m.buffers())]
 
 
+@pytest.fixture
+def no_fold():
+    """The paired graphs without the BatchNorm-backward fold, so that their gradients are
+    bit-comparable with the separate passes' (the fold reassociates the column sums)."""
+    prev = AF._fold_bn
+    AF._fold_bn = False
+    yield
+    AF._fold_bn = prev
+
+
 @pytest.mark.parametrize("N,kw,rows", [(16, dict(L=4, H=64, nb=2, K=8), 96), (64, A2, 256), (16, dict(L=3, H=32, nb=1,
                                                                                                      K=5), 37)],
                          ids=["n16-h64", "a2-n64", "n16-ragged"])
-def test_paired_step_matches_separate_passes(N, kw, rows):
+def test_paired_step_matches_separate_passes(N, kw, rows, no_fold):
     ma, mb = _model(N, kw), _model(N, kw)
     fbn = AF.FlatBatchNorm(mb)
     x = _batch(N, rows)
@@ -66,9 +76,10 @@ def test_paired_step_matches_separate_passes(N, kw, rows):
     assert int(fbn.nbt[0]) == 2
 
 
-def test_paired_graphed_steps_match_separate():
+def test_paired_graphed_steps_match_separate(no_fold):
     """GraphedTrainStep with the shared launches (the default) against paired=False over a
-    few replays: parameters, Adam moments and BatchNorm buffers identical."""
+    few replays: parameters, Adam moments and BatchNorm buffers identical (the BatchNorm
+    backward fold, which reassociates its column sums, off: test_bn_fold_matches_unfolded)."""
     N, rows = 16, 128
     kw = dict(L=4, H=64, nb=2, K=8)
     out = []
@@ -153,3 +164,50 @@ def test_coupling_waves_bit_identical(N, kw, rows):
     assert len(outs[0]) == len(outs[1])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,kw,rows", [(16, dict(L=4, H=64, nb=2, K=8), 96), (64, A2, 256), (16, dict(L=3, H=32, nb=1,
+                                                                                                     K=5), 37)],
+                         ids=["n16-h64", "a2-n64", "n16-ragged"])
+def test_bn_fold_matches_unfolded(N, kw, rows):
+    """Each residual block's second BatchNorm backward folded into the backward pairs around
+    it (fs_linear_f32_pair_bn: per-tile sums in the producing pair's epilogue, dy loaded on
+    the fly by the consuming pair) against the separate fs_bn_relu_train_bwd launch: the same
+    loss and buffers, every gradient within float32 reassociation (the BatchNorm's column
+    sums are taken per 32-row tile, then over tiles), and one BatchNorm-backward launch per
+    block instead of two (batches that are a multiple of 4; the ragged one keeps two)."""
+    from torch.profiler import ProfilerActivity, profile
+
+    outs, counts = [], []
+    prev = AF._fold_bn
+    try:
+        for fold in (True, False):
+            AF._fold_bn = fold
+            m = _model(N, kw, seed=2)
+            fbn = AF.FlatBatchNorm(m)
+            x = _batch(N, rows, seed=6)
+            for p in m.parameters():
+                p.grad = None
+            torch.cuda.manual_seed(13)
+            with profile(activities=[ProfilerActivity.CUDA]) as prof:
+                loss = step_loss(m, x, rows, 1.0, fbn)
+                loss.backward()
+                torch.cuda.synchronize()
+            names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+            counts.append(sum(1 for n in names if "bn_relu_train_bwd" in n))
+            outs.append((loss.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None},
+                         [b.clone() for b in m.buffers()]))
+    finally:
+        AF._fold_bn = prev
+    (la, ga, ba), (lb, gb, bb) = outs
+    assert torch.equal(la, lb)
+    assert ga.keys() == gb.keys()
+    for n in ga:
+        scale = float(gb[n].abs().max()) + 1e-30
+        torch.testing.assert_close(ga[n], gb[n], rtol=1e-4, atol=2e-5 * scale, msg=n)
+    for a, b in zip(ba, bb):
+        assert torch.equal(a, b)
+    if counts[1]:  # the profiler saw device kernels
+        L, nb = kw["L"], kw["nb"]
+        folded = rows % 4 == 0  # the lean weight-gradient kernels reduce the batch in quads
+        assert counts == [L * nb if folded else 2 * L * nb, 2 * L * nb], counts

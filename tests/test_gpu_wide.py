@@ -140,8 +140,9 @@ class trunk16:
         _lib.load().fs_set_wide_trunk16(self.prev)
 
 
-@pytest.mark.parametrize("N,kw,B", [(64, A1, 1000), (16, A1, 4096), (64, A2, 200), (3, dict(L=2, H=32, nb=2, K=5), 77)],
-                         ids=["a1-n64-1000", "a1-n16-4096", "a2-n64-200", "n3-h32-77"])
+@pytest.mark.parametrize("N,kw,B", [(64, A1, 1000), (16, A1, 4096), (64, A2, 200), (3, dict(L=2, H=32, nb=2, K=5), 77),
+                                    (16, dict(L=3, H=64, nb=2, K=8), 130)],
+                         ids=["a1-n64-1000", "a1-n16-4096", "a2-n64-200", "n3-h32-77", "n16-h64-130"])
 def test_trunk16_bit_identical_to_trunk32(N, kw, B):
     """The 16-row trunk (v_mfma_f32_16x16x4_f32 fed the 32x32x2 k order), with and without
     the start merged in, against the 32-row one, density and sampling, and all against
@@ -176,8 +177,8 @@ class final32:
 
 
 @pytest.mark.parametrize("N,kw,B", [(64, A2, 200), (64, A2, 1000), (3, dict(L=2, H=32, nb=2, K=5), 77),
-                                    (16, dict(L=3, H=64, nb=1, K=8), 333)],
-                         ids=["a2-n64-200", "a2-n64-1000", "n3-h32-77", "n16-h64-333"])
+                                    (16, dict(L=3, H=64, nb=1, K=8), 333), (16, dict(L=2, H=256, nb=2, K=15), 150)],
+                         ids=["a2-n64-200", "a2-n64-1000", "n3-h32-77", "n16-h64-333", "n16-h256-k15-150"])
 def test_final32_bit_identical_to_final64(N, kw, B):
     """The final phase on 32-row blocks (one row tile per wave, each chain's spline in both
     lane halves) against 64-row blocks and the fused kernel, density and sampling, with a
