@@ -521,13 +521,20 @@ int fs_linear_f32_pair(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, void *strea
     return hip_rc(fs_linear_f32_pair_impl(a[0], a[1], (hipStream_t)stream), "fs_linear_f32_pair");
 }
 
-int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs_bn_fold *f, int32_t role,
-                          void *stream) {
-    REQUIRE(g0 && g1 && f, "fs_linear_f32_pair_bn: NULL descriptor");
-    REQUIRE(role == 1 || role == 2, "fs_linear_f32_pair_bn: role %d (1 producer, 2 consumer)", role);
-    REQUIRE(f->B >= 2 && f->B <= 32LL * 65535 && f->H >= 1 && f->H <= 256 && f->gu && f->u && f->y && f->mean &&
-                f->invstd && f->part && (role == 1 || f->gamma),
-            "fs_linear_f32_pair_bn: invalid fold (B=%lld, H=%d)", (long long)f->B, f->H);
+int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs_bn_fold *fin,
+                          const fs_bn_fold *fout, void *stream) {
+    REQUIRE(g0 && g1 && (fin || fout), "fs_linear_f32_pair_bn: NULL descriptor");
+    const fs_bn_fold *fs_[2] = {fin, fout};
+    fs::BnFold bf[2];
+    for (int i = 0; i < 2; ++i) {
+        const fs_bn_fold *f = fs_[i];
+        if (!f) continue;
+        REQUIRE(f->B >= 2 && f->B <= 32LL * 65535 && f->H >= 1 && f->H <= 256 && f->gu && f->u && f->y && f->mean &&
+                    f->invstd && f->part && (i == 1 || f->gamma),
+                "fs_linear_f32_pair_bn: invalid %s fold (B=%lld, H=%d)", i ? "output" : "input", (long long)f->B, f->H);
+        bf[i] = fs::BnFold{f->gu, f->u, f->y, f->mean, f->invstd, f->gamma, f->part, f->dgamma, f->dbeta,
+                           f->dx_add, f->a_out, (int)f->B, (int)f->H, (int)((f->B + 31) / 32)};
+    }
     fs::GemmArgs a[2];
     const fs_gemm_f32 *gs[2] = {g0, g1};
     for (int i = 0; i < 2; ++i) {
@@ -537,9 +544,9 @@ int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs
         a[i] = fs::GemmArgs{g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C, g.ldc,
                             g.rowsum_a};
     }
-    const fs::BnFold bf{f->gu, f->u, f->y, f->mean, f->invstd, f->gamma, f->part, f->dgamma, f->dbeta, (int)f->B,
-                        (int)f->H, (int)((f->B + 31) / 32)};
-    return hip_rc(fs_linear_f32_pair_bn_impl(a[0], a[1], bf, role, (hipStream_t)stream), "fs_linear_f32_pair_bn");
+    return hip_rc(fs_linear_f32_pair_bn_impl(a[0], a[1], fin ? &bf[0] : nullptr, fout ? &bf[1] : nullptr,
+                                             (hipStream_t)stream),
+                  "fs_linear_f32_pair_bn");
 }
 
 static bool bn_in_ok(const fs_gemm_f32 &g, const fs_bn_in *bn) {

@@ -126,13 +126,15 @@ struct BnIn {
 struct BnFold {
     const float *gu, *u, *y, *mean, *invstd, *gamma;
     float *part, *dgamma, *dbeta;
+    const float *dx_add;  // (consumer) the residual gradient added to dy, nullable
+    float *a_out;         // (consumer) dy written out by the input gradient's first column tile, nullable
     int B, H, tiles;
 };
 }  // namespace fs
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st);
 hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, hipStream_t st);
-hipError_t fs_linear_f32_pair_bn_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, const fs::BnFold &f, int role,
-                                      hipStream_t st);
+hipError_t fs_linear_f32_pair_bn_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, const fs::BnFold *fin,
+                                      const fs::BnFold *fout, hipStream_t st);
 hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipStream_t st);
 bool fs_linear_ex2_ok(const fs::GemmArgs &g0, const fs::BnIn *b0, const fs::GemmArgs &g1, const fs::BnIn *b1);
 hipError_t fs_linear_ex2_impl(const fs::GemmArgs &g0, const fs::BnIn *b0, const fs::GemmArgs &g1, const fs::BnIn *b1,

@@ -606,17 +606,20 @@ __device__ __forceinline__ float fold_dx(float g, float u, float y, const LinGFL
 // V = 1: A is dy [B][H] (k = column), V = 2: A is dy^T (m = column); a quad of A from gu, u, y
 // (loaded into the ring raw, turned into dy right before its MFMAs)
 struct FoldQ {
-    t4 g, u, y;
+    t4 g, u, y, r;  // r: the residual gradient (dx_add), zero without one
 };
 
 template <int V>
 __device__ __forceinline__ FoldQ fold_raw(__amdgpu_buffer_rsrc_t Gr, __amdgpu_buffer_rsrc_t Ur,
-                                          __amdgpu_buffer_rsrc_t Yr, int base, int stride) {
+                                          __amdgpu_buffer_rsrc_t Yr, __amdgpu_buffer_rsrc_t Rr, bool add, int base,
+                                          int stride) {
     FoldQ q;
+    const t4 zero = {0.f, 0.f, 0.f, 0.f};
     if (V == 1) {
         q.g = lin_ld(Gr, base * 4);
         q.u = lin_ld(Ur, base * 4);
         q.y = lin_ld(Yr, base * 4);
+        q.r = add ? lin_ld(Rr, base * 4) : zero;
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -624,23 +627,29 @@ __device__ __forceinline__ FoldQ fold_raw(__amdgpu_buffer_rsrc_t Gr, __amdgpu_bu
             q.g[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(Gr, off, 0, 0));
             q.u[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(Ur, off, 0, 0));
             q.y[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(Yr, off, 0, 0));
+            q.r[j] = add ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(Rr, off, 0, 0)) : 0.f;
         }
     }
     return q;
 }
 
+// dy of a quad (+ the residual gradient when the BatchNorm backward had one: dx_add)
 template <int V>
-__device__ __forceinline__ t4 fold_apply(const FoldQ &q, int c, const LinGFLds &L) {
+__device__ __forceinline__ t4 fold_apply(const FoldQ &q, int c, const LinGFLds &L, bool add) {
     t4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = fold_dx(q.g[j], q.u[j], q.y[j], L, V == 1 ? c + j : c);
+    for (int j = 0; j < 4; ++j) {
+        const float d = fold_dx(q.g[j], q.u[j], q.y[j], L, V == 1 ? c + j : c);
+        o[j] = add ? d + q.r[j] : d;
+    }
     return o;
 }
 
 // V: (fold consumer) A loaded as dy, 1 row-major, 2 transposed; PS: (fold producer) the
 // epilogue's tile sums; both only in gemm_ling_fold_kernel (LDS = LinGFLds)
 template <bool AK, bool BK, int V = 0, bool PS = false, class LDS = LinGLds>
-__device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned by, LDS &L, const BnFold &F) {
+__device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned by, LDS &L, const BnFold &F,
+                                          const BnFold &Fo) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int M = P.M, N = P.N, K = P.K;
@@ -649,11 +658,15 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
     // rows past M / columns past N: an offset past the operand, read as zero
     const int am = m < M ? m * P.sam : P.abytes / 4, bn = col < N ? col * P.sbn : P.bbytes / 4;
     const __amdgpu_buffer_rsrc_t Ar = lin_rsrc(P.A, P.abytes), Br = lin_rsrc(P.B, P.bbytes);
-    __amdgpu_buffer_rsrc_t Gr = Ar, Ur = Ar, Yr = Ar;
+    __amdgpu_buffer_rsrc_t Gr = Ar, Ur = Ar, Yr = Ar, Rr = Ar;
+    const bool fadd = V != 0 && F.dx_add != nullptr;
+    // (V = 1) this row tile's dy written out by the first column tile's workgroup
+    float *const aout = (V == 1 && by == 0 && F.a_out && m < M) ? F.a_out : nullptr;
     if constexpr (V != 0) {
         Gr = lin_rsrc(F.gu, P.abytes);
         Ur = lin_rsrc(F.u, P.abytes);
         Yr = lin_rsrc(F.y, P.abytes);
+        if (fadd) Rr = lin_rsrc(F.dx_add, P.abytes);
     }
     const int mc = m < M ? m : 0;  // (V = 2) the column of A's row m
     const t4 zero = {0.f, 0.f, 0.f, 0.f};
@@ -664,7 +677,7 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
     for (int s = 0; s < kLingPF; ++s) {
         const int k = kb0 + 64 * s + 4 * h;
         if constexpr (V != 0) {
-            if (k < K) q[s] = fold_raw<V>(Gr, Ur, Yr, am + k * P.sak, P.sak);
+            if (k < K) q[s] = fold_raw<V>(Gr, Ur, Yr, Rr, fadd, am + k * P.sak, P.sak);
         } else {
             a[s] = k < K ? ling_ld<AK>(Ar, am + k * P.sak, P.sak) : zero;
         }
@@ -714,14 +727,14 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
             }
         }
         if (PS) {  // the folded BatchNorm's u, y at this lane's outputs (issued early)
-            ps_mu = F.mean[col];
-            ps_is = F.invstd[col];
+            ps_mu = Fo.mean[col];
+            ps_is = Fo.invstd[col];
 #pragma unroll
             for (int i = 0; i < 16; ++i) {  // rows past M read row M - 1 (excluded from the sums)
                 int row = (int)bx * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
                 row = row < M ? row : M - 1;
-                ps_u[i] = F.u[row * P.ldc + col];
-                ps_y[i] = F.y[row * P.ldc + col];
+                ps_u[i] = Fo.u[row * P.ldc + col];
+                ps_y[i] = Fo.y[row * P.ldc + col];
             }
         }
     }
@@ -734,14 +747,17 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
         for (int s = 0; s < kLingPF; ++s) {
             const int k = kb + 64 * s;
             if (k < K) {  // wave-uniform
-                if constexpr (V != 0) a[s] = fold_apply<V>(q[s], V == 1 ? k + 4 * h : mc, L);
+                if constexpr (V != 0) {
+                    a[s] = fold_apply<V>(q[s], V == 1 ? k + 4 * h : mc, L, fadd);
+                    if (aout) *(t4 *)(aout + am + k + 4 * h) = a[s];
+                }
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][j], b[s][j], acc, 0, 0, 0);
                 if (rows) rs += ((a[s][0] + a[s][1]) + a[s][2]) + a[s][3];
                 const int kn = k + 64 * kLingPF + 4 * h;
                 if constexpr (V != 0) {
-                    if (kn < K) q[s] = fold_raw<V>(Gr, Ur, Yr, am + kn * P.sak, P.sak);
+                    if (kn < K) q[s] = fold_raw<V>(Gr, Ur, Yr, Rr, fadd, am + kn * P.sak, P.sak);
                 } else {
                     a[s] = kn < K ? ling_ld<AK>(Ar, am + kn * P.sak, P.sak) : zero;
                 }
@@ -806,8 +822,8 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
         pd += __shfl_xor(pd, 32);
         pdx += __shfl_xor(pdx, 32);
         if (h == 0 && bok) {
-            F.part[((int)bx * N + col) * 2] = pd;
-            F.part[((int)bx * N + col) * 2 + 1] = pdx;
+            Fo.part[((int)bx * N + col) * 2] = pd;
+            Fo.part[((int)bx * N + col) * 2 + 1] = pdx;
         }
     }
 }
@@ -828,7 +844,7 @@ struct LinGProb {
 struct LinGrp {
     LinGProb p[kLingMax];
     int n;
-    BnFold fold;
+    BnFold fold, fold_out;  // (gemm_ling_fold_kernel) the BatchNorm dy is loaded from / tile sums go to
 };
 
 __global__ __launch_bounds__(512) void gemm_ling_kernel(LinGrp ga) {
@@ -860,14 +876,14 @@ __global__ __launch_bounds__(512) void gemm_ling_kernel(LinGrp ga) {
     }
     if (Q.ak) {
         if (Q.bk)
-            ling_tile<true, true>(c, bx, by, L, ga.fold);
+            ling_tile<true, true>(c, bx, by, L, ga.fold, ga.fold);
         else
-            ling_tile<true, false>(c, bx, by, L, ga.fold);
+            ling_tile<true, false>(c, bx, by, L, ga.fold, ga.fold);
     } else {
         if (Q.bk)
-            ling_tile<false, true>(c, bx, by, L, ga.fold);
+            ling_tile<false, true>(c, bx, by, L, ga.fold, ga.fold);
         else
-            ling_tile<false, false>(c, bx, by, L, ga.fold);
+            ling_tile<false, false>(c, bx, by, L, ga.fold, ga.fold);
     }
 }
 
@@ -879,14 +895,19 @@ __global__ __launch_bounds__(512) void gemm_ling_fold_kernel(LinGrp ga) {
     const int i = (ga.n > 1 && blockIdx.x >= ga.p[1].begin) ? 1 : 0;
     const LinGProb &Q = ga.p[i];
     const unsigned b = blockIdx.x - Q.begin, bx = b % Q.mt, by = b / Q.mt;
-    if (Q.vmode == 1)
-        ling_tile<true, false, 1, false, LinGFLds>(Q.g, bx, by, L, ga.fold);
-    else if (Q.vmode == 2)
-        ling_tile<false, false, 2, false, LinGFLds>(Q.g, bx, by, L, ga.fold);
-    else if (Q.g.pstats)
-        ling_tile<true, false, 0, true, LinGFLds>(Q.g, bx, by, L, ga.fold);
-    else
-        ling_tile<false, false, 0, false, LinGFLds>(Q.g, bx, by, L, ga.fold);
+    const BnFold &Fi = ga.fold, &Fo = ga.fold_out;
+    if (Q.vmode == 1) {
+        if (Q.g.pstats)
+            ling_tile<true, false, 1, true, LinGFLds>(Q.g, bx, by, L, Fi, Fo);
+        else
+            ling_tile<true, false, 1, false, LinGFLds>(Q.g, bx, by, L, Fi, Fo);
+    } else if (Q.vmode == 2) {
+        ling_tile<false, false, 2, false, LinGFLds>(Q.g, bx, by, L, Fi, Fo);
+    } else if (Q.g.pstats) {
+        ling_tile<true, false, 0, true, LinGFLds>(Q.g, bx, by, L, Fi, Fo);
+    } else {
+        ling_tile<false, false, 0, false, LinGFLds>(Q.g, bx, by, L, Fi, Fo);
+    }
 }
 
 // Deferred BatchNorm running statistics: for each of nbn BatchNorms of width H (flat
@@ -1400,17 +1421,24 @@ static hipError_t ling_group(const GemmArgs *gs, int n, float *const *part, cons
     return hipSuccess;
 }
 
-// nn.Linear's backward pair on either side of a folded BatchNorm + ReLU (struct BnFold):
-// role 1, the producer: g0 its input gradient gu [B][H], whose epilogue writes the tile sums;
-// role 2, the consumer: g0 = dy W and g1 = dy^T X with dy loaded on the fly (A = gu as the
-// layout: g0 row-major, g1 its transpose), workgroup 0 writing dgamma / dbeta
-hipError_t fs_linear_f32_pair_bn_impl(const GemmArgs &g0, const GemmArgs &g1, const BnFold &f, int role,
+// nn.Linear's backward pair around folded BatchNorms + ReLU (struct BnFold): fout, the
+// BatchNorm this Linear applies to its input, whose output gradient gu is g0's output (its
+// epilogue writes the tile sums); fin, the BatchNorm that consumes this Linear's output, whose
+// input gradient dy is both products' A, loaded on the fly (A = fin->gu as the layout: g0
+// row-major, g1 its transpose; + fin->dx_add; fin->a_out gets dy from g0's first column
+// tile), workgroup 0 writing that BatchNorm's dgamma / dbeta
+hipError_t fs_linear_f32_pair_bn_impl(const GemmArgs &g0, const GemmArgs &g1, const BnFold *fin, const BnFold *fout,
                                       hipStream_t st) {
-    if (!lean_gemm() || !ling_ok(g0) || !ling_ok(g1) || f.H <= 0 || f.H > kFoldMaxH || f.B <= 0 ||
-        f.tiles != (f.B + 31) / 32 || !f.gu || !f.u || !f.y || !f.mean || !f.invstd || !f.part)
+    auto fold_ok = [](const BnFold &f) {
+        return f.H > 0 && f.H <= kFoldMaxH && f.B > 0 && f.tiles == (f.B + 31) / 32 && f.gu && f.u && f.y && f.mean &&
+               f.invstd && f.part;
+    };
+    if (!lean_gemm() || !ling_ok(g0) || !ling_ok(g1) || (!fin && !fout) || (fin && !fold_ok(*fin)) ||
+        (fout && !fold_ok(*fout)))
         return hipErrorInvalidValue;
     LinGrp ga{};
-    ga.fold = f;
+    if (fin) ga.fold = *fin;
+    if (fout) ga.fold_out = *fout;
     unsigned wg = 0;
     const GemmArgs *gs[2] = {&g0, &g1};
     for (int i = 0; i < 2; ++i) {
@@ -1427,19 +1455,19 @@ hipError_t fs_linear_f32_pair_bn_impl(const GemmArgs &g0, const GemmArgs &g1, co
         Q.begin = wg;
         wg += Q.mt * Q.nt;
     }
-    if (role == 1) {
-        if (g0.M != f.B || g0.N != f.H || g0.ldc != f.H || g0.C != f.gu || !ga.p[0].ak || ga.p[0].bk || ga.p[1].ak ||
-            ga.p[1].bk)
-            return hipErrorInvalidValue;
+    if (ga.p[0].bk || ga.p[1].bk || ga.p[1].ak) return hipErrorInvalidValue;
+    if (fout) {  // g0's output is the BatchNorm output's gradient gu [B][H]
+        const BnFold &f = *fout;
+        if (g0.M != f.B || g0.N != f.H || g0.ldc != f.H || g0.C != f.gu || !ga.p[0].ak) return hipErrorInvalidValue;
         ga.p[0].g.pstats = 1;
-    } else if (role == 2) {
+    }
+    if (fin) {  // A of both products is dy (g0 row-major, g1 transposed), f.gu its layout
+        const BnFold &f = *fin;
         if (!f.gamma || g0.A != f.gu || g1.A != f.gu || g0.M != f.B || g0.K != f.H || g0.sam != f.H || g0.sak != 1 ||
-            !ga.p[0].ak || ga.p[0].bk || g1.M != f.H || g1.K != f.B || g1.sam != 1 || g1.sak != f.H || ga.p[1].bk)
+            !ga.p[0].ak || g1.M != f.H || g1.K != f.B || g1.sam != 1 || g1.sak != f.H)
             return hipErrorInvalidValue;
         ga.p[0].vmode = 1;
         ga.p[1].vmode = 2;
-    } else {
-        return hipErrorInvalidValue;
     }
     hipLaunchKernelGGL(gemm_ling_fold_kernel, dim3(wg), dim3(512), 0, st, ga);
     return hipGetLastError();

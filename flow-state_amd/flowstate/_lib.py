@@ -61,7 +61,8 @@ class BnFold(ctypes.Structure):
     backward pairs around it (fs_linear_f32_pair_bn)."""
     _fields_ = [("gu", ctypes.c_void_p), ("u", ctypes.c_void_p), ("y", ctypes.c_void_p), ("mean", ctypes.c_void_p),
                 ("invstd", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("part", ctypes.c_void_p),
-                ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p), ("B", ctypes.c_int64), ("H", ctypes.c_int32)]
+                ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p), ("dx_add", ctypes.c_void_p),
+                ("a_out", ctypes.c_void_p), ("B", ctypes.c_int64), ("H", ctypes.c_int32)]
 
 
 class FlowStateError(RuntimeError):
@@ -115,7 +116,7 @@ _SIGS = {
                                      _P, _P]),
     "fs_linear_f32_pair": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(GemmF32), _P]),
     "fs_linear_f32_pair_bn": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(GemmF32),
-                                             ctypes.POINTER(BnFold), ctypes.c_int32, _P]),
+                                             ctypes.POINTER(BnFold), ctypes.POINTER(BnFold), _P]),
     "fs_linear_f32_splitk_floats": (_I64, [ctypes.POINTER(GemmF32)]),
     "fs_linear_f32_splitk": (ctypes.c_int, [ctypes.POINTER(GemmF32), _P, _I64, _P]),
     "fs_linear_f32_ex": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(BnIn), _P, _P]),

@@ -228,19 +228,22 @@ def _zero_grad_placeholder(dev, M, K):
 
 
 class _BnFoldLink:
-    """Carries a residual block's second BatchNorm backward from its second Linear's
-    backward (which computes gu = dL/du and the per-tile sums, fs_linear_f32_pair_bn role 1)
-    to its first Linear's backward (whose weight / input gradient pair loads dy = dL/dy from
-    them, role 2, and writes that BatchNorm's dgamma / dbeta): the BatchNorm backward launch
-    and dy itself disappear.  A side channel like _ResidualGrad: the second Linear hands
-    autograd a zero placeholder for dy, so it is only built where the whole backward runs
-    through the block (paired_kld's graphs); the first Linear takes the BatchNorm's gamma
-    and beta as extra inputs to return their gradients."""
+    """Carries a BatchNorm backward between the two Linear backward pairs around it
+    (fs_linear_f32_pair_bn): the producer, the Linear that applies the BatchNorm to its
+    input, computes its output gradient gu and the per-tile sums (fout); the consumer, the
+    Function whose output the BatchNorm normalises, loads the BatchNorm's input gradient dy
+    from them (+ the block's residual gradient for a block's first BatchNorm, fin) and writes
+    that BatchNorm's dgamma / dbeta: the BatchNorm-backward launches and dy disappear.  A side
+    channel like _ResidualGrad: the producer hands autograd a zero placeholder for dy, so it
+    is only built where the whole backward runs through the conditioner (paired_kld's
+    graphs); the consumer takes the BatchNorm's gamma and beta as extra inputs to return
+    their gradients, and writes dy out where the residual needs it (a_out)."""
 
-    __slots__ = ("pending",)
+    __slots__ = ("pending", "consumer_ok")
 
     def __init__(self):
         self.pending = None
+        self.consumer_ok = False  # set by the consuming Function's forward (it runs first)
 
 
 def _grad_out(*ps, direct=False):
@@ -408,7 +411,7 @@ class _LinearStats(torch.autograd.Function):
     batch statistics of the BatchNorm that consumes y, fs_linear_f32_ex stats_out)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, pair=None):
+    def forward(ctx, x, w, b, pair=None, fold_in=None, gamma2=None, beta2=None):
         from .. import _lib
 
         x = x.contiguous()
@@ -416,6 +419,11 @@ class _LinearStats(torch.autograd.Function):
         N = w.shape[0]
         y = torch.empty((M, N), dtype=torch.float32, device=x.device)
         st = torch.empty(((M + 31) // 32, N, 2), dtype=torch.float32, device=x.device)
+        ok = fold_in is not None and _fold_ok(M, K, N)  # the first block's first BatchNorm folded in here
+        ctx.fold_in = fold_in if ok else None
+        if fold_in is not None:
+            fold_in.consumer_ok = ok
+        ctx.gparams2 = (gamma2, beta2)
         _lib.require_device(x, w, b)
         if pair is None:
             _lib.check(_lib.load().fs_linear_f32_ex(_gemm_desc(x, w, b, None, y), None, _lib.ptr(st),
@@ -438,17 +446,29 @@ class _LinearStats(torch.autograd.Function):
 
         x, w = ctx.saved_tensors
         if gy is None:  # y unused by the loss
-            return None, None, None, None
-        gy = gy.contiguous()
+            return None, None, None, None, None, None, None
+        fin = ctx.fold_in.pending if ctx.fold_in is not None else None
         M, K = x.shape
         N = w.shape[0]
         gx, gw = torch.empty_like(x), _grad_out(w, direct=ctx.direct)
         gb = _grad_out(ctx.bias, direct=ctx.direct)
         p = _lib.ptr
+        if fin is not None:  # dy of the first block's first BatchNorm, loaded on the fly
+            ctx.fold_in.pending = None
+            gu2, u2, y2, mean2, invstd2, gamma2, part2, add2 = fin
+            gg2 = _grad_out(ctx.gparams2[0], direct=ctx.direct)
+            gbeta2 = _grad_out(ctx.gparams2[1], direct=ctx.direct)
+            g0 = _lib.GemmF32(M, K, N, p(gu2), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
+            g1 = _lib.GemmF32(N, K, M, p(gu2), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
+            fi = _lib.BnFold(p(gu2), p(u2), p(y2), p(mean2), p(invstd2), p(gamma2), p(part2), p(gg2), p(gbeta2),
+                             p(add2), None, M, N)
+            _lib.check(_lib.load().fs_linear_f32_pair_bn(g0, g1, fi, None, _lib.stream_ptr()), "fs_linear_f32_pair_bn")
+            return gx, gw, gb, None, None, gg2, gbeta2
+        gy = gy.contiguous()
         g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
         g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
         _lib.check(_lib.load().fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
-        return gx, gw, gb, None
+        return gx, gw, gb, None, None, None, None
 
 
 class _BnReluLinear(torch.autograd.Function):
@@ -462,7 +482,7 @@ class _BnReluLinear(torch.autograd.Function):
     _BnRelu)."""
 
     @staticmethod
-    def forward(ctx, x, x_stats, gamma, beta, bn, w, b, r, res=None, pair=None, op=None, fold=None, fold_role=0,
+    def forward(ctx, x, x_stats, gamma, beta, bn, w, b, r, res=None, pair=None, op=None, fold_in=None, fold_out=None,
                 gamma2=None, beta2=None):
         from .. import _lib
 
@@ -473,12 +493,14 @@ class _BnReluLinear(torch.autograd.Function):
         st = torch.empty(((M + 31) // 32, N, 2), dtype=torch.float32, device=x.device)
         invstd = torch.empty((K,), dtype=torch.float32, device=x.device)
         u = torch.empty_like(x) if any(ctx.needs_input_grad) else None
-        # fold_role 1: this Linear follows the folded BatchNorm; 2: precedes it (gamma2, beta2
-        # are that BatchNorm's, their gradients returned here)
-        # (the lean kernels' limits: the weight gradients reduce over the batch in quads)
-        ctx.fold = fold if (fold is not None and _fold_bn and _direct_grads and N <= 256 and K <= 256 and M % 4 == 0
-                            and _lib.load().fs_set_lean_gemm(-1) == 1) else None
-        ctx.fold_role = fold_role
+        # fold_out: this Linear's own BatchNorm (applied to x); fold_in: the BatchNorm that
+        # normalises y (gamma2, beta2, their gradients returned here).  The lean kernels'
+        # limits: widths <= 256, the weight gradients reduce over the batch in quads.
+        ok = _fold_ok(M, K, N)
+        ctx.fold_in = fold_in if ok else None
+        if fold_in is not None:
+            fold_in.consumer_ok = ok
+        ctx.fold_out = fold_out if ok else None
         ctx.gparams2 = (gamma2, beta2)
         p = _lib.ptr
         _lib.require_device(x, x_stats, gamma, beta, w, b, r)
@@ -518,68 +540,71 @@ class _BnReluLinear(torch.autograd.Function):
         N = w.shape[0]
         L = _lib.load()
         p = _lib.ptr
-        fold = ctx.fold
-        if fold is not None and ctx.fold_role == 2 and fold.pending is None:
-            fold = None  # the following Linear did not fold (its backward ran unfolded)
-        if fold is not None and ctx.fold_role == 1 and (ctx.res is None or not ctx.has_r):
-            fold = None
+        # dy of the BatchNorm that normalises y, not materialised (its producer folded it)
+        fin = ctx.fold_in.pending if ctx.fold_in is not None else None
+        if fin is not None:
+            ctx.fold_in.pending = None
+        fout = ctx.fold_out if (ctx.fold_out is not None and ctx.fold_out.consumer_ok) else None
         gw = _grad_out(w, direct=ctx.direct)
         gb = _grad_out(ctx.gparams[1], direct=ctx.direct)
-        if fold is not None and ctx.fold_role == 1:
-            # gu = dL/du and the folded BatchNorm's tile sums; dy is left to the preceding
-            # Linear's backward (fs_linear_f32_pair_bn, _BnFoldLink)
-            gy = gy.contiguous()
-            gu = torch.empty_like(u)
-            part = torch.empty(((M + 31) // 32, K, 2), dtype=torch.float32, device=x.device)
-            g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
-            g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
-            f = _lib.BnFold(p(gu), p(u), p(x), p(mean), p(invstd), p(gamma), p(part), None, None, M, K)
-            _lib.check(L.fs_linear_f32_pair_bn(g0, g1, f, 1, _lib.stream_ptr()), "fs_linear_f32_pair_bn")
-            fold.pending = (gu, u, x, mean, invstd, gamma, part)
-            ctx.res.g = gy  # to the block's first BatchNorm backward (its dx_add)
-            gx = _zero_grad_placeholder(x.device, M, K)  # the placeholder for dy
-            return gx, None, None, None, None, gw, gb, None, None, None, None, None, None, None, None
-        add = None
+        add = None  # the block's residual gradient, for its first BatchNorm (this Linear's own)
         if ctx.res is not None and ctx.res.g is not None:
             add, ctx.res.g = ctx.res.g, None
+        if fin is None:
+            gy = gy.contiguous()
+        dy = fin[0] if fin is not None else gy  # (fin: only the layout, gu of the folded BatchNorm)
+        gu = torch.empty_like(u)
+        g0 = _lib.GemmF32(M, K, N, p(dy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
+        g1 = _lib.GemmF32(N, K, M, p(dy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
+        gg2 = gbeta2 = a_out = None
+        fi = fo = None
+        if fin is not None:
+            gu2, u2, y2, mean2, invstd2, gamma2, part2, add2 = fin
+            gg2 = _grad_out(ctx.gparams2[0], direct=ctx.direct)
+            gbeta2 = _grad_out(ctx.gparams2[1], direct=ctx.direct)
+            if ctx.has_r and ctx.needs_input_grad[7]:
+                a_out = torch.empty((M, N), dtype=torch.float32, device=x.device)  # dy for the residual
+            fi = _lib.BnFold(p(gu2), p(u2), p(y2), p(mean2), p(invstd2), p(gamma2), p(part2), p(gg2), p(gbeta2),
+                             p(add2), p(a_out), M, N)
+        if fout is not None:
+            part = torch.empty(((M + 31) // 32, K, 2), dtype=torch.float32, device=x.device)
+            fo = _lib.BnFold(p(gu), p(u), p(x), p(mean), p(invstd), p(gamma), p(part), None, None, None, None, M, K)
+        # the input / weight gradient pair over 48 workgroups, then the BatchNorm + ReLU
+        # backward unless it is folded into the pair before (r04): 10.9 us per layer in a
+        # graph, against 18.1 us for one launch whose column strips own the BatchNorm sums
+        # (tools/linbn_probe.py, profiles/r03/r03k_linbn_probe.log), and 148 against 239
+        # steps/s for the BatchNorm backward run by each strip's last tile in the pair's launch
+        # (device-scope fences; DESIGN "Training", profiles/r03/r03v_*)
+        if fi is not None or fo is not None:
+            _lib.check(L.fs_linear_f32_pair_bn(g0, g1, fi, fo, _lib.stream_ptr()), "fs_linear_f32_pair_bn")
+        else:
+            _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
+        gr = None
+        if ctx.has_r and ctx.needs_input_grad[7]:
+            g_out = a_out if fin is not None else gy
+            if ctx.res is not None:
+                ctx.res.g = g_out  # to the block's first BatchNorm backward (its dx_add)
+            else:
+                gr = g_out
+        if fout is not None:
+            fout.pending = (gu, u, x, mean, invstd, gamma, part, add)
+            gx = _zero_grad_placeholder(x.device, M, K)  # the placeholder for this BatchNorm's dy
+            return gx, None, None, None, None, gw, gb, gr, None, None, None, None, None, gg2, gbeta2
         gx = torch.empty_like(x)
         gg = _grad_out(gamma, direct=ctx.direct)
         gbeta = _grad_out(ctx.gparams[0], direct=ctx.direct)
-        if fold is not None and ctx.fold_role == 2:
-            # dy = dL/dy loaded from the following Linear's gu and tile sums; that BatchNorm's
-            # dgamma / dbeta written by the same launch
-            gu2, u2, y2, mean2, invstd2, gamma2, part = fold.pending
-            fold.pending = None
-            gg2 = _grad_out(ctx.gparams2[0], direct=ctx.direct)
-            gbeta2 = _grad_out(ctx.gparams2[1], direct=ctx.direct)
-            gu = torch.empty_like(u)
-            g0 = _lib.GemmF32(M, K, N, p(gu2), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
-            g1 = _lib.GemmF32(N, K, M, p(gu2), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
-            f = _lib.BnFold(p(gu2), p(u2), p(y2), p(mean2), p(invstd2), p(gamma2), p(part), p(gg2), p(gbeta2), M, N)
-            _lib.check(L.fs_linear_f32_pair_bn(g0, g1, f, 2, _lib.stream_ptr()), "fs_linear_f32_pair_bn")
-            _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
-                                              p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
-            return gx, None, gg, gbeta, None, gw, gb, None, None, None, None, None, None, gg2, gbeta2
-        gy = gy.contiguous()
-        # the input / weight gradient pair over 48 workgroups, then the BatchNorm + ReLU
-        # backward: 10.9 us per layer in a graph, against 18.1 us for one launch whose
-        # column strips own the BatchNorm sums (4 workgroups carry the whole input gradient;
-        # tools/linbn_probe.py, profiles/r03/r03k_linbn_probe.log), and 148 against 239
-        # steps/s for the BatchNorm backward run by each strip's last tile in the pair's
-        # launch (device-scope fences; DESIGN "Training", profiles/r03/r03v_*)
-        gu = torch.empty_like(u)
-        g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
-        g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
-        _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
         _lib.check(L.fs_bn_relu_train_bwd(M, K, p(x), p(u), p(gu), p(gamma), p(mean), p(invstd), p(gx), p(add),
                                           p(gg), p(gbeta), _lib.stream_ptr()), "fs_bn_relu_train_bwd")
-        gr = None
-        if ctx.has_r and ctx.needs_input_grad[7]:
-            if ctx.res is not None:
-                ctx.res.g = gy  # to the block's first BatchNorm backward (its dx_add)
-            else:
-                gr = gy
-        return gx, None, gg, gbeta, None, gw, gb, gr, None, None, None, None, None, None, None
+        return gx, None, gg, gbeta, None, gw, gb, gr, None, None, None, None, None, gg2, gbeta2
+
+
+def _fold_ok(M, K, N):
+    """A BatchNorm-backward fold applies to a Linear of this shape (lean kernels, widths <= 256,
+    batch a multiple of 4) in the graphs paired_kld builds."""
+    from .. import _lib
+
+    return (_fold_bn and _direct_grads and N <= 256 and K <= 256 and M % 4 == 0
+            and _lib.load().fs_set_lean_gemm(-1) == 1)
 
 
 def _fused_ok(net, t):
@@ -623,16 +648,22 @@ def _conditioner_fused(net, t, pair=None, final=True):
     BatchNorm backward with the residual gradient added by the block's first one."""
     li = net.initial_layer
     if _bn_in_load_ok(net):
-        t, st = _LinearStats.apply(t, li.weight, li.bias, pair)
-        for i, blk in enumerate(net.blocks):
+        blocks = list(net.blocks)
+        links0 = [_BnFoldLink() for _ in blocks]  # each block's first BatchNorm
+        first = blocks[0].batch_norm_layers[0] if blocks else None
+        t, st = _LinearStats.apply(t, li.weight, li.bias, pair, links0[0] if blocks else None,
+                                   first.weight if blocks else None, first.bias if blocks else None)
+        for i, blk in enumerate(blocks):
             bn0, bn1 = blk.batch_norm_layers
             l0, l1 = blk.linear_layers
             res = _ResidualGrad()
-            fold = _BnFoldLink()
+            link1 = _BnFoldLink()  # its second BatchNorm
             u, su = _BnReluLinear.apply(t, st, bn0.weight, bn0.bias, bn0, l0.weight, l0.bias, None, res, pair, (i, 0),
-                                        fold, 2, bn1.weight, bn1.bias)
+                                        link1, links0[i], bn1.weight, bn1.bias)
+            nxt = blocks[i + 1].batch_norm_layers[0] if i + 1 < len(blocks) else None
             t, st = _BnReluLinear.apply(u, su, bn1.weight, bn1.bias, bn1, l1.weight, l1.bias, t, res, pair, (i, 1),
-                                        fold, 1)
+                                        links0[i + 1] if nxt is not None else None, link1,
+                                        nxt.weight if nxt is not None else None, nxt.bias if nxt is not None else None)
         if not final:  # the caller fuses the final Linear into its next Function (_FinalSplines)
             return t
         lf = net.final_layer

@@ -358,27 +358,31 @@ typedef struct fs_gemm_f32 {
 } fs_gemm_f32;
 int fs_linear_f32_pair(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, void *stream);
 
-/* nn.Linear's backward pairs on either side of a BatchNorm1d (train) + ReLU, with the
- * BatchNorm's backward folded into them (replaces the pair, fs_bn_relu_train_bwd, pair
- * sequence inside a residual block: resnet.py:44-49, the block's second BatchNorm).
- * role 1 (producer): g0, g1 = the pair of the Linear after the BatchNorm; g0's output must be
- *   gu = dL/du, u = relu(BN(y)), [B][H] contiguous (g0.C == f->gu); its epilogue writes per
- *   32-row tile the column sums of dz = gu (u > 0) and dz xhat into f->part.
- * role 2 (consumer): g0 = dy W and g1 = dy^T X of the Linear before it, where dy = dL/dy is
- *   not materialised: both take A = f->gu as its layout (g0: row-major, sam = H, sak = 1;
- *   g1: the transpose, sam = 1, sak = H) and load dy = gamma invstd (dz - sum dz / B -
- *   xhat sum(dz xhat) / B) from gu, u, y and the tile sums; workgroup 0 writes dgamma and
- *   dbeta (nullable).  Lean kernels only (fs_set_lean_gemm(1)); H <= 256, no residual. */
+/* nn.Linear's backward pair with the BatchNorm1d (train) + ReLU backwards around it folded
+ * in (replaces the pair, fs_bn_relu_train_bwd sequence of a ResidualNet: resnet.py:37-51).
+ * fout (nullable): the BatchNorm this Linear applies to its input.  g0's output must be that
+ *   BatchNorm's output gradient gu = dL/du, u = relu(BN(y)), [B][H] contiguous
+ *   (g0.C == fout->gu); its epilogue writes per 32-row tile the column sums of
+ *   dz = gu (u > 0) and dz xhat into fout->part.
+ * fin (nullable): the BatchNorm that consumes this Linear's output.  Its input gradient
+ *   dy = gamma invstd (dz - sum dz / B - xhat sum(dz xhat) / B) (+ fin->dx_add, the residual
+ *   gradient) is not materialised: g0 = dy W and g1 = dy^T X take A = fin->gu as its layout
+ *   (g0: row-major, sam = H, sak = 1; g1: the transpose, sam = 1, sak = H) and load dy from
+ *   gu, u, y and the tile sums; workgroup 0 writes dgamma and dbeta (nullable); fin->a_out
+ *   (nullable) receives dy.
+ * Lean kernels only (fs_set_lean_gemm(1)); H <= 256, B a multiple of 4, no residual output. */
 typedef struct fs_bn_fold {
     const float *gu, *u, *y;            /* [B][H] */
     const float *mean, *invstd, *gamma; /* [H] */
     float *part;                        /* [ceil(B / 32)][H][2] */
-    float *dgamma, *dbeta;              /* [H], nullable */
+    float *dgamma, *dbeta;              /* [H], nullable (fin) */
+    const float *dx_add;                /* [B][H], nullable (fin) */
+    float *a_out;                       /* [B][H], nullable (fin) */
     int64_t B;
     int32_t H;
 } fs_bn_fold;
-int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs_bn_fold *f, int32_t role,
-                          void *stream);
+int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs_bn_fold *fin,
+                          const fs_bn_fold *fout, void *stream);
 
 /* fs_linear_f32 with the ResidualNet's BatchNorm plumbing fused in (resnet.py:35-51):
  * stats_out (nullable) [ceil(M/32)][N][2] receives each 32-row tile's column mean and sum
