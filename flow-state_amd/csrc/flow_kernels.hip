@@ -363,27 +363,21 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
     return 0.f;
 }
 
-// cond_spline for a feature pair (K <= 16): both tiles of the pair first, then each
-// feature's spline from its 16 columns (c0 = 0 or 16) of the lane-per-chain tiles.
-// RM: lane -> chain mask (31: a 32-chain tile pair duplicated into both lane halves, whose
-// upper half only computes)
-template <int XS, int H, int K, bool INV, int RM = 63>
-__device__ __forceinline__ float spline_from_tiles(const f32x16 (&tS)[2][1], const f32x16 (&tO)[2][1], int c0,
-                                                   const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int dsec,
-                                                   const float *__restrict__ bd, float *CO, int cs, int p,
-                                                   const FlowArgs &a, bool &nan_any, Prof &pf) {
+// The conditional spline of one feature of one chain from its width / height logits (uS:
+// the searched set, uO: the other): knots, bin, the derivative logits d_bin, d_bin+1 by
+// dot products of the chain's hidden vector xr with the gathered rows of the final layer,
+// the spline; co: the chain's coordinates (element p updated when inside and store).
+template <int H, int K, bool INV>
+__device__ __forceinline__ float spline_from_logits(const float (&uS)[K], const float (&uO)[K],
+                                                    const float *__restrict__ xr, __amdgpu_buffer_rsrc_t W, int dsec,
+                                                    const float *__restrict__ bd, float *co, int p, bool store,
+                                                    const FlowArgs &a, bool &nan_any, Prof &pf) {
     constexpr int NQ = H / 4;
     constexpr int QB = NQ >= 8 ? 4 : NQ / 2;
-    const int lane = (int)threadIdx.x & RM;
-    const float x = CO[lane * cs + p];
+    const float x = co[p];
     const bool inside = (x >= a.negB) && (x <= a.B);
     float ks[K + 1];
-    {
-        float u[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) u[k] = tile_row(tS[0][0], tS[1][0], c0 + k);
-        knots_from_logits<K>(u, ks, INV ? kMinHd : kMinWd, a);
-    }
+    knots_from_logits<K>(uS, ks, INV ? kMinHd : kMinWd, a);
     int bin = 0;
     float s0 = ks[0], s1 = ks[1];
 #pragma unroll
@@ -400,10 +394,8 @@ __device__ __forceinline__ float spline_from_tiles(const f32x16 (&tS)[2][1], con
     f32x2 ud0 = {bd[bin], 0.f}, ud1 = {bd[bin + 1], 0.f};
     float o0, o1;
     {
-        float u[K], ko[K + 1];
-#pragma unroll
-        for (int k = 0; k < K; ++k) u[k] = tile_row(tO[0][0], tO[1][0], c0 + k);
-        knots_from_logits<K>(u, ko, INV ? kMinWd : kMinHd, a);
+        float ko[K + 1];
+        knots_from_logits<K>(uO, ko, INV ? kMinWd : kMinHd, a);
         o0 = ko[0];
         o1 = ko[1];
 #pragma unroll
@@ -415,7 +407,6 @@ __device__ __forceinline__ float spline_from_tiles(const f32x16 (&tS)[2][1], con
         }
     }
     pf.mark(PH_SPLINE);
-    const float *xr = X + lane * XS;
 #pragma unroll 1
     for (int q0 = 0; q0 < NQ; q0 += 2 * QB) {
         drows_issue<QB, K>(g1, W, voff, dsec, q0 + QB);
@@ -433,11 +424,31 @@ __device__ __forceinline__ float spline_from_tiles(const f32x16 (&tS)[2][1], con
     rqs_eval<INV>(x, icw, cw1 - icw, ich, ch1 - ich, d0, d1, y, l, nd);
     pf.mark(PH_SPLINE);
     if (inside) {
-        if (RM == 63 || (threadIdx.x & 32) == 0) CO[lane * cs + p] = y;
+        if (store) co[p] = y;
         nan_any |= nd;
         return l;
     }
     return 0.f;
+}
+
+// cond_spline for a feature pair (K <= 16): both tiles of the pair first, then each
+// feature's spline from its 16 columns (c0 = 0 or 16) of the lane-per-chain tiles.
+// RM: lane -> chain mask (31: a 32-chain tile pair duplicated into both lane halves, whose
+// upper half only computes)
+template <int XS, int H, int K, bool INV, int RM = 63>
+__device__ __forceinline__ float spline_from_tiles(const f32x16 (&tS)[2][1], const f32x16 (&tO)[2][1], int c0,
+                                                   const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int dsec,
+                                                   const float *__restrict__ bd, float *CO, int cs, int p,
+                                                   const FlowArgs &a, bool &nan_any, Prof &pf) {
+    const int lane = (int)threadIdx.x & RM;
+    float uS[K], uO[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        uS[k] = tile_row(tS[0][0], tS[1][0], c0 + k);
+        uO[k] = tile_row(tO[0][0], tO[1][0], c0 + k);
+    }
+    return spline_from_logits<H, K, INV>(uS, uO, X + lane * XS, W, dsec, bd, CO + lane * cs, p,
+                                         RM == 63 || (threadIdx.x & 32) == 0, a, nan_any, pf);
 }
 
 #pragma clang fp contract(on)
@@ -1326,6 +1337,131 @@ __global__ void __launch_bounds__(64 * WPB) wide_final_kernel(WideArgs w) {
     if (nan_any && store && row0 + lane < a.nrows && a.err) atomicOr(a.err, 1);
 }
 
+// The final phase on 16-row blocks (K <= 16, small batches): the feature pair's two tiles
+// for 16 chains on v_mfma_f32_16x16x4_f32 fed the 32x32x2 k order (the 16-row trunk's
+// trick: the same exact chain, bit-identical), a quarter of the 64-row blocks' MFMA chain
+// per wave; the tiles go through LDS to one lane per (chain, feature), so the pair's two
+// splines run side by side instead of one after the other.
+// acc[c]: columns 16 c + 4 q + i of the pair tile (c = 0: feature a, 1: feature b) for the
+// lane's chain r, bias preset (the bias add rides on the MFMAs, as in final_tile_pair).
+template <int XS, int PD>
+__device__ __forceinline__ void final_pair16(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
+                                             int tile, const float *__restrict__ ba, const float *__restrict__ bb,
+                                             f32x4 (&acc)[2]) {
+    const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15, qo = q & 1, qh = q >> 1;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[c][i] = (c == 0 ? ba : bb)[4 * q + i];
+    const float *xr = X + r * XS + 4 * qo + qh;
+    // lane (q, r) of half c takes the 32-row fragment's lane 32 qo + 16 c + r, elements qh, 2 + qh
+    const int vb = (32 * qo + r) * 16;
+    const int fb = sec + tile * kg * 1024;
+    f32x4 rw[PD][2];
+    float rx[PD][2];
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+        if (s < kg) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) rw[s][c] = ldb_frag(W, vb + 256 * c, fb + s * 1024);
+            rx[s][0] = xr[8 * s];
+            rx[s][1] = xr[8 * s + 2];
+        }
+    for (int g0 = 0; g0 < kg; g0 += PD) {
+#pragma unroll
+        for (int s = 0; s < PD; ++s) {
+            const int g = g0 + s;
+            if (g < kg) {
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const float e0 = qh ? rw[s][c][1] : rw[s][c][0], e1 = qh ? rw[s][c][3] : rw[s][c][2];
+                    acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(e0, rx[s][0], acc[c], 0, 0, 0);
+                    acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(e1, rx[s][1], acc[c], 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const int gn = g + PD;
+                if (gn < kg) {
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) rw[s][c] = ldb_frag(W, vb + 256 * c, fb + gn * 1024);
+                    rx[s][0] = xr[8 * gn];
+                    rx[s][1] = xr[8 * gn + 2];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+}
+
+template <int H, int K, int MODE, int WPB>
+__global__ void __launch_bounds__(64 * WPB) wide_final16_kernel(WideArgs w) {
+    static_assert(K <= 16, "16-row final blocks: feature pairs only");
+    constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
+    constexpr bool INV = MODE != MODE_DENSITY;
+    constexpr int TS = INV ? 1 : 0;
+    __shared__ __attribute__((aligned(16))) float X[16 * XS];
+    __shared__ float T[WPB][2][16][33];  // per wave: the two tiles, chain-major (33: no bank conflicts)
+    const FlowArgs &a = w.a;
+    const int N = a.N, D = 2 * N;
+    const PackLayout PL = pack_layout(N, H, a.nb, a.K);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, r = lane & 15;
+    const int u = __builtin_amdgcn_readfirstlane((int)blockIdx.y * WPB + wv);
+    const int64_t row0 = (int64_t)blockIdx.x * 16;
+    const float *Xg = w.XB + row0 * XS;
+    for (int e = threadIdx.x; e < 16 * (H / 4); e += blockDim.x) {
+        const int rr = e / (H / 4), qq = e - rr * (H / 4);
+        *(f32x4 *)(X + rr * XS + 4 * qq) = *(const f32x4 *)(Xg + rr * XS + 4 * qq);
+    }
+    __syncthreads();
+    if (2 * u >= N) return;
+    float *CO = w.CO + row0 * D;
+    const int cs = D, off = w.off;
+    const float *P = a.packed + (int64_t)w.layer * PL.stride;
+    const float *V = P + PL.vec;
+    const __amdgpu_buffer_rsrc_t W =
+        __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
+    const int pp = u, ja = 2 * pp, jb = 2 * pp + 1;
+    const bool hb = jb < N;
+    const float *ba = V + PL.v_bf + 96 * ja;
+    const float *bb = hb ? V + PL.v_bf + 96 * jb : ba + 16;
+    f32x4 tS[2], tO[2];
+    final_pair16<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + TS, ba + 32 * TS, bb + 32 * TS, tS);
+    final_pair16<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * pp + 1 - TS, ba + 32 * (1 - TS),
+                               bb + 32 * (1 - TS), tO);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            T[wv][0][r][16 * c + 4 * q + i] = tS[c][i];
+            T[wv][1][r][16 * c + 4 * q + i] = tO[c][i];
+        }
+    wave_lds_sync();  // this wave's tiles are in LDS
+    // lane (f, chain): the spline of feature ja + f of chain lane & 15 (lanes 32-63 repeat
+    // lanes 0-31 without storing)
+    const int ch = lane & 15, f = (lane >> 4) & 1;
+    const bool store = lane < 32;
+    const int j = f ? jb : ja;
+    bool nan_any = false;
+    Prof pf;
+    if (!f || hb) {
+        float uS[K], uO[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            uS[k] = T[wv][0][ch][16 * f + k];
+            uO[k] = T[wv][1][ch][16 * f + k];
+        }
+        const float l = spline_from_logits<H, K, INV>(uS, uO, X + ch * XS, W,
+                                                      (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
+                                                      V + PL.v_bd + j * (K + 1), CO + ch * cs, (2 * j + 1 + off) % D,
+                                                      store, a, nan_any, pf);
+        if (store) w.LDC[(row0 + ch) * N + j] = l;
+        if (MODE == MODE_DENSITY && store) {
+            const float lu = uncond_at<K, false>(P + PL.unc, CO + ch * cs, (2 * j + off) % D, a, nan_any, j);
+            w.LDU[(row0 + ch) * N + j] = lu;
+        }
+    }
+    if (nan_any && store && row0 + ch < a.nrows && a.err) atomicOr(a.err, 1);
+}
+
 template <int K, int MODE>
 __global__ void __launch_bounds__(kThreads) wide_output_kernel(WideArgs w) {
     const FlowArgs &a = w.a;
@@ -1619,18 +1755,18 @@ static int wide_trunk16() {
     return v;
 }
 
-// the final phase on 32-row blocks for small batches (default, or FS_WIDE_FINAL32=0 /
-// fs_set_wide_final32(0) for 64-row blocks); bit-identical either way
+// the final phase on 16- or 32-row blocks for small batches (2, default), 32-row at most (1),
+// or 64-row blocks (0): FS_WIDE_FINAL32, fs_set_wide_final32; bit-identical in every setting
 static std::atomic<int> g_final32{-1};
-static bool wide_final32() {
+static int wide_final32() {
     int v = g_final32.load(std::memory_order_relaxed);
     if (v < 0) {
         const char *e = getenv("FS_WIDE_FINAL32");
         int expect = -1;
-        g_final32.compare_exchange_strong(expect, (e && e[0] == '0') ? 0 : 1);
+        g_final32.compare_exchange_strong(expect, (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2);
         v = g_final32.load(std::memory_order_relaxed);
     }
-    return v != 0;
+    return v;
 }
 
 static size_t wide_bytes(int64_t R, int N, int H) {
@@ -1805,12 +1941,15 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     // that the 32-row tiles' higher arithmetic intensity wins (8192 rows: 9.0 vs 11.6 ms per
     // A1 N=16 pass, profiles/r04/)
     const int trunk16 = R / 16 <= device_cus() ? wide_trunk16() : 0;
-    // 32-row final-phase blocks (feature pairs) while twice the 64-row grid fits the chip
-    const int fgy = (units + WPW - 1) / WPW;
-    const bool final32 = K <= 16 && wide_final32() && (R / 32) * fgy <= device_cus();
+    // 16- or 32-row final-phase blocks (feature pairs) while the grid fits the chip in a round
+    const int fgy = (units + WPW - 1) / WPW, fsel = K <= 16 ? wide_final32() : 0;
+    const int frows = (fsel >= 2 && (R / 16) * fgy <= device_cus()) ? 16
+                      : (fsel >= 1 && (R / 32) * fgy <= device_cus()) ? 32 : kRows;
     const void *final_fn = (const void *)wide_final_kernel<H, K, MODE, WPW>;
-    if constexpr (K <= 16)
-        if (final32) final_fn = (const void *)wide_final_kernel<H, K, MODE, WPW, 32>;
+    if constexpr (K <= 16) {
+        if (frows == 32) final_fn = (const void *)wide_final_kernel<H, K, MODE, WPW, 32>;
+        if (frows == 16) final_fn = (const void *)wide_final16_kernel<H, K, MODE, WPW>;
+    }
     std::vector<WideLaunch> seq;
     seq.reserve(4 + (size_t)a.L * 3);
     auto add = [&](const void *f, dim3 g, dim3 b, unsigned lds) { seq.push_back({f, g, b, lds, w}); };
@@ -1830,7 +1969,9 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
             add((const void *)wide_trunk16_kernel<H>, dim3((unsigned)(R / 16)), dim3(64 * (H / 32)), 0);
         else if (trunk16 == 0)
             add((const void *)wide_trunk_kernel<H>, dim3((unsigned)(R / 32)), dim3(64 * (H / 32)), 0);
-        if (final32)
+        if (frows == 16)
+            add(final_fn, dim3((unsigned)(R / 16), fgy), dim3(64 * WPW), 0);
+        else if (frows == 32)
             add(final_fn, dim3((unsigned)(R / 32), fgy), dim3(64 * WPW), fin_lds / 2);
         else
             add(final_fn, dim3(nblk, fgy), dim3(64 * WPW), fin_lds);
@@ -1839,7 +1980,7 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     w.pending = 1;
     add((const void *)wide_output_kernel<K, MODE>, dim3(nblk), dim3(kThreads), 0);
     w.off = w.layer = w.jb = w.pending = 0;
-    hipError_t e = wide_run(seq, wide_key(w, seq.front().func, H, K, MODE, trunk16 | (final32 ? 4 : 0)), st);
+    hipError_t e = wide_run(seq, wide_key(w, seq.front().func, H, K, MODE, trunk16 | (frows << 4)), st);
     if (e == hipSuccess) used = true;
     return e;
 }
@@ -1865,8 +2006,8 @@ int32_t fs_set_wide_trunk16_impl(int32_t on) {
 }
 
 int32_t fs_set_wide_final32_impl(int32_t on) {
-    const int32_t prev = wide_final32() ? 1 : 0;
-    if (on >= 0) g_final32.store(on ? 1 : 0, std::memory_order_relaxed);
+    const int32_t prev = wide_final32();
+    if (on >= 0) g_final32.store(on > 2 ? 2 : on, std::memory_order_relaxed);
     return prev;
 }
 

@@ -164,7 +164,8 @@ def test_trunk16_bit_identical_to_trunk32(N, kw, B):
 
 
 class final32:
-    """The wide path's final phase on 32-row blocks (1, small batches) or 64-row ones (0)."""
+    """The wide path's final phase on 16- or 32-row blocks (2), 32-row at most (1) or 64-row
+    blocks (0), for small batches."""
 
     def __init__(self, on):
         self.on = on
@@ -180,20 +181,21 @@ class final32:
                                     (16, dict(L=3, H=64, nb=1, K=8), 333), (16, dict(L=2, H=256, nb=2, K=15), 150)],
                          ids=["a2-n64-200", "a2-n64-1000", "n3-h32-77", "n16-h64-333", "n16-h256-k15-150"])
 def test_final32_bit_identical_to_final64(N, kw, B):
-    """The final phase on 32-row blocks (one row tile per wave, each chain's spline in both
-    lane halves) against 64-row blocks and the fused kernel, density and sampling, with a
-    few out-of-bound inputs among the rows."""
+    """The final phase on 16-row blocks (v_mfma_f32_16x16x4_f32 fed the 32x32x2 k order, one
+    lane per chain and feature for the splines) and 32-row blocks (one row tile per wave,
+    each chain's spline in both lane halves) against 64-row blocks and the fused kernel,
+    density and sampling, with a few out-of-bound inputs among the rows."""
     dims, sd, m = _model(N, kw, seed=12)
     g = torch.Generator().manual_seed(B + 1)
     x = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B * 1.001).cuda()  # a few rows outside the bound
     zb = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
     outs = []
     with wide_rows(16384):
-        for on in (1, 0):
+        for on in (2, 1, 0):
             with final32(on):
                 outs.append([m.log_prob(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)])
     with wide_rows(0):
         outs.append([m.log_prob(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)])
     torch.cuda.synchronize()
-    for a, b, c in zip(*outs):
-        assert torch.equal(a, b) and torch.equal(a, c)
+    for a, b, c, d in zip(*outs):
+        assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(a, d)
