@@ -167,8 +167,9 @@ def test_coupling_waves_bit_identical(N, kw, rows):
 
 
 @pytest.mark.parametrize("N,kw,rows", [(16, dict(L=4, H=64, nb=2, K=8), 96), (64, A2, 256), (16, dict(L=3, H=32, nb=1,
-                                                                                                     K=5), 37)],
-                         ids=["n16-h64", "a2-n64", "n16-ragged"])
+                                                                                                     K=5), 37),
+                                       (16, dict(L=2, H=256, nb=3, K=8), 64), (64, A2, 232)],
+                         ids=["n16-h64", "a2-n64", "n16-ragged", "n16-h256-nb3", "a2-n64-232"])
 def test_bn_fold_matches_unfolded(N, kw, rows):
     """Every BatchNorm backward of the conditioner folded into the backward pairs around it
     (fs_linear_f32_pair_bn: per-tile sums in the producing pair's epilogue, dy loaded on the
