@@ -462,6 +462,18 @@ int fs_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg
                   "fs_adam_step");
 }
 
+int fs_kld_loss(const float *log_q, int64_t B, const float *energy, const float *lq_rev, int64_t R,
+                const int32_t *nan_word, float *loss, uint8_t *nan_out, void *stream) {
+    REQUIRE(B >= 1 && log_q && loss && (!energy || (R >= 1 && lq_rev)), "fs_kld_loss: invalid arguments");
+    return hip_rc(fs_kld_loss_impl(log_q, B, energy, lq_rev, R, nan_word, loss, nan_out, (hipStream_t)stream),
+                  "fs_kld_loss");
+}
+
+int fs_kld_loss_backward(const float *grad_loss, int64_t B, float *grad_log_q, void *stream) {
+    REQUIRE(B >= 1 && grad_loss && grad_log_q, "fs_kld_loss_backward: invalid arguments");
+    return hip_rc(fs_kld_loss_bwd_impl(grad_loss, B, grad_log_q, (hipStream_t)stream), "fs_kld_loss_backward");
+}
+
 int fs_target_energy(const float *x, int64_t B, int32_t N, double bound, double temperature, int32_t num_wells,
                      double V0_0, double V0_1, double r0, double k, float *E, float *grad_x, void *stream) {
     REQUIRE(B >= 0 && N >= 1 && N <= 1024 && bound > 0.0 && temperature > 0.0 && num_wells >= 0 && num_wells <= 2 &&

@@ -146,6 +146,9 @@ int64_t fs_linear_f32_splitk_floats_impl(const fs::GemmArgs &g);
 hipError_t fs_linear_f32_splitk_impl(const fs::GemmArgs &g, float *part, int64_t part_floats, hipStream_t st);
 hipError_t fs_adam_step_impl(float *p, const float *g, float *m, float *v, int64_t n, float *step, const float *loss,
                              const int32_t *skip, double lr, double beta1, double beta2, double eps, double weight_decay, hipStream_t st);
+hipError_t fs_kld_loss_impl(const float *log_q, int64_t B, const float *E, const float *lq_rev, int64_t R,
+                            const int32_t *nan_word, float *loss, uint8_t *nan_out, hipStream_t st);
+hipError_t fs_kld_loss_bwd_impl(const float *g, int64_t B, float *grad_log_q, hipStream_t st);
 hipError_t fs_linear_f32_group_impl(const fs::GemmArgs *gs, int n, float *ws, int64_t ws_floats, hipStream_t st);
 hipError_t fs_bn_relu_train_fwd_impl(int64_t B, int H, const float *x, const float *gamma, const float *beta,
                                      float *rm, float *rv, int64_t *nbt, float momentum, float eps, float *y,

@@ -90,6 +90,54 @@ __global__ void adam_count_kernel(float *step, const float *loss, const int32_t 
     *step = *step + 1.f;
 }
 
+// The Algorithm-2 loss head (main_algorithm_2.py:316-318 with ALPHA = 1; core.py
+// forward_kld / reverse_kld): loss = -mean(log_q) + 0 * (mean(E) + mean(lq_rev)), the
+// three means, the negation, the zero-weighted reverse term (NaN / inf when it is, so the
+// skip rule sees it) and the adds in one workgroup instead of seven launches; nan_out (a
+// torch bool) = the sticky spline-NaN word is set.  Each mean is an ordered tree sum: the
+// value agrees with torch's reduction within float32 rounding, not bit for bit.
+__device__ __forceinline__ float block_sum256(const float *__restrict__ x, int64_t n, float *red) {
+    const int t = threadIdx.x;
+    float a = 0.f;
+    for (int64_t i = t; i < n; i += 256) a += x[i];
+    red[t] = a;
+    __syncthreads();
+#pragma unroll
+    for (int w = 128; w > 0; w >>= 1) {
+        if (t < w) red[t] = red[t] + red[t + w];
+        __syncthreads();
+    }
+    const float r = red[0];
+    __syncthreads();
+    return r;
+}
+
+__global__ void __launch_bounds__(256) kld_loss_kernel(const float *__restrict__ log_q, int64_t B,
+                                                       const float *__restrict__ E, const float *__restrict__ lq_rev,
+                                                       int64_t R, const int32_t *__restrict__ nan_word,
+                                                       float *__restrict__ loss, uint8_t *__restrict__ nan_out) {
+    __shared__ float red[256];
+    const float sq = block_sum256(log_q, B, red);
+    float energy = 0.f;
+    if (E) {
+        const float se = block_sum256(E, R, red);
+        const float sl = block_sum256(lq_rev, R, red);
+        energy = se * (1.f / (float)R) + sl * (1.f / (float)R);  // torch's MeanOps: sum x (1 / n)
+    }
+    if (threadIdx.x == 0) {
+        const float sample = -(sq * (1.f / (float)B));
+        loss[0] = sample + 0.f * energy;
+        if (nan_out) nan_out[0] = (nan_word && nan_word[0] != 0) ? 1 : 0;
+    }
+}
+
+// d loss / d log_q = -g x (1 / B) per row (torch's NegBackward then MeanBackward)
+__global__ void __launch_bounds__(256) kld_loss_bwd_kernel(const float *__restrict__ g, int64_t B,
+                                                           float *__restrict__ out) {
+    const float v = (-g[0]) * (1.f / (float)B);  // torch divides by a scalar as a product with its reciprocal
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B; i += (int64_t)gridDim.x * 256) out[i] = v;
+}
+
 }  // namespace fs
 
 using namespace fs;
@@ -111,5 +159,17 @@ hipError_t fs_adam_step_impl(float *p, const float *g, float *m, float *v, int64
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(adam_count_kernel, dim3(1), dim3(1), 0, st, step, loss, skip);
+    return hipGetLastError();
+}
+
+hipError_t fs_kld_loss_impl(const float *log_q, int64_t B, const float *E, const float *lq_rev, int64_t R,
+                            const int32_t *nan_word, float *loss, uint8_t *nan_out, hipStream_t st) {
+    hipLaunchKernelGGL(kld_loss_kernel, dim3(1), dim3(256), 0, st, log_q, B, E, lq_rev, R, nan_word, loss, nan_out);
+    return hipGetLastError();
+}
+
+hipError_t fs_kld_loss_bwd_impl(const float *g, int64_t B, float *grad_log_q, hipStream_t st) {
+    const int64_t blocks = B / 256 + 1 < 64 ? B / 256 + 1 : 64;
+    hipLaunchKernelGGL(kld_loss_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, st, g, B, grad_log_q);
     return hipGetLastError();
 }

@@ -133,6 +133,80 @@ __global__ void __launch_bounds__(256) target_energy_kernel(const float *__restr
     if (lane == 0) E[b] = (float)e_lj / a.temp + (float)e_dw;
 }
 
+// The energy alone (reverse_kld's score in the training step, where nothing needs dE/dx):
+// one workgroup per row, the N + 1 points (the origin first) staged in LDS and the
+// (N + 1) N / 2 unordered pairs spread over all 256 threads as (i, i + d mod (N + 1)),
+// d <= (N + 1) / 2, instead of one wave walking every ordered pair.  Each pair's energy is
+// the same float32 arithmetic as above; only the order of the double sums differs.
+__global__ void __launch_bounds__(256) target_energy_only_kernel(const float *__restrict__ x, int N, TargetArgs a,
+                                                                 float *__restrict__ E) {
+    extern __shared__ float sm[];
+    __shared__ double red[2][256];
+    const int t = threadIdx.x;
+    const int64_t b = blockIdx.x;
+    const int M = N + 1;
+    float *sx = sm, *sy = sm + M;
+    const float *xr = x + b * 2 * N;
+    for (int p = t; p < M; p += 256) {
+        if (p == 0) {
+            sx[0] = 0.0f;
+            sy[0] = 0.0f;
+        } else {
+            const float px = xr[2 * (p - 1)], py = xr[2 * (p - 1) + 1];
+            sx[p] = px - a.two_b * rintf(px / a.two_b);
+            sy[p] = py - a.two_b * rintf(py / a.two_b);
+        }
+    }
+    __syncthreads();
+    const float bk = 0.82f;
+    const int D = M / 2;
+    const bool even = (M & 1) == 0;
+    double e_lj = 0.0, e_dw = 0.0;
+    for (int q = t; q < M * D; q += 256) {
+        const int i = q / D, d = q - i * D + 1;
+        if (even && d == D && i >= D) continue;  // the antipodal pairs once
+        const int j = i + d < M ? i + d : i + d - M;
+        const float dx = sx[i] - sx[j], dy = sy[i] - sy[j];
+        const float r = sqrt_rn_f(dx * dx + dy * dy);
+        float e;
+        if (r <= bk) {
+            e = -80.0f * (r - bk) + 30.0f;
+        } else {
+            const float ir = 1.0f / r;
+            const double u = ir, u2 = u * u, u3 = u2 * u, u6 = u3 * u3;
+            e = 4.0f * ((float)(u6 * u6) - (float)u6);
+        }
+        e_lj += (double)e;
+    }
+    for (int p = t; p < N; p += 256) {
+        const float px = xr[2 * p], py = xr[2 * p + 1];
+        const float L = a.two_b;
+        float vp = 0.0f;
+        for (int w = 0; w < a.num_wells; ++w) {
+            float dx = px - a.cx[w], dy = py - 0.0f;
+            dx = dx - L * rintf(dx / L);
+            dy = dy - L * rintf(dy / L);
+            const float r = sqrt_rn_f(dx * dx + dy * dy);
+            const float th = tanhf(a.k * (r - a.r0));
+            const float tr = 0.5f * (1.0f + th);
+            vp = vp + a.v0[w] * (1.0f - tr);
+        }
+        e_dw += (double)vp;
+    }
+    red[0][t] = e_lj;
+    red[1][t] = e_dw;
+    __syncthreads();
+#pragma unroll
+    for (int w = 128; w > 0; w >>= 1) {
+        if (t < w) {
+            red[0][t] = red[0][t] + red[0][t + w];
+            red[1][t] = red[1][t] + red[1][t + w];
+        }
+        __syncthreads();
+    }
+    if (t == 0) E[b] = (float)red[0][0] / a.temp + (float)red[1][0];
+}
+
 }  // namespace fs
 
 hipError_t fs_target_energy_impl(const float *x, int64_t B, int N, double bound, double temperature, int num_wells,
@@ -150,6 +224,11 @@ hipError_t fs_target_energy_impl(const float *x, int64_t B, int N, double bound,
     a.k = (float)k;
     a.num_wells = num_wells;
     a.want_grad = gx != nullptr;
+    if (!gx) {
+        const size_t lds1 = (size_t)2 * (N + 1) * sizeof(float);
+        hipLaunchKernelGGL(fs::target_energy_only_kernel, dim3((unsigned)B), dim3(256), lds1, st, x, N, a, E);
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)4 * 2 * N * sizeof(float);
     hipLaunchKernelGGL(fs::target_energy_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), lds, st, x, B, N, a, E,
                        gx);

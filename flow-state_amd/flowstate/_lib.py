@@ -143,6 +143,8 @@ _SIGS = {
     "fs_set_wide_final32": (ctypes.c_int32, [ctypes.c_int32]),
     "fs_set_coupling_waves": (ctypes.c_int32, [ctypes.c_int32]),
     "fs_set_lean_gemm": (ctypes.c_int32, [ctypes.c_int32]),
+    "fs_kld_loss": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P, _P, _P, _P]),
+    "fs_kld_loss_backward": (ctypes.c_int, [_P, _I64, _P, _P]),
     "fs_adam_step": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P, _P] + [ctypes.c_double] * 5 + [_P]),
     "fs_target_energy": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_int32]
                          + [ctypes.c_double] * 4 + [_P, _P, _P]),

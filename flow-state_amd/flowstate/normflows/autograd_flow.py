@@ -91,13 +91,76 @@ _defer_nan = False  # set while a training step is captured in a graph (train.py
 _sticky_nan = None
 
 
+# Set by paired_kld when its spline flags went straight into the captured graph's sticky
+# word (nothing appended to _nan_flags); kld_loss then writes "sticky word set" as a bool
+# in its own launch (_sticky_flag_out) and reduce_nan_flags returns that.
+_flags_in_sticky = False
+_sticky_flag_out = None
+
+
 def reduce_nan_flags(device):
-    """All pending NaN flags as one device bool (graph-capturable, no host read)."""
+    """All pending NaN flags as one device bool (graph-capturable, no host read).  Returns
+    (flag, only_sticky): only_sticky when the flag is the sticky word's own state, so the
+    caller need not OR it back in."""
+    global _flags_in_sticky, _sticky_flag_out
     flags = [f.reshape(()).to(device) for f in _nan_flags]
     _nan_flags.clear()
+    only_sticky = _flags_in_sticky and not flags
+    if _flags_in_sticky:
+        flags.append(_sticky_flag_out if _sticky_flag_out is not None else _sticky_nan[0] != 0)
+    _flags_in_sticky, _sticky_flag_out = False, None
     if not flags:
-        return torch.zeros((), dtype=torch.bool, device=device)
-    return torch.stack(flags).any()
+        return torch.zeros((), dtype=torch.bool, device=device), False
+    if len(flags) == 1:
+        return flags[0], only_sticky
+    return torch.stack(flags).any(), False
+
+
+class _KldLoss(torch.autograd.Function):
+    """loss = -mean(log_q) + 0 * (mean(energy) + mean(lq_rev)) (main_algorithm_2.py:316-318,
+    ALPHA = 1) in one launch each way (fs_kld_loss / fs_kld_loss_backward) instead of
+    torch's seven forward and three backward kernels; the gradient is torch's
+    (-g) * (1 / B) per row, bit for bit."""
+
+    @staticmethod
+    def forward(ctx, log_q, energy, lq_rev):
+        global _sticky_flag_out
+        from .. import _lib
+
+        loss = torch.empty((), device=log_q.device)
+        word = _sticky_nan if _flags_in_sticky else None
+        if word is not None:
+            _sticky_flag_out = torch.empty((), dtype=torch.bool, device=log_q.device)
+        _lib.check(_lib.load().fs_kld_loss(_lib.ptr(log_q), log_q.shape[0], _lib.ptr(energy), _lib.ptr(lq_rev),
+                                           lq_rev.shape[0], _lib.ptr(word), _lib.ptr(loss),
+                                           _lib.ptr(_sticky_flag_out if word is not None else None),
+                                           _lib.stream_ptr()), "fs_kld_loss")
+        ctx.B = log_q.shape[0]
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _lib
+
+        g = g.detach().contiguous()
+        gq = torch.empty(ctx.B, device=g.device)
+        _lib.check(_lib.load().fs_kld_loss_backward(_lib.ptr(g), ctx.B, _lib.ptr(gq), _lib.stream_ptr()),
+                   "fs_kld_loss_backward")
+        return gq, None, None
+
+
+def kld_loss(log_q, energy, lq_rev):
+    """The ALPHA = 1 training loss from forward_kld's log q and reverse_kld's energies and
+    log q (_KldLoss) for float32 device vectors; the torch expression otherwise."""
+    ok = all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 1 and t.is_contiguous()
+             for t in (log_q, energy, lq_rev)) and log_q.shape[0] >= 1 and energy.shape == lq_rev.shape \
+        and energy.shape[0] >= 1 and not energy.requires_grad and not lq_rev.requires_grad
+    if ok:
+        from .. import _lib
+
+        with _lib.on_device(log_q):
+            return _KldLoss.apply(log_q, energy, lq_rev)
+    return -torch.mean(log_q) + 0.0 * (torch.mean(energy) + torch.mean(lq_rev))
 
 
 def check_nan_flags():
@@ -923,6 +986,7 @@ class _DensitySplines(torch.autograd.Function):
         ctx.layer = layer
         ctx.has_lq = lq_in is not None
         ctx.res = res
+        ctx.set_materialize_grads(False)  # the last layer's out has no gradient: no zero fill
         return out, lq
 
     @staticmethod
@@ -1004,6 +1068,7 @@ class _FinalSplines(torch.autograd.Function):
         ctx.layer = layer
         ctx.has_lq = lq_in is not None
         ctx.res = res
+        ctx.set_materialize_grads(False)  # the last layer's out has no gradient: no zero fill
         return out, lq
 
     @staticmethod
@@ -1345,9 +1410,10 @@ def paired_ok(model, x, z, flat_bn):
     return True
 
 
-def paired_kld(model, x, z, flat_bn):
+def paired_kld(model, x, z, flat_bn, reduce=True):
     """forward_kld(x) (differentiable) and reverse_kld's sampling pass of the base draws z
-    (no autograd) in shared launches; returns (forward_kld loss, samples, their log q)."""
+    (no autograd) in shared launches; returns (forward_kld loss, samples, their log q), or
+    with reduce=False forward_kld's per-row log q in place of the loss."""
     from .. import _lib
 
     flows = model.flows
@@ -1369,8 +1435,11 @@ def paired_kld(model, x, z, flat_bn):
         # the sampling pass's spline flags are in the sticky word already when captured:
         # the failing step and every later one leave the running statistics alone
         flat_bn.update(rider.bnstats, z.shape[0], x.shape[0], skip=_sticky_nan)
-    global _last_paired
+    global _last_paired, _flags_in_sticky
     _last_paired = True
-    _nan_flags.append(rider.nan_flag[0] != 0)
+    if _defer_nan and _sticky_nan is not None and rider.nan_flag is _sticky_nan:
+        _flags_in_sticky = True  # the rider's flags are in the sticky word already
+    else:
+        _nan_flags.append(rider.nan_flag[0] != 0)
     check_nan_flags()
-    return -torch.mean(log_q), rider.z, rider.lq
+    return (-torch.mean(log_q) if reduce else log_q), rider.z, rider.lq

@@ -54,10 +54,10 @@ def step_loss(model, x, n_reverse, alpha, flat_bn=None):
             dev = next(model.parameters()).device
             z = model.q0(n_reverse).to(dev)  # reverse_kld's base draws, first as in the reference
             if AF.paired_ok(model, x, z, flat_bn):
-                sample_loss, zs, lqs = AF.paired_kld(model, x, z, flat_bn)
+                log_q, zs, lqs = AF.paired_kld(model, x, z, flat_bn, reduce=False)
                 with torch.no_grad():
-                    energy_loss = torch.mean(model.p._energy(zs)) + torch.mean(lqs)
-                return sample_loss + 0.0 * energy_loss
+                    energy = model.p._energy(zs)
+                return AF.kld_loss(log_q, energy, lqs)  # -mean(log_q) + 0 * (mean(E) + mean(lqs))
             with torch.no_grad():
                 energy_loss, _ = model._reverse_kld_from(z)
             return model.forward_kld(x) + 0.0 * energy_loss
@@ -106,6 +106,7 @@ class GraphedTrainStep:
         self.flat_bn = AF.FlatBatchNorm.try_build(model) if paired else None
         # sticky spline-NaN word of the replays since the last reset_nan() (see the module doc)
         self._sticky = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._one = torch.ones((), device=dev)  # the captured backward's seed gradient
         model.train()
         self.graphs = {}
         for bs in [self.batch_size] + [int(b) for b in extra_batch_sizes if int(b) != self.batch_size]:
@@ -163,11 +164,12 @@ class GraphedTrainStep:
                         b.copy_(t)
                 self._zero_grad()
                 loss = step_loss(model, x, self.batch_size, self.alpha, self.flat_bn)
-                loss.backward()
+                loss.backward(self._one)  # a constant seed gradient: no fill launch
                 self._gather_grads()
-                nan_flag = AF.reduce_nan_flags(dev)
-                with torch.no_grad():
-                    self._sticky.bitwise_or_(nan_flag.to(torch.int32))
+                nan_flag, only_sticky = AF.reduce_nan_flags(dev)
+                if not only_sticky:  # (the shared-launch passes wrote their flags into it)
+                    with torch.no_grad():
+                        self._sticky.bitwise_or_(nan_flag.to(torch.int32))
                 if self._fused_adam_ok():
                     # skips itself on a non-finite loss or a set sticky word
                     self._adam_step(loss.detach(), skip=self._sticky)
@@ -179,10 +181,11 @@ class GraphedTrainStep:
                     with torch.no_grad():
                         for b, t in zip(self._backup, self._state_tensors):
                             t.copy_(torch.where(keep, t, b))
-                with torch.no_grad():
-                    failed = self._sticky[0] != 0
-                    for b, t in zip(bn_backup, bn_bufs):
-                        t.copy_(torch.where(failed, b, t))
+                if bn_bufs:
+                    with torch.no_grad():
+                        failed = self._sticky[0] != 0
+                        for b, t in zip(bn_backup, bn_bufs):
+                            t.copy_(torch.where(failed, b, t))
         finally:
             AF._defer_nan = False
             AF._sticky_nan = None

@@ -315,6 +315,17 @@ int fs_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg
                  const float *loss, const int32_t *skip, double lr, double beta1, double beta2, double eps,
                  double weight_decay, void *stream);
 
+/* The Algorithm-2 loss with ALPHA = 1 (main_algorithm_2.py:316-318; NF/normflows/core.py
+ * forward_kld / reverse_kld): loss [1] = -mean(log_q [B]) + 0 * (mean(energy [R]) +
+ * mean(lq_rev [R])), NaN / inf when the reverse term is (the step's skip rule reads it);
+ * energy / lq_rev nullable (then the loss is -mean(log_q)).  nan_out (nullable, one byte)
+ * = nan_word [1] (nullable) is non-zero.  One launch; the means are ordered tree sums. */
+int fs_kld_loss(const float *log_q, int64_t B, const float *energy, const float *lq_rev, int64_t R,
+                const int32_t *nan_word, float *loss, uint8_t *nan_out, void *stream);
+
+/* Its gradient: grad_log_q [B] = -grad_loss[0] / B. */
+int fs_kld_loss_backward(const float *grad_loss, int64_t B, float *grad_log_q, void *stream);
+
 /* unconstrained_rational_quadratic_spline, circular tails (NF/normflows/utils/
  * splines.py:16-222) for M independent elements: x [M], unnormalised widths /
  * heights uw, uh [M][K], derivatives ud [M][K+1] (row-major, contiguous).

@@ -66,7 +66,9 @@ def test_paired_step_matches_separate_passes(N, kw, rows, no_fold):
     lb = step_loss(mb, x, rows, 1.0, fbn)
     lb.backward()
     torch.cuda.synchronize()
-    assert torch.equal(la, lb)
+    # the paired step's loss head (fs_kld_loss) sums in its own order: the loss within
+    # float32 rounding, its gradient (-1 / rows per row) and so every parameter's exact
+    torch.testing.assert_close(la, lb, rtol=2e-6, atol=0)
     for (na, pa), (nb_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
         assert (pa.grad is None) == (pb.grad is None), na
         if pa.grad is not None:
@@ -214,3 +216,39 @@ def test_bn_fold_matches_unfolded(N, kw, rows):
         L, nb = kw["L"], kw["nb"]
         folded = rows % 4 == 0  # the lean weight-gradient kernels reduce the batch in quads
         assert counts == [0 if folded else 2 * L * nb, 2 * L * nb], counts
+
+
+@pytest.mark.parametrize("B,R", [(256, 256), (37, 37), (1, 5), (1000, 300)])
+def test_kld_loss_head(B, R):
+    """fs_kld_loss / fs_kld_loss_backward (autograd_flow._KldLoss) against the torch
+    expression of main_algorithm_2.py:316-318 at ALPHA = 1: the value within float32
+    rounding (ordered tree sums), the gradient bit for bit, NaN / inf of the zero-weighted
+    reverse term kept, and the sticky word's state written as a bool."""
+    g = torch.Generator().manual_seed(B)
+    lq = (torch.randn(B, generator=g) * 40 - 100).cuda().requires_grad_(True)
+    E = (torch.randn(R, generator=g) * 1e3).cuda()
+    lqs = (torch.randn(R, generator=g) * 40).cuda()
+    want = -torch.mean(lq) + 0.0 * (torch.mean(E) + torch.mean(lqs))
+    (gw,) = torch.autograd.grad(want, lq)
+    got = AF.kld_loss(lq, E, lqs)
+    assert got.grad_fn is not None and "KldLoss" in type(got.grad_fn).__name__
+    (gg,) = torch.autograd.grad(got, lq)
+    torch.testing.assert_close(got, want, rtol=2e-6, atol=0)
+    assert torch.equal(gg, gw)
+    (gg2,) = torch.autograd.grad(AF.kld_loss(lq, E, lqs), lq, torch.tensor(3.5, device="cuda"))
+    (gw2,) = torch.autograd.grad(-torch.mean(lq) + 0.0 * E.sum(), lq, torch.tensor(3.5, device="cuda"))
+    assert torch.equal(gg2, gw2)
+    for bad in (float("inf"), float("nan")):
+        E2 = E.clone()
+        E2[R // 2] = bad
+        assert torch.isnan(AF.kld_loss(lq.detach(), E2, lqs))
+    L = _lib.load()
+    for word in (0, 4):
+        w = torch.tensor([word], dtype=torch.int32, device="cuda")
+        loss = torch.empty((), device="cuda")
+        flag = torch.full((), True, dtype=torch.bool, device="cuda") if word == 0 else \
+            torch.zeros((), dtype=torch.bool, device="cuda")
+        _lib.check(L.fs_kld_loss(_lib.ptr(lq), B, _lib.ptr(E), _lib.ptr(lqs), R, _lib.ptr(w), _lib.ptr(loss),
+                                 _lib.ptr(flag), _lib.stream_ptr()))
+        assert bool(flag) == (word != 0)
+        torch.testing.assert_close(loss, want.detach(), rtol=2e-6, atol=0)

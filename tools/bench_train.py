@@ -81,6 +81,22 @@ def main(steps=20, warmup=3, batch=256, N=64):
         gl = g.step(data[i * batch:(i + 1) * batch])
     torch.cuda.synchronize()
     dtg = time.perf_counter() - t2
+    # longer runs: 100 checked steps, then 100 back to back as an epoch replays them
+    xb = [data[i * batch:(i + 1) * batch] for i in range(warmup, warmup + steps)]
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    for i in range(100):
+        g.step(xb[i % steps])
+    torch.cuda.synchronize()
+    dt100 = time.perf_counter() - t2
+    g.reset_nan()
+    flags = []
+    t2 = time.perf_counter()
+    for i in range(100):
+        flags.append(g.step(xb[i % steps], check=False)[1])
+    torch.cuda.synchronize()
+    dte = time.perf_counter() - t2
+    assert not bool(torch.stack(flags).any())
     m.eval()
     with torch.no_grad():
         m.sample(8192)
@@ -93,6 +109,7 @@ def main(steps=20, warmup=3, batch=256, N=64):
     print(json.dumps({
         "metric": "Algorithm-2 NF training steps/s (reverse_kld + forward_kld + Adam, A2 flow, N=64, batch 256; HIP-graph step)",
         "value": steps / dtg, "unit": "steps/s", "ms_per_step": dtg / steps * 1e3, "n_gpus": 1,
+        "checked_100_steps_per_s": 100 / dt100, "epoch_100_steps_per_s": 100 / dte,
         "eager_steps_per_s": steps / dt, "graphed_separate_passes_steps_per_s": steps / dt_sep,
         "steps": steps, "warmup": warmup, "dtype": "f32", "data": "synthetic (FCC + jitter configs)",
         "skipped_nan_steps": skipped, "last_loss": losses[-1],
