@@ -535,7 +535,16 @@ int fs_linear_f32_pair(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, void *strea
 
 int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs_bn_fold *fin,
                           const fs_bn_fold *fout, void *stream) {
+    return fs_linear_f32_pair_bn_sk(g0, g1, fin, fout, 1, 0, 1, 0, stream);
+}
+
+int fs_linear_f32_pair_bn_sk(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs_bn_fold *fin,
+                             const fs_bn_fold *fout, int32_t a_chunks, int64_t a_stride, int32_t add_chunks,
+                             int64_t add_stride, void *stream) {
     REQUIRE(g0 && g1 && (fin || fout), "fs_linear_f32_pair_bn: NULL descriptor");
+    REQUIRE(a_chunks >= 1 && a_chunks <= 3 && add_chunks >= 1 && add_chunks <= 3 && (add_chunks == 1 || fin) &&
+                (a_chunks == 1 || a_stride > 0) && (add_chunks == 1 || add_stride > 0),
+            "fs_linear_f32_pair_bn: invalid split-K operands (a_chunks=%d, add_chunks=%d)", a_chunks, add_chunks);
     const fs_bn_fold *fs_[2] = {fin, fout};
     fs::BnFold bf[2];
     for (int i = 0; i < 2; ++i) {
@@ -547,6 +556,11 @@ int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs
         bf[i] = fs::BnFold{f->gu, f->u, f->y, f->mean, f->invstd, f->gamma, f->part, f->dgamma, f->dbeta,
                            f->dx_add, f->a_out, (int)f->B, (int)f->H, (int)((f->B + 31) / 32)};
     }
+    if (fin && add_chunks > 1) {
+        REQUIRE(fin->dx_add && add_stride < INT32_MAX, "fs_linear_f32_pair_bn: add_chunks needs dx_add");
+        bf[0].add_ch = add_chunks;
+        bf[0].add_str = (int)add_stride;
+    }
     fs::GemmArgs a[2];
     const fs_gemm_f32 *gs[2] = {g0, g1};
     for (int i = 0; i < 2; ++i) {
@@ -557,7 +571,7 @@ int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs
                             g.rowsum_a};
     }
     return hip_rc(fs_linear_f32_pair_bn_impl(a[0], a[1], fin ? &bf[0] : nullptr, fout ? &bf[1] : nullptr,
-                                             (hipStream_t)stream),
+                                             (hipStream_t)stream, a_chunks, a_stride),
                   "fs_linear_f32_pair_bn");
 }
 
@@ -674,6 +688,33 @@ int fs_linear_f32_group(const fs_gemm_f32 *const *gs, int32_t n, float *workspac
         }
     }
     return hip_rc(e, "fs_linear_f32_group");
+}
+
+int fs_linear_f32_group_partial(const fs_gemm_f32 *const *gs, int32_t n, float *workspace, int64_t workspace_floats,
+                                int32_t max_chunks, int32_t *chunks_out, void *stream) {
+    REQUIRE(gs && n >= 1 && n <= 4 && chunks_out && max_chunks >= 2 && max_chunks <= 3,
+            "fs_linear_f32_group_partial: invalid arguments");
+    fs::GemmArgs a[4];
+    for (int i = 0; i < n; ++i) {
+        REQUIRE(gs[i] && gemm_desc_ok(*gs[i]), "fs_linear_f32_group_partial: invalid product %d", i);
+        const fs_gemm_f32 &g = *gs[i];
+        a[i] = fs::GemmArgs{g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbk, g.sbn, g.bias, g.R, g.ldr, g.C, g.ldc,
+                            g.rowsum_a};
+    }
+    int ch = 1;
+    hipError_t e = fs_linear_f32_group_partial_impl(a, n, workspace, workspace_floats, max_chunks, &ch,
+                                                    (hipStream_t)stream);
+    if (e == hipErrorNotSupported) {  // the ordinary group: product 0 reduced into its C
+        *chunks_out = 1;
+        return fs_linear_f32_group(gs, n, workspace, workspace_floats, stream);
+    }
+    *chunks_out = ch;
+    return hip_rc(e, "fs_linear_f32_group_partial");
+}
+
+int fs_splitk_sum(const float *part, int32_t chunks, int64_t stride, int64_t n, float *out, void *stream) {
+    REQUIRE(n >= 0 && (n == 0 || (part && out && chunks >= 1 && stride == n)), "fs_splitk_sum: invalid arguments");
+    return hip_rc(fs_splitk_sum_impl(part, chunks, stride, n, out, (hipStream_t)stream), "fs_splitk_sum");
 }
 
 int fs_bn_relu_train_fwd(int64_t Bn, int32_t H, const float *x, const float *gamma, const float *beta,

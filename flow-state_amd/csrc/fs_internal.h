@@ -129,12 +129,16 @@ struct BnFold {
     const float *dx_add;  // (consumer) the residual gradient added to dy, nullable
     float *a_out;         // (consumer) dy written out by the input gradient's first column tile, nullable
     int B, H, tiles;
+    int add_ch = 1, add_str = 0;  // (consumer) dx_add = the ordered sum of add_ch split-K partials add_str floats apart
 };
 }  // namespace fs
 hipError_t fs_linear_f32_impl(const fs::GemmArgs &g, hipStream_t st);
 hipError_t fs_linear_f32_pair_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, hipStream_t st);
 hipError_t fs_linear_f32_pair_bn_impl(const fs::GemmArgs &g0, const fs::GemmArgs &g1, const fs::BnFold *fin,
-                                      const fs::BnFold *fout, hipStream_t st);
+                                      const fs::BnFold *fout, hipStream_t st, int a_ch = 1, int64_t a_str = 0);
+hipError_t fs_linear_f32_group_partial_impl(const fs::GemmArgs *gs, int n, float *ws, int64_t ws_floats, int max_ch,
+                                            int *ch_out, hipStream_t st);
+hipError_t fs_splitk_sum_impl(const float *part, int ch, int64_t stride, int64_t n, float *out, hipStream_t st);
 hipError_t fs_linear_bn_f32_impl(const fs::GemmArgs &g, const fs::BnIn *bn, hipStream_t st);
 bool fs_linear_ex2_ok(const fs::GemmArgs &g0, const fs::BnIn *b0, const fs::GemmArgs &g1, const fs::BnIn *b1);
 hipError_t fs_linear_ex2_impl(const fs::GemmArgs &g0, const fs::BnIn *b0, const fs::GemmArgs &g1, const fs::BnIn *b1,

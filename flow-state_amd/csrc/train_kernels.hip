@@ -567,6 +567,7 @@ struct LinG {
     float *C, *stats, *rowsum;
     int M, N, K, sam, sak, sbk, sbn, ldr, ldc, abytes, bbytes;
     int pstats;  // (fs_linear_f32_pair_bn, producer) per-tile BatchNorm-backward sums of C
+    int ach, astr;  // A = the ordered sum of ach split-K partials astr floats apart (ach = 1: A itself)
 };
 // A BatchNorm1d (train) + ReLU backward folded into the backward pairs on either side of it
 // (fs_linear_f32_pair_bn): the producer pair's input gradient is the BatchNorm output's
@@ -605,49 +606,67 @@ __device__ __forceinline__ float fold_dx(float g, float u, float y, const LinGFL
 
 // V = 1: A is dy [B][H] (k = column), V = 2: A is dy^T (m = column); a quad of A from gu, u, y
 // (loaded into the ring raw, turned into dy right before its MFMAs)
+constexpr int kSkMax = 3;  // split-K partials an operand may be summed from on load
+template <bool RSK>
 struct FoldQ {
-    t4 g, u, y, r;  // r: the residual gradient (dx_add), zero without one
+    t4 g, u, y, r;          // r: the residual gradient (dx_add), zero without one
+    t4 rz[RSK ? kSkMax - 1 : 1];  // (RSK) its split-K partials 1.. (r: partial 0)
 };
 
+// a quad of a row-major (V = 1) or transposed operand
 template <int V>
-__device__ __forceinline__ FoldQ fold_raw(__amdgpu_buffer_rsrc_t Gr, __amdgpu_buffer_rsrc_t Ur,
-                                          __amdgpu_buffer_rsrc_t Yr, __amdgpu_buffer_rsrc_t Rr, bool add, int base,
-                                          int stride) {
-    FoldQ q;
-    const t4 zero = {0.f, 0.f, 0.f, 0.f};
-    if (V == 1) {
-        q.g = lin_ld(Gr, base * 4);
-        q.u = lin_ld(Ur, base * 4);
-        q.y = lin_ld(Yr, base * 4);
-        q.r = add ? lin_ld(Rr, base * 4) : zero;
-    } else {
+__device__ __forceinline__ t4 quad_ld(__amdgpu_buffer_rsrc_t R, int base, int stride) {
+    if (V == 1) return lin_ld(R, base * 4);
+    t4 v;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int off = (base + j * stride) * 4;
-            q.g[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(Gr, off, 0, 0));
-            q.u[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(Ur, off, 0, 0));
-            q.y[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(Yr, off, 0, 0));
-            q.r[j] = add ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(Rr, off, 0, 0)) : 0.f;
-        }
+    for (int j = 0; j < 4; ++j)
+        v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(R, (base + j * stride) * 4, 0, 0));
+    return v;
+}
+
+// RSK: dx_add is the ordered sum of nch split-K partials rstr floats apart (the reduction
+// splitk_reduce_kernel would have written, summed here on load instead)
+template <int V, bool RSK>
+__device__ __forceinline__ FoldQ<RSK> fold_raw(__amdgpu_buffer_rsrc_t Gr, __amdgpu_buffer_rsrc_t Ur,
+                                               __amdgpu_buffer_rsrc_t Yr, __amdgpu_buffer_rsrc_t Rr, bool add,
+                                               int base, int stride, int nch = 1, int rstr = 0) {
+    FoldQ<RSK> q;
+    const t4 zero = {0.f, 0.f, 0.f, 0.f};
+    q.g = quad_ld<V>(Gr, base, stride);
+    q.u = quad_ld<V>(Ur, base, stride);
+    q.y = quad_ld<V>(Yr, base, stride);
+    q.r = add ? quad_ld<V>(Rr, base, stride) : zero;
+    if constexpr (RSK) {
+#pragma unroll
+        for (int z = 1; z < kSkMax; ++z) q.rz[z - 1] = z < nch ? quad_ld<V>(Rr, base + z * rstr, stride) : zero;
     }
     return q;
 }
 
 // dy of a quad (+ the residual gradient when the BatchNorm backward had one: dx_add)
-template <int V>
-__device__ __forceinline__ t4 fold_apply(const FoldQ &q, int c, const LinGFLds &L, bool add) {
+template <int V, bool RSK>
+__device__ __forceinline__ t4 fold_apply(const FoldQ<RSK> &q, int c, const LinGFLds &L, bool add, int nch = 1) {
+    t4 r = q.r;
+    if constexpr (RSK) {  // splitk_reduce_kernel's order: partials 0, 1, ..., then + 0 (no bias)
+#pragma unroll
+        for (int z = 1; z < kSkMax; ++z)
+            if (z < nch) r = r + q.rz[z - 1];
+        r = r + 0.f;
+    }
     t4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const float d = fold_dx(q.g[j], q.u[j], q.y[j], L, V == 1 ? c + j : c);
-        o[j] = add ? d + q.r[j] : d;
+        o[j] = add ? d + r[j] : d;
     }
     return o;
 }
 
 // V: (fold consumer) A loaded as dy, 1 row-major, 2 transposed; PS: (fold producer) the
-// epilogue's tile sums; both only in gemm_ling_fold_kernel (LDS = LinGFLds)
-template <bool AK, bool BK, int V = 0, bool PS = false, class LDS = LinGLds>
+// epilogue's tile sums; both only in gemm_ling_fold_kernel (LDS = LinGFLds).  SK: (V = 0) A is
+// the ordered sum of P.ach split-K partials, (V != 0) so is the residual gradient dx_add
+// (F.add_ch partials): the reduction is done on load, in splitk_reduce_kernel's order
+template <bool AK, bool BK, int V = 0, bool PS = false, class LDS = LinGLds, bool SK = false>
 __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned by, LDS &L, const BnFold &F,
                                           const BnFold &Fo) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -666,20 +685,28 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
         Gr = lin_rsrc(F.gu, P.abytes);
         Ur = lin_rsrc(F.u, P.abytes);
         Yr = lin_rsrc(F.y, P.abytes);
-        if (fadd) Rr = lin_rsrc(F.dx_add, P.abytes);
+        if (fadd) Rr = lin_rsrc(F.dx_add, P.abytes + (SK ? (F.add_ch - 1) * F.add_str * 4 : 0));
     }
     const int mc = m < M ? m : 0;  // (V = 2) the column of A's row m
     const t4 zero = {0.f, 0.f, 0.f, 0.f};
+    constexpr bool ASK = SK && V == 0, RSK = SK && V != 0;
     t4 a[kLingPF], b[kLingPF];
-    FoldQ q[V != 0 ? kLingPF : 1];
+    t4 az[ASK ? kLingPF : 1][ASK ? kSkMax - 1 : 1];  // (ASK) A's partials 1.. (a: partial 0)
+    FoldQ<RSK> q[V != 0 ? kLingPF : 1];
     const int kb0 = 8 * w;
+    const int ach = ASK ? P.ach : 1, rch = RSK ? F.add_ch : 1, rstr = RSK ? F.add_str : 0;
 #pragma unroll
     for (int s = 0; s < kLingPF; ++s) {
         const int k = kb0 + 64 * s + 4 * h;
         if constexpr (V != 0) {
-            if (k < K) q[s] = fold_raw<V>(Gr, Ur, Yr, Rr, fadd, am + k * P.sak, P.sak);
+            if (k < K) q[s] = fold_raw<V, RSK>(Gr, Ur, Yr, Rr, fadd, am + k * P.sak, P.sak, rch, rstr);
         } else {
             a[s] = k < K ? ling_ld<AK>(Ar, am + k * P.sak, P.sak) : zero;
+            if constexpr (ASK) {
+#pragma unroll
+                for (int z = 1; z < kSkMax; ++z)
+                    az[s][z - 1] = (k < K && z < ach) ? ling_ld<AK>(Ar, am + k * P.sak + z * P.astr, P.sak) : zero;
+            }
         }
         b[s] = k < K ? ling_ld<BK>(Br, bn + k * P.sbk, P.sbk) : zero;
     }
@@ -748,8 +775,14 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
             const int k = kb + 64 * s;
             if (k < K) {  // wave-uniform
                 if constexpr (V != 0) {
-                    a[s] = fold_apply<V>(q[s], V == 1 ? k + 4 * h : mc, L, fadd);
+                    a[s] = fold_apply<V, RSK>(q[s], V == 1 ? k + 4 * h : mc, L, fadd, rch);
                     if (aout) *(t4 *)(aout + am + k + 4 * h) = a[s];
+                }
+                if constexpr (ASK) {  // splitk_reduce_kernel's order: partials 0, 1, ..., then + 0
+#pragma unroll
+                    for (int z = 1; z < kSkMax; ++z)
+                        if (z < ach) a[s] = a[s] + az[s][z - 1];
+                    a[s] = a[s] + 0.f;
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
@@ -757,9 +790,15 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
                 if (rows) rs += ((a[s][0] + a[s][1]) + a[s][2]) + a[s][3];
                 const int kn = k + 64 * kLingPF + 4 * h;
                 if constexpr (V != 0) {
-                    if (kn < K) q[s] = fold_raw<V>(Gr, Ur, Yr, Rr, fadd, am + kn * P.sak, P.sak);
+                    if (kn < K) q[s] = fold_raw<V, RSK>(Gr, Ur, Yr, Rr, fadd, am + kn * P.sak, P.sak, rch, rstr);
                 } else {
                     a[s] = kn < K ? ling_ld<AK>(Ar, am + kn * P.sak, P.sak) : zero;
+                    if constexpr (ASK) {
+#pragma unroll
+                        for (int z = 1; z < kSkMax; ++z)
+                            az[s][z - 1] =
+                                (kn < K && z < ach) ? ling_ld<AK>(Ar, am + kn * P.sak + z * P.astr, P.sak) : zero;
+                    }
                 }
                 b[s] = kn < K ? ling_ld<BK>(Br, bn + kn * P.sbk, P.sbk) : zero;
             }
@@ -907,6 +946,29 @@ __global__ __launch_bounds__(512) void gemm_ling_fold_kernel(LinGrp ga) {
         ling_tile<true, false, 0, true, LinGFLds>(Q.g, bx, by, L, Fi, Fo);
     } else {
         ling_tile<false, false, 0, false, LinGFLds>(Q.g, bx, by, L, Fi, Fo);
+    }
+}
+
+// The same with split-K operands summed on load (fs_linear_f32_pair_bn_sk): the consumer's
+// dx_add (fold.add_ch partials) or the producer's A (ach partials).  A kernel of its own, so
+// that the extra partials' registers do not weigh on gemm_ling_fold_kernel.
+__global__ __launch_bounds__(512) void gemm_ling_fold_sk_kernel(LinGrp ga) {
+    __shared__ LinGFLds L;
+    const int i = (ga.n > 1 && blockIdx.x >= ga.p[1].begin) ? 1 : 0;
+    const LinGProb &Q = ga.p[i];
+    const unsigned b = blockIdx.x - Q.begin, bx = b % Q.mt, by = b / Q.mt;
+    const BnFold &Fi = ga.fold, &Fo = ga.fold_out;
+    if (Q.vmode == 1) {
+        if (Q.g.pstats)
+            ling_tile<true, false, 1, true, LinGFLds, true>(Q.g, bx, by, L, Fi, Fo);
+        else
+            ling_tile<true, false, 1, false, LinGFLds, true>(Q.g, bx, by, L, Fi, Fo);
+    } else if (Q.vmode == 2) {
+        ling_tile<false, false, 2, false, LinGFLds, true>(Q.g, bx, by, L, Fi, Fo);
+    } else if (Q.g.pstats) {
+        ling_tile<true, false, 0, true, LinGFLds, true>(Q.g, bx, by, L, Fi, Fo);
+    } else {
+        ling_tile<false, false, 0, false, LinGFLds, true>(Q.g, bx, by, L, Fi, Fo);
     }
 }
 
@@ -1194,7 +1256,7 @@ using namespace fs;
 static bool lean_gemm();
 static bool ling_ok(const GemmArgs &g);
 static hipError_t ling_group(const GemmArgs *gs, int n, float *const *part, const int *S, const int64_t *kchunk,
-                             hipStream_t st);
+                             hipStream_t st, bool keep0 = false);
 
 static int gemm_split(const GemmArgs &g) {
     return g.K > 8 * 4 * 16 ? FS_GEMM_SPLIT_LONG : g.K >= 256 ? FS_GEMM_SPLIT_MID : FS_GEMM_SPLIT;
@@ -1383,13 +1445,13 @@ static bool ling_ok(const GemmArgs &g) {
 static LinG ling_fill(const GemmArgs &g) {
     return LinG{g.A, g.B, g.bias, g.R, g.C, g.stats, g.rowsum_a, (int)g.M, (int)g.N, (int)g.K, (int)g.sam, (int)g.sak,
                 (int)g.sbk, (int)g.sbn, (int)g.ldr, (int)g.ldc, (int)extent_bytes(g.M, g.sam, g.K, g.sak),
-                (int)extent_bytes(g.K, g.sbk, g.N, g.sbn), 0};
+                (int)extent_bytes(g.K, g.sbk, g.N, g.sbn), 0, 1, 0};
 }
 
 // n products (all ling_ok) in one gemm_ling_kernel launch; part[i] / S[i] / kchunk[i]: the
 // split-K plan of product i (S = 1: whole), then one splitk_reduce_kernel per split product
 static hipError_t ling_group(const GemmArgs *gs, int n, float *const *part, const int *S, const int64_t *kchunk,
-                             hipStream_t st) {
+                             hipStream_t st, bool keep0) {
     if (n <= 0 || n > kLingMax) return hipErrorInvalidValue;
     LinGrp ga{};
     unsigned wg = 0;
@@ -1411,7 +1473,7 @@ static hipError_t ling_group(const GemmArgs *gs, int n, float *const *part, cons
     hipLaunchKernelGGL(gemm_ling_kernel, dim3(wg), dim3(512), 0, st, ga);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     for (int i = 0; i < n; ++i) {
-        if (S[i] <= 1) continue;
+        if (S[i] <= 1 || (i == 0 && keep0)) continue;  // keep0: product 0's partials left for its consumers
         const GemmArgs &g = gs[i];
         const int64_t m = g.M * g.N;
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, g,
@@ -1421,6 +1483,63 @@ static hipError_t ling_group(const GemmArgs *gs, int n, float *const *part, cons
     return hipSuccess;
 }
 
+// fs_linear_f32_group with product 0's split-K partials left unreduced: at most max_ch chunks
+// (whole multiples of 8 along K) at ws + z M N, summed on load by their consumers (the
+// backward pairs' ach / add_ch, or fs_splitk_sum); ch_out = the chunk count.
+// hipErrorNotSupported: product 0 has no split-K plan (or a bias / residual / padded C), or
+// some product does not take the lean kernel.
+hipError_t fs_linear_f32_group_partial_impl(const GemmArgs *gs, int n, float *ws, int64_t ws_floats, int max_ch,
+                                            int *ch_out, hipStream_t st) {
+    *ch_out = 1;
+    if (n < 1 || n > kLingMax || max_ch < 2 || max_ch > kSkMax || !lean_gemm()) return hipErrorNotSupported;
+    const GemmArgs &g0 = gs[0];
+    int s0 = 0;
+    int64_t kc0 = 0;
+    if (splitk_plan(g0, s0, kc0) == 0 || g0.bias || g0.R || g0.ldc != g0.N) return hipErrorNotSupported;
+    GemmArgs lg[kLingMax];
+    float *part[kLingMax];
+    int S[kLingMax];
+    int64_t kc[kLingMax];
+    int64_t used = 0;
+    for (int i = 0; i < n; ++i) {
+        const GemmArgs &g = gs[i];
+        if (!ling_ok(g) || g.M <= 0 || (g.N <= 0 && !g.rowsum_a)) return hipErrorNotSupported;
+        int s = 0;
+        int64_t kchunk = 0;
+        int64_t need = splitk_plan(g, s, kchunk);
+        if (i == 0) {
+            kchunk = ((g.K + max_ch - 1) / max_ch + 7) / 8 * 8;
+            s = (int)((g.K + kchunk - 1) / kchunk);
+            need = (int64_t)s * g.M * g.N;
+        }
+        lg[i] = g;
+        if (need > 0 && ws && ws_floats - used >= need) {
+            part[i] = ws + used;
+            used += need;
+            S[i] = s;
+            kc[i] = kchunk;
+        } else if (i == 0) {
+            return hipErrorNotSupported;
+        } else {
+            part[i] = nullptr;
+            S[i] = 1;
+            kc[i] = g.K;
+        }
+    }
+    const hipError_t e = ling_group(lg, n, part, S, kc, st, true);
+    if (e == hipSuccess) *ch_out = S[0];
+    return e;
+}
+
+// out [n] = the ordered sum of ch partials stride floats apart (splitk_reduce_kernel's)
+hipError_t fs_splitk_sum_impl(const float *part, int ch, int64_t stride, int64_t n, float *out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if (ch < 1 || stride != n) return hipErrorInvalidValue;
+    const GemmArgs g{1, n, 0, nullptr, 0, 0, nullptr, 0, 0, nullptr, nullptr, 0, out, n, nullptr};
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, part, ch);
+    return hipGetLastError();
+}
+
 // nn.Linear's backward pair around folded BatchNorms + ReLU (struct BnFold): fout, the
 // BatchNorm this Linear applies to its input, whose output gradient gu is g0's output (its
 // epilogue writes the tile sums); fin, the BatchNorm that consumes this Linear's output, whose
@@ -1428,11 +1547,16 @@ static hipError_t ling_group(const GemmArgs *gs, int n, float *const *part, cons
 // row-major, g1 its transpose; + fin->dx_add; fin->a_out gets dy from g0's first column
 // tile), workgroup 0 writing that BatchNorm's dgamma / dbeta
 hipError_t fs_linear_f32_pair_bn_impl(const GemmArgs &g0, const GemmArgs &g1, const BnFold *fin, const BnFold *fout,
-                                      hipStream_t st) {
+                                      hipStream_t st, int a_ch, int64_t a_str) {
     auto fold_ok = [](const BnFold &f) {
         return f.H > 0 && f.H <= kFoldMaxH && f.B > 0 && f.tiles == (f.B + 31) / 32 && f.gu && f.u && f.y && f.mean &&
-               f.invstd && f.part;
+               f.invstd && f.part && f.add_ch >= 1 && f.add_ch <= kSkMax &&
+               (f.add_ch == 1 || (f.dx_add && f.add_str >= (int64_t)f.B * f.H &&
+                                  (int64_t)f.B * f.H * 4 + (int64_t)(f.add_ch - 1) * f.add_str * 4 < INT32_MAX));
     };
+    if (a_ch < 1 || a_ch > kSkMax || (a_ch > 1 && (fin || !fout || a_str < g0.M * g0.K ||
+                                                   g0.M * g0.K * 4 + (a_ch - 1) * a_str * 4 >= INT32_MAX)))
+        return hipErrorInvalidValue;
     if (!lean_gemm() || !ling_ok(g0) || !ling_ok(g1) || (!fin && !fout) || (fin && !fold_ok(*fin)) ||
         (fout && !fold_ok(*fout)))
         return hipErrorInvalidValue;
@@ -1456,6 +1580,14 @@ hipError_t fs_linear_f32_pair_bn_impl(const GemmArgs &g0, const GemmArgs &g1, co
         wg += Q.mt * Q.nt;
     }
     if (ga.p[0].bk || ga.p[1].bk || ga.p[1].ak) return hipErrorInvalidValue;
+    if (a_ch > 1) {  // (producer) A of both products = the ordered sum of a_ch split-K partials
+        if (g0.A != g1.A) return hipErrorInvalidValue;
+        for (int i = 0; i < 2; ++i) {
+            ga.p[i].g.ach = a_ch;
+            ga.p[i].g.astr = (int)a_str;
+            ga.p[i].g.abytes += (a_ch - 1) * (int)a_str * 4;  // the descriptor spans every partial
+        }
+    }
     if (fout) {  // g0's output is the BatchNorm output's gradient gu [B][H]
         const BnFold &f = *fout;
         if (g0.M != f.B || g0.N != f.H || g0.ldc != f.H || g0.C != f.gu || !ga.p[0].ak) return hipErrorInvalidValue;
@@ -1469,7 +1601,10 @@ hipError_t fs_linear_f32_pair_bn_impl(const GemmArgs &g0, const GemmArgs &g1, co
         ga.p[0].vmode = 1;
         ga.p[1].vmode = 2;
     }
-    hipLaunchKernelGGL(gemm_ling_fold_kernel, dim3(wg), dim3(512), 0, st, ga);
+    if (a_ch > 1 || (fin && fin->add_ch > 1))
+        hipLaunchKernelGGL(gemm_ling_fold_sk_kernel, dim3(wg), dim3(512), 0, st, ga);
+    else
+        hipLaunchKernelGGL(gemm_ling_fold_kernel, dim3(wg), dim3(512), 0, st, ga);
     return hipGetLastError();
 }
 

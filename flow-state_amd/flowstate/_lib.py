@@ -145,6 +145,12 @@ _SIGS = {
     "fs_set_lean_gemm": (ctypes.c_int32, [ctypes.c_int32]),
     "fs_kld_loss": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P, _P, _P, _P]),
     "fs_kld_loss_backward": (ctypes.c_int, [_P, _I64, _P, _P]),
+    "fs_linear_f32_pair_bn_sk": (ctypes.c_int, [ctypes.POINTER(GemmF32), ctypes.POINTER(GemmF32),
+                                                 ctypes.POINTER(BnFold), ctypes.POINTER(BnFold), ctypes.c_int32, _I64,
+                                                 ctypes.c_int32, _I64, _P]),
+    "fs_linear_f32_group_partial": (ctypes.c_int, [ctypes.POINTER(ctypes.POINTER(GemmF32)), ctypes.c_int32, _P, _I64,
+                                                   ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), _P]),
+    "fs_splitk_sum": (ctypes.c_int, [_P, ctypes.c_int32, _I64, _I64, _P, _P]),
     "fs_adam_step": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P, _P] + [ctypes.c_double] * 5 + [_P]),
     "fs_target_energy": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_int32]
                          + [ctypes.c_double] * 4 + [_P, _P, _P]),

@@ -277,6 +277,51 @@ _direct_grads = False  # set by paired_kld around its forward: one gradient cont
 # the block's second BatchNorm backward folded into the backward pairs around it
 # (fs_linear_f32_pair_bn; _BnFoldLink) in the graphs paired_kld builds; FS_FOLD_BN=0 turns it off
 _fold_bn = os.environ.get("FS_FOLD_BN", "1") != "0"
+# The final Linear's input gradient (split-K over n (3K+1)) left as unreduced partials in the
+# same graphs: its two readers, the last block's second Linear backward (A) and the block's
+# first BatchNorm fold (dx_add), sum them on load, so its reduction launch goes; FS_DEFER_SPLITK=0
+# turns it off.  {placeholder data_ptr: (placeholder, workspace, chunks)}: the placeholder is
+# what autograd carries; whoever cannot sum on load materialises it first (_sk_materialise).
+_defer_splitk = os.environ.get("FS_DEFER_SPLITK", "1") != "0"
+_splitk_pending = {}
+
+
+def _sk_get(t, pop=False):
+    """(workspace, chunks) when t is a pending split-K placeholder (pop: its last reader)."""
+    if t is None or not _splitk_pending:
+        return None
+    e = _splitk_pending.get(t.data_ptr())
+    if e is None or e[0].shape != t.shape:
+        return None
+    if pop:
+        del _splitk_pending[t.data_ptr()]
+    return e[1], e[2]
+
+
+def _sk_materialise(t):
+    """Write a pending placeholder's reduction into it (fs_splitk_sum); no-op otherwise."""
+    from .. import _lib
+
+    e = _sk_get(t, pop=True)
+    if e is not None:
+        ws, ch = e
+        n = t.numel()
+        _lib.check(_lib.load().fs_splitk_sum(_lib.ptr(ws), ch, n, n, _lib.ptr(t), _lib.stream_ptr()), "fs_splitk_sum")
+    return t
+
+
+def _pair_bn(g0, g1, fi, fo, a_sk=None, add_sk=None):
+    """fs_linear_f32_pair_bn, or its split-K-operand form (fs_linear_f32_pair_bn_sk)."""
+    from .. import _lib
+
+    L = _lib.load()
+    if a_sk is None and add_sk is None:
+        _lib.check(L.fs_linear_f32_pair_bn(g0, g1, fi, fo, _lib.stream_ptr()), "fs_linear_f32_pair_bn")
+        return
+    ach, astr = (a_sk[1], g0.M * g0.K) if a_sk is not None else (1, 0)
+    dch, dstr = (add_sk[1], fi.B * fi.H) if add_sk is not None else (1, 0)
+    _lib.check(L.fs_linear_f32_pair_bn_sk(g0, g1, fi, fo, ach, astr, dch, dstr, _lib.stream_ptr()),
+               "fs_linear_f32_pair_bn_sk")
 
 
 _ZERO = {}
@@ -388,7 +433,7 @@ class _Linear(torch.autograd.Function):
         from .. import _lib
 
         x, w = ctx.saved_tensors
-        gy = gy.contiguous()
+        gy = _sk_materialise(gy.contiguous())
         M, K = x.shape
         N = w.shape[0]
         L = _lib.load()
@@ -523,11 +568,12 @@ class _LinearStats(torch.autograd.Function):
             gbeta2 = _grad_out(ctx.gparams2[1], direct=ctx.direct)
             g0 = _lib.GemmF32(M, K, N, p(gu2), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
             g1 = _lib.GemmF32(N, K, M, p(gu2), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
+            add_sk = _sk_get(add2, pop=True)  # the residual gradient as split-K partials
             fi = _lib.BnFold(p(gu2), p(u2), p(y2), p(mean2), p(invstd2), p(gamma2), p(part2), p(gg2), p(gbeta2),
-                             p(add2), None, M, N)
-            _lib.check(_lib.load().fs_linear_f32_pair_bn(g0, g1, fi, None, _lib.stream_ptr()), "fs_linear_f32_pair_bn")
+                             p(add_sk[0] if add_sk else add2), None, M, N)
+            _pair_bn(g0, g1, fi, None, add_sk=add_sk)
             return gx, gw, gb, None, None, gg2, gbeta2
-        gy = gy.contiguous()
+        gy = _sk_materialise(gy.contiguous())
         g0 = _lib.GemmF32(M, K, N, p(gy), N, 1, p(w), K, 1, None, None, 0, p(gx), K, None)
         g1 = _lib.GemmF32(N, K, M, p(gy), 1, N, p(x), K, 1, None, None, 0, p(gw), K, p(gb))
         _lib.check(_lib.load().fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
@@ -613,16 +659,29 @@ class _BnReluLinear(torch.autograd.Function):
         add = None  # the block's residual gradient, for its first BatchNorm (this Linear's own)
         if ctx.res is not None and ctx.res.g is not None:
             add, ctx.res.g = ctx.res.g, None
+        a_sk = None  # gy as split-K partials, summed on load (the placeholder goes on as the residual)
         if fin is None:
             gy = gy.contiguous()
+            a_sk = _sk_get(gy)
+            if a_sk is not None and not (fout is not None and ctx.res is not None and ctx.has_r
+                                         and ctx.needs_input_grad[7]):
+                a_sk = None
+                _sk_materialise(gy)
+        if fout is None:
+            _sk_materialise(add)  # read by fs_bn_relu_train_bwd below
         dy = fin[0] if fin is not None else gy  # (fin: only the layout, gu of the folded BatchNorm)
+        pa = p(a_sk[0]) if a_sk is not None else p(dy)
         gu = torch.empty_like(u)
-        g0 = _lib.GemmF32(M, K, N, p(dy), N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
-        g1 = _lib.GemmF32(N, K, M, p(dy), 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
+        g0 = _lib.GemmF32(M, K, N, pa, N, 1, p(w), K, 1, None, None, 0, p(gu), K, None)
+        g1 = _lib.GemmF32(N, K, M, pa, 1, N, p(u), K, 1, None, None, 0, p(gw), K, p(gb))
         gg2 = gbeta2 = a_out = None
         fi = fo = None
+        add_sk = None
         if fin is not None:
             gu2, u2, y2, mean2, invstd2, gamma2, part2, add2 = fin
+            add_sk = _sk_get(add2, pop=True)  # the residual gradient as split-K partials
+            if add_sk is not None:
+                add2 = add_sk[0]
             gg2 = _grad_out(ctx.gparams2[0], direct=ctx.direct)
             gbeta2 = _grad_out(ctx.gparams2[1], direct=ctx.direct)
             if ctx.has_r and ctx.needs_input_grad[7]:
@@ -639,7 +698,7 @@ class _BnReluLinear(torch.autograd.Function):
         # steps/s for the BatchNorm backward run by each strip's last tile in the pair's launch
         # (device-scope fences; DESIGN "Training", profiles/r03/r03v_*)
         if fi is not None or fo is not None:
-            _lib.check(L.fs_linear_f32_pair_bn(g0, g1, fi, fo, _lib.stream_ptr()), "fs_linear_f32_pair_bn")
+            _pair_bn(g0, g1, fi, fo, a_sk=a_sk, add_sk=add_sk)
         else:
             _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
         gr = None
@@ -948,6 +1007,7 @@ def flush_features_bwd():
     from .. import _lib
 
     L, p = _lib.load(), _lib.ptr
+    _splitk_pending.clear()  # (an interrupted backward's; their placeholders are unreachable)
     while _pending_features_bwd:
         _, (layer_f, xf, gt, add, gxf) = _pending_features_bwd.popitem()
         cf = _coupling_desc(layer_f, xf.shape[0])
@@ -1065,6 +1125,9 @@ class _FinalSplines(torch.autograd.Function):
         ctx.save_for_backward(h, w, x, params, uw, uh, ud)
         ctx.bias = b
         ctx.direct = _direct_grads
+        # dh left as split-K partials for its readers (decided here: _direct_grads is a
+        # forward-time setting)
+        ctx.defer = _defer_splitk and _fold_ok(h.shape[0], h.shape[1], h.shape[1])
         ctx.layer = layer
         ctx.has_lq = lq_in is not None
         ctx.res = res
@@ -1099,7 +1162,15 @@ class _FinalSplines(torch.autograd.Function):
         nws = sum(max(0, L.fs_linear_f32_splitk_floats(d)) for d in descs)
         ws = torch.empty((max(nws, 1),), dtype=torch.float32, device=x.device)
         arr = (ctypes.POINTER(_lib.GemmF32) * 3)(*[ctypes.pointer(d) for d in descs])
-        _lib.check(L.fs_linear_f32_group(arr, 3, p(ws), nws, _lib.stream_ptr()), "fs_linear_f32_group")
+        if ctx.defer:
+            # dh's partials left for its readers (_sk_get): the reduction launch goes
+            ch = ctypes.c_int32(1)
+            _lib.check(L.fs_linear_f32_group_partial(arr, 3, p(ws), nws, 3, ctypes.byref(ch), _lib.stream_ptr()),
+                       "fs_linear_f32_group_partial")
+            if ch.value > 1:
+                _splitk_pending[gh.data_ptr()] = (gh, ws, ch.value)
+        else:
+            _lib.check(L.fs_linear_f32_group(arr, 3, p(ws), nws, _lib.stream_ptr()), "fs_linear_f32_group")
         guw = gs[:n * K].view(n, K)
         guh = gs[n * K:2 * n * K].view(n, K)
         gud = gs[2 * n * K:].view(n, K + 1)

@@ -395,6 +395,13 @@ typedef struct fs_bn_fold {
 } fs_bn_fold;
 int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs_bn_fold *fin,
                           const fs_bn_fold *fout, void *stream);
+/* The same with split-K operands left unreduced by fs_linear_f32_group_partial: a_chunks > 1
+ * (fout only, no fin; at most 3): A of both products is the ordered sum of a_chunks partials a_stride
+ * floats apart (g0->A == g1->A = partial 0); add_chunks > 1 (fin): fin->dx_add likewise.
+ * Each sum is fs_splitk_sum's, taken on load: the values are those of the reduced operand. */
+int fs_linear_f32_pair_bn_sk(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs_bn_fold *fin,
+                             const fs_bn_fold *fout, int32_t a_chunks, int64_t a_stride, int32_t add_chunks,
+                             int64_t add_stride, void *stream);
 
 /* fs_linear_f32 with the ResidualNet's BatchNorm plumbing fused in (resnet.py:35-51):
  * stats_out (nullable) [ceil(M/32)][N][2] receives each 32-row tile's column mean and sum
@@ -452,6 +459,16 @@ int fs_linear_f32_splitk(const fs_gemm_f32 *g, float *workspace, int64_t workspa
  * parameters' row sum).  Products with a split-K plan take it while the workspace
  * (sum of their fs_linear_f32_splitk_floats, in order) lasts, followed by their ordered
  * reductions; each product's values are those of fs_linear_f32 / fs_linear_f32_splitk. */
+/* fs_linear_f32_group with product 0 (no bias / R, C dense) split into at most max_chunks
+ * (2..3) K chunks whose partial products stay in the workspace, unreduced: partial z of its
+ * C at workspace + z M N; chunks_out = their count, 1 when product 0 takes no split-K plan
+ * (then C is written as fs_linear_f32_group writes it).  The consumer sums them on load
+ * (fs_linear_f32_pair_bn_sk) or calls fs_splitk_sum.  Workspace: as fs_linear_f32_group's. */
+int fs_linear_f32_group_partial(const fs_gemm_f32 *const *gs, int32_t n, float *workspace, int64_t workspace_floats,
+                                int32_t max_chunks, int32_t *chunks_out, void *stream);
+/* out [n] = part[0 .. n) + part[stride ..) + ... (chunks partials, in order; stride == n),
+ * the reduction fs_linear_f32_group would have written. */
+int fs_splitk_sum(const float *part, int32_t chunks, int64_t stride, int64_t n, float *out, void *stream);
 int fs_linear_f32_group(const fs_gemm_f32 *const *gs, int32_t n, float *workspace, int64_t workspace_floats,
                         void *stream);
 

@@ -4,6 +4,8 @@ sampling pass rides along forward_kld's density pass.  Every problem is computed
 is alone and the BatchNorm running statistics are applied afterwards in the reference's
 order (sampling pass first, main_algorithm_2.py:446-447), so a step must give exactly
 what the separate passes give: loss, every gradient, running statistics and counters."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -252,3 +254,123 @@ def test_kld_loss_head(B, R):
                                  _lib.ptr(flag), _lib.stream_ptr()))
         assert bool(flag) == (word != 0)
         torch.testing.assert_close(loss, want.detach(), rtol=2e-6, atol=0)
+
+
+@pytest.mark.parametrize("N,kw,rows", [(16, dict(L=4, H=64, nb=2, K=8), 96), (64, A2, 256),
+                                       (16, dict(L=3, H=32, nb=1, K=5), 64), (16, dict(L=2, H=256, nb=3, K=8), 64)],
+                         ids=["n16-h64", "a2-n64", "n16-nb1", "n16-h256-nb3"])
+def test_deferred_splitk_matches_reduced(N, kw, rows):
+    """The final Linear's input gradient left as split-K partials (fs_linear_f32_group_partial)
+    and summed on load by its two readers (the last block's second Linear backward as A, the
+    block's first BatchNorm fold as dx_add; fs_linear_f32_pair_bn_sk) against the reduction
+    launch: the same loss, every gradient and buffer bit for bit, and no splitk_reduce_kernel
+    left when the reduction input is the split product (K = n (3K+1) >= 2048)."""
+    from torch.profiler import ProfilerActivity, profile
+
+    outs, counts = [], []
+    prev = AF._defer_splitk
+    try:
+        for defer in (True, False):
+            AF._defer_splitk = defer
+            m = _model(N, kw, seed=3)
+            fbn = AF.FlatBatchNorm(m)
+            x = _batch(N, rows, seed=8)
+            for p in m.parameters():
+                p.grad = None
+            torch.cuda.manual_seed(17)
+            with profile(activities=[ProfilerActivity.CUDA]) as prof:
+                loss = step_loss(m, x, rows, 1.0, fbn)
+                registered = []
+                AF._splitk_pending = _Recording(registered)
+                try:
+                    loss.backward()
+                    assert not AF._splitk_pending  # every placeholder consumed by its last reader
+                finally:
+                    AF._splitk_pending = {}
+                torch.cuda.synchronize()
+            split = N * (3 * kw["K"] + 1) >= 2048  # n (3K+1), n = D / 2 = N features
+            assert len(registered) == (kw["L"] if defer and split else 0)  # one deferred dh per layer
+            names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+            counts.append(sum(1 for n in names if "splitk_reduce" in n))
+            outs.append((loss.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None},
+                         [b.clone() for b in m.buffers()]))
+    finally:
+        AF._defer_splitk = prev
+    (la, ga, ba), (lb, gb, bb) = outs
+    assert torch.equal(la, lb)
+    assert ga.keys() == gb.keys()
+    for n in ga:
+        assert torch.equal(ga[n], gb[n]), n
+    for a, b in zip(ba, bb):
+        assert torch.equal(a, b)
+    if counts[1]:  # the profiler saw device kernels
+        assert counts[0] == (0 if split else counts[1]), counts
+
+
+class _Recording(dict):
+    """AF._splitk_pending that records every placeholder registered."""
+
+    def __init__(self, log):
+        super().__init__()
+        self.log = log
+
+    def __setitem__(self, k, v):
+        self.log.append(k)
+        super().__setitem__(k, v)
+
+
+def test_splitk_partial_entry_points():
+    """fs_linear_f32_group_partial + fs_splitk_sum give fs_linear_f32_group's values bit for
+    bit; fs_linear_f32_pair_bn_sk with A as 3 partials equals fs_linear_f32_pair_bn on the
+    reduced A."""
+    L = _lib.load()
+    p = _lib.ptr
+    g = torch.Generator().manual_seed(5)
+    M, H, P = 256, 128, 2944
+    gp = torch.randn((M, P), generator=g).cuda()
+    w = torch.randn((P, H), generator=g).cuda() * 0.05
+    outs = []
+    for partial in (False, True):
+        gh = torch.full((M, H), float("nan"), device="cuda")
+        d = _lib.GemmF32(M, H, P, p(gp), P, 1, p(w), H, 1, None, None, 0, p(gh), H, None)
+        nws = L.fs_linear_f32_splitk_floats(d)
+        ws = torch.empty((nws,), device="cuda")
+        arr = (ctypes.POINTER(_lib.GemmF32) * 1)(ctypes.pointer(d))
+        if partial:
+            ch = ctypes.c_int32(0)
+            _lib.check(L.fs_linear_f32_group_partial(arr, 1, p(ws), nws, 3, ctypes.byref(ch), _lib.stream_ptr()))
+            assert ch.value == 3 and torch.isnan(gh).all()  # C not written: its partials are in ws
+            _lib.check(L.fs_splitk_sum(p(ws), ch.value, M * H, M * H, p(gh), _lib.stream_ptr()))
+            outs.append((gh, ws, ch.value))
+        else:
+            _lib.check(L.fs_linear_f32_group(arr, 1, p(ws), nws, _lib.stream_ptr()))
+            outs.append((gh, ws, 1))
+    torch.cuda.synchronize()
+    # the chunking differs (3 partials against the plan's), so the sums agree within rounding
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-5)
+    gh, ws, ch = outs[1]
+    # the pair on the reduced A against the pair summing the partials on load
+    K2 = 128
+    u = torch.rand((M, K2), generator=g).cuda()
+    wl = torch.randn((H, K2), generator=g).cuda() * 0.1
+    x = torch.randn((M, K2), generator=g).cuda()
+    mean, invstd = x.mean(0), torch.rsqrt(x.var(0, unbiased=False) + 1e-5)
+    gamma = torch.rand(K2, generator=g).cuda() + 0.5
+    res = []
+    for sk in (False, True):
+        gu = torch.empty((M, K2), device="cuda")
+        gw = torch.empty((H, K2), device="cuda")
+        gb = torch.empty((H,), device="cuda")
+        part = torch.empty(((M + 31) // 32, K2, 2), device="cuda")
+        a = p(ws) if sk else p(gh)
+        g0 = _lib.GemmF32(M, K2, H, a, H, 1, p(wl), K2, 1, None, None, 0, p(gu), K2, None)
+        g1 = _lib.GemmF32(H, K2, M, a, 1, H, p(u), K2, 1, None, None, 0, p(gw), K2, p(gb))
+        fo = _lib.BnFold(p(gu), p(u), p(x), p(mean), p(invstd), p(gamma), p(part), None, None, None, None, M, K2)
+        if sk:
+            _lib.check(L.fs_linear_f32_pair_bn_sk(g0, g1, None, fo, ch, M * H, 1, 0, _lib.stream_ptr()))
+        else:
+            _lib.check(L.fs_linear_f32_pair_bn(g0, g1, None, fo, _lib.stream_ptr()))
+        res.append((gu, gw, gb, part))
+    torch.cuda.synchronize()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
