@@ -568,6 +568,7 @@ struct LinG {
     int M, N, K, sam, sak, sbk, sbn, ldr, ldc, abytes, bbytes;
     int pstats;  // (fs_linear_f32_pair_bn, producer) per-tile BatchNorm-backward sums of C
     int ach, astr;  // A = the ordered sum of ach split-K partials astr floats apart (ach = 1: A itself)
+    float *aout;    // (ach > 1, row-major A) the summed A written out by the first column tile
 };
 // A BatchNorm1d (train) + ReLU backward folded into the backward pairs on either side of it
 // (fs_linear_f32_pair_bn): the producer pair's input gradient is the BatchNorm output's
@@ -681,6 +682,8 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
     const bool fadd = V != 0 && F.dx_add != nullptr;
     // (V = 1) this row tile's dy written out by the first column tile's workgroup
     float *const aout = (V == 1 && by == 0 && F.a_out && m < M) ? F.a_out : nullptr;
+    // (SK, V = 0) this row tile's summed A written out by the first column tile's workgroup
+    float *const skout = (SK && V == 0 && AK && by == 0 && P.aout && m < M) ? P.aout : nullptr;
     if constexpr (V != 0) {
         Gr = lin_rsrc(F.gu, P.abytes);
         Ur = lin_rsrc(F.u, P.abytes);
@@ -783,6 +786,7 @@ __device__ __forceinline__ void ling_tile(const LinG &P, unsigned bx, unsigned b
                     for (int z = 1; z < kSkMax; ++z)
                         if (z < ach) a[s] = a[s] + az[s][z - 1];
                     a[s] = a[s] + 0.f;
+                    if (skout) *(t4 *)(skout + am + k + 4 * h) = a[s];
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
@@ -1445,7 +1449,7 @@ static bool ling_ok(const GemmArgs &g) {
 static LinG ling_fill(const GemmArgs &g) {
     return LinG{g.A, g.B, g.bias, g.R, g.C, g.stats, g.rowsum_a, (int)g.M, (int)g.N, (int)g.K, (int)g.sam, (int)g.sak,
                 (int)g.sbk, (int)g.sbn, (int)g.ldr, (int)g.ldc, (int)extent_bytes(g.M, g.sam, g.K, g.sak),
-                (int)extent_bytes(g.K, g.sbk, g.N, g.sbn), 0, 1, 0};
+                (int)extent_bytes(g.K, g.sbk, g.N, g.sbn), 0, 1, 0, nullptr};
 }
 
 // n products (all ling_ok) in one gemm_ling_kernel launch; part[i] / S[i] / kchunk[i]: the
@@ -1587,6 +1591,7 @@ hipError_t fs_linear_f32_pair_bn_impl(const GemmArgs &g0, const GemmArgs &g1, co
             ga.p[i].g.astr = (int)a_str;
             ga.p[i].g.abytes += (a_ch - 1) * (int)a_str * 4;  // the descriptor spans every partial
         }
+        ga.p[0].g.aout = fout->a_out;  // nullable: the reduced A for its other readers
     }
     if (fout) {  // g0's output is the BatchNorm output's gradient gu [B][H]
         const BnFold &f = *fout;

@@ -278,9 +278,9 @@ _direct_grads = False  # set by paired_kld around its forward: one gradient cont
 # (fs_linear_f32_pair_bn; _BnFoldLink) in the graphs paired_kld builds; FS_FOLD_BN=0 turns it off
 _fold_bn = os.environ.get("FS_FOLD_BN", "1") != "0"
 # The final Linear's input gradient (split-K over n (3K+1)) left as unreduced partials in the
-# same graphs: its two readers, the last block's second Linear backward (A) and the block's
-# first BatchNorm fold (dx_add), sum them on load, so its reduction launch goes; FS_DEFER_SPLITK=0
-# turns it off.  {placeholder data_ptr: (placeholder, workspace, chunks)}: the placeholder is
+# same graphs: its first reader, the last block's second Linear backward, sums them on load as
+# its A and writes the sum out for the other (the block's first BatchNorm fold, dx_add), so the
+# reduction launch goes; FS_DEFER_SPLITK=0 turns it off.  {placeholder data_ptr: (placeholder, workspace, chunks)}: the placeholder is
 # what autograd carries; whoever cannot sum on load materialises it first (_sk_materialise).
 _defer_splitk = os.environ.get("FS_DEFER_SPLITK", "1") != "0"
 _splitk_pending = {}
@@ -690,7 +690,10 @@ class _BnReluLinear(torch.autograd.Function):
                              p(add2), p(a_out), M, N)
         if fout is not None:
             part = torch.empty(((M + 31) // 32, K, 2), dtype=torch.float32, device=x.device)
-            fo = _lib.BnFold(p(gu), p(u), p(x), p(mean), p(invstd), p(gamma), p(part), None, None, None, None, M, K)
+            # (a_sk) the pair also writes the reduced gy into its placeholder (a_out) for the
+            # residual's reader
+            fo = _lib.BnFold(p(gu), p(u), p(x), p(mean), p(invstd), p(gamma), p(part), None, None, None,
+                             p(gy) if a_sk is not None else None, M, K)
         # the input / weight gradient pair over 48 workgroups, then the BatchNorm + ReLU
         # backward unless it is folded into the pair before (r04): 10.9 us per layer in a
         # graph, against 18.1 us for one launch whose column strips own the BatchNorm sums
@@ -699,6 +702,8 @@ class _BnReluLinear(torch.autograd.Function):
         # (device-scope fences; DESIGN "Training", profiles/r03/r03v_*)
         if fi is not None or fo is not None:
             _pair_bn(g0, g1, fi, fo, a_sk=a_sk, add_sk=add_sk)
+            if a_sk is not None:
+                _sk_get(gy, pop=True)  # materialised by the pair: its other reader loads it plainly
         else:
             _lib.check(L.fs_linear_f32_pair(g0, g1, _lib.stream_ptr()), "fs_linear_f32_pair")
         gr = None

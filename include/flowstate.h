@@ -398,7 +398,9 @@ int fs_linear_f32_pair_bn(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs
 /* The same with split-K operands left unreduced by fs_linear_f32_group_partial: a_chunks > 1
  * (fout only, no fin; at most 3): A of both products is the ordered sum of a_chunks partials a_stride
  * floats apart (g0->A == g1->A = partial 0); add_chunks > 1 (fin): fin->dx_add likewise.
- * Each sum is fs_splitk_sum's, taken on load: the values are those of the reduced operand. */
+ * Each sum is fs_splitk_sum's, taken on load: the values are those of the reduced operand.
+ * With a_chunks > 1, fout->a_out (nullable) receives the reduced A ([B][K] of g0's layout),
+ * written by g0's first column tile, for A's other readers. */
 int fs_linear_f32_pair_bn_sk(const fs_gemm_f32 *g0, const fs_gemm_f32 *g1, const fs_bn_fold *fin,
                              const fs_bn_fold *fout, int32_t a_chunks, int64_t a_stride, int32_t add_chunks,
                              int64_t add_stride, void *stream);

@@ -322,7 +322,7 @@ class _Recording(dict):
 def test_splitk_partial_entry_points():
     """fs_linear_f32_group_partial + fs_splitk_sum give fs_linear_f32_group's values bit for
     bit; fs_linear_f32_pair_bn_sk with A as 3 partials equals fs_linear_f32_pair_bn on the
-    reduced A."""
+    reduced A, and writes that reduced A out (fout->a_out)."""
     L = _lib.load()
     p = _lib.ptr
     g = torch.Generator().manual_seed(5)
@@ -365,7 +365,9 @@ def test_splitk_partial_entry_points():
         a = p(ws) if sk else p(gh)
         g0 = _lib.GemmF32(M, K2, H, a, H, 1, p(wl), K2, 1, None, None, 0, p(gu), K2, None)
         g1 = _lib.GemmF32(H, K2, M, a, 1, H, p(u), K2, 1, None, None, 0, p(gw), K2, p(gb))
-        fo = _lib.BnFold(p(gu), p(u), p(x), p(mean), p(invstd), p(gamma), p(part), None, None, None, None, M, K2)
+        aout = torch.full((M, H), float("nan"), device="cuda")
+        fo = _lib.BnFold(p(gu), p(u), p(x), p(mean), p(invstd), p(gamma), p(part), None, None, None,
+                         p(aout) if sk else None, M, K2)
         if sk:
             _lib.check(L.fs_linear_f32_pair_bn_sk(g0, g1, None, fo, ch, M * H, 1, 0, _lib.stream_ptr()))
         else:
@@ -374,3 +376,4 @@ def test_splitk_partial_entry_points():
     torch.cuda.synchronize()
     for a, b in zip(*res):
         assert torch.equal(a, b)
+    assert torch.equal(aout, gh)  # the reduced A written out (fout->a_out) for its other readers
