@@ -401,21 +401,38 @@ __device__ __forceinline__ t4 lin_ld(__amdgpu_buffer_rsrc_t r, int off) {
     return __builtin_bit_cast(t4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
-// bn_prologue's arithmetic (column k = thread k, Chan's update over the producer's tiles
-// in order, biased variance, invstd; the lead workgroup's outputs and running statistics)
+typedef float f2s __attribute__((ext_vector_type(2)));
+// the first round of producer tile statistics (column k = thread k), loaded before the GEMM
+// operands so that waiting for them does not wait for the operands (in-order vmcnt)
 template <int K>
-__device__ __forceinline__ void lin_bn_prologue(const LinBn &bn, int rows, bool lead, BnLds &S) {
+__device__ __forceinline__ void lin_bn_first(const LinBn &bn, f2s (&v)[kBnStTiles], float &gk, float &bk) {
+    const int k = threadIdx.x;
+    if (k < K) {
+        const int nt = bn.tiles < kBnStTiles ? bn.tiles : kBnStTiles;
+        const f2s *src = (const f2s *)bn.st + k;
+#pragma unroll
+        for (int t = 0; t < kBnStTiles; ++t) v[t] = t < nt ? src[t * K] : f2s{0.f, 0.f};
+        gk = bn.gamma[k];
+        bk = bn.beta[k];
+    }
+}
+
+// bn_prologue's arithmetic (column k = thread k, Chan's update over the producer's tiles
+// in order, biased variance, invstd; the lead workgroup's outputs and running statistics);
+// v0 / gk / bk: lin_bn_first's loads
+template <int K>
+__device__ __forceinline__ void lin_bn_prologue(const LinBn &bn, int rows, bool lead, BnLds &S,
+                                                const f2s (&v0)[kBnStTiles], float gk, float bk) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     const int k = threadIdx.x;
     if (k < K) {
-        const float gk = bn.gamma[k], bk = bn.beta[k];
         float n = 0.f, mean = 0.f, m2 = 0.f;
         for (int t0 = 0; t0 < bn.tiles; t0 += kBnStTiles) {
             const int nt = bn.tiles - t0 < kBnStTiles ? bn.tiles - t0 : kBnStTiles;
             const f2 *src = (const f2 *)bn.st + t0 * K + k;
             f2 v[kBnStTiles];
 #pragma unroll
-            for (int t = 0; t < kBnStTiles; ++t) v[t] = t < nt ? src[t * K] : f2{0.f, 0.f};
+            for (int t = 0; t < kBnStTiles; ++t) v[t] = t0 == 0 ? v0[t] : (t < nt ? src[t * K] : f2{0.f, 0.f});
 #pragma unroll
             for (int t = 0; t < kBnStTiles; ++t) {
                 if (t < nt) {
@@ -459,6 +476,9 @@ __device__ __forceinline__ void lin_tile(const LinP &P, const LinBn &bn, unsigne
     const bool aok = m < M;
     const __amdgpu_buffer_rsrc_t Ar = lin_rsrc(P.A, M * K * 4), Wr = lin_rsrc(P.W, P.N * K * 4);
     const int kq = 8 * w + 4 * h;  // this lane's first k in each k-block
+    f2s st0[kBnStTiles];
+    float gk = 0.f, bk = 0.f;
+    if (bn.on) lin_bn_first<K>(bn, st0, gk, bk);
     t4 a[KBW], b[KBW];
 #pragma unroll
     for (int s = 0; s < KBW; ++s) {
@@ -469,17 +489,22 @@ __device__ __forceinline__ void lin_tile(const LinP &P, const LinBn &bn, unsigne
 #pragma unroll
     for (int i = 0; i < 16; ++i) ep_r[i] = 0.f;
     if (w == 0) {
-        ep_bias = P.bias ? P.bias[col] : 0.f;
+        // buffer loads, the bias last: rows past M read zero, no per-row branch, and no load
+        // waits for another's result register (the bias's once fed an address computation)
         if (P.R) {
+            const __amdgpu_buffer_rsrc_t Rr = lin_rsrc(P.R, M * P.ldr * 4);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int row = (int)bx * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
-                if (row < M) ep_r[i] = P.R[row * P.ldr + col];
+                ep_r[i] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(Rr, (row < M ? row * P.ldr + col : M * P.ldr) * 4, 0, 0));
             }
         }
+        if (P.bias)
+            ep_bias = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lin_rsrc(P.bias, P.N * 4), col * 4, 0, 0));
     }
     if (bn.on) {
-        lin_bn_prologue<K>(bn, M, bx == 0 && by == 0, L.S);
+        lin_bn_prologue<K>(bn, M, bx == 0 && by == 0, L.S, st0, gk, bk);
         const int nt = P.N / 32;
 #pragma unroll
         for (int s = 0; s < KBW; ++s) {
@@ -1394,7 +1419,7 @@ static bool lin_ok(const GemmArgs &g, const BnIn *bn) {
     const int64_t lim = (int64_t)1 << 30;
     return g.M > 0 && g.N > 0 && g.K > 0 && g.K % 64 == 0 && g.K <= 256 && g.N % 32 == 0 && g.sak == 1 &&
            g.sam == g.K && g.sbk == 1 && g.sbn == g.K && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
-           !g.rowsum_a && g.M * g.K < lim && g.N * g.K < lim && g.M * g.ldc < lim && (!g.R || g.M * g.ldr < lim) &&
+           !g.rowsum_a && g.M * g.K < lim && g.N * g.K < lim && g.M * g.ldc < lim && (!g.R || g.M * g.ldr < lim / 2) &&
            g.M <= 32LL * 65535 && (!bn || (bn->rows == g.M && (!bn->a_out || ((uintptr_t)bn->a_out & 15) == 0)));
 }
 
