@@ -296,7 +296,7 @@ def config2(steps=16, C=4096, N=16):
             "acceptance_rate": rate}
 
 
-def config5(cycles=10, train_steps=20):
+def config5(cycles=10, train_steps=100):
     """BASELINE config 5 (Algorithm 2 on-the-fly retrain + sample, N=64, A2 flow) on one
     GPU as a secondary line, at the reference's sizes (main_algorithm_2.py:33-52): 100
     runs, UPDATE_NUM_SAMPLES=1000 (100 local moves per run, sample() every 10), one

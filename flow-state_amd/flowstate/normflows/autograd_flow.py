@@ -139,6 +139,7 @@ class _KldLoss(torch.autograd.Function):
         return loss
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, g):
         from .. import _lib
 
