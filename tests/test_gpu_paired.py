@@ -377,3 +377,51 @@ def test_splitk_partial_entry_points():
     for a, b in zip(*res):
         assert torch.equal(a, b)
     assert torch.equal(aout, gh)  # the reduced A written out (fout->a_out) for its other readers
+
+
+def test_splitk_dx_add_consumer():
+    """fs_linear_f32_pair_bn_sk's consumer form: the folded BatchNorm's residual gradient
+    dx_add given as 3 split-K partials (add_chunks) against the same pair on the reduced
+    dx_add: input / weight / bias gradients, dgamma / dbeta and dy written out, bit for bit."""
+    L = _lib.load()
+    p = _lib.ptr
+    g = torch.Generator().manual_seed(9)
+    M, H, P, K3 = 256, 128, 2944, 128
+    gp = torch.randn((M, P), generator=g).cuda()
+    w = torch.randn((P, H), generator=g).cuda() * 0.05
+    gh = torch.empty((M, H), device="cuda")
+    d = _lib.GemmF32(M, H, P, p(gp), P, 1, p(w), H, 1, None, None, 0, p(gh), H, None)
+    nws = L.fs_linear_f32_splitk_floats(d)
+    ws = torch.empty((nws,), device="cuda")
+    ch = ctypes.c_int32(0)
+    arr = (ctypes.POINTER(_lib.GemmF32) * 1)(ctypes.pointer(d))
+    _lib.check(L.fs_linear_f32_group_partial(arr, 1, p(ws), nws, 3, ctypes.byref(ch), _lib.stream_ptr()))
+    _lib.check(L.fs_splitk_sum(p(ws), ch.value, M * H, M * H, p(gh), _lib.stream_ptr()))
+    gu2 = torch.randn((M, H), generator=g).cuda()
+    y2 = torch.randn((M, H), generator=g).cuda()
+    u2 = torch.relu(y2 + 0.1)
+    mean2, invstd2 = y2.mean(0), torch.rsqrt(y2.var(0, unbiased=False) + 1e-5)
+    gamma2 = (torch.rand(H, generator=g) + 0.5).cuda()
+    part2 = torch.randn(((M + 31) // 32, H, 2), generator=g).cuda()
+    w3 = torch.randn((H, K3), generator=g).cuda() * 0.1
+    x3 = torch.randn((M, K3), generator=g).cuda()
+    res = []
+    for sk in (False, True):
+        gx = torch.empty((M, K3), device="cuda")
+        gw3 = torch.empty((H, K3), device="cuda")
+        gb3 = torch.empty((H,), device="cuda")
+        dg = torch.empty((H,), device="cuda")
+        db = torch.empty((H,), device="cuda")
+        aout = torch.empty((M, H), device="cuda")
+        g0 = _lib.GemmF32(M, K3, H, p(gu2), H, 1, p(w3), K3, 1, None, None, 0, p(gx), K3, None)
+        g1 = _lib.GemmF32(H, K3, M, p(gu2), 1, H, p(x3), K3, 1, None, None, 0, p(gw3), K3, p(gb3))
+        fi = _lib.BnFold(p(gu2), p(u2), p(y2), p(mean2), p(invstd2), p(gamma2), p(part2), p(dg), p(db),
+                         p(ws) if sk else p(gh), p(aout), M, H)
+        if sk:
+            _lib.check(L.fs_linear_f32_pair_bn_sk(g0, g1, fi, None, 1, 0, ch.value, M * H, _lib.stream_ptr()))
+        else:
+            _lib.check(L.fs_linear_f32_pair_bn(g0, g1, fi, None, _lib.stream_ptr()))
+        res.append((gx, gw3, gb3, dg, db, aout))
+    torch.cuda.synchronize()
+    for a, b in zip(*res):
+        assert torch.isfinite(a).all() and torch.equal(a, b)
