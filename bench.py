@@ -73,12 +73,22 @@ def synthetic_model(N, device):
     return m.to(device).eval()
 
 
-def synthetic_states(N, C, c0, seed=7):
-    """FCC lattice (initialise.py:8-116) + small per-chain jitter, float64 box coords."""
+def synthetic_states(N, C, c0, seed=7, block=1024):
+    """FCC lattice (initialise.py:8-116) + small per-chain jitter, float64 box coords.
+    Global chain g's jitter comes from block g // `block` of a generator keyed by
+    (seed, block), so a chain's start state does not depend on how the chains are
+    sharded over ranks (a 1-rank run over world*C chains holds the same states)."""
     base, box = initialise_fcc(num_particles=N, rho=0.03, aspect_ratio=1.0)
-    rng = np.random.default_rng(seed + c0)
     L = float(box.box_size_x)
-    return np.mod(base[None] + rng.normal(0, 0.05, (C, N, 2)), L), L
+    jit = np.empty((C, N, 2))
+    g = c0
+    while g < c0 + C:
+        b = g // block
+        rows = np.random.default_rng([seed, b]).normal(0, 0.05, (block, N, 2))
+        n = min(c0 + C, (b + 1) * block) - g
+        jit[g - c0:g - c0 + n] = rows[g - b * block:g - b * block + n]
+        g += n
+    return np.mod(base[None] + jit, L), L
 
 
 def alt_precisions(bmc, stepper, steps=3):
@@ -441,6 +451,24 @@ def final_reduction(bmc):
     return parallel.final_reduction(bmc)
 
 
+FLOW_SOURCES = ("flow-state_amd/csrc/flow_kernels.hip", "flow-state_amd/csrc/flow_device.h",
+                "flow-state_amd/csrc/flow_layout.h", "flow-state_amd/csrc/fs_internal.h",
+                "flow-state_amd/csrc/Makefile")
+
+
+def flow_source_sha16():
+    """Fingerprint of the sources the f32 flow kernel is built from: a PMC traffic profile
+    (profiles/traffic.json, tools/pmc_traffic.py) carries the fingerprint of the sources it
+    was collected on, so the bench can say whether its `traffic` is that of THIS kernel."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in FLOW_SOURCES:
+        with open(os.path.join(REPO, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def _pmc_traffic(C):
     """HBM bytes per flow-pass launch of THIS bench's shape (C rows: grid C/64*512) from
     the committed rocprofv3 PMC passes (profiles/traffic.json, tools/pmc_traffic.py:
@@ -459,8 +487,10 @@ def _pmc_traffic(C):
             and isinstance(v, dict) and grid in v]
     if not vals:
         return None, None
+    src = t.get("flow_src_sha16")
     return sum(vals) / len(vals), {"profile": "profiles/traffic.json", "head": t.get("head"), "grid": int(grid),
-                                   "launch_kinds": len(vals)}
+                                   "launch_kinds": len(vals), "flow_src_sha16": src,
+                                   "matches_flow_sources": src == flow_source_sha16()}
 
 
 def flow_algorithmic_bytes(model, C, N):
@@ -671,6 +701,9 @@ def main():
                     help="skip the secondary measurement of the opt-in single-pass log q mode")
     ap.add_argument("--no-config5", action="store_true",
                     help="skip the secondary BASELINE config-5 line (Algorithm 2 cycle, A2 flow, N=64)")
+    ap.add_argument("--dump", default=None,
+                    help="write each rank's final per-chain state to DUMP.rank<r>.npz (rehearsals: a sharded "
+                         "run must hold the chains a 1-rank run over the same global chains holds)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -730,7 +763,12 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     bmc.check_errors()
-    n_acc = torch.tensor([int(bmc.n_accept.item()) - acc0], dtype=torch.int64, device=dev)
+    if args.dump:
+        np.savez(f"{args.dump}.rank{rank}.npz", chain_offset=c0, state=bmc.state.cpu().numpy(),
+                 state_is_f32=bmc.state_is_f32.cpu().numpy(), E_old=bmc.E_old.cpu().numpy(),
+                 nll_old=bmc.nll_old.cpu().numpy(), accepted=bmc.accepted.cpu().numpy(),
+                 attempts=bmc.attempts.cpu().numpy(), pcg=bmc.pcg.cpu().numpy())
+    n_acc =torch.tensor([int(bmc.n_accept.item()) - acc0], dtype=torch.int64, device=dev)
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     # per-rank attribution of the timed region (gathered to rank 0): its own wall time,
     # its steps alone, the end reduction's RCCL calls (which also absorb the wait for the

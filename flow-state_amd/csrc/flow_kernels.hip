@@ -38,19 +38,9 @@
 
 namespace fs {
 
-// timing-only A/B builds (wrong results): FS_TIMING_NO_EPI_VALU stores the accumulators
-// without the BatchNorm / ReLU arithmetic, FS_TIMING_NO_GROUP_BARRIER drops the row-group
-// barriers of the residual blocks
-#ifdef FS_TIMING_NO_EPI_VALU
-#define FS_EPI(v, a, b) (v)
-#else
+// eval-BatchNorm (folded) + ReLU epilogue of a ResNet accumulator
 #define FS_EPI(v, a, b) fmaxf(fmaf((v), (a), (b)), 0.f)
-#endif
-#ifdef FS_TIMING_NO_GROUP_BARRIER
-#define FS_GROUP_BARRIER(c, ph) ((void)0)
-#else
 #define FS_GROUP_BARRIER(c, ph) group_barrier((c), (ph))
-#endif
 #ifndef FS_RPD
 #define FS_RPD 3  // weight-fragment ring depth of the ResNet GEMMs
 #endif
@@ -281,13 +271,7 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
         float u[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) u[k] = tile_row(acc[0][0], acc[1][0], k);
-#ifdef FS_TIMING_NO_KNOTS  // timing-only A/B build (wrong results): the knot arithmetic removed
-#pragma unroll
-        for (int k = 0; k < K; ++k) ks[k] = u[k];
-        ks[K] = a.B;
-#else
         knots_from_logits<K>(u, ks, INV ? kMinHd : kMinWd, a);
-#endif
     }
     // searchsorted (splines.py:11-13): knots are non-decreasing, so the last k
     // with x >= knot[k] is the bin; the gathered knots ride along the scan
@@ -316,13 +300,7 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
         float u[K], ko[K + 1];
 #pragma unroll
         for (int k = 0; k < K; ++k) u[k] = tile_row(acc[0][0], acc[1][0], k);
-#ifdef FS_TIMING_NO_KNOTS
-#pragma unroll
-        for (int k = 0; k < K; ++k) ko[k] = u[k];
-        ko[K] = a.B;
-#else
         knots_from_logits<K>(u, ko, INV ? kMinWd : kMinHd, a);
-#endif
         o0 = ko[0];
         o1 = ko[1];
 #pragma unroll
@@ -335,7 +313,6 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
     }
     pf.mark(PH_SPLINE);
     const float *xr = X + lane * XS;
-#ifndef FS_TIMING_NO_GATHER  // timing-only A/B build: the derivative dot products removed
 #pragma unroll 1
     for (int q0 = 0; q0 < NQ; q0 += 2 * QB) {
         drows_issue<QB, K>(g1, W, voff, dsec, q0 + QB);
@@ -343,9 +320,6 @@ __device__ __forceinline__ float cond_spline(const float *__restrict__ X, __amdg
         if (q0 + 2 * QB < NQ) drows_issue<QB, K>(g0, W, voff, dsec, q0 + 2 * QB);
         drows_dot<QB>(g1, xr, q0 + QB, ud0, ud1);
     }
-#else
-    drows_dot<QB>(g0, xr, 0, ud0, ud1);
-#endif
     pf.mark(PH_FINAL_GEMM);
     const float icw = INV ? o0 : s0, cw1 = INV ? o1 : s1;
     const float ich = INV ? s0 : o0, ch1 = INV ? s1 : o1;
@@ -515,9 +489,6 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
     int *gbar = (int *)(smem + LL.ld + kWaves * kRows * 4);  // one arrival counter per row group
     int gphase = 0;
     if (tid < 4) gbar[tid] = 0;
-#ifdef FS_PRIO_HI
-    if (wid >= 4) __builtin_amdgcn_s_setprio(1);  // second-dispatched half wins VALU arbitration
-#endif
     Prof pf;
     __syncthreads();
     pf.mark(PH_INPUT);
@@ -530,9 +501,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
             __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
         if (MODE != MODE_DENSITY) {
             off = (off + N) % D;  // Coupling.inverse rolls first (coupling.py:113-114)
-#ifndef FS_TIMING_NO_UNC  // timing-only A/B build (wrong results): no unconditional spline
             ld += uncond_spline<K, true>(P + PL.unc, CO, cs, N, D, off, a, nan_any);
-#endif
             pf.mark(PH_UNCOND);
             __syncthreads();
             pf.mark(PH_BARRIER);
@@ -541,13 +510,8 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
         for (int f = wid; f < N; f += kWaves) {
             const float v = CO[lane * cs + (2 * f + off) % D];
             const float sv = a.scale_pf * v;
-#ifdef FS_TIMING_NO_PF  // timing-only A/B build (wrong results): no cos / sin
-            X[lane * XS + f] = sv;
-            X[lane * XS + N + f] = sv;
-#else
             X[lane * XS + f] = cosf(sv);
             X[lane * XS + N + f] = sinf(sv);
-#endif
         }
         for (int c = D + wid; c < 8 * PL.kg_in; c += kWaves) X[lane * XS + c] = 0.f;
         pf.mark(PH_PF);
@@ -643,11 +607,6 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
         pf.mark(PH_EPI);
         __syncthreads();
         pf.mark(PH_BARRIER);
-#ifdef FS_STAGGER
-        // waves 4-7 start the final phase FS_STAGGER x 64 x 127 cycles late (A/B experiment)
-        if (wid >= 4)
-            for (int z = 0; z < FS_STAGGER; ++z) __builtin_amdgcn_s_sleep(127);
-#endif
         // final layer + conditional spline, feature by feature
         if constexpr (K <= 16) {  // feature pairs share the widths / heights tiles
             constexpr bool INV = MODE != MODE_DENSITY;
@@ -672,11 +631,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
                                                            a, nan_any, pf);
             }
         } else {
-#ifdef FS_TIMING_NO_FINAL  // timing-only A/B build (wrong results): no final layer / conditional spline
-        for (int j = wid; j < 0; j += kWaves) {
-#else
         for (int j = wid; j < N; j += kWaves) {
-#endif
             const int p = (2 * j + 1 + off) % D;
             ld += cond_spline<XS, H, K, MODE != MODE_DENSITY>(
                 X, W, (int)(PL.wf * 4), PL.kg_h, V + PL.v_bf + 96 * j, (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
@@ -684,9 +639,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_pass_kernel(FlowArgs a) {
         }
         }
         if (MODE == MODE_DENSITY) {
-#ifndef FS_TIMING_NO_UNC
             ld += uncond_spline<K, false>(P + PL.unc, CO, cs, N, D, off, a, nan_any);
-#endif
             off = (off + N) % D;  // Coupling.forward rolls last (coupling.py:100-101)
             pf.mark(PH_UNCOND);
         }

@@ -223,22 +223,6 @@ __device__ __forceinline__ void store_tile(char *XP, int plane, int xsb, int til
 template <int P, int H, int CTW, int RTW, bool RELU>
 __device__ __forceinline__ void split_epilogue(char *XP, int plane, int xsb, int tile0, int rt0,
                                                const EpiVec<CTW> &e, const f32x16 (&acc)[CTW][RTW]) {
-#ifdef FS_TIMING_NO_EPI  // timing-only A/B build (wrong results): stores without arithmetic or plane split
-#pragma unroll
-    for (int ct = 0; ct < CTW; ++ct)
-#pragma unroll
-        for (int rt = 0; rt < RTW; ++rt) {
-            uint2 pk[4][P];
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-#pragma unroll
-                for (int q = 0; q < P; ++q)
-                    pk[g][q] = make_uint2(__builtin_bit_cast(uint32_t, acc[ct][rt][4 * g]),
-                                          __builtin_bit_cast(uint32_t, acc[ct][rt][4 * g + 1]));
-            store_tile<P>(XP, plane, xsb, tile0 + ct, rt0 + rt, pk);
-        }
-    return;
-#endif
 #pragma unroll
     for (int ct = 0; ct < CTW; ++ct) {
         float a[16], c[16];
@@ -496,11 +480,7 @@ __global__ void __launch_bounds__(kThreads, 2) flow_split_kernel(FlowArgs a) {
         }
         pf.mark(PH_TAIL_GEMM);
         // final layer + conditional spline, feature by feature (TL column j: written by this wave only)
-#ifdef FS_TIMING_NO_FINAL  // timing-only A/B build (wrong results): no final layer / conditional spline
-        for (int j = j0; j < j0; ++j) {
-#else
         for (int j = j0; j < j1; ++j) {
-#endif
             const int p = (2 * j + 1 + off) % D;
             ld += split_cond_spline<P, K, MODE != MODE_DENSITY, RD>(
                 XP, plane, xsb, W, (int)((SL.wf + (int64_t)3 * j * SL.kst_h * 256 * P) * 4), SL.kst_h,

@@ -1416,7 +1416,8 @@ hipError_t fs_linear_f32_group_impl(const GemmArgs *gs, int n, float *ws, int64_
 // gemm_lin_kernel takes a product: nn.Linear's forward layout, K = 64, 128, 192 or 256, N a
 // multiple of 32, 16-byte aligned operands, no row sum, 32-bit offsets
 static bool lin_ok(const GemmArgs &g, const BnIn *bn) {
-    const int64_t lim = (int64_t)1 << 30;
+    // element counts whose byte offsets (x 4, computed in 32-bit int) stay below 2^31
+    const int64_t lim = (int64_t)1 << 29;
     return g.M > 0 && g.N > 0 && g.K > 0 && g.K % 64 == 0 && g.K <= 256 && g.N % 32 == 0 && g.sak == 1 &&
            g.sam == g.K && g.sbk == 1 && g.sbn == g.K && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
            !g.rowsum_a && g.M * g.K < lim && g.N * g.K < lim && g.M * g.ldc < lim && (!g.R || g.M * g.ldr < lim / 2) &&
@@ -1467,8 +1468,9 @@ static bool ling_ok(const GemmArgs &g) {
     if (g.M <= 0 || g.K <= 0 || g.K % 4 != 0 || (g.N <= 0 && !g.rowsum_a) || g.N < 0) return false;
     if (g.sam < 0 || g.sak < 0 || g.sbk < 0 || g.sbn < 0 || g.M > 32LL * 65535 || g.N > 32LL * 65535) return false;
     const int64_t ab = extent_bytes(g.M, g.sam, g.K, g.sak), bb = extent_bytes(g.K, g.sbk, g.N, g.sbn);
-    return ab < lim && bb < lim && g.M * g.ldc < lim && (!g.R || g.M * g.ldr < lim) && g.K < lim / 4 &&
-           g.M * g.sam < lim && g.K * g.sak < lim && g.K * g.sbk < lim && g.N * g.sbn < lim && g.M * g.N < lim;
+    const int64_t el = lim / 2;  // element counts: byte offsets (x 4, 32-bit int) below 2^31
+    return ab < lim && bb < lim && g.M * g.ldc < el && (!g.R || g.M * g.ldr < el) && g.K < lim / 4 &&
+           g.M * g.sam < el && g.K * g.sak < el && g.K * g.sbk < el && g.N * g.sbn < el && g.M * g.N < el;
 }
 
 static LinG ling_fill(const GemmArgs &g) {

@@ -285,6 +285,7 @@ _fold_bn = os.environ.get("FS_FOLD_BN", "1") != "0"
 # what autograd carries; whoever cannot sum on load materialises it first (_sk_materialise).
 _defer_splitk = os.environ.get("FS_DEFER_SPLITK", "1") != "0"
 _splitk_pending = {}
+_sk_deferred = 0  # forwards that took the deferral (tests: the handshake is met on the product path)
 
 
 def _sk_get(t, pop=False):
@@ -637,6 +638,10 @@ class _BnReluLinear(torch.autograd.Function):
         ctx.res = res
         ctx.mark_non_differentiable(st)
         ctx.set_materialize_grads(False)
+        if r is not None and res is not None and ctx.fold_out is not None:
+            # handshake with _FinalSplines: this backward can take y's gradient as split-K
+            # partials (summed on load, written out for the residual's reader)
+            y._fs_splitk_reader = True
         return y, st
 
     @staticmethod
@@ -1133,7 +1138,15 @@ class _FinalSplines(torch.autograd.Function):
         ctx.direct = _direct_grads
         # dh left as split-K partials for its readers (decided here: _direct_grads is a
         # forward-time setting)
-        ctx.defer = _defer_splitk and _fold_ok(h.shape[0], h.shape[1], h.shape[1])
+        # Only when h's producer said in its forward that its backward sums the partials on
+        # load (_BnReluLinear, _fs_splitk_reader) and nothing else is registered to read gh
+        # (retain_grad, tensor hooks): any other reader would see the unreduced placeholder.
+        ctx.defer = (_defer_splitk and _fold_ok(h.shape[0], h.shape[1], h.shape[1])
+                     and getattr(h, "_fs_splitk_reader", False) and not h.retains_grad
+                     and not getattr(h, "_backward_hooks", None))
+        if ctx.defer:
+            global _sk_deferred
+            _sk_deferred += 1
         ctx.layer = layer
         ctx.has_lq = lq_in is not None
         ctx.res = res

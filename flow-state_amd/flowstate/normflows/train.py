@@ -358,8 +358,12 @@ class GraphedTrainStep:
         until reset_nan()."""
         c = self.graphs.get(int(batch.shape[0]))
         if c is None:
+            if not check and bool(self.nan_state()):
+                # an earlier replay of this epoch hit a NaN: write nothing (the state stays
+                # that of the last good step) and hand back the sticky flag
+                return torch.full((), float("nan"), device=self._sticky.device), self.nan_state()
             loss = self.eager_step(batch)
-            return loss if check else (loss, torch.zeros((), dtype=torch.bool, device=loss.device))
+            return loss if check else (loss, self.nan_state())
         if check:
             self.reset_nan()  # a NaN of an earlier checked step has raised already
         c.x.copy_(batch)

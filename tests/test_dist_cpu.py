@@ -64,7 +64,7 @@ def _worker(rank, world, port, C, N, L, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 8])
 def test_sharded_reduction_matches_single_process(world, tmp_path):
     C, N = 64, 16
     L = float(np.sqrt(N / 0.03))
@@ -139,14 +139,24 @@ def _train_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_training_collectives(tmp_path):
+@pytest.mark.parametrize("world", [2, 8])
+def test_training_collectives(world, tmp_path):
     out = str(tmp_path / "train.npy")
-    mp.spawn(_train_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-    (own0, got0, p0, c0), (own1, got1, p1, c1) = np.load(out, allow_pickle=True)
-    for a, b in zip(p0, p1):
-        np.testing.assert_array_equal(a, b)  # broadcast made the replicas identical
-    for o0, o1, g0, g1 in zip(own0, own1, got0, got1):
-        np.testing.assert_allclose(g0, (o0 + o1) / 2, rtol=1e-6, atol=1e-7)
-        np.testing.assert_array_equal(g0, g1)
-    assert c0.shape == (7, 4, 2) and (c0[:3] == 0).all() and (c0[3:] == 1).all()
-    np.testing.assert_array_equal(c0, c1)
+    mp.spawn(_train_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    ranks = np.load(out, allow_pickle=True)
+    p0, c0 = ranks[0][2], ranks[0][3]
+    for _, _, p, c in ranks[1:]:
+        for a, b in zip(p0, p):
+            np.testing.assert_array_equal(a, b)  # broadcast made the replicas identical
+        np.testing.assert_array_equal(c0, c)
+    own = [r[0] for r in ranks]
+    for i, g0 in enumerate(ranks[0][1]):
+        np.testing.assert_allclose(g0, sum(o[i] for o in own) / world, rtol=1e-5, atol=1e-7)
+        for r in ranks[1:]:
+            np.testing.assert_array_equal(g0, r[1][i])
+    sizes = [3 + r for r in range(world)]
+    assert c0.shape == (sum(sizes), 4, 2)
+    off = 0
+    for r, n in enumerate(sizes):
+        assert (c0[off:off + n] == r).all()
+        off += n

@@ -128,3 +128,52 @@ def test_split_single_pass_log_q(prec):
     lq2 = m.log_prob(cen)
     rel = ((lq1.double() - lq2.double()).abs() / lq2.double().abs()).cpu().numpy()
     assert np.median(rel) < 1e-5 and rel.max() < 1e-3, (np.median(rel), rel.max())
+
+
+def test_bf16x6_headline_flow_matches_reference_golden():
+    """The bf16x6 image on the headline flow (A1, N=64, the bench's weights) against the
+    REFERENCE's log_prob (tests/golden/flow_a1.npz), with test_gpu_flow's f32 bound written
+    out: every row within 1e-5 relative of the exact (float64) value, and each row within
+    1e-5 of the reference's float32 value or no further from the exact value than it."""
+    from test_gpu_flow import a1_golden_model
+
+    f, m = a1_golden_model()
+    m.set_precision("bf16x6")
+    got = m.log_prob(torch.from_numpy(f["x"]).cuda()).double().cpu().numpy()
+    ref = f["log_prob"].astype(np.float64)
+    exact = f["log_prob_f64"]
+    r_ref = np.abs(got - ref) / np.abs(ref)
+    e_gpu = np.abs(got - exact) / np.abs(exact)
+    e_ref = np.abs(ref - exact) / np.abs(exact)
+    assert e_gpu.max() <= 1e-5, e_gpu.max()
+    ok = (r_ref <= 1e-5) | (e_gpu <= e_ref)
+    assert ok.all(), (np.flatnonzero(~ok), r_ref[~ok], e_gpu[~ok], e_ref[~ok])
+
+
+def test_bf16x6_acceptance_match_at_headline_flow():
+    """The metric's qualifier for the bf16x6 image: the bench's own
+    acceptance-rate replay (bench.acceptance_match) on the headline flow and synthetic
+    states, both flow passes on the bf16x6 image: 2048 chains x 10 steps = 20480
+    decisions re-derived by the oracle's restatement of the reference (float32 energies,
+    log q and PCG64 draws from the same proposals).  Bound: no decision differs on
+    identical inputs; log q of the last step's proposals within 1e-5 relative of the exact
+    (float64) value at p99.9 (the f32 kernel's own bound, test_gpu_flow)."""
+    import bench
+    from flowstate.MCMC import BatchedMonteCarlo, Physics
+
+    N, C = 64, 4096
+    dev = torch.device("cuda")
+    model = bench.synthetic_model(N, dev).set_precision("bf16x6")
+    init, L = bench.synthetic_states(N, C, 0)
+    bmc = BatchedMonteCarlo(model, init, Physics(L, L), np.arange(42, 42 + C, dtype=np.uint64), device=dev)
+    bench.decorrelate(bmc)
+    st = bench.Stepper(bmc)
+    for _ in range(2):
+        st.step(timed=False)
+    am = bench.acceptance_match(bmc, st, n_chains=2048, steps=10)
+    print({k: am[k] for k in ("gpu_accepts", "oracle_accepts", "mismatched_decisions",
+                              "mismatched_on_identical_inputs")}, am["log_q_vs_f64"])
+    assert am["gpu_accepts"] > 0
+    assert am["mismatched_on_identical_inputs"] == 0, am["per_step"]
+    assert am["log_q_vs_f64"]["gpu_f32"]["rows"] >= 2000
+    assert am["log_q_vs_f64"]["gpu_f32"]["max_rel"] <= 2 * am["log_q_vs_f64"]["reference_order_f32"]["max_rel"]

@@ -11,9 +11,13 @@ Both are in KiB.  Usage (in the build container, after the box's passes came bac
 """
 import csv
 import json
+import os
 import subprocess
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import flow_source_sha16  # noqa: E402
 
 
 def per_kernel(d, counter):
@@ -34,7 +38,8 @@ def main():
         head = None
     out = {"note": "bytes per launch = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE counts half of "
                    "wide reads); kernels[name][grid_size] = [bytes, launches averaged]",
-           "head": head, "source": [sys.argv[1], sys.argv[2]], "kernels": {}}
+           "head": head, "flow_src_sha16": flow_source_sha16(), "source": [sys.argv[1], sys.argv[2]],
+           "kernels": {}}
     for (k, grid), (f, n) in sorted(fetch.items()):
         if not k.startswith(("fs::", "void fs::")):
             continue
