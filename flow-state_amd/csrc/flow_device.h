@@ -191,18 +191,7 @@ __device__ __forceinline__ void rqs_eval(float x, float icw, float ibw, float ic
         const float tomt = theta * (1.f - theta);
         const float num = ih * (idl * (theta * theta) + d0 * tomt);
         const float den = idl + sdd * tomt;
-#ifdef FS_RQS_Y_F64  // accuracy experiment (tools/logq_error_split.py): the output map in double
-        {
-            const double th = ((double)x - (double)icw) / (double)ibw;
-            const double tm = th * (1.0 - th);
-            const double dl = (double)ih / (double)ibw;
-            const double nm = (double)ih * (dl * (th * th) + (double)d0 * tm);
-            const double dn = dl + (((double)d0 + (double)d1) - 2.0 * dl) * tm;
-            y = (float)((double)ich + nm / dn);
-        }
-#else
         y = ich + num / den;
-#endif
         const float omt = 1.f - theta;
         const float dnum = (idl * idl) * ((d1 * (theta * theta) + (2.f * idl) * tomt) + d0 * (omt * omt));
         lad = logf(dnum) - 2.f * logf(den);

@@ -156,8 +156,9 @@ def test_bf16x6_acceptance_match_at_headline_flow():
     states, both flow passes on the bf16x6 image: 2048 chains x 10 steps = 20480
     decisions re-derived by the oracle's restatement of the reference (float32 energies,
     log q and PCG64 draws from the same proposals).  Bound: no decision differs on
-    identical inputs; log q of the last step's proposals within 1e-5 relative of the exact
-    (float64) value at p99.9 (the f32 kernel's own bound, test_gpu_flow)."""
+    identical inputs; log q of the last 4 steps' proposals (8192 rows) against the exact
+    (float64) value within the f32 kernel's own bounds (test_gpu_flow): p99.9 within 1e-5,
+    max within 1.25e-5, closer than the reference's float32 op order at the maximum."""
     import bench
     from flowstate.MCMC import BatchedMonteCarlo, Physics
 
@@ -175,5 +176,7 @@ def test_bf16x6_acceptance_match_at_headline_flow():
                               "mismatched_on_identical_inputs")}, am["log_q_vs_f64"])
     assert am["gpu_accepts"] > 0
     assert am["mismatched_on_identical_inputs"] == 0, am["per_step"]
-    assert am["log_q_vs_f64"]["gpu_f32"]["rows"] >= 2000
-    assert am["log_q_vs_f64"]["gpu_f32"]["max_rel"] <= 2 * am["log_q_vs_f64"]["reference_order_f32"]["max_rel"]
+    g, r = am["log_q_vs_f64"]["gpu_f32"], am["log_q_vs_f64"]["reference_order_f32"]
+    assert g["rows"] >= 8000
+    assert g["p999_rel"] <= 1e-5 and g["max_rel"] <= 1.25e-5, g
+    assert g["max_rel"] < r["max_rel"], (g, r)
