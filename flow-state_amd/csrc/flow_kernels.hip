@@ -1019,6 +1019,97 @@ __device__ __forceinline__ void trunk16_run(float *X, const WideArgs &w, int64_t
     }
 }
 
+// The 16-row trunk with each 32-column tile split over two waves, one 16-column half each
+// (wide_trunk16s_kernel, trunk16 = 3, the default).  trunk16_run's waves were parked on
+// their weight loads and barriers ~40 % of the time with two waves per SIMD (r05 PMC:
+// SQ_VALU_MFMA_BUSY 0.61 of SIMD cycles); halving each wave's tile doubles the waves per SIMD
+// that hide those waits, and at H = 128 the merged kernel's 8 waves all run the trunk instead
+// of 4.  A half's accumulator takes the same MFMAs in the same order as gemm16's acc[c]
+// (per k-group m = 0 then 1), so the results are bit-identical.
+template <int XS16, int PD, bool ACC>
+__device__ __forceinline__ void gemm16h(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
+                                        int tile, int c, f32x4 &acc) {
+    const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15, h = lane >> 5, qo = q & 1;
+    if (!ACC)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = 0.f;
+    const float *xa = X + r * XS16 + 4 * qo + ((2 * h) ^ (((r >> 3) & 1) << 1));
+    const int vb = (32 * qo + r) * 16 + 8 * h + 256 * c;
+    const int fb = sec + tile * kg * 1024;
+    f32x2 rb[PD], ra[PD];
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+        if (s < kg) {
+            rb[s] = ldb_pair(W, vb, fb + s * 1024);
+            ra[s] = *(const f32x2 *)(xa + 8 * s);
+        }
+    for (int g0 = 0; g0 < kg; g0 += PD) {
+#pragma unroll
+        for (int s = 0; s < PD; ++s) {
+            const int g = g0 + s;
+            if (g < kg) {
+#pragma unroll
+                for (int m = 0; m < 2; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[s][m], rb[s][m], acc, 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                const int gn = g + PD;
+                if (gn < kg) {
+                    ra[s] = *(const f32x2 *)(xa + 8 * gn);
+                    rb[s] = ldb_pair(W, vb, fb + gn * 1024);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+}
+
+#ifndef FS_WIDE16H_PD
+#define FS_WIDE16H_PD 24  // k-groups in flight per half-tile wave (one 8-byte weight load each)
+#endif
+
+// trunk16_run with wave w computing half (w & 1) of column tile w >> 1 (2 H / 32 trunk waves)
+template <int H, int NW = 2 * (H / 32)>
+__device__ __forceinline__ void trunk16h_run(float *X, const WideArgs &w, int64_t rowt) {
+    constexpr int XS = Trunk16<H>::XS, XS16 = Trunk16<H>::XS16;
+    const FlowArgs &a = w.a;
+    const int N = a.N;
+    const PackLayout PL = pack_layout(N, H, a.nb, a.K);
+    const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tile = wv >> 1, c = wv & 1;
+    const bool act = NW == 2 * (H / 32) || wv < 2 * (H / 32);
+    const float *P = a.packed + (int64_t)w.layer * PL.stride;
+    const float *V = P + PL.vec;
+    const __amdgpu_buffer_rsrc_t W =
+        __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
+    const int col = act ? 32 * tile + 16 * c + r : 0;
+    int pos[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pos[i] = t16_pos(4 * q + i, col, XS16);
+    f32x4 hr, acc;
+    if (act) gemm16h<XS16, FS_WIDE16H_PD, false>(X, W, (int)(PL.win * 4), PL.kg_in, tile, c, hr);  // initial_layer
+    for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
+        const float *VB = V + PL.v_blocks + (int64_t)4 * H * jb;
+        const float e0 = VB[col], e1 = VB[H + col], e2 = VB[2 * H + col], e3 = VB[3 * H + col];
+        const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4);
+        __syncthreads();
+        if (act)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) X[pos[i]] = FS_EPI(hr[i], e0, e1);
+        __syncthreads();
+        if (act) gemm16h<XS16, FS_WIDE16H_PD, false>(X, W, w0, PL.kg_h, tile, c, acc);
+        __syncthreads();
+        if (act)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) X[pos[i]] = FS_EPI(acc[i], e2, e3);
+        __syncthreads();
+        if (act) gemm16h<XS16, FS_WIDE16H_PD, true>(X, W, w0 + (int)(PL.block_stride * 2), PL.kg_h, tile, c, hr);  // h += Lin1(t)
+    }
+    if (!act) return;
+    const float sh = V[col];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w.XB[(rowt + 4 * q + i) * XS + col] = hr[i] + sh;
+}
+
 template <int H>
 __global__ void __launch_bounds__(64 * (H / 32)) wide_trunk16_kernel(WideArgs w) {
     constexpr int XS = Trunk16<H>::XS, XS16 = Trunk16<H>::XS16;
@@ -1137,13 +1228,13 @@ __global__ void __launch_bounds__(kThreads) wide_start_s_kernel(WideArgs w) {
 // and the XA round trip.  Sampling modes write CO, LDU / LDU2 and LDW as
 // wide_start_s_kernel does, density LDW as wide_start_kernel: the same device code on the
 // same operands, so the pass stays bit-identical (tests/test_gpu_wide.py).
-template <int H>
-constexpr int trunk16s_waves() {  // twice the trunk's waves (the start's splines) up to 8
-    return 2 * (H / 32) < 8 ? 2 * (H / 32) : (H / 32 > 8 ? H / 32 : 8);
+template <int H, bool HALF = false>
+constexpr int trunk16s_waves() {  // twice the trunk's waves (the start's splines) up to 8; HALF: two per tile
+    return HALF ? 2 * (H / 32) : (2 * (H / 32) < 8 ? 2 * (H / 32) : (H / 32 > 8 ? H / 32 : 8));
 }
 
-template <int H, int K, int MODE>
-__global__ void __launch_bounds__(64 * trunk16s_waves<H>()) wide_trunk16s_kernel(WideArgs w) {
+template <int H, int K, int MODE, bool HALF = false>
+__global__ void __launch_bounds__((64 * trunk16s_waves<H, HALF>())) wide_trunk16s_kernel(WideArgs w) {
     constexpr int XS16 = Trunk16<H>::XS16;
     __shared__ __attribute__((aligned(16))) float X[16 * XS16];
     __shared__ float TU[MODE != MODE_DENSITY ? kMaxN * 3 * (K + 1) : 1];  // unconditional spline tables
@@ -1168,7 +1259,7 @@ __global__ void __launch_bounds__(64 * trunk16s_waves<H>()) wide_trunk16s_kernel
     float *lu_cur = (w.layer & 1) ? w.LDU2 : w.LDU;
     // every thread's coordinates first (independent loads in flight together), the
     // sampling modes' spline tables staged in LDS (one coalesced pass), then the features
-    constexpr int NW = trunk16s_waves<H>(), NT = 64 * NW, IT = (16 * kMaxN + NT - 1) / NT;
+    constexpr int NW = trunk16s_waves<H, HALF>(), NT = 64 * NW, IT = (16 * kMaxN + NT - 1) / NT;
     float xv[IT];
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
@@ -1205,7 +1296,10 @@ __global__ void __launch_bounds__(64 * trunk16s_waves<H>()) wide_trunk16s_kernel
         X[t16_pos(rr, D + e - rr * npad, XS16)] = 0.f;
     }
     __syncthreads();
-    trunk16_run<H, NW>(X, w, rowt);
+    if constexpr (HALF)
+        trunk16h_run<H, NW>(X, w, rowt);
+    else
+        trunk16_run<H, NW>(X, w, rowt);
 }
 
 // Final layer + conditional spline of one feature unit (a transform feature, or a pair of
@@ -1693,16 +1787,17 @@ static int device_cus() {
     return v;
 }
 
-// the trunk on 16-row tiles with the layer's start merged in (wide_trunk16s_kernel, 2, the
-// default), on 16-row tiles after a start launch (1) or on 32-row ones (0); FS_WIDE_TRUNK16,
-// fs_set_wide_trunk16.  Bit-identical in every setting.
+// the trunk on 16-row tiles with the layer's start merged in and each 32-column tile split
+// over two waves (wide_trunk16s_kernel<..., true>, 3, the default), the same with one wave per
+// tile (2), on 16-row tiles after a separate start launch (1) or on 32-row ones (0);
+// FS_WIDE_TRUNK16, fs_set_wide_trunk16.  Bit-identical in every setting.
 static std::atomic<int> g_trunk16{-1};
 static int wide_trunk16() {
     int v = g_trunk16.load(std::memory_order_relaxed);
     if (v < 0) {
         const char *e = getenv("FS_WIDE_TRUNK16");
         int expect = -1;
-        g_trunk16.compare_exchange_strong(expect, (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2);
+        g_trunk16.compare_exchange_strong(expect, (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3);
         v = g_trunk16.load(std::memory_order_relaxed);
     }
     return v;
@@ -1911,7 +2006,10 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
         w.layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
         if (MODE != MODE_DENSITY) w.off = (w.off + N) % D;
         w.pending = s > 0;
-        if (trunk16 == 2)
+        if (trunk16 == 3)
+            add((const void *)wide_trunk16s_kernel<H, K, MODE, true>, dim3((unsigned)(R / 16)),
+                dim3(64 * trunk16s_waves<H, true>()), 0);
+        else if (trunk16 == 2)
             add((const void *)wide_trunk16s_kernel<H, K, MODE>, dim3((unsigned)(R / 16)), dim3(64 * trunk16s_waves<H>()),
                 0);
         else if (MODE == MODE_DENSITY)
@@ -1954,7 +2052,7 @@ using namespace fs;
 
 int32_t fs_set_wide_trunk16_impl(int32_t on) {
     const int32_t prev = wide_trunk16();
-    if (on >= 0) g_trunk16.store(on > 2 ? 2 : on, std::memory_order_relaxed);
+    if (on >= 0) g_trunk16.store(on > 3 ? 3 : on, std::memory_order_relaxed);
     return prev;
 }
 

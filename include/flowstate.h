@@ -271,10 +271,11 @@ int64_t fs_set_wide_rows(int64_t rows);
 /* Kernel-variant switches for A/B measurements and bit-identity tests, process-wide; each
  * returns the previous value (a negative argument only reads it).  The results do not
  * depend on them.
- * fs_set_wide_trunk16: 2 (default, or FS_WIDE_TRUNK16) = the wide path's ResidualNet on
+ * fs_set_wide_trunk16: 3 (default, or FS_WIDE_TRUNK16) = the wide path's ResidualNet on
  *   16-row tiles (v_mfma_f32_16x16x4_f32, twice the workgroups) with each layer's start
- *   phase merged into the trunk launch, 1 = 16-row tiles after a separate start launch,
- *   0 = 32-row tiles.
+ *   phase merged into the trunk launch and each 32-column tile split over two waves (one
+ *   16-column half each), 2 = the same with one wave per tile, 1 = 16-row tiles after a
+ *   separate start launch, 0 = 32-row tiles.
  * fs_set_wide_final32: 2 (default, or FS_WIDE_FINAL32) = the wide path's final phase on
  *   16- or 32-row blocks when that grid fits the chip in one round (spline bins K <= 16;
  *   16-row blocks on v_mfma_f32_16x16x4_f32), 1 = 32-row blocks at most, 0 = always 64-row

@@ -127,8 +127,9 @@ def test_fused_steps_bit_identical(N, kw, C):
 
 
 class trunk16:
-    """The wide path's trunk for a block: 16-row tiles with the layer's start merged in (2),
-    16-row tiles after a start launch (1) or 32-row tiles (0)."""
+    """The wide path's trunk for a block: 16-row tiles with the layer's start merged in and
+    two waves per 32-column tile (3), the same with one wave per tile (2), 16-row tiles after
+    a start launch (1) or 32-row tiles (0)."""
 
     def __init__(self, on):
         self.on = on
@@ -144,23 +145,23 @@ class trunk16:
                                     (16, dict(L=3, H=64, nb=2, K=8), 130)],
                          ids=["a1-n64-1000", "a1-n16-4096", "a2-n64-200", "n3-h32-77", "n16-h64-130"])
 def test_trunk16_bit_identical_to_trunk32(N, kw, B):
-    """The 16-row trunk (v_mfma_f32_16x16x4_f32 fed the 32x32x2 k order), with and without
-    the start merged in, against the 32-row one, density and sampling, and all against
-    the fused kernel."""
+    """The 16-row trunk (v_mfma_f32_16x16x4_f32 fed the 32x32x2 k order), with the start
+    merged in (one or two waves per column tile) and without, against the 32-row one,
+    density and sampling, and all against the fused kernel."""
     dims, sd, m = _model(N, kw, seed=11)
     g = torch.Generator().manual_seed(B)
     x = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
     zb = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
     outs = []
     with wide_rows(16384):
-        for on in (2, 1, 0):
+        for on in (3, 2, 1, 0):
             with trunk16(on):
                 outs.append([m.log_prob(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)])
     with wide_rows(0):
         outs.append([m.log_prob(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)])
     torch.cuda.synchronize()
-    for a, b, c, d in zip(*outs):
-        assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(a, d)
+    for t in zip(*outs):
+        assert all(torch.equal(t[0], u) for u in t[1:])
 
 
 class final32:
