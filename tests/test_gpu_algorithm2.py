@@ -137,17 +137,19 @@ def test_config5_cycle_at_reference_sizes():
     loss2 = b2.train()
     np.testing.assert_allclose(loss, loss2, rtol=1e-4)
     # the graphed epoch runs torch's capturable Adam arithmetic (fs_adam_step: float32 bias
-    # corrections), the eager one torch's default Adam (bias corrections in double): updates
-    # differ by ~1e-5 relative per step, and Adam's near-sign(g) step turns that into a
-    # full +-lr on the few elements whose gradient sits at the noise level, so after 4
-    # steps a tensor may differ by several per cent of its update (measured up to 4.1 %
-    # on a 128-element BatchNorm bias); the reference itself is pinned by
+    # corrections) and the paired passes' summation orders, the eager one torch's default
+    # Adam (bias corrections in double): updates differ at float32 noise per step, which
+    # Adam's near-sign(g) step turns into a full +-lr on elements whose gradient sits at the
+    # noise level.  Measured at r05 (tools/a2_drift_bisect.py, profiles/r05/r05g_drift.log):
+    # worst tensor 0.70 % of its update (a 128-element BatchNorm bias), median 0.007 %, the
+    # same with every kernel-variant switch (FS_FOLD_BN, FS_DEFER_SPLITK, FS_LEAN_GEMM,
+    # FS_COUPLING_WAVES) off.  Bound: 2 %.  The reference itself is pinned by
     # test_graphed_step_matches_reference_at_config5_size
     for k, v in twin.state_dict().items():
         if "running" in k or not v.is_floating_point():
             continue
         step = (sd[k] - before[k]).norm().item()
-        assert (v - sd[k]).norm().item() <= 8e-2 * step + 1e-6, k
+        assert (v - sd[k]).norm().item() <= 2e-2 * step + 1e-6, k
 
     # --- refeed against the oracle
     hw = phys.half_width
@@ -243,8 +245,12 @@ def test_graphed_epoch_writes_nothing_after_a_nan_step():
         zs.copy_(bad if i == 0 else z0)
         _, fl = step.step(x, check=False)
         flags.append(fl)
+    # a batch size without a captured graph (an epoch's partial last batch runs eagerly) writes
+    # nothing either once the sticky word is set, and hands back the sticky flag
+    _, fl = step.step(x[:200], check=False)
+    flags.append(fl)
     torch.cuda.synchronize()
-    assert bool(flags[0]) and bool(step.nan_state())
+    assert bool(flags[0]) and bool(flags[-1]) and bool(step.nan_state())
     now = [t.detach() for t in step._state_tensors] + step.flat_bn.buffers()
     for a, b in zip(now, after1):
         assert torch.equal(a, b)
