@@ -306,6 +306,46 @@ def config2(steps=16, C=4096, N=16):
             "acceptance_rate": rate}
 
 
+def algorithm1_regime(attempts=1000, runs=10, N=3, interval=1000, sampling=150, equilibration=5000):
+    """The reference's own Algorithm-1 regime (main_algorithm_1.py:33-35, 40-71, 136-210,
+    340-343, 375-424) end to end on one MI355X, as a secondary line (VERDICT r04 missing #4):
+    NUM_PARTICLES = 3, NUM_MC_RUNS = 10 runs started low-left / low-right alternately with
+    seeds 42 + i, EQUILIBRATION_STEPS = 5000 local moves (adjust every 5000, sample() every
+    150; untimed), then the testing phase, timed: BIG_MOVE_ATTEMPTS = 1000 attempts, each
+    BIG_MOVE_INTERVAL = 1000 particle_displacement calls per run with sample() every 150 and
+    one nf_big_move per run with its own flow proposal (generate_samples + HALF_BOX, float32;
+    A1 flow L=15 H=256 32 blocks K=32 at N=3, random-init as synthetic_model).  Reports
+    big-move attempts/s and local moves/s over the whole phase (flowstate.algorithm1)."""
+    from flowstate import algorithm1 as A1D
+    from flowstate.analysis import generate_samples
+    from flowstate.MCMC import initialise_low_left, initialise_low_right
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    model = synthetic_model(N, dev)
+    B = half_box(N)
+    init = np.array([(initialise_low_left if i % 2 == 0 else initialise_low_right)(N, 0.03, 1.0)[0]
+                     for i in range(runs)])
+    bmc = BatchedMonteCarlo(model, init, Physics(2 * B), [42 + i for i in range(runs)], device=dev,
+                            initial_max_displacement=0.65)
+    A1D.equilibrate(bmc, equilibration, 5000, sampling)
+    n = attempts * runs
+    cfg = (generate_samples(model, N, 2, n_iterations=n // 5000 + 1, samples_per_iteration=5000,
+                            device_output=True) + B).to(torch.float32)
+    A1D.testing_phase(bmc, cfg, 2, interval, sampling)  # warm-up: graphs, code objects
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = A1D.testing_phase(bmc, cfg, attempts, interval, sampling)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    acc = int(res.accepts.sum().item())
+    return {"workload": f"Algorithm-1 testing phase as the reference runs it: N={N}, {runs} runs, {attempts} attempts "
+                        f"x ({interval} local moves + 1 NF big move) per run, sample() every {sampling}, A1 flow",
+            "value": n / dt, "unit": "big-move attempts/s", "local_moves_per_s": n * interval / dt,
+            "seconds": dt, "big_move_acceptance": acc / n,
+            "what": "main_algorithm_1.py's testing phase on the device (flowstate.algorithm1.testing_phase); "
+                    "equilibration and proposal generation untimed"}
+
+
 def config5(cycles=10, train_steps=100):
     """BASELINE config 5 (Algorithm 2 on-the-fly retrain + sample, N=64, A2 flow) on one
     GPU as a secondary line, at the reference's sizes (main_algorithm_2.py:33-52): 100
@@ -705,6 +745,8 @@ def main():
                     help="skip the secondary measurement of the opt-in single-pass log q mode")
     ap.add_argument("--no-config5", action="store_true",
                     help="skip the secondary BASELINE config-5 line (Algorithm 2 cycle, A2 flow, N=64)")
+    ap.add_argument("--no-algorithm1-regime", action="store_true",
+                    help="skip the secondary line of the reference's own Algorithm-1 regime (N=3, 10 runs)")
     ap.add_argument("--dump", default=None,
                     help="write each rank's final per-chain state to DUMP.rank<r>.npz (rehearsals: a sharded "
                          "run must hold the chains a 1-rank run over the same global chains holds)")
@@ -874,6 +916,8 @@ def main():
         leg("config2", config2)
     if world == 1 and not args.no_config5:
         leg("config5", config5)
+    if world == 1 and not args.no_algorithm1_regime:
+        leg("algorithm1_regime", algorithm1_regime)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         leg("cpu_baseline", cpu_baseline, N, args.cpu_budget)
         # vs_baseline stays null: BASELINE.md has no published number for this metric

@@ -166,18 +166,23 @@ def build_a2(device):
 # in front of a train-mode BatchNorm have an exactly-zero true gradient (the batch mean
 # removes them); both sides compute rounding noise of ~1e-9 there, covered by grad_abs
 # (weight decay dominates their Adam update).
+# Measured (r05): the CPU restatement at 1.00x the reference's float32 error (its order); the
+# graphed HIP step at 1.01x on whole gradients (1.14x on their max-abs) and 1.67x on the Adam
+# update (layer 0's initial-layer weight: Adam's near-sign step amplifies float32 noise on
+# near-zero gradients); the bounds sit at 1.5x (gradients) and 2x (update) so a regression of
+# the device path's accuracy shows (4x until r04).
 A2_TOL = dict(loss_rtol=1e-5,           # the step's loss (forward_kld at ALPHA = 1) vs the reference's
-              grad_vs_f32_err=4.0,      # per tensor: |g - g64| <= 4 |g_ref32 - g64| + grad_abs (2-norm)
-              grad_max_vs_f32_err=4.0,  # whole tensors: max|g - g64| <= 4 max|g_ref32 - g64| + grad_abs
+              grad_vs_f32_err=1.5,      # per tensor: |g - g64| <= 1.5 |g_ref32 - g64| + grad_abs (2-norm)
+              grad_max_vs_f32_err=1.5,  # whole tensors: max|g - g64| <= 1.5 max|g_ref32 - g64| + grad_abs
               grad_abs=1e-7,
               bn_rtol=1e-4, bn_atol=1e-6,  # running statistics after the step
               # Adam's first update is -lr g'/(|g'| + eps), g' = g + wd p: nearly -lr sign(g'),
               # so it amplifies the float32 noise of every near-zero g' to a sizeable fraction
               # of lr.  Checked: (i) the update is Adam's on this path's own gradients, to
               # float32 rounding of p (every tensor); (ii) on the whole tensors, its distance
-              # to Adam's update on the exact (float64) gradients is within 4x the reference's
+              # to Adam's update on the exact (float64) gradients is within 2x the reference's
               # own float32 update's distance to it
-              update_vs_f32_err=4.0)
+              update_vs_f32_err=2.0)
 
 
 def check_a2_step(m, f, loss, grads, before):
@@ -188,7 +193,7 @@ def check_a2_step(m, f, loss, grads, before):
     names = [str(n) for n in f["names"]]
     params = dict(m.named_parameters())
     assert names == list(params)
-    worst = 0.0
+    worst = worst_n = worst_mx = 0.0
     for n, gn, e32 in zip(names, f["grad_norm"], f["grad_err32_norm"]):
         g = grads.get(n)
         if gn < 0:  # no gradient in the reference (unused preprocessing weights)
@@ -198,6 +203,8 @@ def check_a2_step(m, f, loss, grads, before):
         # error (only g32's norm and |g32 - g64| are stored for all of them)
         d32 = abs(float(g.double().norm()) - gn)
         assert d32 <= t["grad_vs_f32_err"] * e32 + t["grad_abs"], (n, d32, e32)
+        if e32 > t["grad_abs"]:
+            worst_n = max(worst_n, d32 / e32)
         if "grad/" + n in f:
             g64 = torch.from_numpy(f["grad64/" + n]).double()
             ref32 = torch.from_numpy(f["grad/" + n]).double()
@@ -209,7 +216,9 @@ def check_a2_step(m, f, loss, grads, before):
             assert e <= t["grad_vs_f32_err"] * e_ref + t["grad_abs"], (n, e, e_ref)
             assert mx <= t["grad_max_vs_f32_err"] * mx_ref + t["grad_abs"], (n, mx, mx_ref)
             worst = max(worst, e / max(e_ref, 1e-30))
-    print(f"A2 step: worst whole-tensor gradient error vs float64 = {worst:.2f} x the reference's float32 error")
+            worst_mx = max(worst_mx, mx / max(mx_ref, 1e-30))
+    print(f"A2 step: worst whole-tensor gradient error vs float64 = {worst:.2f} x the reference's float32 error "
+          f"(max-abs {worst_mx:.2f} x; per-tensor norm {worst_n:.2f} x)")
     for k, v in m.state_dict().items():
         if "bn/" + k in f:
             ref = f["bn/" + k]
