@@ -1026,9 +1026,23 @@ __device__ __forceinline__ void trunk16_run(float *X, const WideArgs &w, int64_t
 // that hide those waits, and at H = 128 the merged kernel's 8 waves all run the trunk instead
 // of 4.  A half's accumulator takes the same MFMAs in the same order as gemm16's acc[c]
 // (per k-group m = 0 then 1), so the results are bit-identical.
+// The weight half of gemm16h's ring prologue.  (Issuing it before the epilogue and barrier
+// that precede the GEMM, as the fused and split kernels do, made the trunk 18 % slower,
+// r05j_bw_v001 vs v000; so did loading the next block's epilogue vectors a GEMM early, 2-3 %.)
+template <int PD>
+__device__ __forceinline__ void gemm16h_pre(__amdgpu_buffer_rsrc_t W, int sec, int kg, int tile, int c,
+                                            f32x2 (&rb)[PD]) {
+    const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15, h = lane >> 5, qo = q & 1;
+    const int vb = (32 * qo + r) * 16 + 8 * h + 256 * c;
+    const int fb = sec + tile * kg * 1024;
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+        if (s < kg) rb[s] = ldb_pair(W, vb, fb + s * 1024);
+}
+
 template <int XS16, int PD, bool ACC>
 __device__ __forceinline__ void gemm16h(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
-                                        int tile, int c, f32x4 &acc) {
+                                        int tile, int c, f32x4 &acc, f32x2 (&rb)[PD]) {
     const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15, h = lane >> 5, qo = q & 1;
     if (!ACC)
 #pragma unroll
@@ -1036,13 +1050,10 @@ __device__ __forceinline__ void gemm16h(const float *__restrict__ X, __amdgpu_bu
     const float *xa = X + r * XS16 + 4 * qo + ((2 * h) ^ (((r >> 3) & 1) << 1));
     const int vb = (32 * qo + r) * 16 + 8 * h + 256 * c;
     const int fb = sec + tile * kg * 1024;
-    f32x2 rb[PD], ra[PD];
+    f32x2 ra[PD];  // rb: gemm16h_pre's loads of k-groups 0 .. PD - 1
 #pragma unroll
     for (int s = 0; s < PD; ++s)
-        if (s < kg) {
-            rb[s] = ldb_pair(W, vb, fb + s * 1024);
-            ra[s] = *(const f32x2 *)(xa + 8 * s);
-        }
+        if (s < kg) ra[s] = *(const f32x2 *)(xa + 8 * s);
     for (int g0 = 0; g0 < kg; g0 += PD) {
 #pragma unroll
         for (int s = 0; s < PD; ++s) {
@@ -1066,9 +1077,12 @@ __device__ __forceinline__ void gemm16h(const float *__restrict__ X, __amdgpu_bu
 #define FS_WIDE16H_PD 24  // k-groups in flight per half-tile wave (one 8-byte weight load each)
 #endif
 
-// trunk16_run with wave w computing half (w & 1) of column tile w >> 1 (2 H / 32 trunk waves)
+// trunk16_run with wave w computing half (w & 1) of column tile w >> 1 (2 H / 32 trunk waves).
+// The activation image is double-buffered (X: the features, then every other epilogue; Y: the
+// rest), so an epilogue never overwrites the image the GEMM before it read: one barrier per
+// epilogue (its writes before the next GEMM's reads) instead of two.
 template <int H, int NW = 2 * (H / 32)>
-__device__ __forceinline__ void trunk16h_run(float *X, const WideArgs &w, int64_t rowt) {
+__device__ __forceinline__ void trunk16h_run(float *X, float *Y, const WideArgs &w, int64_t rowt) {
     constexpr int XS = Trunk16<H>::XS, XS16 = Trunk16<H>::XS16;
     const FlowArgs &a = w.a;
     const int N = a.N;
@@ -1086,23 +1100,34 @@ __device__ __forceinline__ void trunk16h_run(float *X, const WideArgs &w, int64_
 #pragma unroll
     for (int i = 0; i < 4; ++i) pos[i] = t16_pos(4 * q + i, col, XS16);
     f32x4 hr, acc;
-    if (act) gemm16h<XS16, FS_WIDE16H_PD, false>(X, W, (int)(PL.win * 4), PL.kg_in, tile, c, hr);  // initial_layer
+    f32x2 rb[FS_WIDE16H_PD];
+    if (act) {
+        gemm16h_pre<FS_WIDE16H_PD>(W, (int)(PL.win * 4), PL.kg_in, tile, c, rb);
+        gemm16h<XS16, FS_WIDE16H_PD, false>(X, W, (int)(PL.win * 4), PL.kg_in, tile, c, hr, rb);  // initial_layer
+    }
     for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
         const float *VB = V + PL.v_blocks + (int64_t)4 * H * jb;
         const float e0 = VB[col], e1 = VB[H + col], e2 = VB[2 * H + col], e3 = VB[3 * H + col];
-        const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4);
-        __syncthreads();
+        const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4), w1 = w0 + (int)(PL.block_stride * 2);
+        // Y was last read by the previous block's first GEMM (or never): every wave has passed
+        // the barrier after it, so these writes need no barrier before them
         if (act)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) X[pos[i]] = FS_EPI(hr[i], e0, e1);
+            for (int i = 0; i < 4; ++i) Y[pos[i]] = FS_EPI(hr[i], e0, e1);
         __syncthreads();
-        if (act) gemm16h<XS16, FS_WIDE16H_PD, false>(X, W, w0, PL.kg_h, tile, c, acc);
-        __syncthreads();
+        if (act) {
+            gemm16h_pre<FS_WIDE16H_PD>(W, w0, PL.kg_h, tile, c, rb);
+            gemm16h<XS16, FS_WIDE16H_PD, false>(Y, W, w0, PL.kg_h, tile, c, acc, rb);
+        }
+        // X was last read by the GEMM before the barrier above (initial layer / second GEMM)
         if (act)
 #pragma unroll
             for (int i = 0; i < 4; ++i) X[pos[i]] = FS_EPI(acc[i], e2, e3);
         __syncthreads();
-        if (act) gemm16h<XS16, FS_WIDE16H_PD, true>(X, W, w0 + (int)(PL.block_stride * 2), PL.kg_h, tile, c, hr);  // h += Lin1(t)
+        if (act) {
+            gemm16h_pre<FS_WIDE16H_PD>(W, w1, PL.kg_h, tile, c, rb);
+            gemm16h<XS16, FS_WIDE16H_PD, true>(X, W, w1, PL.kg_h, tile, c, hr, rb);  // h += Lin1(t)
+        }
     }
     if (!act) return;
     const float sh = V[col];
@@ -1238,6 +1263,7 @@ __global__ void __launch_bounds__((64 * trunk16s_waves<H, HALF>())) wide_trunk16
     constexpr int XS16 = Trunk16<H>::XS16;
     __shared__ __attribute__((aligned(16))) float X[16 * XS16];
     __shared__ float TU[MODE != MODE_DENSITY ? kMaxN * 3 * (K + 1) : 1];  // unconditional spline tables
+    __shared__ __attribute__((aligned(16))) float Y[HALF ? 16 * XS16 : 4];  // trunk16h_run's second image
     const FlowArgs &a = w.a;
     const int N = a.N, D = 2 * N;
     const PackLayout PL = pack_layout(N, H, a.nb, a.K);
@@ -1297,7 +1323,7 @@ __global__ void __launch_bounds__((64 * trunk16s_waves<H, HALF>())) wide_trunk16
     }
     __syncthreads();
     if constexpr (HALF)
-        trunk16h_run<H, NW>(X, w, rowt);
+        trunk16h_run<H, NW>(X, Y, w, rowt);
     else
         trunk16_run<H, NW>(X, w, rowt);
 }
