@@ -84,7 +84,9 @@ __global__ void adjust_kernel(int64_t C, double *max_disp, const int64_t *attemp
 // with a wave-uniform index, smaller groups a ds_bpermute shuffle
 template <int LPC>
 __device__ __forceinline__ double bcast(double v, int src) {
-    if constexpr (LPC == 64) {
+    if constexpr (LPC == 1) {
+        return v;
+    } else if constexpr (LPC == 64) {
         const uint64_t u = __double_as_longlong(v);
         const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, src);
         const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
@@ -118,6 +120,10 @@ __device__ __forceinline__ double pick(const double (&v)[PPL], int q) {
 // LPC lanes per chain, PPL particles per lane (particle j = gl + LPC * q): LPC*PPL >= N.
 // Several chains per wave amortise the per-move work that does not scale with N
 // (the PCG64 stream, broadcasts, the reduction tree, the double well, the accept).
+// LPC = 1 / 2 (few particles, few chains: the reference's N = 3 regime) keep a chain in
+// one or two lanes, each lane taking RPL of the four sum rows and double-well roles, so a
+// move has no or one shuffle level on its dependent path; the sums are the same
+// additions in the same order, so every layout gives the same bits.
 template <int LPC, int PPL>
 __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_moves_kernel(LocalArgs a) {
     constexpr int G = 64 / LPC;          // chains per wave
@@ -152,10 +158,9 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
     const int n = N - 1;
     const int nfull = n - (n % 8);
     const uint64_t gmask = (LPC == 64) ? ~0ull : (((1ull << LPC) - 1ull) << (g * LPC));
-    // double-well role of this lane: 0/1 = old position well 0/1, 2/3 = new position
-    const int dw_well = gl & 1;
-    const bool dw_lane = gl < 4 && dw_well < P.num_wells;
-    const double dw_V0 = P.V0[dw_well];
+    // double-well roles / sum rows of this lane: gl + LPC k (role 0/1 = old position well
+    // 0/1, 2/3 = new position; rows eno, viro, enn, virn)
+    constexpr int RPL = LPC >= 4 ? 1 : 4 / LPC;
     int64_t samp = 0;
     unsigned long long n_acc_local = 0;
 
@@ -230,43 +235,56 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
         }
         const bool hit_old = (__ballot(ho) & gmask) != 0;
         const bool hit_new = (__ballot(hn) & gmask) != 0;
-        double dw = 0.0;
-        if (dw_lane)
-            dw = dw_term(gl < 2 ? ox : nx, gl < 2 ? oy : ny, dw_well, P.Lx, P.Ly, dw_V0, P.r0, P.k, iLx, iLy);
+        double dw[RPL];
+#pragma unroll
+        for (int k = 0; k < RPL; ++k) {
+            const int role = gl + LPC * k, well = role & 1;
+            dw[k] = 0.0;
+            if (role < 4 && well < P.num_wells)
+                dw[k] = dw_term(role < 2 ? ox : nx, role < 2 ? oy : ny, well, P.Lx, P.Ly, P.V0[well], P.r0, P.k, iLx,
+                                iLy);
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // numpy pairwise sums of the four compacted rows (eno, viro, enn, virn), lane gl < 4
-        // summing row gl over its flagged terms only: the terms left out are +0.0 and no
-        // term or partial sum is -0.0, so adding them changes nothing (x + 0 == x)
-        double r = 0.0;
-        if (gl < 4) {
-            const uint64_t m = gl < 2 ? mo : mn;
-            const double *row = &lds[wid][gl][sb];
-            if (n < 8) {
-                for (uint64_t b = m; b; b &= b - 1) r += row[__builtin_ctzll(b)];
-            } else {
-                const uint64_t body = nfull >= 64 ? ~0ull : ((1ull << nfull) - 1);
-                double acc[8];
+        // numpy pairwise sums of the four compacted rows (eno, viro, enn, virn), lane gl + LPC u
+        // summing row gl + LPC u over its flagged terms only: the terms left out are +0.0 and
+        // no term or partial sum is -0.0, so adding them changes nothing (x + 0 == x)
+        double rs[RPL];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {  // partial k: terms k, k+8, k+16, ... in order
-                    acc[k] = 0.0;
-                    for (uint64_t b = m & body & (0x0101010101010101ull << k); b; b &= b - 1)
-                        acc[k] += row[__builtin_ctzll(b)];
+        for (int u = 0; u < RPL; ++u) {
+            const int rw = gl + LPC * u;
+            double r = 0.0;
+            if (rw < 4) {
+                const uint64_t m = rw < 2 ? mo : mn;
+                const double *row = &lds[wid][rw][sb];
+                if (n < 8) {
+                    for (uint64_t b = m; b; b &= b - 1) r += row[__builtin_ctzll(b)];
+                } else {
+                    const uint64_t body = nfull >= 64 ? ~0ull : ((1ull << nfull) - 1);
+                    double acc[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {  // partial k: terms k, k+8, k+16, ... in order
+                        acc[k] = 0.0;
+                        for (uint64_t b = m & body & (0x0101010101010101ull << k); b; b &= b - 1)
+                            acc[k] += row[__builtin_ctzll(b)];
+                    }
+                    r = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+                    for (uint64_t b = m & ~body; b; b &= b - 1) r += row[__builtin_ctzll(b)];
                 }
-                r = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-                for (uint64_t b = m & ~body; b; b &= b - 1) r += row[__builtin_ctzll(b)];
             }
+            rs[u] = r;
         }
+        auto from = [&](const double (&v)[RPL], int q) { return bcast<LPC>(pick<RPL>(v, q / LPC), q % LPC); };
         double sums[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sums[q] = bcast<LPC>(r, q);
+        for (int q = 0; q < 4; ++q) sums[q] = from(rs, q);
         double eno = sums[0], viro = sums[1], enn = sums[2], virn = sums[3];
         if (P.num_wells > 0) {  // V = 0; V += term(well 0); V += term(well 1)  (potential.py:96-112)
-            double vo = 0.0 + bcast<LPC>(dw, 0), vn = 0.0 + bcast<LPC>(dw, 2);
+            double vo = 0.0 + from(dw, 0), vn = 0.0 + from(dw, 2);
             if (P.num_wells > 1) {
-                vo += bcast<LPC>(dw, 1);
-                vn += bcast<LPC>(dw, 3);
+                vo += from(dw, 1);
+                vn += from(dw, 3);
             }
             eno += vo;
             enn += vn;
@@ -362,8 +380,16 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
     // Measured at 65536 chains x 1000 moves (sparse in-cutoff sums): N=64 8x8 2.41 G moves/s
     // (16x4 1.88 G, 64x1 1.06 G, 4x16 1.69 G: register-limited); N=32 4x8 4.04 G (8x4 3.20 G);
     // N=16 4x4 5.52 G (8x2 4.78 G).  More chains per wave amortise the per-move work.
+    // N = 3 (the reference's Algorithm-1 runs), 1000 moves: 10 chains 8x1 2.47 ms, 4x1 2.29,
+    // 2x4 3.94, 1x4 5.80 (the double-well and sum work, serial in fewer lanes, outweighs the
+    // shuffles it saves); 65536 chains 8x1 10.2 ms, 4x1 5.71, 2x4 5.28, 1x4 5.52
+    // (profiles/r05/r05m_local_layouts.log).
     int lpc = N > 32 ? 8 : N > 8 ? 4 : 8;
     int ppl = N > 32 ? 8 : N > 16 ? 8 : N > 8 ? 4 : 1;
+    if (N <= 4) {
+        lpc = C >= 16384 ? 2 : 4;
+        ppl = C >= 16384 ? 4 : 1;
+    }
     if (const char *e = getenv("FS_LOCAL_LAYOUT")) {
         int l = 0, q = 0;
         if (sscanf(e, "%dx%d", &l, &q) == 2 && l * q >= N) {
@@ -379,7 +405,7 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
         return hipGetLastError();                                                     \
     }
     FS_LCASE(8, 1) FS_LCASE(8, 2) FS_LCASE(8, 4) FS_LCASE(8, 8) FS_LCASE(64, 1) FS_LCASE(16, 4) FS_LCASE(4, 16)
-    FS_LCASE(4, 8) FS_LCASE(4, 4)
+    FS_LCASE(4, 8) FS_LCASE(4, 4) FS_LCASE(1, 4) FS_LCASE(1, 8) FS_LCASE(2, 4) FS_LCASE(4, 1)
 #undef FS_LCASE
     return hipErrorInvalidValue;
 }

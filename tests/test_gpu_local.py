@@ -157,8 +157,8 @@ def _random_batch(N, C, seed, spread):
     return L, init, f32
 
 
-@pytest.mark.parametrize("N,C,moves", [(1, 64, 50), (5, 256, 300), (16, 256, 300), (24, 128, 200), (33, 128, 200),
-                                     (64, 256, 200)])
+@pytest.mark.parametrize("N,C,moves", [(1, 64, 50), (3, 10, 1000), (5, 256, 300), (16, 256, 300), (24, 128, 200),
+                                     (33, 128, 200), (64, 256, 200)])
 def test_local_moves_match_oracle(N, C, moves):
     L, init, f32 = _random_batch(N, C, seed=N, spread=0.3)
     state = np.where(f32[:, None, None], init.astype(np.float32).astype(np.float64), init)
@@ -183,10 +183,10 @@ def test_local_moves_match_oracle(N, C, moves):
         assert b.attempts[c].item() == ch.cnt[0] and b.accepted[c].item() == ch.cnt[1]
 
 
-LAYOUTS = [(8, 1), (8, 2), (8, 4), (8, 8), (64, 1), (16, 4), (4, 16), (4, 8), (4, 4)]
+LAYOUTS = [(8, 1), (8, 2), (8, 4), (8, 8), (64, 1), (16, 4), (4, 16), (4, 8), (4, 4), (1, 4), (1, 8), (2, 4), (4, 1)]
 
 
-@pytest.mark.parametrize("N", [7, 16, 30, 64])
+@pytest.mark.parametrize("N", [3, 7, 16, 30, 64])
 def test_every_local_layout_gives_the_same_chains(N, monkeypatch):
     """Every instantiated lanes-per-chain x particles-per-lane layout (FS_LOCAL_LAYOUT) runs
     the same chains bit for bit (the default layout is the one the oracle test covers)."""
