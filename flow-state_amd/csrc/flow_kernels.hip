@@ -1040,9 +1040,10 @@ __device__ __forceinline__ void gemm16h_pre(__amdgpu_buffer_rsrc_t W, int sec, i
         if (s < kg) rb[s] = ldb_pair(W, vb, fb + s * 1024);
 }
 
-template <int XS16, int PD, bool ACC>
+template <int XS16, int PD, int XB, bool ACC>
 __device__ __forceinline__ void gemm16h(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
                                         int tile, int c, f32x4 &acc, f32x2 (&rb)[PD]) {
+    static_assert(PD % XB == 0, "activation ring depth divides the weight ring's");
     const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15, h = lane >> 5, qo = q & 1;
     if (!ACC)
 #pragma unroll
@@ -1050,9 +1051,11 @@ __device__ __forceinline__ void gemm16h(const float *__restrict__ X, __amdgpu_bu
     const float *xa = X + r * XS16 + 4 * qo + ((2 * h) ^ (((r >> 3) & 1) << 1));
     const int vb = (32 * qo + r) * 16 + 8 * h + 256 * c;
     const int fb = sec + tile * kg * 1024;
-    f32x2 ra[PD];  // rb: gemm16h_pre's loads of k-groups 0 .. PD - 1
+    // rb: gemm16h_pre's loads of k-groups 0 .. PD - 1; the activations (LDS, short latency)
+    // run XB k-groups ahead
+    f32x2 ra[XB];
 #pragma unroll
-    for (int s = 0; s < PD; ++s)
+    for (int s = 0; s < XB; ++s)
         if (s < kg) ra[s] = *(const f32x2 *)(xa + 8 * s);
     for (int g0 = 0; g0 < kg; g0 += PD) {
 #pragma unroll
@@ -1060,21 +1063,26 @@ __device__ __forceinline__ void gemm16h(const float *__restrict__ X, __amdgpu_bu
             const int g = g0 + s;
             if (g < kg) {
 #pragma unroll
-                for (int m = 0; m < 2; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[s][m], rb[s][m], acc, 0, 0, 0);
+                for (int m = 0; m < 2; ++m)
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[s % XB][m], rb[s][m], acc, 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
-                const int gn = g + PD;
-                if (gn < kg) {
-                    ra[s] = *(const f32x2 *)(xa + 8 * gn);
-                    rb[s] = ldb_pair(W, vb, fb + gn * 1024);
-                }
+                if (g + XB < kg) ra[s % XB] = *(const f32x2 *)(xa + 8 * (g + XB));
+                if (g + PD < kg) rb[s] = ldb_pair(W, vb, fb + (g + PD) * 1024);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
     }
 }
 
+// k-groups in flight per half-tile wave: weights (one 8-byte load each) and activation
+// reads from LDS.  Shallow rings run faster than deep ones (A1-N16 propose pass, 16 and 4096
+// rows: 24/24 5.6-5.75 ms, 24/4 5.4-5.7, 16/4 5.3-5.4, 12/4 and 8/4 5.27-5.30;
+// profiles/r05/r05q_trunk16h_rings.log).
 #ifndef FS_WIDE16H_PD
-#define FS_WIDE16H_PD 24  // k-groups in flight per half-tile wave (one 8-byte weight load each)
+#define FS_WIDE16H_PD 12
+#endif
+#ifndef FS_WIDE16H_XB
+#define FS_WIDE16H_XB 4
 #endif
 
 // trunk16_run with wave w computing half (w & 1) of column tile w >> 1 (2 H / 32 trunk waves).
@@ -1103,7 +1111,7 @@ __device__ __forceinline__ void trunk16h_run(float *X, float *Y, const WideArgs 
     f32x2 rb[FS_WIDE16H_PD];
     if (act) {
         gemm16h_pre<FS_WIDE16H_PD>(W, (int)(PL.win * 4), PL.kg_in, tile, c, rb);
-        gemm16h<XS16, FS_WIDE16H_PD, false>(X, W, (int)(PL.win * 4), PL.kg_in, tile, c, hr, rb);  // initial_layer
+        gemm16h<XS16, FS_WIDE16H_PD, FS_WIDE16H_XB, false>(X, W, (int)(PL.win * 4), PL.kg_in, tile, c, hr, rb);  // initial_layer
     }
     for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
         const float *VB = V + PL.v_blocks + (int64_t)4 * H * jb;
@@ -1117,7 +1125,7 @@ __device__ __forceinline__ void trunk16h_run(float *X, float *Y, const WideArgs 
         __syncthreads();
         if (act) {
             gemm16h_pre<FS_WIDE16H_PD>(W, w0, PL.kg_h, tile, c, rb);
-            gemm16h<XS16, FS_WIDE16H_PD, false>(Y, W, w0, PL.kg_h, tile, c, acc, rb);
+            gemm16h<XS16, FS_WIDE16H_PD, FS_WIDE16H_XB, false>(Y, W, w0, PL.kg_h, tile, c, acc, rb);
         }
         // X was last read by the GEMM before the barrier above (initial layer / second GEMM)
         if (act)
@@ -1126,7 +1134,7 @@ __device__ __forceinline__ void trunk16h_run(float *X, float *Y, const WideArgs 
         __syncthreads();
         if (act) {
             gemm16h_pre<FS_WIDE16H_PD>(W, w1, PL.kg_h, tile, c, rb);
-            gemm16h<XS16, FS_WIDE16H_PD, true>(X, W, w1, PL.kg_h, tile, c, hr, rb);  // h += Lin1(t)
+            gemm16h<XS16, FS_WIDE16H_PD, FS_WIDE16H_XB, true>(X, W, w1, PL.kg_h, tile, c, hr, rb);  // h += Lin1(t)
         }
     }
     if (!act) return;
