@@ -1026,9 +1026,9 @@ __device__ __forceinline__ void trunk16_run(float *X, const WideArgs &w, int64_t
 // that hide those waits, and at H = 128 the merged kernel's 8 waves all run the trunk instead
 // of 4.  A half's accumulator takes the same MFMAs in the same order as gemm16's acc[c]
 // (per k-group m = 0 then 1), so the results are bit-identical.
-// The weight half of gemm16h's ring prologue.  (Issuing it before the epilogue and barrier
-// that precede the GEMM, as the fused and split kernels do, made the trunk 18 % slower,
-// r05j_bw_v001 vs v000; so did loading the next block's epilogue vectors a GEMM early, 2-3 %.)
+// The weight half of gemm16h's ring prologue, issued before the epilogue and barrier that
+// precede the GEMM (its loads do not depend on the activations).  (Loading the next block's
+// epilogue vectors a GEMM early lost 2-3 %, r05j.)
 template <int PD>
 __device__ __forceinline__ void gemm16h_pre(__amdgpu_buffer_rsrc_t W, int sec, int kg, int tile, int c,
                                             f32x2 (&rb)[PD]) {
@@ -1077,13 +1077,16 @@ __device__ __forceinline__ void gemm16h(const float *__restrict__ X, __amdgpu_bu
 // k-groups in flight per half-tile wave: weights (one 8-byte load each) and activation
 // reads from LDS.  Shallow rings run faster than deep ones (A1-N16 propose pass, 16 and 4096
 // rows: 24/24 5.6-5.75 ms, 24/4 5.4-5.7, 16/4 5.3-5.4, 12/4 and 8/4 5.27-5.30;
-// profiles/r05/r05q_trunk16h_rings.log).
+// profiles/r05/r05q_trunk16h_rings.log).  With the ring this shallow, issuing the next GEMM's
+// weights before the epilogue barrier gains ~2 % (8/4: 5.18 ms at 4096 rows, r05s); at 24/24
+// it had lost 18 % (r05j).
 #ifndef FS_WIDE16H_PD
-#define FS_WIDE16H_PD 12
+#define FS_WIDE16H_PD 8
 #endif
 #ifndef FS_WIDE16H_XB
 #define FS_WIDE16H_XB 4
 #endif
+
 
 // trunk16_run with wave w computing half (w & 1) of column tile w >> 1 (2 H / 32 trunk waves).
 // The activation image is double-buffered (X: the features, then every other epilogue; Y: the
@@ -1119,13 +1122,15 @@ __device__ __forceinline__ void trunk16h_run(float *X, float *Y, const WideArgs 
         const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4), w1 = w0 + (int)(PL.block_stride * 2);
         // Y was last read by the previous block's first GEMM (or never): every wave has passed
         // the barrier after it, so these writes need no barrier before them
-        if (act)
+        if (act) {
+            gemm16h_pre<FS_WIDE16H_PD>(W, w0, PL.kg_h, tile, c, rb);  // ahead of the barrier
 #pragma unroll
             for (int i = 0; i < 4; ++i) Y[pos[i]] = FS_EPI(hr[i], e0, e1);
+        }
         __syncthreads();
         if (act) {
-            gemm16h_pre<FS_WIDE16H_PD>(W, w0, PL.kg_h, tile, c, rb);
             gemm16h<XS16, FS_WIDE16H_PD, FS_WIDE16H_XB, false>(Y, W, w0, PL.kg_h, tile, c, acc, rb);
+            gemm16h_pre<FS_WIDE16H_PD>(W, w1, PL.kg_h, tile, c, rb);
         }
         // X was last read by the GEMM before the barrier above (initial layer / second GEMM)
         if (act)
@@ -1133,7 +1138,6 @@ __device__ __forceinline__ void trunk16h_run(float *X, float *Y, const WideArgs 
             for (int i = 0; i < 4; ++i) X[pos[i]] = FS_EPI(acc[i], e2, e3);
         __syncthreads();
         if (act) {
-            gemm16h_pre<FS_WIDE16H_PD>(W, w1, PL.kg_h, tile, c, rb);
             gemm16h<XS16, FS_WIDE16H_PD, FS_WIDE16H_XB, true>(X, W, w1, PL.kg_h, tile, c, hr, rb);  // h += Lin1(t)
         }
     }
