@@ -144,7 +144,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
                     v[j] = o > 0.f ? o : 0.f;
                 }
             }
-#ifndef FS_PROBE_NOAOUT
             // k0 is a multiple of 4: the four elements sit in one 32-wide k slice
             if (bnl->a_out && (k0 >> 5) % bnl->nt == bnl->by) {
                 float *dst = bnl->a_out + (m0 + r) * bnl->lda + k0;
@@ -156,7 +155,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int64_t bx, int64_t
                         if (k0 + j < g.K) dst[j] = v[j];
                 }
             }
-#endif
         }
         return v;
     };
@@ -264,22 +262,14 @@ __global__ __launch_bounds__(64 * SPLIT) void gemm_f32_kernel(GemmArgs g) {
 // the running statistics.  Thread k owns column k (the host guarantees blockDim.x >= K) and
 // loads its kBnStTiles (mean, M2) pairs of a round at once, straight into registers: one
 // round trip per round and a single barrier, where staging the statistics through LDS
-// cost two more barriers (tools/linbn_probe.py, profiles/r03/).
+// cost two more barriers (profiles/r03/).
 struct BnLds {
     float mu[kBnMaxK], is[kBnMaxK], gm[kBnMaxK], bt[kBnMaxK];
 };
 
-#ifndef FS_PROBE_PRO
-#define FS_PROBE_PRO 0  // timing-only builds (tools/linbn_probe.py): 1 = no Chan loop, 2 = no statistics loads
-#endif
 template <int NT>
 __device__ __forceinline__ void bn_prologue(const GemmArgs &g, const BnIn &bn, bool lead, BnLds &S) {
     const int k = threadIdx.x;
-#if FS_PROBE_PRO == 2
-    if (k < g.K) { S.mu[k] = 0.f; S.is[k] = 1.f; S.gm[k] = 1.f; S.bt[k] = 0.f; }
-    __syncthreads();
-    return;
-#endif
     typedef float f2 __attribute__((ext_vector_type(2)));
     // gamma / beta loads issued with the statistics' (one round trip for all)
     const float gk = k < g.K ? bn.gamma[k] : 0.f, bk = k < g.K ? bn.beta[k] : 0.f;
@@ -293,7 +283,7 @@ __device__ __forceinline__ void bn_prologue(const GemmArgs &g, const BnIn &bn, b
             for (int t = 0; t < kBnStTiles; ++t) v[t] = t < nt ? src[t * g.K] : f2{0.f, 0.f};
 #pragma unroll
             for (int t = 0; t < kBnStTiles; ++t) {  // Chan's pairwise update, tiles in order
-                if (t < (FS_PROBE_PRO == 1 ? 1 : nt)) {
+                if (t < nt) {
                     const int64_t row0 = 32 * (t0 + t);
                     const float nb = (float)(bn.rows - row0 < 32 ? bn.rows - row0 : 32);
                     const float nn = n + nb, d = v[t][0] - mean;

@@ -703,7 +703,7 @@ class _BnReluLinear(torch.autograd.Function):
         # the input / weight gradient pair over 48 workgroups, then the BatchNorm + ReLU
         # backward unless it is folded into the pair before (r04): 10.9 us per layer in a
         # graph, against 18.1 us for one launch whose column strips own the BatchNorm sums
-        # (tools/linbn_probe.py, profiles/r03/r03k_linbn_probe.log), and 148 against 239
+        # (profiles/r03/r03k_linbn_probe.log), and 148 against 239
         # steps/s for the BatchNorm backward run by each strip's last tile in the pair's launch
         # (device-scope fences; DESIGN "Training", profiles/r03/r03v_*)
         if fi is not None or fo is not None:
