@@ -346,6 +346,44 @@ def algorithm1_regime(attempts=1000, runs=10, N=3, interval=1000, sampling=150, 
                     "equilibration and proposal generation untimed"}
 
 
+def algorithm1_regime_cpu(N=3, interval=1000, budget_s=8.0):
+    """A bounded CPU sample of algorithm1_regime's testing phase (oracle/, test
+    infrastructure): one run (low-left start, seed 42) at a time, as the reference's driver
+    runs them, each attempt `interval` particle_displacement calls by the oracle's C
+    restatement of monte_carlo.py:146-223 (faster than the reference's numpy-per-move loop,
+    so the ratio to the GPU is understated), then nf_big_move: batch-1 float32 log_prob of
+    the current and the proposed configuration in torch-CPU (the reference's op sequence),
+    the proposal's energy and the PCG64 accept (monte_carlo.py:235-303).  Proposals
+    generated beforehand, untimed, as on the GPU; sample() snapshots (a copy every 150
+    moves) left out."""
+    from oracle import flow as OF
+    from oracle import physics as OP
+    from flowstate.MCMC import initialise_low_left
+
+    dims = OF.FlowDims(N=N, B=half_box(N), **A1)
+    sd = {k: v.detach().cpu() for k, v in synthetic_model(N, "cpu").state_dict().items()}
+    hw = np.float32(dims.B)
+    g = torch.Generator().manual_seed(77)
+    z = (torch.rand((64, dims.D), generator=g) * 2 - 1) * dims.B
+    props = (OF.sample_from(sd, z, dims).numpy() + hw).astype(np.float32).reshape(-1, N, 2)
+    ch = OP.LocalChain(initialise_low_left(N, 0.03, 1.0)[0], 42, OP.make_phys(N), max_disp=0.65)
+    threads = torch.get_num_threads()
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < budget_s or n == 0:
+        ch.local_moves(interval)
+        cfg = props[n % len(props)]
+        old = torch.tensor((ch.particles - hw).reshape(1, -1), dtype=torch.float)
+        new = torch.tensor((cfg - hw).reshape(1, -1), dtype=torch.float)
+        ch.big_move(cfg, -OF.log_prob(sd, old, dims).item(), -OF.log_prob(sd, new, dims).item())
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "big-move attempts/s", "kind": "port", "cores": threads,
+            "sample": f"{n} attempts of one run ({interval} local moves + 1 NF big move each, A1 flow, N={N}), "
+                      f"{dt:.1f} s wall; local moves by the oracle's single-threaded C restatement, log_prob "
+                      f"by the reference's torch-CPU float32 op sequence at batch 1 on {threads} threads"}
+
+
 def config5(cycles=10, train_steps=100):
     """BASELINE config 5 (Algorithm 2 on-the-fly retrain + sample, N=64, A2 flow) on one
     GPU as a secondary line, at the reference's sizes (main_algorithm_2.py:33-52): 100
@@ -918,6 +956,13 @@ def main():
         leg("config5", config5)
     if world == 1 and not args.no_algorithm1_regime:
         leg("algorithm1_regime", algorithm1_regime)
+        if not args.no_cpu_baseline and "error" not in out["algorithm1_regime"]:
+            reg = out["algorithm1_regime"]
+            try:
+                reg["cpu_baseline"] = algorithm1_regime_cpu()
+                reg["vs_cpu_baseline"] = reg["value"] / reg["cpu_baseline"]["value"]
+            except Exception as e:  # noqa: BLE001
+                reg["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         leg("cpu_baseline", cpu_baseline, N, args.cpu_budget)
         # vs_baseline stays null: BASELINE.md has no published number for this metric
