@@ -210,6 +210,25 @@ __device__ __forceinline__ void final_tile_pair32(const float *__restrict__ X, _
     lanes_to_chains(t[0][0], t[1][0]);
 }
 
+// final_tile for the 32 chains of X's first row tile, duplicated into both lane halves
+// (K > 16: one transform feature per tile; the wide path's 32-row final blocks)
+template <int XS, int FPD = 4>
+__device__ __forceinline__ void final_tile32(const float *__restrict__ X, __amdgpu_buffer_rsrc_t W, int sec, int kg,
+                                             int tile, const float *__restrict__ b, f32x16 (&t)[2][1]) {
+    const int h = (threadIdx.x >> 5) & 1;
+    f32x16 t1[1][1];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *(const f32x4 *)(b + 8 * g + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t1[0][0][4 * g + j] = v[j];
+    }
+    gemm64<XS, 1, 1, FPD, true, true>(X, W, sec, kg, 0, tile, t1);
+    t[0][0] = t1[0][0];
+    t[1][0] = t1[0][0];
+    lanes_to_chains(t[0][0], t[1][0]);
+}
+
 #pragma clang fp contract(off)
 
 // Derivative-row gathers of cond_spline: QB quads (16-byte pieces of rows bin and
@@ -1347,9 +1366,10 @@ __global__ void __launch_bounds__((64 * trunk16s_waves<H, HALF>())) wide_trunk16
 // next start / output launch adds them in the fused kernel's order (wide_fold).
 template <int H, int K, int MODE, int WPB, int RB = kRows>
 __global__ void __launch_bounds__(64 * WPB) wide_final_kernel(WideArgs w) {
-    // RB = 32 (K <= 16): 32-row blocks, half the MFMA chain per wave for batches that leave
-    // most of the chip idle; each chain's spline runs in both lane halves, the lower one stores
-    static_assert(RB == kRows || (RB == 32 && K <= 16), "32-row final blocks: feature pairs only");
+    // RB = 32: 32-row blocks, half the MFMA chain per wave for batches that leave most of the
+    // chip idle (or, K > 16, at two workgroups per CU); each chain's spline runs in both lane
+    // halves, the lower one stores
+    static_assert(RB == kRows || RB == 32, "64- or 32-row final blocks");
     constexpr int XS = (H < 2 * kMaxN ? 2 * kMaxN : H) + 4;
     constexpr int RM = RB - 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1408,11 +1428,24 @@ __global__ void __launch_bounds__(64 * WPB) wide_final_kernel(WideArgs w) {
                                                                   (2 * jb + 1 + off) % D, a, nan_any, pf);
             if (store) lc[jb] = lb;
         }
-    } else {
+    } else if constexpr (RB == kRows) {
         const int j = u;
         lc[j] = cond_spline<XS, H, K, MODE != MODE_DENSITY, kWideFPD>(
             X, W, (int)(PL.wf * 4), PL.kg_h, V + PL.v_bf + 96 * j, (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
             V + PL.v_bd + j * (K + 1), CO, cs, (2 * j + 1 + off) % D, j, a, nan_any, pf);
+    } else {  // K > 16 on 32-row blocks: cond_spline's tiles and spline, split as for the pairs
+        constexpr bool INV = MODE != MODE_DENSITY;
+        constexpr int TS = INV ? 1 : 0;
+        const int j = u;
+        const float *bf = V + PL.v_bf + 96 * j;
+        f32x16 tS[2][1], tO[2][1];
+        final_tile32<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * j + TS, bf + 32 * TS, tS);
+        final_tile32<XS, kWideFPD>(X, W, (int)(PL.wf * 4), PL.kg_h, 2 * j + 1 - TS, bf + 32 * (1 - TS), tO);
+        const float l = spline_from_tiles<XS, H, K, INV, RM>(tS, tO, 0, X, W,
+                                                             (int)((PL.wd + (int64_t)j * H * (K + 1)) * 4),
+                                                             V + PL.v_bd + j * (K + 1), CO, cs, (2 * j + 1 + off) % D,
+                                                             a, nan_any, pf);
+        if (store) lc[j] = l;
     }
     if (MODE == MODE_DENSITY && store) {
         float *lu = w.LDU + (row0 + lane) * N;
@@ -2015,6 +2048,9 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
 #ifndef FS_WIDE_WPW
 #define FS_WIDE_WPW 4
 #endif
+#ifndef FS_FINAL32_CUS
+#define FS_FINAL32_CUS 1  // K > 16: 32-row final blocks while the grid is at most this many per CU
+#endif
     constexpr int WPW = FS_WIDE_WPW;  // feature units (waves) per final-phase workgroup
     const int units = K <= 16 ? (N + 1) / 2 : N;
     const unsigned fin_lds = (unsigned)(kRows * XS * 4);
@@ -2027,13 +2063,17 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     // that the 32-row tiles' higher arithmetic intensity wins (8192 rows: 9.0 vs 11.6 ms per
     // A1 N=16 pass, profiles/r04/)
     const int trunk16 = R / 16 <= device_cus() ? wide_trunk16() : 0;
-    // 16- or 32-row final-phase blocks (feature pairs) while the grid fits the chip in a round
-    const int fgy = (units + WPW - 1) / WPW, fsel = K <= 16 ? wide_final32() : 0;
-    const int frows = (fsel >= 2 && (R / 16) * fgy <= device_cus()) ? 16
-                      : (fsel >= 1 && (R / 32) * fgy <= device_cus()) ? 32 : kRows;
+    // 16- or 32-row final-phase blocks (feature pairs) while the grid fits the chip in a round;
+    // K > 16 (one feature per wave): 32-row blocks on the same rule (at two workgroups per CU,
+    // A1 N=16 4096 rows, no faster than 64-row blocks; 1024 rows ~2 % faster:
+    // profiles/r05/r05y_final32_k32.log)
+    const int fgy = (units + WPW - 1) / WPW, fsel = wide_final32();
+    const int frows = K <= 16 ? ((fsel >= 2 && (R / 16) * fgy <= device_cus()) ? 16
+                                 : (fsel >= 1 && (R / 32) * fgy <= device_cus()) ? 32 : kRows)
+                              : ((fsel >= 1 && (R / 32) * fgy <= FS_FINAL32_CUS * device_cus()) ? 32 : kRows);
     const void *final_fn = (const void *)wide_final_kernel<H, K, MODE, WPW>;
+    if (frows == 32) final_fn = (const void *)wide_final_kernel<H, K, MODE, WPW, 32>;
     if constexpr (K <= 16) {
-        if (frows == 32) final_fn = (const void *)wide_final_kernel<H, K, MODE, WPW, 32>;
         if (frows == 16) final_fn = (const void *)wide_final16_kernel<H, K, MODE, WPW>;
     }
     std::vector<WideLaunch> seq;

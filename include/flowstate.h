@@ -277,9 +277,9 @@ int64_t fs_set_wide_rows(int64_t rows);
  *   16-column half each), 2 = the same with one wave per tile, 1 = 16-row tiles after a
  *   separate start launch, 0 = 32-row tiles.
  * fs_set_wide_final32: 2 (default, or FS_WIDE_FINAL32) = the wide path's final phase on
- *   16- or 32-row blocks when that grid fits the chip in one round (spline bins K <= 16;
- *   16-row blocks on v_mfma_f32_16x16x4_f32), 1 = 32-row blocks at most, 0 = always 64-row
- *   blocks.
+ *   16- or 32-row blocks when that grid fits the chip in one round (16-row blocks on
+ *   v_mfma_f32_16x16x4_f32 for spline bins K <= 16 only; K > 16, one feature per wave:
+ *   32-row blocks), 1 = 32-row blocks at most, 0 = always 64-row blocks.
  * fs_set_coupling_waves: 1 (default, or FS_COUPLING_WAVES) = the training step's coupling
  *   launches (fs_coupling_pair_step, fs_coupling_bwd_step) with each row's splines spread
  *   over two / four waves (one knot set per wave), 0 = one / two waves per row.

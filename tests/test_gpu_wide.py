@@ -179,13 +179,17 @@ class final32:
 
 
 @pytest.mark.parametrize("N,kw,B", [(64, A2, 200), (64, A2, 1000), (3, dict(L=2, H=32, nb=2, K=5), 77),
-                                    (16, dict(L=3, H=64, nb=1, K=8), 333), (16, dict(L=2, H=256, nb=2, K=15), 150)],
-                         ids=["a2-n64-200", "a2-n64-1000", "n3-h32-77", "n16-h64-333", "n16-h256-k15-150"])
+                                    (16, dict(L=3, H=64, nb=1, K=8), 333), (16, dict(L=2, H=256, nb=2, K=15), 150),
+                                    (16, dict(L=2, H=256, nb=2, K=32), 150), (3, dict(L=3, H=128, nb=1, K=32), 77),
+                                    (16, dict(L=2, H=256, nb=2, K=32), 4096)],
+                         ids=["a2-n64-200", "a2-n64-1000", "n3-h32-77", "n16-h64-333", "n16-h256-k15-150",
+                              "n16-h256-k32-150", "n3-h128-k32-77", "n16-h256-k32-4096"])
 def test_final32_bit_identical_to_final64(N, kw, B):
-    """The final phase on 16-row blocks (v_mfma_f32_16x16x4_f32 fed the 32x32x2 k order, one
-    lane per chain and feature for the splines) and 32-row blocks (one row tile per wave,
-    each chain's spline in both lane halves) against 64-row blocks and the fused kernel,
-    density and sampling, with a few out-of-bound inputs among the rows."""
+    """The final phase on 16-row blocks (K <= 16: v_mfma_f32_16x16x4_f32 fed the 32x32x2 k
+    order, one lane per chain and feature for the splines) and 32-row blocks (one row tile per
+    wave, each chain's spline in both lane halves; K = 32 too, A1's final phase) against
+    64-row blocks and the fused kernel, density and sampling, with a few out-of-bound inputs
+    among the rows."""
     dims, sd, m = _model(N, kw, seed=12)
     g = torch.Generator().manual_seed(B + 1)
     x = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B * 1.001).cuda()  # a few rows outside the bound
