@@ -136,6 +136,15 @@ int fs_energy_lj_dw(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C
                   "fs_energy_lj_dw");
 }
 
+int fs_energy_state(const fs_phys *p, const double *state, const uint8_t *state_is_f32, int64_t C, int32_t N,
+                    double *E, double *W, void *stream) {
+    REQUIRE(p && C >= 0 && (C == 0 || (state && state_is_f32 && E && W)), "fs_energy_state: invalid arguments");
+    REQUIRE(N >= 1 && N <= fs::kMaxN, "fs_energy_state: N=%d outside [1, %d]", N, fs::kMaxN);
+    REQUIRE(p->Lx > 0 && p->Ly > 0, "fs_energy_state: box must be positive");
+    return hip_rc(fs_energy_impl(p, state, 0, C, N, E, W, nullptr, nullptr, (hipStream_t)stream, state_is_f32),
+                  "fs_energy_state");
+}
+
 int fs_pcg64_seed(const uint64_t *seeds, int64_t C, uint64_t *state, void *stream) {
     REQUIRE(C >= 0 && (C == 0 || (seeds && state)), "fs_pcg64_seed: invalid arguments");
     return hip_rc(fs_pcg64_seed_impl(seeds, C, state, (hipStream_t)stream), "fs_pcg64_seed");

@@ -178,12 +178,11 @@ class BatchedMonteCarlo:
         (EnergyCalculator.__init__, energy_calculator.py:46)."""
         E = torch.empty(self.C, dtype=torch.float64, device=self.device)
         W = torch.empty_like(E)
-        f32 = self.state_is_f32.bool()
-        for mask, dt in ((f32, torch.float32), (~f32, torch.float64)):
-            idx = mask.nonzero().flatten()
-            if idx.numel():
-                e, w, _ = total_energy(self.state[idx].to(dt), self.phys.c)
-                E[idx], W[idx] = e, w
+        # one launch over the float64 states with the per-chain dtype flags (no host round
+        # trip to split the chains, which cost each Algorithm-1 attempt a synchronisation)
+        _lib.check(_lib.load().fs_energy_state(self.phys.c, _lib.ptr(self.state), _lib.ptr(self.state_is_f32),
+                                               self.C, self.N, _lib.ptr(E), _lib.ptr(W), _lib.stream_ptr()),
+                   "fs_energy_state")
         return E, W
 
     def _need_model(self):

@@ -89,6 +89,7 @@ _SIGS = {
     "fs_flow_propose_lq": (ctypes.c_int, [_D, _P, _I64, ctypes.c_uint64, ctypes.c_uint64, _I64, ctypes.c_double]
                            + [_P] * 5 + [_P]),
     "fs_energy_lj_dw": (ctypes.c_int, [_PH, _P, ctypes.c_int, _I64, ctypes.c_int32, _P, _P, _P, _P, _P]),
+    "fs_energy_state": (ctypes.c_int, [_PH, _P, _P, _I64, ctypes.c_int32, _P, _P, _P]),
     "fs_pcg64_seed": (ctypes.c_int, [_P, _I64, _P, _P]),
     "fs_pcg64_random": (ctypes.c_int, [_P, _I64, _P, _P]),
     "fs_min_image": (ctypes.c_int, [_PH, _P, _I64, _P, ctypes.c_int, _I64, _P, _P, _P]),

@@ -146,6 +146,13 @@ int fs_flow_propose_lq(const fs_flow_dims *d, const void *packed, int64_t B, uin
 int fs_energy_lj_dw(const fs_phys *p, const void *pos, int pos_is_f32, int64_t C, int32_t N,
                     double *E, double *W, uint8_t *overlap, uint64_t *nbr, void *stream);
 
+/* The same over chain states held as float64 with a per-chain reference dtype
+ * (state_is_f32[c] = 1: a float32 state after an accepted big move, monte_carlo.py:296, whose
+ * energy the reference computes in float32; EnergyCalculator.__init__,
+ * energy_calculator.py:46): one launch, no host round trip to split the chains by dtype. */
+int fs_energy_state(const fs_phys *p, const double *state, const uint8_t *state_is_f32, int64_t C, int32_t N,
+                    double *E, double *W, void *stream);
+
 /* SimulationBox.minimum_image / compute_distance / compute_distances
  * (simulation_box.py:31-65) for n pairs (pos1[i * stride1], pos2[i]) of [2] positions,
  * float32 (pos_is_f32=1) or float64 (both the same dtype, numpy's promotion done by the
