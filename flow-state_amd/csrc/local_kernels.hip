@@ -96,6 +96,39 @@ __device__ __forceinline__ double bcast(double v, int src) {
     }
 }
 
+// Within-group exchanges with a compile-time pattern: groups of 2 or 4 lanes sit inside one
+// DPP quad, so quad_perm moves them through the VALU (a few cycles) instead of an LDS-path
+// ds_bpermute round trip; other group sizes fall back to the shuffles.
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// lane SRC of the group
+template <int LPC, int SRC>
+__device__ __forceinline__ double bcast_c(double v) {
+    if constexpr (LPC == 1) {
+        return v;
+    } else if constexpr (LPC == 2 || LPC == 4) {  // quad_perm [SRC x4] / [SRC, SRC, 2+SRC, 2+SRC]
+        constexpr int ctrl = LPC == 4 ? SRC * 0x55 : (SRC == 0 ? 0xA0 : 0xF5);
+        return __longlong_as_double((long long)dpp_u64<ctrl>((uint64_t)__double_as_longlong(v)));
+    } else {
+        return bcast<LPC>(v, SRC);
+    }
+}
+
+// lane (lane ^ O) of the group
+template <int LPC, int O>
+__device__ __forceinline__ uint64_t xor_c(uint64_t v) {
+    if constexpr (LPC == 2 || LPC == 4) {  // quad_perm [1,0,3,2] / [2,3,0,1]
+        return dpp_u64<O == 1 ? 0xB1 : 0x4E>(v);
+    } else {
+        return __shfl_xor(v, O, LPC);
+    }
+}
+
 template <int LPC>
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
     if constexpr (LPC == 64) {  // one chain per wave: keep the chain's scalars in SGPRs
@@ -228,8 +261,16 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
                 }
             }
         }
+        if constexpr (LPC >= 2) {
+            mo |= xor_c<LPC, 1>(mo);
+            mn |= xor_c<LPC, 1>(mn);
+        }
+        if constexpr (LPC >= 4) {
+            mo |= xor_c<LPC, 2>(mo);
+            mn |= xor_c<LPC, 2>(mn);
+        }
 #pragma unroll
-        for (int o = 1; o < LPC; o <<= 1) {
+        for (int o = 4; o < LPC; o <<= 1) {
             mo |= __shfl_xor(mo, o, LPC);
             mn |= __shfl_xor(mn, o, LPC);
         }
@@ -275,17 +316,16 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
             }
             rs[u] = r;
         }
-        auto from = [&](const double (&v)[RPL], int q) { return bcast<LPC>(pick<RPL>(v, q / LPC), q % LPC); };
-        double sums[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sums[q] = from(rs, q);
-        double eno = sums[0], viro = sums[1], enn = sums[2], virn = sums[3];
+        // row / role q lives in lane q % LPC of the group, slot q / LPC
+#define FS_FROM(v, q) bcast_c<LPC, (q) % LPC>(pick<RPL>(v, (q) / LPC))
+        double eno = FS_FROM(rs, 0), viro = FS_FROM(rs, 1), enn = FS_FROM(rs, 2), virn = FS_FROM(rs, 3);
         if (P.num_wells > 0) {  // V = 0; V += term(well 0); V += term(well 1)  (potential.py:96-112)
-            double vo = 0.0 + from(dw, 0), vn = 0.0 + from(dw, 2);
+            double vo = 0.0 + FS_FROM(dw, 0), vn = 0.0 + FS_FROM(dw, 2);
             if (P.num_wells > 1) {
-                vo += from(dw, 1);
-                vn += from(dw, 3);
+                vo += FS_FROM(dw, 1);
+                vn += FS_FROM(dw, 3);
             }
+#undef FS_FROM
             eno += vo;
             enn += vn;
         }
