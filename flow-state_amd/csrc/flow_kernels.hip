@@ -753,6 +753,9 @@ struct WideArgs {
     int off;       // physical index of logical coordinate 0 in this phase
     int layer;
     int jb;
+    float *XG;     // (column-split trunk) [R / 16][2][H][16] handed-off column slices
+    unsigned *CNT;  // [2][R / 16] hand-off counters (launch parity x tile)
+    int T;          // R / 16
 };
 
 template <int MODE>
@@ -760,6 +763,9 @@ __global__ void __launch_bounds__(256) wide_input_kernel(WideArgs w) {
     const FlowArgs &a = w.a;
     const int N = a.N, D = 2 * N;
     const int64_t row0 = (int64_t)blockIdx.x * kRows;
+    if (w.CNT)  // the column-split trunk's counters start every pass at zero
+        for (int e = (int)(blockIdx.x * blockDim.x + threadIdx.x); e < 2 * w.T; e += (int)(gridDim.x * blockDim.x))
+            __hip_atomic_store(w.CNT + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     float *CO = w.CO + row0 * D;
     if (MODE == MODE_PROPOSE) {
         const int nq = (D + 3) / 4;
@@ -1359,6 +1365,199 @@ __global__ void __launch_bounds__((64 * trunk16s_waves<H, HALF>())) wide_trunk16
         trunk16_run<H, NW>(X, w, rowt);
 }
 
+// ---------------------------------------------------------------------------
+// Column-split trunk for small batches (trunk16 = 4): a 16-row tile's columns spread over G
+// workgroups (CUs), each running 2 H / 32 / G of trunk16h_run's half-tile waves (the same
+// MFMA chain per column, so bit-identical).  A CU's MFMA rate bounds the half-tile trunk
+// however few rows there are (one tile takes as long per layer as 256 tiles on 256 CUs,
+// profiles/r05/r05n_*); here every epilogue's column slice goes to the tile's other G - 1
+// workgroups through an in-launch hand-off instead.  Its form is the guide's first Valid-forms
+// row (MI355X_MICROARCH.md, inter-workgroup visibility): every slice stored sc1
+// (write-through), each storing wave's vmcnt(0), a workgroup barrier, then ONE lane's
+// agent-scope atomic add on the tile's counter; the consumer's lane 0 polls it with sc1
+// loads, a barrier, then every load of the handed-off bytes is an sc1 buffer load.  The poll
+// is bounded: a timeout sets err bit 2 and the workgroup stops waiting, so the grid always
+// drains.  Slices in XG[tile][step & 1][H][16] (column-major: a lane's four rows are one
+// 16-byte store); counters CNT[launch & 1][tile], the other parity reset here for the next
+// launch (the input kernel resets both).  Only workgroup 0 of a tile writes the start's
+// side outputs (LDW, LDU, CO), the coordinates after the first hand-off, when every
+// workgroup of the tile has read them.
+#ifndef FS_GSPLIT
+#define FS_GSPLIT 4  // workgroups (CUs) per 16-row tile
+#endif
+#ifndef FS_GSPLIT_AUTO_WG
+#define FS_GSPLIT_AUTO_WG 64  // the default trunk's limit on column-split workgroups (A1 N=16:
+                              // 16 / 64 / 128 / 256 rows 4.2-4.7 ms per pass against 5.0-5.3 on
+                              // the half-tile trunk, 512 rows 6.3-6.5 against 5.3;
+                              // profiles/r05/r05af_gsplit.log)
+#endif
+constexpr unsigned kGSpinMax = 1u << 20;  // polls (sc1 load + s_sleep) before a hand-off gives up
+
+template <int H>
+constexpr bool gsplit_ok() {
+    return 2 * (H / 32) % FS_GSPLIT == 0 && 2 * (H / 32) >= FS_GSPLIT;
+}
+
+template <int H, int K, int MODE, int G>
+__global__ void __launch_bounds__(64 * (2 * (H / 32) / G)) wide_trunk16g_kernel(WideArgs w) {
+    constexpr int XS = Trunk16<H>::XS, XS16 = Trunk16<H>::XS16;
+    constexpr int NW = 2 * (H / 32) / G, NT = 64 * NW;  // waves / threads per workgroup
+    constexpr int CPG = H / G;                          // columns per workgroup
+    static_assert(NW >= 1 && NW * G == 2 * (H / 32), "G divides the trunk's half-tile waves");
+    __shared__ __attribute__((aligned(16))) float X[16 * XS16];
+    __shared__ __attribute__((aligned(16))) float Y[16 * XS16];
+    __shared__ float TU[MODE != MODE_DENSITY ? kMaxN * 3 * (K + 1) : 1];
+    __shared__ int dead_s;
+    const FlowArgs &a = w.a;
+    const int N = a.N, D = 2 * N;
+    const PackLayout PL = pack_layout(N, H, a.nb, a.K);
+    const int t = (int)blockIdx.x / G, g = (int)blockIdx.x - t * G;
+    const int64_t rowt = (int64_t)t * 16;
+    const int launch = MODE == MODE_DENSITY ? a.L - 1 - w.layer : w.layer;
+    unsigned *cnt = w.CNT + (launch & 1) * w.T + t;
+    if (threadIdx.x == 0) {
+        dead_s = 0;
+        if (g == 0)
+            __hip_atomic_store(w.CNT + ((launch + 1) & 1) * w.T + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (g == 0 && w.pending)  // the previous final phase folded into LDW (wide_fold's order)
+        for (int e = threadIdx.x; e < 16 * kWaves; e += NT) {
+            const int64_t row = rowt + (e >> 3);
+            const int vw = e & (kWaves - 1);
+            float ld = w.LDW[row * kWaves + vw];
+            if (MODE != MODE_DENSITY) {
+                const float *lu_prev = (w.layer & 1) ? w.LDU : w.LDU2;
+                float su = 0.f;
+                for (int f = vw; f < N; f += kWaves) su += lu_prev[row * N + f];
+                ld += su;
+            }
+            w.LDW[row * kWaves + vw] = wide_fold<K, MODE>(w, row, vw, ld);
+        }
+    const float *P = a.packed + (int64_t)w.layer * PL.stride;
+    float *lu_cur = (w.layer & 1) ? w.LDU2 : w.LDU;
+    constexpr int IT = (16 * kMaxN + NT - 1) / NT;
+    float xv[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = (int)threadIdx.x + it * NT;
+        if (e < 16 * N) xv[it] = w.CO[(rowt + (e & 15)) * D + (2 * (e >> 4) + w.off) % D];
+    }
+    const float *U = P + PL.unc;
+    if (MODE != MODE_DENSITY) {
+        const int nu = N * 3 * (K + 1);
+        for (int e = threadIdx.x; e < nu; e += NT) TU[e] = U[e];
+        __syncthreads();
+    }
+    float nv[IT], nl[IT];  // workgroup 0's deferred side outputs (sampling modes)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = (int)threadIdx.x + it * NT;
+        if (e >= 16 * N) break;
+        const int rr = e & 15, f = e >> 4;
+        float v = xv[it];
+        if (MODE != MODE_DENSITY) {
+            bool nan_any = false;
+            const float x = v;
+            nl[it] = uncond_eval<K, true>(TU, x, a, nan_any, f, v);
+            nv[it] = v;
+            if (nan_any && g == 0 && rowt + rr < a.nrows && a.err) atomicOr(a.err, 1);
+        }
+        const float sv = a.scale_pf * v;
+        X[t16_pos(rr, f, XS16)] = cosf(sv);
+        X[t16_pos(rr, N + f, XS16)] = sinf(sv);
+    }
+    const int npad = 8 * PL.kg_in - D;
+    for (int e = threadIdx.x; e < 16 * npad; e += NT) {
+        const int rr = e / npad;
+        X[t16_pos(rr, D + e - rr * npad, XS16)] = 0.f;
+    }
+    __syncthreads();
+    auto flush_start = [&]() {
+        if (MODE != MODE_DENSITY && g == 0)
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int e = (int)threadIdx.x + it * NT;
+                if (e >= 16 * N) break;
+                const int64_t row = rowt + (e & 15);
+                const int f = e >> 4;
+                lu_cur[row * N + f] = nl[it];
+                const float x = xv[it];
+                if ((x >= a.negB) && (x <= a.B)) w.CO[row * D + (2 * f + w.off) % D] = nv[it];
+            }
+    };
+
+    // the trunk (trunk16h_run on this workgroup's waves)
+    const int lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int hw = g * NW + wv, tile = hw >> 1, c = hw & 1;
+    const float *V = P + PL.vec;
+    const __amdgpu_buffer_rsrc_t W =
+        __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)(PL.stride * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t XGr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(w.XG + (int64_t)t * 2 * H * 16), (short)0, 2 * H * 16 * 4, 0x00020000);
+    const int col = 32 * tile + 16 * c + r;
+    int pos[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pos[i] = t16_pos(4 * q + i, col, XS16);
+    // own slice (already in img at pos) out, the other workgroups' slices in
+    auto hand_off = [&](int step, float *img, const f32x4 &v) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), XGr,
+                                               (((step & 1) * H + col) * 16 + 4 * q) * 4, 0, 16);  // sc1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // every wave's slice stored and drained, img's own columns written
+        if (threadIdx.x == 0) {
+            __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!dead_s) {
+                const unsigned target = (unsigned)(G * (step + 1));
+                unsigned spins = 0;
+                while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > kGSpinMax) {
+                        dead_s = 1;
+                        if (a.err) atomicOr(a.err, 4);
+                        break;
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler only: loads stay below)
+        __syncthreads();
+        if (step == 0) flush_start();
+        for (int e = threadIdx.x; e < (H - CPG) * 4; e += NT) {
+            const int cc = e >> 2, qq = e & 3;
+            const int colf = cc < g * CPG ? cc : cc + CPG;
+            const f32x4 f = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(XGr, (((step & 1) * H + colf) * 16 + 4 * qq) * 4, 0, 16));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) img[t16_pos(4 * qq + i, colf, XS16)] = f[i];
+        }
+        __syncthreads();
+    };
+    f32x4 hr, acc;
+    f32x2 rb[FS_WIDE16H_PD];
+    gemm16h_pre<FS_WIDE16H_PD>(W, (int)(PL.win * 4), PL.kg_in, tile, c, rb);
+    gemm16h<XS16, FS_WIDE16H_PD, FS_WIDE16H_XB, false>(X, W, (int)(PL.win * 4), PL.kg_in, tile, c, hr, rb);
+    for (int jb = 0; jb < a.nb; ++jb) {  // ResidualBlock (resnet.py:37-50), eval BN folded
+        const float *VB = V + PL.v_blocks + (int64_t)4 * H * jb;
+        const float e0 = VB[col], e1 = VB[H + col], e2 = VB[2 * H + col], e3 = VB[3 * H + col];
+        const int w0 = (int)((PL.blocks + jb * PL.block_stride) * 4), w1 = w0 + (int)(PL.block_stride * 2);
+        f32x4 v;
+        gemm16h_pre<FS_WIDE16H_PD>(W, w0, PL.kg_h, tile, c, rb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Y[pos[i]] = v[i] = FS_EPI(hr[i], e0, e1);
+        hand_off(2 * jb, Y, v);
+        gemm16h<XS16, FS_WIDE16H_PD, FS_WIDE16H_XB, false>(Y, W, w0, PL.kg_h, tile, c, acc, rb);
+        gemm16h_pre<FS_WIDE16H_PD>(W, w1, PL.kg_h, tile, c, rb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) X[pos[i]] = v[i] = FS_EPI(acc[i], e2, e3);
+        hand_off(2 * jb + 1, X, v);
+        gemm16h<XS16, FS_WIDE16H_PD, FS_WIDE16H_XB, true>(X, W, w1, PL.kg_h, tile, c, hr, rb);  // h += Lin1(t)
+    }
+    const float sh = V[col];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w.XB[(rowt + 4 * q + i) * XS + col] = hr[i] + sh;
+}
+
 // Final layer + conditional spline of one feature unit (a transform feature, or a pair of
 // them for K <= 16) per wave, for one 64-row block; (density) also the unconditional
 // spline of the same-index identity feature(s).  WPB waves per workgroup share the
@@ -1868,7 +2067,7 @@ static int wide_trunk16() {
     if (v < 0) {
         const char *e = getenv("FS_WIDE_TRUNK16");
         int expect = -1;
-        g_trunk16.compare_exchange_strong(expect, (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3);
+        g_trunk16.compare_exchange_strong(expect, (e && e[0] >= '0' && e[0] <= '5') ? e[0] - '0' : 5);
         v = g_trunk16.load(std::memory_order_relaxed);
     }
     return v;
@@ -1891,7 +2090,7 @@ static int wide_final32() {
 static size_t wide_bytes(int64_t R, int N, int H) {
     const int64_t XS = flow_xw(H) + 4;
     return (size_t)(rup(R * 2 * N * 4, 256) + 2 * rup(R * XS * 4, 256) + rup(R * kWaves * 4, 256) +
-                    3 * rup(R * N * 4, 256));
+                    3 * rup(R * N * 4, 256) + rup(R * 2 * H * 4, 256) + rup((R / 16) * 2 * 4, 256));
 }
 
 struct WideLaunch {
@@ -2043,6 +2242,11 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     w.LDU = (float *)p;
     p += rup(R * N * 4, 256);
     w.LDU2 = (float *)p;
+    p += rup(R * N * 4, 256);
+    w.XG = (float *)p;  // the column-split trunk's hand-off slices and counters
+    p += rup(R * 2 * H * 4, 256);
+    w.CNT = (unsigned *)p;
+    w.T = (int)(R / 16);
     w.pending = 0;
     const unsigned nblk = (unsigned)(R / kRows);
 #ifndef FS_WIDE_WPW
@@ -2062,7 +2266,13 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     // 16-row trunk tiles while they fit the chip in one round (4096 rows on 256 CUs): past
     // that the 32-row tiles' higher arithmetic intensity wins (8192 rows: 9.0 vs 11.6 ms per
     // A1 N=16 pass, profiles/r04/)
-    const int trunk16 = R / 16 <= device_cus() ? wide_trunk16() : 0;
+    // 5 (default): the column-split trunk (4) for the A1 trunk (H = 256, 64 GEMMs per layer) on
+    // batches of at most FS_GSPLIT_AUTO_WG / FS_GSPLIT tiles, else two waves per column tile (3).
+    // 4 forces it wherever the tiles x FS_GSPLIT fit half the chip.
+    int trunk16 = R / 16 <= device_cus() ? wide_trunk16() : 0;
+    const bool gfit = gsplit_ok<H>() && a.nb > 0 && (R / 16) * FS_GSPLIT <= device_cus() / 2;
+    if (trunk16 == 5) trunk16 = (gfit && H >= 256 && (R / 16) * FS_GSPLIT <= FS_GSPLIT_AUTO_WG) ? 4 : 3;
+    if (trunk16 == 4 && !gfit) trunk16 = 3;
     // 16- or 32-row final-phase blocks (feature pairs) while the grid fits the chip in a round;
     // K > 16 (one feature per wave): 32-row blocks on the same rule (at two workgroups per CU,
     // A1 N=16 4096 rows, no faster than 64-row blocks; 1024 rows ~2 % faster:
@@ -2084,7 +2294,11 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
         w.layer = (MODE == MODE_DENSITY) ? a.L - 1 - s : s;
         if (MODE != MODE_DENSITY) w.off = (w.off + N) % D;
         w.pending = s > 0;
-        if (trunk16 == 3)
+        if (trunk16 == 4) {
+            if constexpr (gsplit_ok<H>())
+                add((const void *)wide_trunk16g_kernel<H, K, MODE, FS_GSPLIT>, dim3((unsigned)(R / 16) * FS_GSPLIT),
+                    dim3(64 * (2 * (H / 32) / FS_GSPLIT)), 0);
+        } else if (trunk16 == 3)
             add((const void *)wide_trunk16s_kernel<H, K, MODE, true>, dim3((unsigned)(R / 16)),
                 dim3(64 * trunk16s_waves<H, true>()), 0);
         else if (trunk16 == 2)
@@ -2130,7 +2344,7 @@ using namespace fs;
 
 int32_t fs_set_wide_trunk16_impl(int32_t on) {
     const int32_t prev = wide_trunk16();
-    if (on >= 0) g_trunk16.store(on > 3 ? 3 : on, std::memory_order_relaxed);
+    if (on >= 0) g_trunk16.store(on > 5 ? 5 : on, std::memory_order_relaxed);
     return prev;
 }
 

@@ -375,7 +375,10 @@ class BatchedMonteCarlo:
         made, as the reference raises when it pre-generates its proposals in batches
         (main_algorithm_1.py:340-343, utils.py:422-450), even if a later weight change
         retires the bank before those steps run."""
-        if int(self.err.item()) & 1:
+        v = int(self.err.item())
+        if v & 4:  # (not the reference's: a wide-path column hand-off gave up waiting)
+            raise _lib.FlowStateError("a wide-path trunk hand-off timed out")
+        if v & 1:
             raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
 
     # ------------------------------------------------------------------ judging

@@ -134,7 +134,10 @@ def _prepare_input(x, D):
 
 
 def _raise_on_nan(err):
-    if int(err.item()) & 1:
+    v = int(err.item())
+    if v & 4:  # (not the reference's: a wide-path column hand-off gave up waiting)
+        raise _lib.FlowStateError("a wide-path trunk hand-off timed out")
+    if v & 1:
         raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
 
 

@@ -99,7 +99,8 @@ int fs_flow_pack(const fs_flow_dims *d, const float *raw, void *packed, void *st
  * the density direction (CircularCoupled...inverse = Coupling.forward,
  * wrapper.py:273-275, coupling.py:71-102) + UniformParticle.log_prob
  * (Energy/Uniform.py:50-74).  x, z_out: [B][2N] float32 (z_out nullable);
- * log_q: [B].  err (nullable, device int32): bit0 set on a NaN discriminant. */
+ * log_q: [B].  err (nullable, device int32): bit0 set on a NaN discriminant (|= 4: a
+ * wide-path trunk hand-off timed out, fs_set_wide_trunk16). */
 int fs_flow_log_prob(const fs_flow_dims *d, const void *packed, const float *x, int64_t B,
                      float *log_q, float *z_out, int32_t *err, void *stream);
 
@@ -278,11 +279,14 @@ int64_t fs_set_wide_rows(int64_t rows);
 /* Kernel-variant switches for A/B measurements and bit-identity tests, process-wide; each
  * returns the previous value (a negative argument only reads it).  The results do not
  * depend on them.
- * fs_set_wide_trunk16: 3 (default, or FS_WIDE_TRUNK16) = the wide path's ResidualNet on
- *   16-row tiles (v_mfma_f32_16x16x4_f32, twice the workgroups) with each layer's start
- *   phase merged into the trunk launch and each 32-column tile split over two waves (one
- *   16-column half each), 2 = the same with one wave per tile, 1 = 16-row tiles after a
- *   separate start launch, 0 = 32-row tiles.
+ * fs_set_wide_trunk16: 5 (default, or FS_WIDE_TRUNK16) = by batch: 4 for the A1 trunk
+ *   (H = 256) on at most 256 rows, else 3; 4 = each 16-row tile's columns split over four
+ *   workgroups (CUs) that hand their epilogue slices to each other inside the launch (where
+ *   the tiles x 4 fit half the chip, else 3; err |= 4 if a hand-off wait gave up); 3 = the
+ *   wide path's ResidualNet on 16-row tiles (v_mfma_f32_16x16x4_f32, twice the workgroups)
+ *   with each layer's start phase merged into the trunk launch and each 32-column tile split
+ *   over two waves (one 16-column half each), 2 = the same with one wave per tile, 1 = 16-row
+ *   tiles after a separate start launch, 0 = 32-row tiles.
  * fs_set_wide_final32: 2 (default, or FS_WIDE_FINAL32) = the wide path's final phase on
  *   16- or 32-row blocks when that grid fits the chip in one round (16-row blocks on
  *   v_mfma_f32_16x16x4_f32 for spline bins K <= 16 only; K > 16, one feature per wave:

@@ -127,9 +127,11 @@ def test_fused_steps_bit_identical(N, kw, C):
 
 
 class trunk16:
-    """The wide path's trunk for a block: 16-row tiles with the layer's start merged in and
-    two waves per 32-column tile (3), the same with one wave per tile (2), 16-row tiles after
-    a start launch (1) or 32-row tiles (0)."""
+    """The wide path's trunk for a block: by batch size (5, the default: 4 for small batches,
+    else 3), each 16-row tile's columns split over several workgroups with in-launch hand-offs
+    (4, where the tiles fit half the chip, else 3), 16-row tiles with the layer's start merged
+    in and two waves per 32-column tile (3), the same with one wave per tile (2), 16-row tiles
+    after a start launch (1) or 32-row tiles (0)."""
 
     def __init__(self, on):
         self.on = on
@@ -154,7 +156,7 @@ def test_trunk16_bit_identical_to_trunk32(N, kw, B):
     zb = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
     outs = []
     with wide_rows(16384):
-        for on in (3, 2, 1, 0):
+        for on in (5, 4, 3, 2, 1, 0):
             with trunk16(on):
                 outs.append([m.log_prob(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)])
     with wide_rows(0):
@@ -204,3 +206,39 @@ def test_final32_bit_identical_to_final64(N, kw, B):
     torch.cuda.synchronize()
     for a, b, c, d in zip(*outs):
         assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(a, d)
+
+
+@pytest.mark.parametrize("N,kw,B", [(16, A1, 100), (3, dict(L=3, H=128, nb=2, K=32), 10), (64, A2, 500)],
+                         ids=["a1-n16-100", "n3-h128-10", "a2-n64-500"])
+def test_column_split_trunk_hand_offs_complete(N, kw, B):
+    """The column-split trunk (4): every in-launch hand-off completes (err word 0, no bounded
+    poll gave up) across density and propose passes replayed back to back (the counters are
+    reset per pass and per launch parity), and the results equal the half-tile trunk's (3)."""
+    dims, sd, m = _model(N, kw, seed=9)
+    L = _lib.load()
+    g = torch.Generator().manual_seed(B)
+    x = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
+
+    def run():
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        lq = torch.empty(B, device="cuda")
+        cfg = torch.empty((B, dims.D), device="cuda")
+        cen = torch.empty_like(cfg)
+        lq2 = torch.empty(B, device="cuda")
+        outs = []
+        for rep in range(3):
+            _lib.check(L.fs_flow_log_prob(m.dims(), _lib.ptr(m.packed()), _lib.ptr(x), B, _lib.ptr(lq), None,
+                                          _lib.ptr(err), _lib.stream_ptr()))
+            _lib.check(L.fs_flow_propose_lq(m.dims(), _lib.ptr(m.packed()), B, 99, rep, 0, dims.B, _lib.ptr(cfg),
+                                            _lib.ptr(cen), None, _lib.ptr(lq2), _lib.ptr(err), _lib.stream_ptr()))
+            outs += [lq.clone(), cfg.clone(), lq2.clone()]
+        torch.cuda.synchronize()
+        return int(err.item()), outs
+
+    with wide_rows(16384):
+        with trunk16(4):
+            e4, o4 = run()
+        with trunk16(3):
+            e3, o3 = run()
+    assert e4 == 0 and e3 == 0
+    assert all(torch.equal(a, b) for a, b in zip(o4, o3))
