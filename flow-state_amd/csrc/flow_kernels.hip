@@ -1377,7 +1377,10 @@ __global__ void __launch_bounds__((64 * trunk16s_waves<H, HALF>())) wide_trunk16
 // agent-scope atomic add on the tile's counter; the consumer's lane 0 polls it with sc1
 // loads, a barrier, then every load of the handed-off bytes is an sc1 buffer load.  The poll
 // is bounded: a timeout sets err bit 2 and the workgroup stops waiting, so the grid always
-// drains.  Slices in XG[tile][step & 1][H][16] (column-major: a lane's four rows are one
+// drains.  (The guide's tagged-granule form, each value an 8-byte {value, tag} sc1 store and
+// every consumer thread re-reading its granules until the tags match, ran slower: 4.6-4.7
+// against 4.2-4.3 ms per A1 N=16 pass at 16-64 rows, profiles/r05/r05ah_gsplit_granule.log.)
+// Slices in XG[tile][step & 1][H][16] (column-major: a lane's four rows are one
 // 16-byte store); counters CNT[launch & 1][tile], the other parity reset here for the next
 // launch (the input kernel resets both).  Only workgroup 0 of a tile writes the start's
 // side outputs (LDW, LDU, CO), the coordinates after the first hand-off, when every
