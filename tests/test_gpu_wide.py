@@ -242,3 +242,41 @@ def test_column_split_trunk_hand_offs_complete(N, kw, B):
             e3, o3 = run()
     assert e4 == 0 and e3 == 0
     assert all(torch.equal(a, b) for a, b in zip(o4, o3))
+
+
+def test_column_split_hand_offs_under_uneven_load():
+    """The column-split trunk's hand-offs while a large fused pass (A1, N=64, 32768 rows,
+    ~40 ms) runs on another stream, so the tile's workgroups start and run at uneven times
+    (the guide's advice: test hand-offs under uneven load): every hand-off completes (err 0)
+    and the results equal the half-tile trunk's, over repeated small passes."""
+    dims, sd, m = _model(16, A1, seed=13)
+    dbig, sdb, mb = _model(64, A1, seed=14)
+    L = _lib.load()
+    B = 48
+    g = torch.Generator().manual_seed(5)
+    x = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
+    xb = ((torch.rand((32768, dbig.D), generator=g) * 2 - 1) * dbig.B).cuda()
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    def small(mode, reps):
+        out = []
+        with trunk16(mode):
+            for _ in range(reps):
+                lq = torch.empty(B, device="cuda")
+                _lib.check(L.fs_flow_log_prob(m.dims(), _lib.ptr(m.packed()), _lib.ptr(x), B, _lib.ptr(lq), None,
+                                              _lib.ptr(err), _lib.stream_ptr()))
+                out.append(lq)
+        return out
+
+    with wide_rows(16384):
+        ref = small(3, 1)[0].clone()
+        side = torch.cuda.Stream()
+        mb.packed()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                mb.log_prob(xb)
+        got = small(4, 12)
+        torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert all(torch.equal(t, ref) for t in got)
