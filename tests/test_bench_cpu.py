@@ -17,6 +17,18 @@ def _bench(args, env_extra, drop=()):
                           text=True, timeout=240)
 
 
+def test_algorithm1_regime_cpu_sample_is_bounded():
+    """The regime leg's CPU sample (oracle C local moves + torch-CPU log_prob) runs at
+    least one attempt, stops near its budget and reports itself as a port."""
+    import time
+    import bench
+    t0 = time.perf_counter()
+    r = bench.algorithm1_regime_cpu(N=3, interval=50, budget_s=0.3)
+    assert time.perf_counter() - t0 < 30
+    assert r["value"] > 0 and r["kind"] == "port" and r["unit"] == "big-move attempts/s"
+    assert r["cores"] >= 1 and "attempts of one run" in r["sample"]
+
+
 def test_world_size_must_match_gpus():
     r = _bench(["--gpus", "2"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2, r.stderr[-2000:]
