@@ -196,9 +196,12 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
     constexpr int RPL = LPC >= 4 ? 1 : 4 / LPC;
     int64_t samp = 0;
     unsigned long long n_acc_local = 0;
+    // (step0 + t + 1) mod adjust_every / sample_every, carried as counters: one 64-bit
+    // remainder per launch instead of one per move
+    int ra = a.adjust_every > 0 ? (int)((a.step0 + 1) % a.adjust_every) : 1;
+    int rsm = a.sample_every > 0 ? (int)((a.step0 + 1) % a.sample_every) : 1;
 
     for (int64_t t = 0; t < a.n_moves; ++t) {
-        const int64_t step = a.step0 + t + 1;
         att += 1;
         const int p = (int)pcg64_integers(rng, (uint32_t)N);
         const int pq = p / LPC, pl = p % LPC;
@@ -350,8 +353,11 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
             }
         }
         if (a.accept_log && gl == 0) a.accept_log[c * a.n_moves + t] = accept ? 1 : 0;
-        if (a.adjust_every > 0 && step % a.adjust_every == 0) adjust_md(md, att, acc_n, prev_att, prev_acc, a.target);
-        if (a.sample_every > 0 && step % a.sample_every == 0 && samp < a.n_samp) {
+        if (a.adjust_every > 0 && ra == 0) adjust_md(md, att, acc_n, prev_att, prev_acc, a.target);
+        const bool take = a.sample_every > 0 && rsm == 0;
+        if (a.adjust_every > 0) ra = ra + 1 == a.adjust_every ? 0 : ra + 1;
+        if (a.sample_every > 0) rsm = rsm + 1 == a.sample_every ? 0 : rsm + 1;
+        if (take && samp < a.n_samp) {
             if (a.samples_xy) {
 #pragma unroll
                 for (int q = 0; q < PPL; ++q) {
@@ -423,7 +429,10 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
     // N = 3 (the reference's Algorithm-1 runs), 1000 moves: 10 chains 8x1 2.47 ms, 4x1 2.29,
     // 2x4 3.94, 1x4 5.80 (the double-well and sum work, serial in fewer lanes, outweighs the
     // shuffles it saves); 65536 chains 8x1 10.2 ms, 4x1 5.71, 2x4 5.28, 1x4 5.52
-    // (profiles/r05/r05m_local_layouts.log).
+    // (profiles/r05/r05m_local_layouts.log).  Chains stay packed 64 / LPC per wave even when
+    // that leaves SIMDs idle: spreading 10 or 256 chains one per wave (one wave per CU or four)
+    // was 1.1-2.3x slower than one packed wave, though a packed wave runs the union of its
+    // chains' branches (profiles/r05/r05ap_cpw_sweep.log, r05aq_wpb_sweep.log).
     int lpc = N > 32 ? 8 : N > 8 ? 4 : 8;
     int ppl = N > 32 ? 8 : N > 16 ? 8 : N > 8 ? 4 : 1;
     if (N <= 4) {

@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sample-every", type=int, default=0, help="sample() snapshots every k moves")
+    ap.add_argument("--f32-chains", type=int, default=0, help="the first k chains hold float32 states")
     args = ap.parse_args()
     N, C = args.particles, args.chains
     base, box = initialise_fcc(num_particles=N, rho=0.03, aspect_ratio=1.0)
@@ -57,16 +59,22 @@ def main():
     rng = np.random.default_rng(7)
     init = np.mod(base[None] + rng.normal(0, 0.05, (C, N, 2)), L)
     seeds = np.arange(42, 42 + C, dtype=np.uint64)
+    if args.f32_chains:
+        init[:args.f32_chains] = init[:args.f32_chains].astype(np.float32)
     b = BatchedMonteCarlo(None, init, Physics(L, L), seeds, initial_max_displacement=0.65)
+    if args.f32_chains:
+        b.state_is_f32[:args.f32_chains] = 1
+        b.E_old, b.W_old = b._energy_of_state()
+    kw = {"sample_every": args.sample_every} if args.sample_every else {}
     for _ in range(args.warmup):
-        b.local_moves(args.moves)
+        b.local_moves(args.moves, **kw)
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     a0 = b.accepted.sum().item()
     t0 = time.perf_counter()
     for e0, e1 in evs:
         e0.record()
-        b.local_moves(args.moves)
+        b.local_moves(args.moves, **kw)
         e1.record()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -77,7 +85,8 @@ def main():
         "value": n_moves / dt, "unit": "moves/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3, "kernel_ms_per_launch": k_ms, "higher_is_better": True,
         "dtype": "f64", "data": "synthetic (FCC + jitter, float64 states)",
-        "config": {"workload": f"{C} chains x {args.moves} local moves per launch, N={N}"},
+        "config": {"workload": f"{C} chains x {args.moves} local moves per launch, N={N}",
+                   "sample_every": args.sample_every, "f32_chains": args.f32_chains},
         "pair_evals_per_s": n_moves * 2 * (N - 1) / dt,
         "acceptance_rate": (b.accepted.sum().item() - a0) / n_moves,
     }
