@@ -455,6 +455,7 @@ int fs_rqs_backward(int64_t M, int32_t K, int32_t inverse, const float *x, const
 int64_t fs_set_wide_rows(int64_t rows) { return fs_set_wide_rows_impl(rows); }
 int32_t fs_set_wide_trunk16(int32_t on) { return fs_set_wide_trunk16_impl(on); }
 int32_t fs_set_wide_final32(int32_t on) { return fs_set_wide_final32_impl(on); }
+int64_t fs_set_wide_handoff_spins(int64_t spins) { return fs_set_wide_handoff_spins_impl(spins); }
 int32_t fs_set_coupling_waves(int32_t on) { return fs_set_coupling_waves_impl(on); }
 int32_t fs_set_lean_gemm(int32_t on) { return fs_set_lean_gemm_impl(on); }
 

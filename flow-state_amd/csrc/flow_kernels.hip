@@ -756,6 +756,8 @@ struct WideArgs {
     float *XG;     // (column-split trunk) [R / 16][2][H][16] handed-off column slices
     unsigned *CNT;  // [2][R / 16] hand-off counters (launch parity x tile)
     int T;          // R / 16
+    unsigned spin;  // (column-split trunk) polls before a hand-off wait gives up; 0: give up at
+                    // once (the timeout test hook, fs_set_wide_handoff_spins)
 };
 
 template <int MODE>
@@ -1394,7 +1396,7 @@ __global__ void __launch_bounds__((64 * trunk16s_waves<H, HALF>())) wide_trunk16
                               // the half-tile trunk, 512 rows 6.3-6.5 against 5.3;
                               // profiles/r05/r05af_gsplit.log)
 #endif
-constexpr unsigned kGSpinMax = 1u << 20;  // polls (sc1 load + s_sleep) before a hand-off gives up
+constexpr unsigned kGSpinMax = 1u << 20;  // default polls (sc1 load + s_sleep) before a hand-off gives up
 
 template <int H>
 constexpr bool gsplit_ok() {
@@ -1513,9 +1515,9 @@ __global__ void __launch_bounds__(64 * (2 * (H / 32) / G)) wide_trunk16g_kernel(
             if (!dead_s) {
                 const unsigned target = (unsigned)(G * (step + 1));
                 unsigned spins = 0;
-                while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                while (w.spin == 0 || __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                     __builtin_amdgcn_s_sleep(1);
-                    if (++spins > kGSpinMax) {
+                    if (++spins > w.spin) {
                         dead_s = 1;
                         if (a.err) atomicOr(a.err, 4);
                         break;
@@ -2065,6 +2067,7 @@ static int device_cus() {
 // tile (2), on 16-row tiles after a separate start launch (1) or on 32-row ones (0);
 // FS_WIDE_TRUNK16, fs_set_wide_trunk16.  Bit-identical in every setting.
 static std::atomic<int> g_trunk16{-1};
+static std::atomic<unsigned> g_gspin{kGSpinMax};
 static int wide_trunk16() {
     int v = g_trunk16.load(std::memory_order_relaxed);
     if (v < 0) {
@@ -2250,6 +2253,7 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     p += rup(R * 2 * H * 4, 256);
     w.CNT = (unsigned *)p;
     w.T = (int)(R / 16);
+    w.spin = g_gspin.load(std::memory_order_relaxed);
     w.pending = 0;
     const unsigned nblk = (unsigned)(R / kRows);
 #ifndef FS_WIDE_WPW
@@ -2272,8 +2276,10 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
     // 5 (default): the column-split trunk (4) for the A1 trunk (H = 256, 64 GEMMs per layer) on
     // batches of at most FS_GSPLIT_AUTO_WG / FS_GSPLIT tiles, else two waves per column tile (3).
     // 4 forces it wherever the tiles x FS_GSPLIT fit half the chip.
+    // The column-split trunk reports a hand-off that gave up waiting only through err
+    // (|= 4, its output is then wrong): without an err word to report it in, never take it.
     int trunk16 = R / 16 <= device_cus() ? wide_trunk16() : 0;
-    const bool gfit = gsplit_ok<H>() && a.nb > 0 && (R / 16) * FS_GSPLIT <= device_cus() / 2;
+    const bool gfit = gsplit_ok<H>() && a.nb > 0 && a.err && (R / 16) * FS_GSPLIT <= device_cus() / 2;
     if (trunk16 == 5) trunk16 = (gfit && H >= 256 && (R / 16) * FS_GSPLIT <= FS_GSPLIT_AUTO_WG) ? 4 : 3;
     if (trunk16 == 4 && !gfit) trunk16 = 3;
     // 16- or 32-row final-phase blocks (feature pairs) while the grid fits the chip in a round;
@@ -2348,6 +2354,12 @@ using namespace fs;
 int32_t fs_set_wide_trunk16_impl(int32_t on) {
     const int32_t prev = wide_trunk16();
     if (on >= 0) g_trunk16.store(on > 5 ? 5 : on, std::memory_order_relaxed);
+    return prev;
+}
+
+int64_t fs_set_wide_handoff_spins_impl(int64_t spins) {
+    const int64_t prev = g_gspin.load(std::memory_order_relaxed);
+    if (spins >= 0) g_gspin.store(spins > 0xffffffffll ? 0xffffffffu : (unsigned)spins, std::memory_order_relaxed);
     return prev;
 }
 

@@ -61,6 +61,7 @@ hipError_t fs_rqs_backward_impl(int64_t M, int K, int inverse, const float *x, c
 int64_t fs_set_wide_rows_impl(int64_t rows);
 int32_t fs_set_wide_trunk16_impl(int32_t on);
 int32_t fs_set_wide_final32_impl(int32_t on);
+int64_t fs_set_wide_handoff_spins_impl(int64_t spins);
 int32_t fs_set_coupling_waves_impl(int32_t on);
 int32_t fs_set_lean_gemm_impl(int32_t on);
 hipError_t fs_target_energy_impl(const float *x, int64_t B, int N, double bound, double temperature, int num_wells,

@@ -461,7 +461,7 @@ class BatchedMonteCarlo:
         cfg = cfg.reshape(-1, self.N, 2).contiguous()
         self._need_model()
         E, W, _ = total_energy(cfg, self.phys.c)
-        lq = self.model.log_prob(self._centered_f32(cfg.to(torch.float64)))
+        lq = self.model._log_prob(self._centered_f32(cfg.to(torch.float64)), self.err)
         return E, W, lq
 
     @_on_own_device
@@ -484,11 +484,11 @@ class BatchedMonteCarlo:
         self._need_model()
         stale = self._moved
         if stale:  # old NLL of the current state (monte_carlo.py:251-261); energy for a reject (:299-301)
-            self.nll_old = -(self.model.log_prob(self._centered_f32(self.state)).to(torch.float64))
+            self.nll_old = -(self.model._log_prob(self._centered_f32(self.state), self.err).to(torch.float64))
             E_cur, W_cur = self._energy_of_state()
         if terms is None:
             E_new, W_new, _ = total_energy(cfg if cfg64 is None else cfg64, self.phys.c)
-            lq = self.model.log_prob(self._centered_f32(cfg.to(torch.float64) if cfg64 is None else cfg64))
+            lq = self.model._log_prob(self._centered_f32(cfg.to(torch.float64) if cfg64 is None else cfg64), self.err)
         else:
             E_new, W_new, lq = terms
             for t, dt in ((E_new, torch.float64), (W_new, torch.float64), (lq, torch.float32)):

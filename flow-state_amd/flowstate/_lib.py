@@ -142,6 +142,7 @@ _SIGS = {
     "fs_set_wide_rows": (_I64, [_I64]),
     "fs_set_wide_trunk16": (ctypes.c_int32, [ctypes.c_int32]),
     "fs_set_wide_final32": (ctypes.c_int32, [ctypes.c_int32]),
+    "fs_set_wide_handoff_spins": (_I64, [_I64]),
     "fs_set_coupling_waves": (ctypes.c_int32, [ctypes.c_int32]),
     "fs_set_lean_gemm": (ctypes.c_int32, [ctypes.c_int32]),
     "fs_kld_loss": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _P, _P, _P, _P]),

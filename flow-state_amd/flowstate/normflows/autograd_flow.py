@@ -224,9 +224,16 @@ class _CircularRQS(torch.autograd.Function):
 
 
 def circular_rqs(x, uw, uh, ud, B, inverse):
-    """Dispatch: the fused HIP spline for device tensors (K instantiated), the torch
-    restatement below otherwise (CPU tensors in tests and host-side use)."""
-    if x.is_cuda and uw.shape[-1] in _HIP_K:
+    """Dispatch: the fused HIP spline for device tensors, the torch restatement below for
+    CPU tensors (tests and host-side use).  A device tensor with a bin count K the HIP
+    spline does not instantiate raises (DESIGN.md 'The path and its boundary': unsupported
+    options raise instead of computing something else)."""
+    if x.is_cuda:
+        if uw.shape[-1] not in _HIP_K:
+            from .. import _lib
+
+            raise _lib.FlowStateError(f"the HIP spline is instantiated for K in {sorted(_HIP_K)}, "
+                                      f"not K={uw.shape[-1]}")
         shp = x.shape
         K = uw.shape[-1]
         out, lad = _CircularRQS.apply(x.reshape(-1), uw.reshape(-1, K), uh.reshape(-1, K), ud.reshape(-1, K + 1),
@@ -1181,7 +1188,9 @@ class _FinalSplines(torch.autograd.Function):
         nws = sum(max(0, L.fs_linear_f32_splitk_floats(d)) for d in descs)
         ws = torch.empty((max(nws, 1),), dtype=torch.float32, device=x.device)
         arr = (ctypes.POINTER(_lib.GemmF32) * 3)(*[ctypes.pointer(d) for d in descs])
-        if ctx.defer:
+        # re-checked now: a retain_grad() or tensor hook registered on h after the forward
+        # would otherwise receive the unreduced placeholder
+        if ctx.defer and not (h.retains_grad or getattr(h, "_backward_hooks", None)):
             # dh's partials left for its readers (_sk_get): the reduction launch goes
             ch = ctypes.c_int32(1)
             _lib.check(L.fs_linear_f32_group_partial(arr, 3, p(ws), nws, 3, ctypes.byref(ch), _lib.stream_ptr()),

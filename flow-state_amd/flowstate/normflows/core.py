@@ -134,22 +134,40 @@ def _prepare_input(x, D):
 
 
 def _raise_on_nan(err):
-    v = int(err.item())
-    if v & 4:  # (not the reference's: a wide-path column hand-off gave up waiting)
-        raise _lib.FlowStateError("a wide-path trunk hand-off timed out")
-    if v & 1:
+    if int(err.item()) & 1:
         raise ValueError("Discriminant computation resulted in NaN.")  # splines.py:176-183
 
 
-def _run_stack(layers, x, direction, cache=None, base_log_prob=None):
+# A pass of at most this many rows may run its A1 trunk on the column-split kernel, whose
+# in-launch hand-offs report a wait that gave up as err |= 4 (fs_set_wide_trunk16).
+_GSPLIT_MAX_ROWS = 256
+
+
+def _run_stack(layers, x, direction, cache=None, base_log_prob=None, err=None):
     """Run the coupling stack in one launch.  direction: 'forward' (sampling,
     layers 0..L-1) or 'inverse' (density, layers L-1..0).  Returns (out, log_det).
-    Runs on x's device (its current stream); the parameters must live there too."""
+    Runs on x's device (its current stream); the parameters must live there too.
+    err: the caller's sticky device int32 error word (density direction only), checked by
+    the caller later (BatchedMonteCarlo.check_errors); without it the pass checks its own."""
     with _lib.on_device(x):
-        return _run_stack_here(layers, x, direction, cache, base_log_prob)
+        return _run_stack_here(layers, x, direction, cache, base_log_prob, err)
 
 
-def _run_stack_here(layers, x, direction, cache, base_log_prob):
+def _launch_stack(L, dims, packed, x, B, out, ld, err, direction, base_log_prob):
+    st = _lib.stream_ptr()
+    e = None if err is None else _lib.ptr(err)
+    if direction == "forward":
+        _lib.check(L.fs_flow_forward(dims, _lib.ptr(packed), _lib.ptr(x), B, _lib.ptr(out), _lib.ptr(ld), e, st),
+                   "fs_flow_forward")
+    elif base_log_prob:
+        _lib.check(L.fs_flow_log_prob(dims, _lib.ptr(packed), _lib.ptr(x), B, _lib.ptr(ld), _lib.ptr(out), e, st),
+                   "fs_flow_log_prob")
+    else:
+        _lib.check(L.fs_flow_inverse(dims, _lib.ptr(packed), _lib.ptr(x), B, _lib.ptr(out), _lib.ptr(ld), e, st),
+                   "fs_flow_inverse")
+
+
+def _run_stack_here(layers, x, direction, cache, base_log_prob, err=None):
     _check_stack(layers)
     cache = cache or getattr(layers[0], "_fs_cache", None)
     if cache is None:
@@ -163,19 +181,28 @@ def _run_stack_here(layers, x, direction, cache, base_log_prob):
     B = x.shape[0]
     out = torch.empty_like(x)
     ld = torch.empty(B, dtype=torch.float32, device=x.device)
-    err = torch.zeros(1, dtype=torch.int32, device=x.device)
     L = _lib.load()
-    st = _lib.stream_ptr()
+    if err is not None:
+        if direction == "forward":
+            raise ValueError("a sticky err word is for the density direction")
+        _launch_stack(L, dims, packed, x, B, out, ld, err, direction, base_log_prob)
+        return out, ld
+    own = torch.zeros(1, dtype=torch.int32, device=x.device)
+    _launch_stack(L, dims, packed, x, B, out, ld, own, direction, base_log_prob)
     if direction == "forward":
-        _lib.check(L.fs_flow_forward(dims, _lib.ptr(packed), _lib.ptr(x), B, _lib.ptr(out), _lib.ptr(ld),
-                                     _lib.ptr(err), st), "fs_flow_forward")
-        _raise_on_nan(err)
-    elif base_log_prob:
-        _lib.check(L.fs_flow_log_prob(dims, _lib.ptr(packed), _lib.ptr(x), B, _lib.ptr(ld), _lib.ptr(out),
-                                      _lib.ptr(err), st), "fs_flow_log_prob")
-    else:
-        _lib.check(L.fs_flow_inverse(dims, _lib.ptr(packed), _lib.ptr(x), B, _lib.ptr(out), _lib.ptr(ld),
-                                     _lib.ptr(err), st), "fs_flow_inverse")
+        if int(own.item()) & 4:  # a column-split hand-off gave up: the same pass on trunk 3
+            own.zero_()
+            prev = L.fs_set_wide_trunk16(3)
+            try:
+                _launch_stack(L, dims, packed, x, B, out, ld, own, direction, base_log_prob)
+            finally:
+                L.fs_set_wide_trunk16(prev)
+        _raise_on_nan(own)
+    elif B <= _GSPLIT_MAX_ROWS and int(own.item()) & 4:
+        # (no NaN check in this direction: the density pass solves no root) a column-split
+        # hand-off gave up waiting, so these outputs are wrong: re-run without an err word,
+        # which never takes the column-split trunk (bit-identical results)
+        _launch_stack(L, dims, packed, x, B, out, ld, None, direction, base_log_prob)
     return out, ld
 
 
@@ -253,8 +280,14 @@ class NormalizingFlow(nn.Module):
     @torch.no_grad()
     def log_prob(self, x):
         """core.py:198-214: sum of layer log-dets + UniformParticle.log_prob, in x.dtype."""
+        return self._log_prob(x)
+
+    @torch.no_grad()
+    def _log_prob(self, x, err=None):
+        """log_prob; err: the caller's sticky device int32 error word (a column-split
+        hand-off timeout is then reported there, |= 4, instead of re-run here)."""
         self._base_check()
-        _, lq = _run_stack(self._layers(), x, "inverse", self._cache, base_log_prob=True)
+        _, lq = _run_stack(self._layers(), x, "inverse", self._cache, base_log_prob=True, err=err)
         return lq.to(x.dtype)
 
     @torch.no_grad()

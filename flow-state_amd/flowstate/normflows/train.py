@@ -351,11 +351,13 @@ class GraphedTrainStep:
     def step(self, batch, check=True):
         """One training step on `batch` (B, D); returns the loss tensor (device scalar).
         A batch size without a captured graph runs eagerly with the same optimizer.
-        check=False: no host synchronisation for the spline's NaN flag; the step returns
-        (loss, nan_flag) instead, both device tensors owned by the caller, and the caller
-        raises (an epoch checks all its steps' flags at once, Algorithm2.train).  The
-        sticky word is not cleared then: after a NaN step every later replay writes nothing
-        until reset_nan()."""
+        check=False: no host synchronisation for the spline's NaN flag on a graphed batch
+        size; the step returns (loss, nan_flag) instead, both device tensors owned by the
+        caller, and the caller raises (an epoch checks all its steps' flags at once,
+        Algorithm2.train).  The sticky word is not cleared then: after a NaN step every
+        later replay writes nothing until reset_nan().  An ungraphed (eager) batch size
+        synchronises either way: the eager step tests the loss on the host (the reference's
+        skip of a non-finite loss) and reads the sticky word before it runs."""
         c = self.graphs.get(int(batch.shape[0]))
         if c is None:
             if not check and bool(self.nan_state()):

@@ -100,7 +100,8 @@ int fs_flow_pack(const fs_flow_dims *d, const float *raw, void *packed, void *st
  * wrapper.py:273-275, coupling.py:71-102) + UniformParticle.log_prob
  * (Energy/Uniform.py:50-74).  x, z_out: [B][2N] float32 (z_out nullable);
  * log_q: [B].  err (nullable, device int32): bit0 set on a NaN discriminant (|= 4: a
- * wide-path trunk hand-off timed out, fs_set_wide_trunk16). */
+ * wide-path trunk hand-off timed out and the outputs are wrong; the pass can then be re-run
+ * with err = NULL, which never takes the column-split trunk, fs_set_wide_trunk16). */
 int fs_flow_log_prob(const fs_flow_dims *d, const void *packed, const float *x, int64_t B,
                      float *log_q, float *z_out, int32_t *err, void *stream);
 
@@ -291,6 +292,11 @@ int64_t fs_set_wide_rows(int64_t rows);
  *   16- or 32-row blocks when that grid fits the chip in one round (16-row blocks on
  *   v_mfma_f32_16x16x4_f32 for spline bins K <= 16 only; K > 16, one feature per wave:
  *   32-row blocks), 1 = 32-row blocks at most, 0 = always 64-row blocks.
+ * fs_set_wide_handoff_spins: polls (an sc1 load and an s_sleep each) a column-split trunk
+ *   workgroup makes before a hand-off wait gives up (err |= 4; default 2^20); 0 makes every
+ *   wait give up at once, the hook the timeout tests use.  Returns the previous value; a
+ *   negative argument only reads it.  The column-split trunk runs only when the pass has an
+ *   err word to report a timeout in (err == NULL: trunk 3 instead).
  * fs_set_coupling_waves: 1 (default, or FS_COUPLING_WAVES) = the training step's coupling
  *   launches (fs_coupling_pair_step, fs_coupling_bwd_step) with each row's splines spread
  *   over two / four waves (one knot set per wave), 0 = one / two waves per row.
@@ -298,6 +304,7 @@ int64_t fs_set_wide_rows(int64_t rows);
  *   kernels (32-bit buffer offsets), 0 = the generic strided kernels. */
 int32_t fs_set_wide_trunk16(int32_t on);
 int32_t fs_set_wide_final32(int32_t on);
+int64_t fs_set_wide_handoff_spins(int64_t spins);
 int32_t fs_set_coupling_waves(int32_t on);
 int32_t fs_set_lean_gemm(int32_t on);
 

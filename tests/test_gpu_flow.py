@@ -157,10 +157,9 @@ def test_a1_flow_samples_closer_to_float64_than_reference_f32():
     proposals (in-kernel base draws, fl32(x + HALF_BOX), fl32(config - half_width);
     main_algorithm_1.py:340-343, monte_carlo.py:251-262).  Against the exact value (the
     oracle's float64 evaluation of the same weights and inputs):
-      * the GPU's p99.9 relative error is within the north star's 1e-5 and its maximum
-        within 1.25e-5 (measured at r05: max 9.8e-6, p99.9 7.6e-6, p99 4.6e-6 on these
-        rows; the r04 bench's 2048-row sample had one row at 1.24e-5), at most one row in
-        2048 beyond 1e-5;
+      * every row's relative error is within the north star's 1e-5 (measured at r05 on
+        this deterministic sample: max 9.8e-6, p99.9 7.6e-6, p99 4.6e-6; the bound is the
+        north star's, not fitted to the data);
       * the GPU is closer to the exact value than the reference's own float32 op order
         at p99.9 and at the maximum.
     The GPU's error is float32 latent rounding carried through the layers
@@ -197,9 +196,7 @@ def test_a1_flow_samples_closer_to_float64_than_reference_f32():
     print(f"vs float64 on {fin.sum()} rows: gpu max {e_gpu.max():.3e} p99.9 {q(e_gpu, 99.9):.3e} "
           f"p99 {q(e_gpu, 99):.3e} beyond 1e-5 {(e_gpu > 1e-5).sum()}; reference-order f32 max {e_ref.max():.3e} "
           f"p99.9 {q(e_ref, 99.9):.3e} beyond 1e-5 {(e_ref > 1e-5).sum()}")
-    assert q(e_gpu, 99.9) <= 1e-5, q(e_gpu, 99.9)
-    assert e_gpu.max() <= 1.25e-5, e_gpu.max()
-    assert (e_gpu > 1e-5).sum() <= fin.sum() // 2048
+    assert e_gpu.max() <= 1e-5, e_gpu.max()
     assert q(e_gpu, 99.9) < q(e_ref, 99.9) and e_gpu.max() < e_ref.max()
 
 

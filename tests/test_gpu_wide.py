@@ -280,3 +280,66 @@ def test_column_split_hand_offs_under_uneven_load():
         torch.cuda.synchronize()
     assert int(err.item()) == 0
     assert all(torch.equal(t, ref) for t in got)
+
+
+class handoff_spins:
+    """The column-split trunk's poll budget for a block (0: every hand-off wait gives up at
+    once, the timeout hook)."""
+
+    def __init__(self, spins):
+        self.spins = spins
+
+    def __enter__(self):
+        self.prev = _lib.load().fs_set_wide_handoff_spins(self.spins)
+
+    def __exit__(self, *exc):
+        _lib.load().fs_set_wide_handoff_spins(self.prev)
+
+
+def test_column_split_timeout_reported_and_recovered():
+    """A column-split hand-off that gives up waiting (forced: fs_set_wide_handoff_spins(0))
+    leaves wrong outputs and err |= 4.  It can never pass unnoticed: the public
+    passes (log_prob, inverse, forward) see the bit and re-run on the half-tile trunk, so
+    they return the correct values; the MCMC engine's passes report it in its sticky err
+    word, so check_errors() raises; and a pass given no err word never takes the
+    column-split trunk at all."""
+    N, B = 16, 100
+    dims, sd, m = _model(N, A1, seed=9)
+    L = _lib.load()
+    g = torch.Generator().manual_seed(2)
+    x = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
+    zb = ((torch.rand((B, dims.D), generator=g) * 2 - 1) * dims.B).cuda()
+    with wide_rows(16384):
+        with trunk16(3):
+            want = [m.log_prob(x).clone(), m.inverse(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)]
+        with trunk16(4), handoff_spins(0):
+            # the hook fires: the raw pass reports the timeout
+            err = torch.zeros(1, dtype=torch.int32, device="cuda")
+            lq = torch.empty(B, device="cuda")
+            _lib.check(L.fs_flow_log_prob(m.dims(), _lib.ptr(m.packed()), _lib.ptr(x), B, _lib.ptr(lq), None,
+                                          _lib.ptr(err), _lib.stream_ptr()))
+            assert int(err.item()) & 4
+            # no err word: the half-tile trunk, correct values
+            lq0 = torch.empty(B, device="cuda")
+            _lib.check(L.fs_flow_log_prob(m.dims(), _lib.ptr(m.packed()), _lib.ptr(x), B, _lib.ptr(lq0), None,
+                                          None, _lib.stream_ptr()))
+            assert torch.equal(lq0, want[0])
+            # the public passes recover
+            got = [m.log_prob(x).clone(), m.inverse(x).clone()] + [t.clone() for t in m.forward_and_log_det(zb)]
+            for a, b in zip(got, want):
+                assert torch.equal(a, b)
+            # the engine's sticky word: a density pass of its own (stale NLL) and the fused step
+            Lb = float(np.sqrt(N / 0.03))
+            init = np.mod(OP.fcc_lattice(N)[None] + np.random.default_rng(1).normal(0, 0.05, (64, N, 2)), Lb)
+            bmc = BatchedMonteCarlo(m, init, Physics(Lb), np.arange(42, 42 + 64, dtype=np.uint64))
+            bmc.check_errors()  # construction's NLL pass went through the public path
+            bmc.invalidate_nll()
+            bmc.nf_big_move(torch.from_numpy(init.astype(np.float32)).cuda())
+            with pytest.raises(_lib.FlowStateError, match="hand-off"):
+                bmc.check_errors()
+            bmc2 = BatchedMonteCarlo(m, init, Physics(Lb), np.arange(42, 42 + 64, dtype=np.uint64))
+            bmc2.MAX_STEPS_PER_LAUNCH = 1
+            bmc2.step()
+            with pytest.raises(_lib.FlowStateError, match="hand-off"):
+                bmc2.check_errors()
+    assert L.fs_set_wide_handoff_spins(-1) == 1 << 20

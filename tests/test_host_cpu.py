@@ -204,3 +204,20 @@ def test_pack_cache_tracks_versions_and_structure():
     bn = layers[0].prqct.transform_net.blocks[0].batch_norm_layers[0]
     bn.running_mean = torch.zeros_like(bn.running_mean)
     assert any(t is bn.running_mean for t in cache._tensor_list(layers))
+
+
+def test_device_spline_with_uninstantiated_bins_raises():
+    """circular_rqs on a device tensor with a bin count the HIP spline does not instantiate
+    raises instead of falling back to torch ops on the device (no silent
+    fallback); CPU tensors take the torch restatement."""
+    from flowstate.normflows import autograd_flow as AF
+
+    class FakeDevice:  # stands for a device tensor (no GPU here): only is_cuda is read
+        is_cuda = True
+
+    uw, ud = torch.zeros(4, 10), torch.zeros(4, 11)
+    with pytest.raises(_lib.FlowStateError, match="K=10"):
+        AF.circular_rqs(FakeDevice(), uw, uw, ud, 3.0, False)
+    x = torch.linspace(-2.0, 2.0, 4)
+    out, lad = AF.circular_rqs(x, uw, uw, ud, 3.0, False)
+    assert out.shape == x.shape and torch.isfinite(lad).all()
