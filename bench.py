@@ -346,16 +346,19 @@ def algorithm1_regime(attempts=1000, runs=10, N=3, interval=1000, sampling=150, 
                     "equilibration and proposal generation untimed"}
 
 
-def algorithm1_regime_cpu(N=3, interval=1000, budget_s=8.0):
-    """A bounded CPU sample of algorithm1_regime's testing phase (oracle/, test
-    infrastructure): one run (low-left start, seed 42) at a time, as the reference's driver
-    runs them, each attempt `interval` particle_displacement calls by the oracle's C
-    restatement of monte_carlo.py:146-223 (faster than the reference's numpy-per-move loop,
-    so the ratio to the GPU is understated), then nf_big_move: batch-1 float32 log_prob of
-    the current and the proposed configuration in torch-CPU (the reference's op sequence),
-    the proposal's energy and the PCG64 accept (monte_carlo.py:235-303).  Proposals
-    generated beforehand, untimed, as on the GPU; sample() snapshots (a copy every 150
-    moves) left out."""
+def algorithm1_regime_cpu(N=3, interval=1000, budget_s=8.0, sample_every=150):
+    """A bounded CPU sample of algorithm1_regime's testing phase, timed as the reference
+    runs it (oracle/, test infrastructure): one run (low-left start, seed 42) at a time, as
+    the reference's driver runs them (main_algorithm_1.py:378-395), each attempt `interval`
+    particle_displacement calls in the reference's per-call numpy form
+    (oracle.physics.NumpyLocalChain: monte_carlo.py:146-223 over
+    energy_calculator.py:48-119, a Python loop of minimum_image + np.linalg.norm per pair,
+    numpy's own Generator; bit-identical to the reference's local-move traces,
+    tests/test_oracle_local.py) with sample() every `sample_every` moves, then nf_big_move
+    (monte_carlo.py:235-303): batch-1 float32 log_prob of the current and the proposed
+    configuration in torch-CPU (the reference's op sequence), the proposal's energy by the
+    reference's pair loop and the accept.  Proposals generated beforehand, untimed, as on
+    the GPU."""
     from oracle import flow as OF
     from oracle import physics as OP
     from flowstate.MCMC import initialise_low_left
@@ -366,22 +369,25 @@ def algorithm1_regime_cpu(N=3, interval=1000, budget_s=8.0):
     g = torch.Generator().manual_seed(77)
     z = (torch.rand((64, dims.D), generator=g) * 2 - 1) * dims.B
     props = (OF.sample_from(sd, z, dims).numpy() + hw).astype(np.float32).reshape(-1, N, 2)
-    ch = OP.LocalChain(initialise_low_left(N, 0.03, 1.0)[0], 42, OP.make_phys(N), max_disp=0.65)
+    ch = OP.NumpyLocalChain(initialise_low_left(N, 0.03, 1.0)[0], 42, OP.make_phys(N), max_disp=0.65)
+    hw2 = np.array([ch.Lx / 2, ch.Lx / 2])
     threads = torch.get_num_threads()
     t0 = time.perf_counter()
     n = 0
     while time.perf_counter() - t0 < budget_s or n == 0:
-        ch.local_moves(interval)
+        ch.local_moves(interval, sample_every=sample_every)
         cfg = props[n % len(props)]
-        old = torch.tensor((ch.particles - hw).reshape(1, -1), dtype=torch.float)
-        new = torch.tensor((cfg - hw).reshape(1, -1), dtype=torch.float)
+        old = torch.tensor((ch.particles - hw2).reshape(1, -1), dtype=torch.float)
+        new = torch.tensor((cfg - hw2).reshape(1, -1), dtype=torch.float)
         ch.big_move(cfg, -OF.log_prob(sd, old, dims).item(), -OF.log_prob(sd, new, dims).item())
         n += 1
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "big-move attempts/s", "kind": "port", "cores": threads,
-            "sample": f"{n} attempts of one run ({interval} local moves + 1 NF big move each, A1 flow, N={N}), "
-                      f"{dt:.1f} s wall; local moves by the oracle's single-threaded C restatement, log_prob "
-                      f"by the reference's torch-CPU float32 op sequence at batch 1 on {threads} threads"}
+            "sample": f"{n} attempts of one run ({interval} local moves + 1 NF big move each, sample() every "
+                      f"{sample_every}, A1 flow, N={N}), {dt:.1f} s wall; local moves in the reference's per-call "
+                      f"numpy form (oracle.physics.NumpyLocalChain: per-pair minimum_image + np.linalg.norm loop, "
+                      f"numpy's Generator; bit-identical to the reference's traces), log_prob by the reference's "
+                      f"torch-CPU float32 op sequence at batch 1 on {threads} threads"}
 
 
 def config5(cycles=10, train_steps=100):

@@ -311,6 +311,140 @@ class LocalChain:
         return bool(acc[0])
 
 
+class NumpyLocalChain:
+    """One MonteCarlo chain's local moves in the reference's own per-call numpy form: the
+    timed CPU baseline of bench.py's Algorithm-1 regime (LocalChain, the C restatement, is
+    the parity checker; tests/test_oracle_local.py shows the two bit-identical).
+
+    particle_displacement (monte_carlo.py:146-189): rng.integers(N); the particle's energy
+    before and after by calculate_particle_energy_virial (energy_calculator.py:48-119):
+    np.delete of the particle, compute_distances as a Python loop of minimum_image (np.round)
+    + np.linalg.norm per pair (simulation_box.py:31-65), the r < 0.5 hard core, the masked
+    lennard_jones_energy_virial (potential.py:3-29) summed by np.sum, plus the particle's
+    double_well_potential (potential.py:55-116); displacement (rng.random(2) - 0.5) *
+    max_displacement on a copy, apply_pbc by %; the Metropolis rule (:191-223); on accept
+    the running totals += the differences.  The generator is numpy's own
+    np.random.default_rng(seed) (monte_carlo.py:92-95).  nf_big_move given both NLLs
+    (:235-301) and sample() (:416-444) as the reference runs them."""
+
+    def __init__(self, particles, seed, phys, max_disp=0.65, beta=1.0, target=0.5):
+        self.particles = np.array(particles, np.float64)
+        self.target, self.prev_attempts, self.prev_accepted = target, 0, 0
+        self.N = self.particles.shape[0]
+        self.Lx, self.Ly = np.float64(phys.Lx), np.float64(phys.Ly)
+        self.phys, self.beta, self.max_disp = phys, beta, max_disp
+        self.rng = np.random.default_rng(seed)
+        self.E, self.W = total_energy_pairloop(self.particles, phys)
+        self.attempts = self.accepted = 0
+        rc = phys.r_cut
+        self._e_cut = 4.0 * ((1.0 / rc) ** 6 * (1.0 / rc) ** 6 - (1.0 / rc) ** 6)
+        self.samples = []
+
+    def _well(self, pos):
+        x, y = pos[0], pos[1]
+        Lx, Ly = self.Lx, self.Ly
+        centres = [[Lx / 4, Ly / 2]] + ([[3 * Lx / 4, Ly / 2]] if self.phys.num_wells == 2 else [])
+        V = np.zeros(1, dtype=np.float64)
+        for i, c in enumerate(np.array(centres)):
+            dx = np.atleast_1d(x - c[0])
+            dy = np.atleast_1d(y - c[1])
+            dx -= Lx * np.round(dx / Lx)
+            dy -= Ly * np.round(dy / Ly)
+            r = np.sqrt(dx ** 2 + dy ** 2)
+            V += self.phys.V0[i] * (1 - 0.5 * (1 + np.tanh(self.phys.k * (r - self.phys.r0))))
+        return V[0]
+
+    def particle_energy(self, positions, p):
+        pos = positions[p]
+        others = np.delete(positions, p, axis=0)
+        r = np.zeros(len(others))
+        for j, q in enumerate(others):
+            d = pos - q
+            d[0] -= self.Lx * np.round(d[0] / self.Lx)
+            d[1] -= self.Ly * np.round(d[1] / self.Ly)
+            r[j] = np.linalg.norm(d)
+        if np.any(r < self.phys.r_core):
+            return float("inf"), float("inf")
+        e = np.zeros_like(r)
+        w = np.zeros_like(r)
+        m = r <= self.phys.r_cut
+        sr6 = (1.0 / r[m]) ** 6
+        sr12 = sr6 * sr6
+        e[m] = 4.0 * (sr12 - sr6)
+        w[m] = 48.0 * (sr12 - 0.5 * sr6)
+        e[m] -= self._e_cut
+        E, W = np.sum(e), np.sum(w)
+        if self.phys.num_wells > 0:
+            E += self._well(pos)
+        return E, W
+
+    def _metropolis(self, old, new):
+        if new <= old:
+            return True
+        if np.isinf(new):
+            return False
+        return self.rng.random() < np.exp(-self.beta * (new - old))
+
+    def adjust_displacement(self):
+        """MonteCarlo.adjust_displacement (monte_carlo.py:375-403)."""
+        if self.attempts > self.prev_attempts:
+            d_att = self.attempts - self.prev_attempts
+            frac = (self.accepted - self.prev_accepted) / d_att
+            new = self.max_disp * (frac / self.target)
+            ratio = new / self.max_disp
+            if ratio > 1.5:
+                new = self.max_disp * 1.5
+            elif ratio < 0.5:
+                new = self.max_disp * 0.5
+            self.max_disp = new
+            self.prev_attempts, self.prev_accepted = self.attempts, self.accepted
+
+    def local_moves(self, n, adjust_every=0, sample_every=0, step0=0):
+        """n particle_displacement calls numbered step0 + 1 .. step0 + n, with
+        adjust_displacement after every adjust_every-th and sample() after every
+        sample_every-th (the drivers' loops, main_algorithm_1.py:384-390).  Returns the
+        per-move accept flags."""
+        log = np.zeros(n, np.int8)
+        for i in range(n):
+            step = step0 + i + 1
+            self.attempts += 1
+            p = self.rng.integers(self.N)
+            eno, viro = self.particle_energy(self.particles, p)
+            new = self.particles.copy()
+            new[p] += (self.rng.random(2) - 0.5) * self.max_disp
+            new[p] = np.array([new[p][0] % self.Lx, new[p][1] % self.Ly])
+            enn, virn = self.particle_energy(new, p)
+            if self._metropolis(eno, enn):
+                self.particles = new
+                self.accepted += 1
+                self.E += enn - eno
+                self.W += virn - viro
+                log[i] = 1
+            if adjust_every and step % adjust_every == 0:
+                self.adjust_displacement()
+            if sample_every and step % sample_every == 0:
+                area = self.Lx * self.Ly
+                self.samples.append((step, self.E / self.N, self.N / area,
+                                     self.N / area / self.beta + self.W / (2.0 * area), self.Lx, self.Ly,
+                                     self.particles.copy()))
+        return log
+
+    def big_move(self, cfg, nll_old, nll_new):
+        """nf_big_move (monte_carlo.py:235-301) given both NLLs (reference sign)."""
+        self.attempts += 1
+        cfg = np.asarray(cfg, np.float32)
+        En, Wn = total_energy_pairloop(cfg, self.phys)
+        ratio = np.exp(-self.beta * (En - self.E) - (nll_new - nll_old))
+        acc = bool(ratio >= 1 or self.rng.random() < ratio)
+        if acc:
+            self.particles = cfg.copy()
+            self.accepted += 1
+            self.E, self.W = En, Wn
+        else:
+            self.E, self.W = total_energy_pairloop(self.particles, self.phys)
+        return acc
+
+
 def pcg64_integers(state6, n):
     """Generator.integers(n) (buffered 32-bit Lemire) on a u64[6] state."""
     return int(lib().oracle_pcg64_integers(_ptr(state6), int(n)))

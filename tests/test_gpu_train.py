@@ -290,3 +290,52 @@ def test_lean_backward_products_match_generic_kernel(M, K, N):
     torch.testing.assert_close(outs[0][1], gy.t() @ x, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(outs[0][2], gy.sum(0), rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(outs[0][3], gy.sum(0), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("M", [2, 33, 179, 256])
+def test_batchnorm_combine_on_ill_conditioned_columns(M):
+    """The BatchNorm-in-load combine (lin_bn_prologue: Chan's update over the producer's
+    32-row tile statistics, tiles in order) on columns whose variance is ~1e-9 of their
+    squared mean, on ragged batches (a partial last tile): the batch variance stays
+    non-negative, invstd finite, the mean within 1e-5 and the variance within 1e-2 relative of
+    float64 statistics (the float32 tile means' rounding, ~3e-5 here, against tile-mean
+    differences of ~2e-3)
+    of the same float32 inputs, for the lean and the generic kernels alike.  A combine that
+    folds the per-tile updates into sum(x^2)/n - mean^2 (one way to constant-fold its
+    divisions) cancels catastrophically here: negative variances, NaN invstd, the NaN
+    discriminant of r05ak (DESIGN_HISTORY.md r06; tests/test_train_cpu.py shows the
+    mechanism on the same statistics)."""
+    from flowstate import _lib
+
+    L, p, st = _lib.load(), _lib.ptr, _lib.stream_ptr
+    K, N = 64, 32
+    g = torch.Generator().manual_seed(M)
+    scale = torch.cat([torch.full((K // 2,), 300.0), torch.ones(K // 2)])
+    spread = torch.cat([torch.full((K // 2,), 1e-2), torch.ones(K // 2)])
+    x = (scale + spread * torch.randn((M, K), generator=g)).float().cuda()
+    w = (torch.randn((N, K), generator=g) * 0.1).cuda()
+    gam, bet = torch.ones(K, device="cuda"), torch.zeros(K, device="cuda")
+    xst = torch.empty(((M + 31) // 32, K, 2), device="cuda")
+    xx = torch.empty_like(x)
+    wi = torch.eye(K, device="cuda")
+    _lib.check(L.fs_linear_f32_ex(_lib.GemmF32(M, K, K, p(x), K, 1, p(wi), 1, K, None, None, 0, p(xx), K, None),
+                                  None, p(xst), st()))
+    x64 = xx.double().cpu()
+    mean64 = x64.mean(0)
+    var64 = ((x64 - mean64) ** 2).mean(0)
+    for lean in (1, 0):
+        prev = L.fs_set_lean_gemm(lean)
+        y = torch.empty((M, N), device="cuda")
+        sto = torch.empty(((M + 31) // 32, N, 2), device="cuda")
+        u = torch.empty_like(x)
+        mo, io, vo = (torch.empty(K, device="cuda") for _ in range(3))
+        bi = _lib.BnIn(p(xst), (M + 31) // 32, M, p(gam), p(bet), 1e-5, 0.1, None, None, None, p(mo), p(io), p(u),
+                       p(vo))
+        _lib.check(L.fs_linear_f32_ex(_lib.GemmF32(M, N, K, p(xx), K, 1, p(w), 1, K, None, None, 0, p(y), N, None),
+                                      bi, p(sto), st()))
+        L.fs_set_lean_gemm(prev)
+        torch.cuda.synchronize()
+        var, mean, inv = vo.double().cpu(), mo.double().cpu(), io.double().cpu()
+        assert (var >= 0).all() and torch.isfinite(inv).all() and torch.isfinite(y).all(), (lean, var.min())
+        assert ((mean - mean64).abs() <= 1e-5 * mean64.abs() + 1e-6).all(), lean
+        assert ((var - var64).abs() <= 1e-2 * var64 + 1e-9).all(), (lean, ((var - var64).abs() / var64).max())

@@ -88,3 +88,43 @@ def test_integers_matches_numpy():
                     assert OP.pcg64_random6(s) == g.random()
             st = g.bit_generator.state
             assert int(s[4]) == st["has_uint32"] and int(s[5]) == st["uinteger"]
+
+
+@pytest.mark.parametrize("N", [3, 16, 64])
+def test_numpy_local_chain_matches_reference_trace(N):
+    """The numpy per-call restatement (oracle.physics.NumpyLocalChain, the regime's timed
+    CPU baseline in bench.py) replays the reference's own traces exactly as the C
+    restatement does: accept flags, running E / W, max_displacement, big-move decisions,
+    the float32 switch, final particles, counters and numpy's PCG64 state."""
+    torch.set_num_threads(1)
+    f = np.load(os.path.join(G, "local_trace.npz"))
+    moves = int(f[f"N{N}_moves"])
+    dims = OF.FlowDims(N=N, L=1, H=32, nb=1, K=5, B=OF.half_box(N))
+    sd = OF.random_state_dict(dims, seed=int(f[f"N{N}_flow_seed"]))
+    phys = OP.make_phys(N)
+    hw = phys.Lx / 2
+    for c in range(int(f[f"N{N}_chains"])):
+        k = f"N{N}_c{c}"
+        ch = OP.NumpyLocalChain(f[k + "_init"], int(f[k + "_seed"]), phys)
+        acc, E, W, md = [], [], [], []
+        for phase in range(3):
+            for t in range(moves):
+                acc.append(ch.local_moves(1, adjust_every=50, step0=t)[0])
+                E.append(ch.E)
+                W.append(ch.W)
+                md.append(ch.max_disp)
+            if phase < 2:
+                cfg = f[k + f"_bigcfg{phase}"]
+                big = ch.big_move(cfg, _nll(sd, dims, ch.particles, hw), _nll(sd, dims, cfg, hw))
+                assert big == bool(f[k + "_big"][phase])
+        np.testing.assert_array_equal(np.array(acc, np.int8), f[k + "_accept"])
+        for a, b in zip(E, f[k + "_E"]):
+            assert _close(a, b)
+        for a, b in zip(W, f[k + "_W"]):
+            assert _close(a, b)
+        np.testing.assert_allclose(md, f[k + "_maxdisp"], rtol=1e-13)
+        assert (ch.particles.dtype == np.float32) == bool(f[k + "_final_dtype32"])
+        np.testing.assert_array_equal(ch.particles, f[k + "_final"])
+        assert ch.attempts == f[k + "_attempts"] and ch.accepted == f[k + "_accepted"]
+        st = ch.rng.bit_generator.state
+        assert st["state"]["state"] == (int(f[k + "_pcg"][0]) << 64 | int(f[k + "_pcg"][1]))

@@ -271,3 +271,54 @@ def test_training_step_matches_reference_at_config5_size_cpu():
     grads = {n: (p.grad.detach().clone() if p.grad is not None else None) for n, p in m.named_parameters()}
     opt.step()
     check_a2_step(m, f, loss.item(), grads, before)
+
+
+def _tile_stats(x):
+    """The producer epilogue's per-32-row-tile (mean, sum of squared deviations) in float32
+    (train_kernels.hip gemm_tile: two passes over the tile)."""
+    out = []
+    for r0 in range(0, x.shape[0], 32):
+        t = x[r0:r0 + 32]
+        m = (t.sum(0, dtype=np.float32) / np.float32(t.shape[0])).astype(np.float32)
+        out.append((m, ((t - m) ** 2).sum(0, dtype=np.float32), t.shape[0]))
+    return out
+
+
+def test_batchnorm_combine_mechanism_cpu():
+    """Why r05ak's constant-folded combine could produce a NaN discriminant (DESIGN_HISTORY.md
+    r06; its diff was never committed, so this is the reconstruction the guard is built on):
+    the consumer's BatchNorm combines the producer's per-tile (mean, M2) pairs.  Chan's update
+    (lin_bn_prologue, restated here in float32 in the kernel's order) has no cancellation; a
+    combine whose per-tile divisions are folded into sum(M2 + n mean^2)/rows - mean^2 does.
+    On a column with variance ~1e-9 of its squared mean (the training step's pre-BatchNorm
+    activations after a few Adam steps can look like that) the folded variance comes out
+    negative, so rsqrt(var + eps) is NaN, the BatchNorm output and with it the spline
+    parameters are NaN, and the sampling pass's root solve reports the NaN discriminant.
+    tests/test_gpu_train.py::test_batchnorm_combine_on_ill_conditioned_columns runs the
+    kernels themselves on such columns."""
+    rng = np.random.default_rng(0)
+    f32 = np.float32
+    x = (300.0 + 1e-2 * rng.standard_normal((179, 256))).astype(f32)
+    x64 = x.astype(np.float64)
+    var64 = ((x64 - x64.mean(0)) ** 2).mean(0)
+    tiles = _tile_stats(x)
+    # Chan's update, tiles in order (the kernel's arithmetic)
+    n, mean, m2 = f32(0), np.zeros(256, f32), np.zeros(256, f32)
+    for tm, tq, nb in tiles:
+        nb = f32(nb)
+        nn = f32(n + nb)
+        d = (tm - mean).astype(f32)
+        mean = (mean + d * f32(nb / nn)).astype(f32)
+        m2 = (m2 + tq + d * d * f32(n * nb / nn)).astype(f32)
+        n = nn
+    var_chan = (m2 / f32(x.shape[0])).astype(f32)
+    assert (var_chan >= 0).all()
+    assert np.abs(var_chan - var64).max() <= 1e-2 * var64.min()  # the tile means' float32 rounding
+    # the folded form: one sum per column, then E[x^2] - mean^2
+    s1 = sum(f32(nb) * tm for tm, tq, nb in tiles).astype(f32)
+    s2 = sum(tq + f32(nb) * tm * tm for tm, tq, nb in tiles).astype(f32)
+    mf = (s1 / f32(x.shape[0])).astype(f32)
+    var_fold = (s2 / f32(x.shape[0]) - mf * mf).astype(f32)
+    assert (var_fold + f32(1e-5) < 0).any()  # rsqrt of a negative number: NaN
+    with np.errstate(invalid="ignore"):
+        assert np.isnan(1 / np.sqrt(var_fold + f32(1e-5))).any()
