@@ -1390,6 +1390,9 @@ __global__ void __launch_bounds__((64 * trunk16s_waves<H, HALF>())) wide_trunk16
 #ifndef FS_GSPLIT
 #define FS_GSPLIT 4  // workgroups (CUs) per 16-row tile
 #endif
+#ifndef FS_GSPLIT_XCD
+#define FS_GSPLIT_XCD 1  // a tile's workgroups dealt to one XCD (0: consecutive blocks; A/B switch)
+#endif
 #ifndef FS_GSPLIT_AUTO_WG
 #define FS_GSPLIT_AUTO_WG 64  // the default trunk's limit on column-split workgroups (A1 N=16:
                               // 16 / 64 / 128 / 256 rows 4.2-4.7 ms per pass against 5.0-5.3 on
@@ -1416,7 +1419,15 @@ __global__ void __launch_bounds__(64 * (2 * (H / 32) / G)) wide_trunk16g_kernel(
     const FlowArgs &a = w.a;
     const int N = a.N, D = 2 * N;
     const PackLayout PL = pack_layout(N, H, a.nb, a.K);
+#if FS_GSPLIT_XCD
+    // a tile's G workgroups at equal blockIdx.x % 8 (one XCD under round-robin dealing; speed
+    // only): b = (t % 8) + 8 (g + G (t / 8)); slots of tiles past T exit at once
+    const int xb = (int)blockIdx.x & 7, yb = (int)blockIdx.x >> 3;
+    const int g = yb % G, t = (yb / G) * 8 + xb;
+    if (t >= w.T) return;
+#else
     const int t = (int)blockIdx.x / G, g = (int)blockIdx.x - t * G;
+#endif
     const int64_t rowt = (int64_t)t * 16;
     const int launch = MODE == MODE_DENSITY ? a.L - 1 - w.layer : w.layer;
     unsigned *cnt = w.CNT + (launch & 1) * w.T + t;
@@ -2305,7 +2316,8 @@ static hipError_t wide_pass_t(const FlowArgs &a, int N, hipStream_t st, bool &us
         w.pending = s > 0;
         if (trunk16 == 4) {
             if constexpr (gsplit_ok<H>())
-                add((const void *)wide_trunk16g_kernel<H, K, MODE, FS_GSPLIT>, dim3((unsigned)(R / 16) * FS_GSPLIT),
+                add((const void *)wide_trunk16g_kernel<H, K, MODE, FS_GSPLIT>,
+                    dim3(FS_GSPLIT_XCD ? (unsigned)((R / 16 + 7) / 8) * 8 * FS_GSPLIT : (unsigned)(R / 16) * FS_GSPLIT),
                     dim3(64 * (2 * (H / 32) / FS_GSPLIT)), 0);
         } else if (trunk16 == 3)
             add((const void *)wide_trunk16s_kernel<H, K, MODE, true>, dim3((unsigned)(R / 16)),
