@@ -1394,10 +1394,12 @@ __global__ void __launch_bounds__((64 * trunk16s_waves<H, HALF>())) wide_trunk16
 #define FS_GSPLIT_XCD 1  // a tile's workgroups dealt to one XCD (0: consecutive blocks; A/B switch)
 #endif
 #ifndef FS_GSPLIT_AUTO_WG
-#define FS_GSPLIT_AUTO_WG 64  // the default trunk's limit on column-split workgroups (A1 N=16:
-                              // 16 / 64 / 128 / 256 rows 4.2-4.7 ms per pass against 5.0-5.3 on
-                              // the half-tile trunk, 512 rows 6.3-6.5 against 5.3;
-                              // profiles/r05/r05af_gsplit.log)
+#define FS_GSPLIT_AUTO_WG 128  // the default trunk's limit on column-split workgroups: up to 512
+                               // rows.  A1 N=16 with a tile's workgroups on one XCD (r06,
+                               // profiles/r06/r06e_gsplit_rows.log): 16-256 rows 3.8-4.0 ms per
+                               // pass against 5.0-5.1 on the half-tile trunk, 384 rows 4.1 against
+                               // 4.9, 512 rows 4.4 against 4.9 (r05, consecutive blocks: 512 rows
+                               // 6.3-6.5 against 5.3, so the limit was 256 rows)
 #endif
 constexpr unsigned kGSpinMax = 1u << 20;  // default polls (sc1 load + s_sleep) before a hand-off gives up
 

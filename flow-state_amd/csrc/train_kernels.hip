@@ -79,6 +79,18 @@ __device__ __forceinline__ float unbiased(float var, int64_t rows) {
     return p / (float)(rows - 1);
 }
 
+// One step of Chan's pairwise update of a column's (n, mean, M2) by a tile of nb rows with
+// statistics v = (tile mean, tile M2), rounded per operation (no contraction into FMAs, which
+// the compiler would otherwise choose per call site and per constant), so that every
+// BatchNorm-in-load prologue (generic, lean, the full-batch fast path) agrees bit for bit.
+__device__ __forceinline__ void chan_update(float &n, float &mean, float &m2, float v_mean, float v_m2, float nb) {
+#pragma clang fp contract(off)
+    const float nn = n + nb, d = v_mean - mean;
+    mean = mean + d * (nb / nn);
+    m2 = m2 + v_m2 + d * d * (n * nb / nn);
+    n = nn;
+}
+
 template <int SPLIT>
 struct GemmLds {
     t16 part[SPLIT > 1 ? SPLIT - 1 : 1][64];
@@ -285,11 +297,7 @@ __device__ __forceinline__ void bn_prologue(const GemmArgs &g, const BnIn &bn, b
             for (int t = 0; t < kBnStTiles; ++t) {  // Chan's pairwise update, tiles in order
                 if (t < nt) {
                     const int64_t row0 = 32 * (t0 + t);
-                    const float nb = (float)(bn.rows - row0 < 32 ? bn.rows - row0 : 32);
-                    const float nn = n + nb, d = v[t][0] - mean;
-                    mean = mean + d * (nb / nn);
-                    m2 = m2 + v[t][1] + d * d * (n * nb / nn);
-                    n = nn;
+                    chan_update(n, mean, m2, v[t][0], v[t][1], (float)(bn.rows - row0 < 32 ? bn.rows - row0 : 32));
                 }
             }
         }
@@ -417,21 +425,28 @@ __device__ __forceinline__ void lin_bn_prologue(const LinBn &bn, int rows, bool 
     const int k = threadIdx.x;
     if (k < K) {
         float n = 0.f, mean = 0.f, m2 = 0.f;
-        for (int t0 = 0; t0 < bn.tiles; t0 += kBnStTiles) {
-            const int nt = bn.tiles - t0 < kBnStTiles ? bn.tiles - t0 : kBnStTiles;
-            const f2 *src = (const f2 *)bn.st + t0 * K + k;
-            f2 v[kBnStTiles];
+        if (bn.tiles == kBnStTiles && rows == 32 * kBnStTiles) {
+            // the full training batch (256 rows, one round of 8 full tiles): the same update
+            // with the tile sizes known, so its divisions fold to constants.  Bit-identical:
+            // nb / nn and n nb / nn are correctly rounded quotients either way (the run-time
+            // form below is the IEEE division) and chan_update rounds per operation.  0.45 us
+            // per launch in a dependent chain (tools/probes/block_fuse: 9.45 -> 8.55 us per
+            // block; tools/train_lin_chain.py 5.70 -> 5.28 us; profiles/r06/).
 #pragma unroll
-            for (int t = 0; t < kBnStTiles; ++t) v[t] = t0 == 0 ? v0[t] : (t < nt ? src[t * K] : f2{0.f, 0.f});
+            for (int t = 0; t < kBnStTiles; ++t) chan_update(n, mean, m2, v0[t][0], v0[t][1], 32.f);
+        } else {
+            for (int t0 = 0; t0 < bn.tiles; t0 += kBnStTiles) {
+                const int nt = bn.tiles - t0 < kBnStTiles ? bn.tiles - t0 : kBnStTiles;
+                const f2 *src = (const f2 *)bn.st + t0 * K + k;
+                f2 v[kBnStTiles];
 #pragma unroll
-            for (int t = 0; t < kBnStTiles; ++t) {
-                if (t < nt) {
-                    const int row0 = 32 * (t0 + t);
-                    const float nb = (float)(rows - row0 < 32 ? rows - row0 : 32);
-                    const float nn = n + nb, d = v[t][0] - mean;
-                    mean = mean + d * (nb / nn);
-                    m2 = m2 + v[t][1] + d * d * (n * nb / nn);
-                    n = nn;
+                for (int t = 0; t < kBnStTiles; ++t) v[t] = t0 == 0 ? v0[t] : (t < nt ? src[t * K] : f2{0.f, 0.f});
+#pragma unroll
+                for (int t = 0; t < kBnStTiles; ++t) {
+                    if (t < nt) {
+                        const int row0 = 32 * (t0 + t);
+                        chan_update(n, mean, m2, v[t][0], v[t][1], (float)(rows - row0 < 32 ? rows - row0 : 32));
+                    }
                 }
             }
         }

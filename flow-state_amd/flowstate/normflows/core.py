@@ -140,7 +140,7 @@ def _raise_on_nan(err):
 
 # A pass of at most this many rows may run its A1 trunk on the column-split kernel, whose
 # in-launch hand-offs report a wait that gave up as err |= 4 (fs_set_wide_trunk16).
-_GSPLIT_MAX_ROWS = 256
+_GSPLIT_MAX_ROWS = 512
 
 
 def _run_stack(layers, x, direction, cache=None, base_log_prob=None, err=None):

@@ -75,10 +75,16 @@ def step_loss(model, x, n_reverse, alpha, flat_bn=None):
 
 
 class _Captured:
-    """One captured step for one batch size: its static input, loss and NaN flag."""
+    """One captured step for one batch size: its static input, loss and NaN flag, and every
+    tensor allocated outside the graph's pool that its replays read or write (`keep`): a
+    replay writes into them, so they must live as long as the graph.  (r05 / r06: the
+    BatchNorm snapshot buffers were locals of _capture; freed after capture, their memory went
+    to later allocations, e.g. another model's Adam state, which every replay then overwrote:
+    the NaN discriminant of tests/test_gpu_train_graph.py at alpha = 0.7, DESIGN_HISTORY r06.)"""
 
-    def __init__(self, graph, x, loss, nan_flag):
+    def __init__(self, graph, x, loss, nan_flag, keep=()):
         self.graph, self.x, self.loss, self.nan_flag = graph, x, loss, nan_flag
+        self.keep = list(keep)
 
 
 class GraphedTrainStep:
@@ -189,7 +195,8 @@ class GraphedTrainStep:
         finally:
             AF._defer_nan = False
             AF._sticky_nan = None
-        return _Captured(graph, x, loss.detach(), nan_flag)  # keep no autograd graph alive
+        # keep no autograd graph alive; keep the snapshot buffers the replays write
+        return _Captured(graph, x, loss.detach(), nan_flag, keep=bn_backup)
 
     def _bn_buffers(self):
         """The running-statistics buffers a training step updates."""

@@ -281,7 +281,7 @@ int64_t fs_set_wide_rows(int64_t rows);
  * returns the previous value (a negative argument only reads it).  The results do not
  * depend on them.
  * fs_set_wide_trunk16: 5 (default, or FS_WIDE_TRUNK16) = by batch: 4 for the A1 trunk
- *   (H = 256) on at most 256 rows, else 3; 4 = each 16-row tile's columns split over four
+ *   (H = 256) on at most 512 rows, else 3; 4 = each 16-row tile's columns split over four
  *   workgroups (CUs) that hand their epilogue slices to each other inside the launch (where
  *   the tiles x 4 fit half the chip, else 3; err |= 4 if a hand-off wait gave up); 3 = the
  *   wide path's ResidualNet on 16-row tiles (v_mfma_f32_16x16x4_f32, twice the workgroups)

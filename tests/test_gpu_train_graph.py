@@ -91,3 +91,25 @@ def test_graphed_step_updates_inference_image():
     fresh.eval()
     assert not torch.equal(lp0, lp1)
     assert torch.equal(lp1, fresh.log_prob(x))
+
+
+def test_graph_replays_write_only_memory_they_own():
+    """Every tensor a captured training step reads or writes outside its own pool lives as
+    long as the graph (train._Captured.keep).  r06 found the BatchNorm snapshot buffers of the
+    non-paired path (ALPHA != 1) freed after capture: the caching allocator handed their
+    blocks to later tensors (another model's Adam state in
+    test_graphed_step_matches_eager[0.7], whose NaN discriminant it caused) and every replay
+    overwrote them.  Here small sentinel tensors allocated after the capture (the freed
+    blocks' size class) must come through several replays unchanged."""
+    from flowstate.normflows.train import GraphedTrainStep
+
+    m, f = build("cuda")
+    x = torch.from_numpy(f["x"]).cuda()
+    g = GraphedTrainStep(m, 64, 5e-3, 1e-4, alpha=0.7, example=x)
+    torch.cuda.synchronize()
+    sentinels = [torch.full((32,), 1234.5, device="cuda") for _ in range(50000)]
+    for i in range(3):
+        g.step(x.roll(i, 0))
+    torch.cuda.synchronize()
+    bad = sum(int((s != 1234.5).any()) for s in sentinels)
+    assert bad == 0, f"{bad} sentinel tensors overwritten by graph replays"
