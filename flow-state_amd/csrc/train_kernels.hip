@@ -418,14 +418,14 @@ __device__ __forceinline__ void lin_bn_first(const LinBn &bn, f2s (&v)[kBnStTile
 // bn_prologue's arithmetic (column k = thread k, Chan's update over the producer's tiles
 // in order, biased variance, invstd; the lead workgroup's outputs and running statistics);
 // v0 / gk / bk: lin_bn_first's loads
-template <int K>
+template <int K, bool FULL>
 __device__ __forceinline__ void lin_bn_prologue(const LinBn &bn, int rows, bool lead, BnLds &S,
                                                 const f2s (&v0)[kBnStTiles], float gk, float bk) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     const int k = threadIdx.x;
     if (k < K) {
         float n = 0.f, mean = 0.f, m2 = 0.f;
-        if (bn.tiles == kBnStTiles && rows == 32 * kBnStTiles) {
+        if constexpr (FULL) {
             // the full training batch (256 rows, one round of 8 full tiles): the same update
             // with the tile sizes known, so its divisions fold to constants.  Bit-identical:
             // nb / nn and n nb / nn are correctly rounded quotients either way (the run-time
@@ -470,8 +470,30 @@ __device__ __forceinline__ void lin_bn_prologue(const LinBn &bn, int rows, bool 
     __syncthreads();
 }
 
+// FULL (the full training batch, bn.tiles == kBnStTiles and M == 32 kBnStTiles, uniform per
+// problem): the producer statistics as unconditional buffer loads and the combine's fast
+// path; the same loads and arithmetic, so the same bits (tools/probes/block_fuse's tile
+// form: 4.3 us per BatchNorm-in-load product in a dependent chain).
+template <int K, bool FULL>
+__device__ __forceinline__ void lin_bn_first_t(const LinBn &bn, f2s (&v)[kBnStTiles], float &gk, float &bk) {
+    if constexpr (FULL) {
+        const int k = threadIdx.x;
+        if (k < K) {
+            const __amdgpu_buffer_rsrc_t Sr =
+                __builtin_amdgcn_make_buffer_rsrc((void *)bn.st, (short)0, kBnStTiles * K * 8, 0x00020000);
+#pragma unroll
+            for (int t = 0; t < kBnStTiles; ++t)
+                v[t] = __builtin_bit_cast(f2s, __builtin_amdgcn_raw_buffer_load_b64(Sr, (t * K + k) * 8, 0, 0));
+            gk = bn.gamma[k];
+            bk = bn.beta[k];
+        }
+    } else {
+        lin_bn_first<K>(bn, v, gk, bk);
+    }
+}
+
 // One 32 x 32 tile (bx, by) of P by 8 waves: wave w reduces the k-blocks 8w + 64s
-template <int KBW>
+template <int KBW, bool FULL = false>
 __device__ __forceinline__ void lin_tile(const LinP &P, const LinBn &bn, unsigned bx, unsigned by, LinLds &L) {
     constexpr int K = 64 * KBW;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -483,7 +505,7 @@ __device__ __forceinline__ void lin_tile(const LinP &P, const LinBn &bn, unsigne
     const int kq = 8 * w + 4 * h;  // this lane's first k in each k-block
     f2s st0[kBnStTiles];
     float gk = 0.f, bk = 0.f;
-    if (bn.on) lin_bn_first<K>(bn, st0, gk, bk);
+    if (bn.on) lin_bn_first_t<K, FULL>(bn, st0, gk, bk);
     t4 a[KBW], b[KBW];
 #pragma unroll
     for (int s = 0; s < KBW; ++s) {
@@ -509,7 +531,7 @@ __device__ __forceinline__ void lin_tile(const LinP &P, const LinBn &bn, unsigne
             ep_bias = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lin_rsrc(P.bias, P.N * 4), col * 4, 0, 0));
     }
     if (bn.on) {
-        lin_bn_prologue<K>(bn, M, bx == 0 && by == 0, L.S, st0, gk, bk);
+        lin_bn_prologue<K, FULL>(bn, M, bx == 0 && by == 0, L.S, st0, gk, bk);
         const int nt = P.N / 32;
 #pragma unroll
         for (int s = 0; s < KBW; ++s) {
@@ -568,17 +590,25 @@ __device__ __forceinline__ void lin_tile(const LinP &P, const LinBn &bn, unsigne
     }
 }
 
+static bool lin_full(const LinP &P, const LinBn &bn) {
+    return bn.tiles == kBnStTiles && P.M == 32 * kBnStTiles;
+}
+
 // workgroups [0, t0) compute problem 0 (column-major over its mt0 row tiles), the rest
 // problem 1; the branch is uniform, so each workgroup reads only its own problem's arguments
-template <int KBW>
+// FULL: every BatchNorm-in-load problem of the launch is a full training batch (lin_full;
+// the host picks the kernel), so the generic kernel keeps its register budget (74 VGPRs, three
+// workgroups per CU for the final Linear's 1472-workgroup launch) and the hidden layers'
+// BatchNorm-in-load products take the full-batch form
+template <int KBW, bool FULL>
 __global__ __launch_bounds__(512) void gemm_lin_kernel(Lin2 a) {
     __shared__ LinLds L;
     const unsigned b = blockIdx.x;
     if (b < a.t0) {
-        lin_tile<KBW>(a.p[0], a.b[0], b % a.mt0, b / a.mt0, L);
+        lin_tile<KBW, FULL>(a.p[0], a.b[0], b % a.mt0, b / a.mt0, L);
     } else {
         const unsigned c = b - a.t0;
-        lin_tile<KBW>(a.p[1], a.b[1], c % a.mt1, c / a.mt1, L);
+        lin_tile<KBW, FULL>(a.p[1], a.b[1], c % a.mt1, c / a.mt1, L);
     }
 }
 
@@ -1669,13 +1699,23 @@ static hipError_t lin_launch(const GemmArgs &g0, const BnIn *b0, const GemmArgs 
         a.mt1 = 1;
     }
     const dim3 grid(a.t0 + t1), block(512);
+    // the full-batch kernel when some problem has a BatchNorm-in-load and every one that has
+    // is a full training batch
+    const bool any_bn = a.b[0].on || (g1 && a.b[1].on);
+    const bool full = any_bn && (!a.b[0].on || lin_full(a.p[0], a.b[0])) && (!g1 || !a.b[1].on || lin_full(a.p[1], a.b[1]));
+#define FS_LIN_K(KB)                                                                               \
+    if (full)                                                                                      \
+        hipLaunchKernelGGL((gemm_lin_kernel<KB, true>), grid, block, 0, st, a);                    \
+    else                                                                                           \
+        hipLaunchKernelGGL((gemm_lin_kernel<KB, false>), grid, block, 0, st, a);
     switch (g0.K) {
-        case 64: hipLaunchKernelGGL(gemm_lin_kernel<1>, grid, block, 0, st, a); break;
-        case 128: hipLaunchKernelGGL(gemm_lin_kernel<2>, grid, block, 0, st, a); break;
-        case 192: hipLaunchKernelGGL(gemm_lin_kernel<3>, grid, block, 0, st, a); break;
-        case 256: hipLaunchKernelGGL(gemm_lin_kernel<4>, grid, block, 0, st, a); break;
+        case 64: FS_LIN_K(1) break;
+        case 128: FS_LIN_K(2) break;
+        case 192: FS_LIN_K(3) break;
+        case 256: FS_LIN_K(4) break;
         default: return hipErrorInvalidValue;
     }
+#undef FS_LIN_K
     return hipGetLastError();
 }
 
