@@ -298,11 +298,11 @@ def config2(steps=16, C=4096, N=16):
     dt_call = time.perf_counter() - t0
     bmc.MAX_STEPS_PER_LAUNCH = 1
     run(1)
-    dt1 = run(4)
+    dt1 = run(steps)
     return {"workload": "config 2: Algorithm 1, N=16, 4096 chains, A1 flow", "value": C * steps / dt,
             "unit": "steps/s", "steps": steps, "ms_per_step": dt / steps * 1e3, "steps_per_launch": S,
             "step1_calls": {"value": C * steps / dt_call, "ms_per_step": dt_call / steps * 1e3},
-            "one_step_per_launch": {"value": C * 4 / dt1, "ms_per_step": dt1 / 4 * 1e3},
+            "one_step_per_launch": {"value": C * steps / dt1, "ms_per_step": dt1 / steps * 1e3},
             "acceptance_rate": rate}
 
 
