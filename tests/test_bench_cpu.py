@@ -24,7 +24,9 @@ def test_algorithm1_regime_cpu_sample_is_bounded():
     import bench
     t0 = time.perf_counter()
     r = bench.algorithm1_regime_cpu(N=3, interval=50, budget_s=0.3)
-    assert time.perf_counter() - t0 < 30
+    # (the A1 flow's construction and 64 untimed CPU proposals dominate: ~2 s alone, more
+    # when the suite runs in parallel workers)
+    assert time.perf_counter() - t0 < 120
     assert r["value"] > 0 and r["kind"] == "port" and r["unit"] == "big-move attempts/s"
     assert r["cores"] >= 1 and "attempts of one run" in r["sample"]
 
