@@ -18,8 +18,9 @@ def _bench(args, env_extra, drop=()):
 
 
 def test_algorithm1_regime_cpu_sample_is_bounded():
-    """The regime leg's CPU sample (oracle C local moves + torch-CPU log_prob) runs at
-    least one attempt, stops near its budget and reports itself as a port."""
+    """The regime leg's CPU sample (the reference's per-call numpy local moves,
+    oracle.physics.NumpyLocalChain, + torch-CPU log_prob) runs at least one attempt, stops
+    near its budget and reports itself as a port of the reference's loop."""
     import time
     import bench
     t0 = time.perf_counter()
@@ -28,7 +29,7 @@ def test_algorithm1_regime_cpu_sample_is_bounded():
     # when the suite runs in parallel workers)
     assert time.perf_counter() - t0 < 120
     assert r["value"] > 0 and r["kind"] == "port" and r["unit"] == "big-move attempts/s"
-    assert r["cores"] >= 1 and "attempts of one run" in r["sample"]
+    assert r["cores"] >= 1 and "attempts of one run" in r["sample"] and "numpy" in r["sample"]
 
 
 def test_world_size_must_match_gpus():
