@@ -78,63 +78,71 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, PairThresh T, co
     const double e_cut = 4.0 * (sr6c * sr6c - sr6c);
     const double iLx = 1.0 / p.Lx, iLy = 1.0 / p.Ly;
     bool hit = false;
-    // pair (i, j): e, w of lennard_jones_energy_virial (potential.py:3-29); the sqrt only
-    // inside the cutoff (PairThresh)
-    auto pair = [&](int i, int j, double &e, double &w, uint64_t &mask) {
-        e = 0.0;
-        w = 0.0;
-        if (as_f32) {
-            const float s = F32 ? sqdist32((float)X[i], (float)Y[i], (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy)
-                                : sqdist_f32((float)X[i], (float)Y[i], (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy);
-            hit |= s <= T.core32;
-            if (s <= T.cut32) {
-                mask |= (uint64_t)1 << j;
-                lj_pair(r_of_sq(s), p.r_cut, e_cut, e, w);
-            }
-        } else {
-            const double s = sqdist_f64(X[i], Y[i], X[j], Y[j], p.Lx, p.Ly, T, iLx, iLy);
-            hit |= s <= T.core64;
-            if (s <= T.cut64) {
-                mask |= (uint64_t)1 << j;
-                lj_pair(r_of_sq(s), p.r_cut, e_cut, e, w);
-            }
-        }
+    // Row i (pairs j > i, t = j - i - 1) in two passes.  Pass 1: the squared minimum-image
+    // distances, the hard-core flag and the in-cutoff mask (PairThresh: one comparison each).
+    // Pass 2: lennard_jones_energy_virial (potential.py:3-29) of the in-cutoff pairs only
+    // (about 1 % at rho = 0.03), added in numpy's pairwise order of the whole row
+    // (loops_utils.h pairwise_sum, n <= 128): a term's accumulator is fixed by its position t,
+    // and the skipped terms are +0.0 while no term or partial sum is -0.0, so x + 0 == x
+    // leaves every sum as the full row's.  Evaluating the LJ term inside pass 1 made a wave
+    // run the sqrt / reciprocal / pow6 chain on every pair some lane had inside the cutoff
+    // (~half of them for 64 lanes).
+    auto sq = [&](int i, int j) -> double {
+        if (as_f32)
+            return F32 ? sqdist32((float)X[i], (float)Y[i], (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy)
+                       : sqdist_f32((float)X[i], (float)Y[i], (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy);
+        return sqdist_f64(X[i], Y[i], X[j], Y[j], p.Lx, p.Ly, T, iLx, iLy);
     };
-    // row i (pairs j > i) summed in numpy's pairwise order (loops_utils.h pairwise_sum, n <= 128)
+    auto term = [&](int i, int j, double &e, double &w) {
+        const double s = sq(i, j);
+        lj_pair(as_f32 ? r_of_sq((float)s) : r_of_sq(s), p.r_cut, e_cut, e, w);
+    };
     auto row = [&](int i) {
         const int n = N - 1 - i;
+        uint64_t mask = 0;  // bit t: pair (i, i + 1 + t) inside the cutoff
+        for (int t = 0; t < n; ++t) {
+            const double s = sq(i, i + 1 + t);
+            const bool core = as_f32 ? (float)s <= T.core32 : s <= T.core64;
+            const bool cut = as_f32 ? (float)s <= T.cut32 : s <= T.cut64;
+            hit |= core;
+            if (cut) mask |= (uint64_t)1 << t;
+        }
         double re = 0.0, rw = 0.0;
-        uint64_t mask = 0;
         if (n < 8) {
-            for (int t = 0; t < n; ++t) {
+            for (uint64_t b = mask; b; b &= b - 1) {
                 double e, w;
-                pair(i, i + 1 + t, e, w, mask);
+                term(i, i + 1 + __builtin_ctzll(b), e, w);
                 re += e;
                 rw += w;
             }
         } else {
+            const int nfull = n - (n % 8);
+            const uint64_t body = nfull >= 64 ? ~0ull : (((uint64_t)1 << nfull) - 1);
             double ae[8], aw[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) pair(i, i + 1 + j, ae[j], aw[j], mask);
-            const int nfull = n - (n % 8);
-            for (int t0 = 8; t0 < nfull; t0 += 8) {
+            for (int k = 0; k < 8; ++k) ae[k] = aw[k] = 0.0;
+            for (uint64_t b = mask & body; b; b &= b - 1) {
+                const int t = __builtin_ctzll(b);
+                double e, w;
+                term(i, i + 1 + t, e, w);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    double e, w;
-                    pair(i, i + 1 + t0 + j, e, w, mask);
-                    ae[j] += e;
-                    aw[j] += w;
-                }
+                for (int k = 0; k < 8; ++k)
+                    if ((t & 7) == k) {
+                        ae[k] += e;
+                        aw[k] += w;
+                    }
             }
             re = ((ae[0] + ae[1]) + (ae[2] + ae[3])) + ((ae[4] + ae[5]) + (ae[6] + ae[7]));
             rw = ((aw[0] + aw[1]) + (aw[2] + aw[3])) + ((aw[4] + aw[5]) + (aw[6] + aw[7]));
-            for (int t = nfull; t < n; ++t) {
+            for (uint64_t b = mask & ~body; b; b &= b - 1) {
                 double e, w;
-                pair(i, i + 1 + t, e, w, mask);
+                term(i, i + 1 + __builtin_ctzll(b), e, w);
                 re += e;
                 rw += w;
             }
         }
+        if (i + 1 < 64) mask <<= (i + 1);  // neighbour mask: bit j of word i
+        else mask = 0;
         se[wid][hh][i] = re;
         sw[wid][hh][i] = rw;
         if (nbr) nbr[c * N + i] = mask;
