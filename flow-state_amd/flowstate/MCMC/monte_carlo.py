@@ -94,7 +94,9 @@ class MonteCarlo:
             raise RuntimeError("set_nf_model() first")
         cfg = self._as_config(config).reshape(1, self.num_particles, 2)
         acc = self._b.nf_big_move(torch.from_numpy(cfg))  # energy and accepted state in the config's dtype
-        return bool(acc[0].item())
+        ok = bool(acc[0].item())
+        self._b.check_errors()
+        return ok
 
     def _log(self, message, level="info"):
         """monte_carlo.py:129-146: the logger's method for `level`, else print."""

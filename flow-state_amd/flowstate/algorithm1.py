@@ -160,6 +160,7 @@ def testing_phase(bmc: BatchedMonteCarlo, test_configs, attempts, interval, samp
         t = tuple(x[o:o + C] for x in terms) if bmc.model is not None else None
         acc.append(bmc.nf_big_move(cfg[a * C:(a + 1) * C], terms=t).clone())
     accepts = torch.stack(acc, 1) if acc else torch.zeros((C, 0), dtype=torch.uint8, device=bmc.device)
+    bmc.check_errors()  # a NaN discriminant or a wide-path hand-off timeout in any pass raises
     p, s, tot, att, nacc = acceptance_history(accepts, int(interval), total_mcmc_steps, big_move_attempts,
                                               big_move_accepts)
     return TestingResult(accepts, snaps, p, s, tot, att, nacc)

@@ -184,6 +184,7 @@ class Algorithm2:
 
             dist.all_reduce(n, group=self.group)
         p = int(n.item()) / (self.bmc.C * self.world)
+        self.bmc.check_errors()
         self.p_acc_history.append(p)
         self.mcmc_steps_history.append(self.total_mcmc_steps)
         return acc, p
