@@ -191,6 +191,8 @@ def _run_stack_here(layers, x, direction, cache, base_log_prob, err=None):
     _launch_stack(L, dims, packed, x, B, out, ld, own, direction, base_log_prob)
     if direction == "forward":
         if int(own.item()) & 4:  # a column-split hand-off gave up: the same pass on trunk 3
+            # (fs_set_wide_trunk16 is process-wide: a pass another thread launches meanwhile
+            # may take trunk 3 too, with the same results; every trunk is bit-identical)
             own.zero_()
             prev = L.fs_set_wide_trunk16(3)
             try:
