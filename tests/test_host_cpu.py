@@ -221,3 +221,26 @@ def test_device_spline_with_uninstantiated_bins_raises():
     x = torch.linspace(-2.0, 2.0, 4)
     out, lad = AF.circular_rqs(x, uw, uw, ud, 3.0, False)
     assert out.shape == x.shape and torch.isfinite(lad).all()
+
+
+def test_column_split_xcd_placement_is_a_bijection():
+    """wide_trunk16g_kernel's block -> (tile, workgroup) map with a tile's workgroups at equal
+    blockIdx.x % 8 (FS_GSPLIT_XCD, flow_kernels.hip): over its grid of ceil(T/8)*8*G blocks
+    every (tile < T, g < G) appears exactly once, the tile's G blocks share b % 8, and every
+    other block is a slot past the last tile (it exits before any barrier or hand-off)."""
+    G = 4
+    for T in range(1, 33):
+        grid = (T + 7) // 8 * 8 * G
+        seen = {}
+        idle = 0
+        for b in range(grid):
+            xb, yb = b & 7, b >> 3
+            g, t = yb % G, (yb // G) * 8 + xb
+            if t >= T:
+                idle += 1
+                continue
+            assert (t, g) not in seen
+            seen[(t, g)] = b
+        assert len(seen) == T * G and idle == grid - T * G
+        for t in range(T):
+            assert len({seen[(t, g)] % 8 for g in range(G)}) == 1
