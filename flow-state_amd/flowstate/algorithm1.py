@@ -19,12 +19,13 @@ the reference dtype each snapshot had (a run's state turns float32 after its fir
 accepted big move, monte_carlo.py:289-292); tuples and files are produced only when
 asked for.
 """
+import copy
 from dataclasses import dataclass, field
 
 import numpy as np
 import torch
 
-from . import analysis, io
+from . import _lib, analysis, io
 from .MCMC.batched import BatchedMonteCarlo
 
 
@@ -92,6 +93,7 @@ class TestingResult:
     total_mcmc_steps: int = 0
     big_move_attempts: int = 0
     big_move_accepts: int = 0
+    speculated: int = 0                    # attempts whose local moves ran ahead of the big move before
 
     def testing_configs(self):
         """(C, A*S, N, 2) f64: every run's mc_run.testing_samples in order."""
@@ -133,11 +135,73 @@ def acceptance_history(accepts, interval, total_mcmc_steps=0, big_move_attempts=
             big_move_accepts + int(acc.sum()))
 
 
+class _Speculator:
+    """The next attempt's local moves, run ahead on a side stream while the big move runs.
+
+    A big move that no chain accepts leaves every chain as it was except for what the
+    reject itself does (mh_accept_kernel / nf_big_move, monte_carlo.py:264-303): one
+    Generator.random() draw (a reject always draws: ratio < 1 or NaN), attempts += 1,
+    and the running energy / virial set to those of the current state (:299-301).  So the
+    next `interval` local moves can start from a shadow copy of the chains with exactly
+    those changes made before the big move is decided.  If no chain accepted, the shadow
+    is the result (bit-identical: the same kernels on the same inputs); if any chain
+    accepted, it is dropped and the local moves run again on the real state.  The
+    reference's acceptance rate in this phase is well under 1 %, so the local moves and
+    the big move, which each fill only a few CUs at this batch size, overlap almost
+    always."""
+
+    FIELDS = ("state", "state_is_f32", "pcg", "pcg_buf", "max_disp", "attempts", "accepted", "prev_counts")
+
+    def __init__(self, bmc):
+        self.bmc = bmc
+        self.main = torch.cuda.current_stream(bmc.device)
+        self.side = torch.cuda.Stream(device=bmc.device)
+        self.shadow = copy.copy(bmc)  # shares the physics and the flow; own chain buffers
+        for k in self.FIELDS:
+            setattr(self.shadow, k, torch.empty_like(getattr(bmc, k)))
+        self.draw = torch.empty(bmc.C, dtype=torch.float64, device=bmc.device)
+
+    def launch(self, interval, sampling_frequency):
+        """Queue the shadow local moves after everything queued on the main stream so far."""
+        b, sh = self.bmc, self.shadow
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            for k in self.FIELDS:
+                getattr(sh, k).copy_(getattr(b, k))
+            _lib.check(_lib.load().fs_pcg64_random(_lib.ptr(sh.pcg), b.C, _lib.ptr(self.draw), _lib.stream_ptr()),
+                       "fs_pcg64_random")
+            sh.attempts += 1
+            sh.E_old, sh.W_old = sh._energy_of_state()
+            return _local(sh, interval, 0, sampling_frequency)
+
+    def adopt(self, snap):
+        """No chain accepted: the shadow chains become the real ones."""
+        b, sh = self.bmc, self.shadow
+        self.main.wait_stream(self.side)
+        for t in (sh.E_old, sh.W_old, snap.xy, snap.ew, snap.is_f32):
+            if t.numel():
+                t.record_stream(self.main)  # made on the side stream, used and freed on the main one
+        for k in self.FIELDS:
+            bk, sk = getattr(b, k), getattr(sh, k)
+            setattr(b, k, sk)
+            setattr(sh, k, bk)
+        b.E_old, b.W_old = sh.E_old, sh.W_old
+        b._moved = True
+        return snap
+
+    def close(self):
+        self.main.wait_stream(self.side)
+
+
 def testing_phase(bmc: BatchedMonteCarlo, test_configs, attempts, interval, sampling_frequency,
-                  total_mcmc_steps=0, big_move_attempts=0, big_move_accepts=0):
+                  total_mcmc_steps=0, big_move_attempts=0, big_move_accepts=0, speculate=None):
     """main_algorithm_1.py:375-424 for all runs: per attempt, `interval` local moves with
     sampling, then nf_big_move with test_configs[attempt * C + run] (float32 box
-    coordinates, (>= attempts*C, N, 2), numpy or device)."""
+    coordinates, (>= attempts*C, N, 2), numpy or device).  speculate (default: on for a
+    device engine with a flow): overlap each attempt's big move with the next attempt's
+    local moves (_Speculator); the results are the same either way, but the engine's chain
+    buffers (bmc.state, bmc.pcg, ...) may afterwards be other tensors of the same shape:
+    read them from bmc after the call, not through references taken before it."""
     C = bmc.C
     cfg = torch.as_tensor(test_configs)
     if cfg.dtype != torch.float32:
@@ -145,25 +209,49 @@ def testing_phase(bmc: BatchedMonteCarlo, test_configs, attempts, interval, samp
     if cfg.shape[0] < attempts * C:
         raise IndexError(f"index {attempts * C - 1} is out of bounds for axis 0 with size {cfg.shape[0]}")
     cfg = cfg.to(bmc.device)
+    A, n, sf = int(attempts), int(interval), int(sampling_frequency)
+    if speculate is None:
+        speculate = bmc.device.type == "cuda" and bmc.model is not None
     snaps, acc = [], []
     # the test configurations' energies and log q do not depend on the chain states: one
     # launch per pass over a block of attempts (bit-identical rows), so each attempt's big
     # move runs only the current states' density pass and energy
     block = max(1, BatchedMonteCarlo.FILL_ROWS // max(1, C))
     terms, a0 = None, 0
-    for a in range(int(attempts)):
-        snaps.append(_local(bmc, int(interval), 0, int(sampling_frequency)))
-        if bmc.model is not None and a % block == 0:
-            a0, a1 = a, min(int(attempts), a + block)
-            terms = bmc.proposal_terms(cfg[a0 * C:a1 * C])
-        o = (a - a0) * C
-        t = tuple(x[o:o + C] for x in terms) if bmc.model is not None else None
-        acc.append(bmc.nf_big_move(cfg[a * C:(a + 1) * C], terms=t).clone())
+    spec = n_acc = None
+    adopted = 0
+    with _lib.on_device(bmc.device):
+        if A > 0:
+            snaps.append(_local(bmc, n, 0, sf))
+        if speculate and A > 1:
+            spec = _Speculator(bmc)
+            n_acc = int(bmc.n_accept.item())
+        try:
+            for a in range(A):
+                ahead = spec.launch(n, sf) if spec is not None and a + 1 < A else None
+                if bmc.model is not None and a % block == 0:
+                    a0, a1 = a, min(A, a + block)
+                    terms = bmc.proposal_terms(cfg[a0 * C:a1 * C])
+                o = (a - a0) * C
+                t = tuple(x[o:o + C] for x in terms) if bmc.model is not None else None
+                acc.append(bmc.nf_big_move(cfg[a * C:(a + 1) * C], terms=t).clone())
+                if a + 1 == A:
+                    break
+                if ahead is not None:
+                    k = int(bmc.n_accept.item())  # the one host synchronisation per attempt
+                    if k == n_acc:
+                        snaps.append(spec.adopt(ahead))
+                        adopted += 1
+                        continue
+                    n_acc = k
+                snaps.append(_local(bmc, n, 0, sf))
+        finally:
+            if spec is not None:
+                spec.close()
     accepts = torch.stack(acc, 1) if acc else torch.zeros((C, 0), dtype=torch.uint8, device=bmc.device)
     bmc.check_errors()  # a NaN discriminant or a wide-path hand-off timeout in any pass raises
-    p, s, tot, att, nacc = acceptance_history(accepts, int(interval), total_mcmc_steps, big_move_attempts,
-                                              big_move_accepts)
-    return TestingResult(accepts, snaps, p, s, tot, att, nacc)
+    p, s, tot, att, nacc = acceptance_history(accepts, n, total_mcmc_steps, big_move_attempts, big_move_accepts)
+    return TestingResult(accepts, snaps, p, s, tot, att, nacc, adopted)
 
 
 def well_statistics(configs, is_f32, half_box, r0=1.2):

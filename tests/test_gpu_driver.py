@@ -107,3 +107,51 @@ def test_driver_testing_phase_rejects_short_config_list():
         A1.testing_phase(bmc, f["test_configs"][:5], 2, 10, 5)
     with pytest.raises(ValueError):
         A1.testing_phase(bmc, f["test_configs"].astype(np.float64), 1, 10, 5)
+
+
+def _regime_engine(runs, N, temperature):
+    dev = torch.device("cuda", torch.cuda.current_device())
+    init = np.array([(initialise_low_left if i % 2 == 0 else initialise_low_right)(N, 0.03, 1.0)[0]
+                     for i in range(runs)])
+    hb = float(np.sqrt(N) * 1.5)
+    bmc = BatchedMonteCarlo(None, init, Physics(2 * hb, temperature=temperature), [42 + i for i in range(runs)],
+                            device=dev, initial_max_displacement=0.65)
+    A1.equilibrate(bmc, 300, 100, 50)
+    dims = OF.FlowDims(N=N, L=2, H=32, nb=1, K=5, B=hb)
+    sd = OF.random_state_dict(dims, seed=3, final_std=0.05)
+    bmc.set_model(flow_from_state_dict(sd, N, L=2, H=32, nb=1, K=5, bound=hb))
+    g = torch.Generator().manual_seed(5)
+    return bmc, hb, g
+
+
+@pytest.mark.parametrize("temperature", [1.0, 40.0])
+def test_speculative_testing_phase_is_bit_identical(temperature):
+    """testing_phase with the next attempt's local moves run ahead on a side stream
+    (algorithm1._Speculator) against the plain sequence, on two engines from the same
+    start: every accept, snapshot, dtype flag, final state, PCG64 state, counter, running
+    energy and max_displacement equal.  At T=40 many big moves accept (the speculative
+    moves are dropped and rerun), at T=1 almost none do (they are adopted)."""
+    runs, N, ATT, INT, SF = 10, 3, 12, 120, 25
+    out = []
+    for spec in (False, True):
+        bmc, hb, g = _regime_engine(runs, N, temperature)
+        cfg = ((torch.rand((ATT * runs, N, 2), generator=g, dtype=torch.float64) * 0.8 + 0.1) * 2 * hb).float()
+        res = A1.testing_phase(bmc, cfg.numpy(), ATT, INT, SF, speculate=spec)
+        torch.cuda.synchronize()
+        out.append((bmc, res))
+    (b0, r0), (b1, r1) = out
+    assert r0.speculated == 0
+    dropped = int((r0.accepts[:, :-1].sum(0) > 0).sum())
+    assert r1.speculated == ATT - 1 - dropped
+    if temperature > 1:
+        assert dropped >= 1  # the drop-and-rerun path ran
+    assert r1.speculated >= 1
+    assert torch.equal(r0.accepts, r1.accepts)
+    assert len(r0.snapshots) == len(r1.snapshots) == ATT
+    for s0, s1 in zip(r0.snapshots, r1.snapshots):
+        assert s0.steps == s1.steps
+        assert torch.equal(s0.xy, s1.xy) and torch.equal(s0.ew, s1.ew) and torch.equal(s0.is_f32, s1.is_f32)
+    for k in ("state", "state_is_f32", "pcg", "pcg_buf", "max_disp", "attempts", "accepted", "E_old", "W_old",
+              "nll_old", "n_accept"):
+        assert torch.equal(getattr(b0, k), getattr(b1, k)), k
+    assert r0.p_acc_history == r1.p_acc_history
