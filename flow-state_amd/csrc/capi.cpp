@@ -410,6 +410,41 @@ int fs_local_moves(const fs_phys *p, int64_t C, int32_t N, double *state, const 
                   "fs_local_moves");
 }
 
+int fs_local_moves_if(const uint8_t *gate, const fs_phys *p, int64_t C, int32_t N, double *state,
+                      const uint8_t *state_is_f32, double *E, double *W, uint64_t *pcg, uint64_t *pcg_buf,
+                      double *max_disp, int64_t *attempts, int64_t *accepted, int64_t *prev_counts,
+                      int64_t n_moves, int64_t step0, int32_t adjust_every, double target_acceptance,
+                      int32_t sample_every, double *samples_xy, double *samples_ew, uint8_t *accept_log,
+                      unsigned long long *n_accept, void *stream) {
+    REQUIRE(gate, "fs_local_moves_if: gate is required");
+    REQUIRE(p && C >= 0 && n_moves >= 0 && step0 >= 0 &&
+                (C == 0 || (state && E && pcg && pcg_buf && max_disp && attempts && accepted)),
+            "fs_local_moves_if: invalid arguments");
+    REQUIRE(N >= 1 && N <= fs::kMaxN, "fs_local_moves_if: N=%d outside [1, %d]", N, fs::kMaxN);
+    REQUIRE(adjust_every <= 0 || (prev_counts && target_acceptance > 0.0),
+            "fs_local_moves_if: adjust_every needs prev_counts and target_acceptance > 0");
+    REQUIRE(fs_local_samples_per_chain(step0, n_moves, sample_every) == 0 || samples_xy || samples_ew,
+            "fs_local_moves_if: sample_every needs a sample buffer");
+    return hip_rc(fs_local_moves_impl(p, C, N, state, state_is_f32, E, W, pcg, pcg_buf, max_disp, attempts, accepted,
+                                      prev_counts, n_moves, step0, adjust_every, target_acceptance, sample_every,
+                                      samples_xy, samples_ew, accept_log, n_accept, (hipStream_t)stream, gate),
+                  "fs_local_moves_if");
+}
+
+int fs_chains_copy_if(const uint8_t *gate, int64_t C, int32_t N, const fs_local_chains *src,
+                      const fs_local_chains *dst, void *stream) {
+    REQUIRE(gate && src && dst && C >= 0, "fs_chains_copy_if: invalid arguments");
+    REQUIRE(N >= 1 && N <= fs::kMaxN, "fs_chains_copy_if: N=%d outside [1, %d]", N, fs::kMaxN);
+    REQUIRE(C == 0 || (src->state && dst->state && src->E && dst->E && src->pcg && dst->pcg && src->pcg_buf &&
+                       dst->pcg_buf && src->max_disp && dst->max_disp && src->attempts && dst->attempts &&
+                       src->accepted && dst->accepted),
+            "fs_chains_copy_if: missing arrays");
+    REQUIRE(!src->state_is_f32 == !dst->state_is_f32 && !src->W == !dst->W &&
+                !src->prev_counts == !dst->prev_counts,
+            "fs_chains_copy_if: src and dst must have the same optional arrays");
+    return hip_rc(fs_chains_copy_if_impl(gate, C, N, src, dst, (hipStream_t)stream), "fs_chains_copy_if");
+}
+
 int fs_adjust_displacement(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,
                            int64_t *prev_counts, double target_acceptance, void *stream) {
     REQUIRE(C >= 0 && target_acceptance > 0.0 && (C == 0 || (max_disp && attempts && accepted && prev_counts)),

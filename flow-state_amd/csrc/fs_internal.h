@@ -72,7 +72,9 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
                                int64_t *attempts, int64_t *accepted, int64_t *prev, int64_t n_moves, int64_t step0,
                                int adjust_every, double target, int sample_every, double *samples_xy,
                                double *samples_ew, uint8_t *accept_log, unsigned long long *n_accept,
-                               hipStream_t st);
+                               hipStream_t st, const uint8_t *gate = nullptr);
+hipError_t fs_chains_copy_if_impl(const uint8_t *gate, int64_t C, int N, const fs_local_chains *src,
+                                  const fs_local_chains *dst, hipStream_t st);
 
 void fs_set_error(const char *fmt, ...);
 

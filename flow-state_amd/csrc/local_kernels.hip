@@ -47,6 +47,7 @@ struct LocalArgs {
     uint8_t *accept_log;
     unsigned long long *n_accept;
     PairThresh T;  // squared-distance / min-image thresholds (physics_device.h)
+    const uint8_t *gate;  // nullable: the launch does nothing when *gate == 0
 };
 
 constexpr int kLocalWaves = 4;
@@ -167,6 +168,7 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
     const int sb = g * SLOTS;            // this chain's slot base
     const int64_t c = ((int64_t)blockIdx.x * kLocalWaves + wid) * G + g;
     if (c >= a.C) return;  // whole groups leave; only group-internal shuffles below
+    if (a.gate && *a.gate == 0) return;  // (launch-uniform)
     const int N = a.N;
     const fs_phys &P = a.p;
     const bool f32 = a.is_f32 && a.is_f32[c];
@@ -416,12 +418,12 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
                                int64_t *attempts, int64_t *accepted, int64_t *prev, int64_t n_moves, int64_t step0,
                                int adjust_every, double target, int sample_every, double *samples_xy,
                                double *samples_ew, uint8_t *accept_log, unsigned long long *n_accept,
-                               hipStream_t st) {
+                               hipStream_t st, const uint8_t *gate) {
     if (C <= 0 || n_moves <= 0) return hipSuccess;
     LocalArgs a{*p,       C,         N,        state,      is_f32,     E,          W,
                 pcg,      pcg_buf,   max_disp, attempts,   accepted,   prev,       n_moves,
                 step0,    adjust_every, target, sample_every, fs_local_samples_per_chain(step0, n_moves, sample_every),
-                samples_xy, samples_ew, accept_log, n_accept, fs_pair_thresh(*p)};
+                samples_xy, samples_ew, accept_log, n_accept, fs_pair_thresh(*p), gate};
     // lanes per chain x particles per lane (FS_LOCAL_LAYOUT=LPCxPPL overrides, for A/B runs).
     // Measured at 65536 chains x 1000 moves (sparse in-cutoff sums): N=64 8x8 2.41 G moves/s
     // (16x4 1.88 G, 64x1 1.06 G, 4x16 1.69 G: register-limited); N=32 4x8 4.04 G (8x4 3.20 G);
@@ -457,6 +459,36 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
     FS_LCASE(4, 8) FS_LCASE(4, 4) FS_LCASE(1, 4) FS_LCASE(1, 8) FS_LCASE(2, 4) FS_LCASE(4, 1)
 #undef FS_LCASE
     return hipErrorInvalidValue;
+}
+
+// dst chain c := src chain c for every chain when *gate != 0 (one thread per chain; the
+// Algorithm-1 pipeline's fix-up after a big move that some chain accepted)
+__global__ void chains_copy_if_kernel(const uint8_t *gate, int64_t C, int N, fs_local_chains src,
+                                      fs_local_chains dst) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C || *gate == 0) return;
+    for (int j = 0; j < 2 * N; ++j) dst.state[c * 2 * N + j] = src.state[c * 2 * N + j];
+    if (src.state_is_f32) dst.state_is_f32[c] = src.state_is_f32[c];
+    dst.E[c] = src.E[c];
+    if (src.W) dst.W[c] = src.W[c];
+    for (int i = 0; i < 4; ++i) dst.pcg[4 * c + i] = src.pcg[4 * c + i];
+    dst.pcg_buf[2 * c] = src.pcg_buf[2 * c];
+    dst.pcg_buf[2 * c + 1] = src.pcg_buf[2 * c + 1];
+    dst.max_disp[c] = src.max_disp[c];
+    dst.attempts[c] = src.attempts[c];
+    dst.accepted[c] = src.accepted[c];
+    if (src.prev_counts) {
+        dst.prev_counts[2 * c] = src.prev_counts[2 * c];
+        dst.prev_counts[2 * c + 1] = src.prev_counts[2 * c + 1];
+    }
+}
+
+hipError_t fs_chains_copy_if_impl(const uint8_t *gate, int64_t C, int N, const fs_local_chains *src,
+                                  const fs_local_chains *dst, hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    hipLaunchKernelGGL(chains_copy_if_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, gate, C, N, *src,
+                       *dst);
+    return hipGetLastError();
 }
 
 hipError_t fs_adjust_displacement_impl(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,

@@ -47,6 +47,12 @@ class GemmF32(ctypes.Structure):
                 ("C", ctypes.c_void_p), ("ldc", ctypes.c_int64), ("rowsum_a", ctypes.c_void_p)]
 
 
+class LocalChains(ctypes.Structure):
+    """fs_local_chains (include/flowstate.h): the per-chain arrays of fs_local_moves."""
+    _fields_ = [(k, ctypes.c_void_p) for k in ("state", "state_is_f32", "E", "W", "pcg", "pcg_buf", "max_disp",
+                                               "attempts", "accepted", "prev_counts")]
+
+
 class BnIn(ctypes.Structure):
     """fs_bn_in (include/flowstate.h): BatchNorm1d (train) + ReLU on fs_linear_f32_ex's A."""
     _fields_ = [("stats", ctypes.c_void_p), ("tiles", ctypes.c_int64), ("rows", ctypes.c_int64),
@@ -107,6 +113,10 @@ _SIGS = {
     "fs_nf_mh_step_banked": (ctypes.c_int, [_D, _P, _PH, _I64, _I64, _I64] + [_P] * 12 + [ctypes.c_int, _P, _P]),
     "fs_local_moves": (ctypes.c_int, [_PH, _I64, ctypes.c_int32] + [_P] * 10
                        + [_I64, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_int32] + [_P] * 5),
+    "fs_local_moves_if": (ctypes.c_int, [_P, _PH, _I64, ctypes.c_int32] + [_P] * 10
+                          + [_I64, _I64, ctypes.c_int32, ctypes.c_double, ctypes.c_int32] + [_P] * 5),
+    "fs_chains_copy_if": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.POINTER(LocalChains),
+                                         ctypes.POINTER(LocalChains), _P]),
     "fs_local_samples_per_chain": (_I64, [_I64, _I64, ctypes.c_int32]),
     "fs_adjust_displacement": (ctypes.c_int, [_I64, _P, _P, _P, _P, ctypes.c_double, _P]),
     "fs_rqs_forward": (ctypes.c_int, [_I64, ctypes.c_int32, ctypes.c_int32] + [_P] * 4 + [ctypes.c_double]

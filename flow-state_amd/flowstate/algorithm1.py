@@ -20,6 +20,7 @@ accepted big move, monte_carlo.py:289-292); tuples and files are produced only w
 asked for.
 """
 import copy
+import ctypes
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -93,7 +94,7 @@ class TestingResult:
     total_mcmc_steps: int = 0
     big_move_attempts: int = 0
     big_move_accepts: int = 0
-    speculated: int = 0                    # attempts whose local moves ran ahead of the big move before
+    speculated: int = 0                    # attempts whose successor kept the speculative local moves
 
     def testing_configs(self):
         """(C, A*S, N, 2) f64: every run's mc_run.testing_samples in order."""
@@ -142,15 +143,17 @@ class _Speculator:
     reject itself does (mh_accept_kernel / nf_big_move, monte_carlo.py:264-303): one
     Generator.random() draw (a reject always draws: ratio < 1 or NaN), attempts += 1,
     and the running energy / virial set to those of the current state (:299-301).  So the
-    next `interval` local moves can start from a shadow copy of the chains with exactly
-    those changes made before the big move is decided.  If no chain accepted, the shadow
-    is the result (bit-identical: the same kernels on the same inputs); if any chain
-    accepted, it is dropped and the local moves run again on the real state.  The
-    reference's acceptance rate in this phase is well under 1 %, so the local moves and
-    the big move, which each fill only a few CUs at this batch size, overlap almost
-    always."""
+    next `interval` local moves can start, before the big move is decided, from a shadow
+    copy of the chains with exactly those changes made (begin).  After the big move
+    (finish), a device byte says whether any chain accepted; only then do
+    fs_chains_copy_if / fs_local_moves_if redo the local moves from the real chains, and
+    the shadow becomes the real chains either way: the same kernels on the same inputs,
+    so the results are bit-identical, and no step waits for the host.  The reference's
+    acceptance rate in this phase is well under 1 %, so the local moves and the big move,
+    which each fill only a few CUs at this batch size, overlap almost always."""
 
-    FIELDS = ("state", "state_is_f32", "pcg", "pcg_buf", "max_disp", "attempts", "accepted", "prev_counts")
+    FIELDS = ("state", "state_is_f32", "pcg", "pcg_buf", "max_disp", "attempts", "accepted", "prev_counts",
+              "E_old", "W_old")
 
     def __init__(self, bmc):
         self.bmc = bmc
@@ -160,34 +163,58 @@ class _Speculator:
         for k in self.FIELDS:
             setattr(self.shadow, k, torch.empty_like(getattr(bmc, k)))
         self.draw = torch.empty(bmc.C, dtype=torch.float64, device=bmc.device)
+        self.L = _lib.load()
 
-    def launch(self, interval, sampling_frequency):
-        """Queue the shadow local moves after everything queued on the main stream so far."""
-        b, sh = self.bmc, self.shadow
+    @staticmethod
+    def _chains(m):
+        return _lib.LocalChains(*(getattr(m, k).data_ptr() for k in (
+            "state", "state_is_f32", "E_old", "W_old", "pcg", "pcg_buf", "max_disp", "attempts", "accepted",
+            "prev_counts")))
+
+    def _moves(self, m, n, sf, gate=None):
+        args = (m.phys.c, m.C, m.N, _lib.ptr(m.state), _lib.ptr(m.state_is_f32), _lib.ptr(m.E_old),
+                _lib.ptr(m.W_old), _lib.ptr(m.pcg), _lib.ptr(m.pcg_buf), _lib.ptr(m.max_disp), _lib.ptr(m.attempts),
+                _lib.ptr(m.accepted), _lib.ptr(m.prev_counts), n, 0, 0, m.target_acceptance, sf, _lib.ptr(self.xy),
+                _lib.ptr(self.ew), None, None, _lib.stream_ptr())
+        if gate is None:
+            _lib.check(self.L.fs_local_moves(*args), "fs_local_moves")
+        else:
+            _lib.check(self.L.fs_local_moves_if(_lib.ptr(gate), *args), "fs_local_moves_if")
+
+    def begin(self, n, sf):
+        """Before the big move: copy the chains (main stream, ahead of the big move's
+        writes), then on the side stream the local moves that follow a reject."""
+        b, sh, L = self.bmc, self.shadow, self.L
+        torch._foreach_copy_([getattr(sh, k) for k in self.FIELDS[:8]], [getattr(b, k) for k in self.FIELDS[:8]])
+        self.n0 = b.n_accept.clone()
+        S = L.fs_local_samples_per_chain(0, n, sf)
+        self.steps = [s for s in range(1, n + 1) if sf and s % sf == 0]
+        self.xy = torch.empty((b.C, S, b.N, 2), dtype=torch.float64, device=b.device)
+        self.ew = torch.empty((b.C, S, 2), dtype=torch.float64, device=b.device)
         self.side.wait_stream(self.main)
         with torch.cuda.stream(self.side):
-            for k in self.FIELDS:
-                getattr(sh, k).copy_(getattr(b, k))
-            _lib.check(_lib.load().fs_pcg64_random(_lib.ptr(sh.pcg), b.C, _lib.ptr(self.draw), _lib.stream_ptr()),
-                       "fs_pcg64_random")
+            st = _lib.stream_ptr()
+            _lib.check(L.fs_pcg64_random(_lib.ptr(sh.pcg), b.C, _lib.ptr(self.draw), st), "fs_pcg64_random")
             sh.attempts += 1
-            sh.E_old, sh.W_old = sh._energy_of_state()
-            return _local(sh, interval, 0, sampling_frequency)
+            _lib.check(L.fs_energy_state(b.phys.c, _lib.ptr(sh.state), _lib.ptr(sh.state_is_f32), b.C, b.N,
+                                         _lib.ptr(sh.E_old), _lib.ptr(sh.W_old), st), "fs_energy_state")
+            self._moves(sh, n, sf)
 
-    def adopt(self, snap):
-        """No chain accepted: the shadow chains become the real ones."""
+    def finish(self, n, sf):
+        """After the big move: redo the local moves from the real chains if any chain
+        accepted (decided on the device), then swap the shadow in.  Returns the Snapshots."""
         b, sh = self.bmc, self.shadow
+        gate = b.n_accept != self.n0
         self.main.wait_stream(self.side)
-        for t in (sh.E_old, sh.W_old, snap.xy, snap.ew, snap.is_f32):
-            if t.numel():
-                t.record_stream(self.main)  # made on the side stream, used and freed on the main one
+        _lib.check(self.L.fs_chains_copy_if(_lib.ptr(gate), b.C, b.N, ctypes.byref(self._chains(b)),
+                                            ctypes.byref(self._chains(sh)), _lib.stream_ptr()), "fs_chains_copy_if")
+        self._moves(sh, n, sf, gate)
         for k in self.FIELDS:
             bk, sk = getattr(b, k), getattr(sh, k)
             setattr(b, k, sk)
             setattr(sh, k, bk)
-        b.E_old, b.W_old = sh.E_old, sh.W_old
         b._moved = True
-        return snap
+        return Snapshots(self.steps, self.xy, self.ew, b.state_is_f32.bool().clone())
 
     def close(self):
         self.main.wait_stream(self.side)
@@ -218,37 +245,30 @@ def testing_phase(bmc: BatchedMonteCarlo, test_configs, attempts, interval, samp
     # move runs only the current states' density pass and energy
     block = max(1, BatchedMonteCarlo.FILL_ROWS // max(1, C))
     terms, a0 = None, 0
-    spec = n_acc = None
-    adopted = 0
+    spec = None
     with _lib.on_device(bmc.device):
         if A > 0:
             snaps.append(_local(bmc, n, 0, sf))
         if speculate and A > 1:
             spec = _Speculator(bmc)
-            n_acc = int(bmc.n_accept.item())
         try:
             for a in range(A):
-                ahead = spec.launch(n, sf) if spec is not None and a + 1 < A else None
+                if spec is not None and a + 1 < A:
+                    spec.begin(n, sf)
                 if bmc.model is not None and a % block == 0:
                     a0, a1 = a, min(A, a + block)
                     terms = bmc.proposal_terms(cfg[a0 * C:a1 * C])
                 o = (a - a0) * C
                 t = tuple(x[o:o + C] for x in terms) if bmc.model is not None else None
                 acc.append(bmc.nf_big_move(cfg[a * C:(a + 1) * C], terms=t).clone())
-                if a + 1 == A:
-                    break
-                if ahead is not None:
-                    k = int(bmc.n_accept.item())  # the one host synchronisation per attempt
-                    if k == n_acc:
-                        snaps.append(spec.adopt(ahead))
-                        adopted += 1
-                        continue
-                    n_acc = k
-                snaps.append(_local(bmc, n, 0, sf))
+                if a + 1 < A:
+                    snaps.append(spec.finish(n, sf) if spec is not None else _local(bmc, n, 0, sf))
         finally:
             if spec is not None:
                 spec.close()
     accepts = torch.stack(acc, 1) if acc else torch.zeros((C, 0), dtype=torch.uint8, device=bmc.device)
+    # attempts whose successor's local moves were the speculative ones (no chain accepted)
+    adopted = int((accepts[:, :-1].sum(0) == 0).sum()) if spec is not None else 0
     bmc.check_errors()  # a NaN discriminant or a wide-path hand-off timeout in any pass raises
     p, s, tot, att, nacc = acceptance_history(accepts, n, total_mcmc_steps, big_move_attempts, big_move_accepts)
     return TestingResult(accepts, snaps, p, s, tot, att, nacc, adopted)

@@ -613,6 +613,36 @@ int fs_local_moves(const fs_phys *p, int64_t C, int32_t N, double *state, const 
                    double *samples_xy, double *samples_ew, uint8_t *accept_log,
                    unsigned long long *n_accept, void *stream);
 
+/* fs_local_moves that does nothing unless *gate != 0 (gate: one device byte, read by
+ * the kernel, so the decision needs no host round trip).  Not in the reference: the
+ * Algorithm-1 testing phase (main_algorithm_1.py:375-424) runs each attempt's local
+ * moves ahead of the previous big move on a second stream, on a copy of the chains that
+ * assumes every chain rejects; when some chain accepted, this reruns them from the real
+ * chains (flowstate.algorithm1._Speculator). */
+int fs_local_moves_if(const uint8_t *gate, const fs_phys *p, int64_t C, int32_t N, double *state,
+                      const uint8_t *state_is_f32, double *E, double *W, uint64_t *pcg, uint64_t *pcg_buf,
+                      double *max_disp, int64_t *attempts, int64_t *accepted, int64_t *prev_counts,
+                      int64_t n_moves, int64_t step0, int32_t adjust_every, double target_acceptance,
+                      int32_t sample_every, double *samples_xy, double *samples_ew, uint8_t *accept_log,
+                      unsigned long long *n_accept, void *stream);
+
+/* The per-chain arrays fs_local_moves reads and writes (state [C][N][2], the rest [C],
+ * pcg [C][4], pcg_buf / prev_counts [C][2]); state_is_f32, W and prev_counts nullable
+ * (then skipped). */
+typedef struct fs_local_chains {
+    double *state;
+    uint8_t *state_is_f32;
+    double *E, *W;
+    uint64_t *pcg, *pcg_buf;
+    double *max_disp;
+    int64_t *attempts, *accepted, *prev_counts;
+} fs_local_chains;
+
+/* dst := src, every array of every chain, when *gate != 0 (device byte); nothing
+ * otherwise.  The fix-up step of the pipeline above. */
+int fs_chains_copy_if(const uint8_t *gate, int64_t C, int32_t N, const fs_local_chains *src,
+                      const fs_local_chains *dst, void *stream);
+
 /* MonteCarlo.adjust_displacement (monte_carlo.py:375-403) for C chains, arrays
  * as in fs_local_moves. */
 int fs_adjust_displacement(int64_t C, double *max_disp, const int64_t *attempts, const int64_t *accepted,

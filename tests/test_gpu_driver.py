@@ -145,7 +145,8 @@ def test_speculative_testing_phase_is_bit_identical(temperature):
     assert r1.speculated == ATT - 1 - dropped
     if temperature > 1:
         assert dropped >= 1  # the drop-and-rerun path ran
-    assert r1.speculated >= 1
+    else:
+        assert r1.speculated >= 1  # the adopt path ran
     assert torch.equal(r0.accepts, r1.accepts)
     assert len(r0.snapshots) == len(r1.snapshots) == ATT
     for s0, s1 in zip(r0.snapshots, r1.snapshots):

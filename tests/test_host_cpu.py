@@ -95,6 +95,15 @@ def test_abi_rejects_invalid_arguments_before_touching_the_device():
     rc = L.fs_local_moves(ph, 4, 16, one, None, one, None, one, one, one, one, one, None, 10, 0, 50, 0.5, 0, None,
                           None, None, None, None)
     assert rc == -1 and b"adjust_every" in L.fs_last_error()
+    rc = L.fs_local_moves_if(None, ph, 4, 16, one, None, one, None, one, one, one, one, one, None, 10, 0, 0, 0.5, 0,
+                             None, None, None, None, None)
+    assert rc == -1 and b"gate" in L.fs_last_error()
+    full = _lib.LocalChains(*([1] * 10))
+    part = _lib.LocalChains(*([1] * 9 + [None]))
+    rc = L.fs_chains_copy_if(one, 4, 3, ctypes.byref(full), ctypes.byref(part), None)
+    assert rc == -1 and b"same optional arrays" in L.fs_last_error()
+    rc = L.fs_chains_copy_if(one, 4, 3, ctypes.byref(_lib.LocalChains()), ctypes.byref(full), None)
+    assert rc == -1 and b"missing arrays" in L.fs_last_error()
     rc = L.fs_rqs_forward(8, 7, 0, one, one, one, one, 3.0, one, one, None, None)
     assert rc == -1 and b"K=7" in L.fs_last_error()
     rc = L.fs_pair_hist(one, 1, 4, 300, 5.0, one, 10, one, None)
