@@ -163,6 +163,7 @@ class _Speculator:
         for k in self.FIELDS:
             setattr(self.shadow, k, torch.empty_like(getattr(bmc, k)))
         self.draw = torch.empty(bmc.C, dtype=torch.float64, device=bmc.device)
+        self.one = torch.ones(1, dtype=torch.uint8, device=bmc.device)  # an always-open gate: one copy launch
         self.L = _lib.load()
 
     @staticmethod
@@ -185,7 +186,8 @@ class _Speculator:
         """Before the big move: copy the chains (main stream, ahead of the big move's
         writes), then on the side stream the local moves that follow a reject."""
         b, sh, L = self.bmc, self.shadow, self.L
-        torch._foreach_copy_([getattr(sh, k) for k in self.FIELDS[:8]], [getattr(b, k) for k in self.FIELDS[:8]])
+        _lib.check(L.fs_chains_copy_if(_lib.ptr(self.one), b.C, b.N, ctypes.byref(self._chains(b)),
+                                       ctypes.byref(self._chains(sh)), _lib.stream_ptr()), "fs_chains_copy_if")
         self.n0 = b.n_accept.clone()
         S = L.fs_local_samples_per_chain(0, n, sf)
         self.steps = [s for s in range(1, n + 1) if sf and s % sf == 0]
@@ -214,7 +216,7 @@ class _Speculator:
             setattr(b, k, sk)
             setattr(sh, k, bk)
         b._moved = True
-        return Snapshots(self.steps, self.xy, self.ew, b.state_is_f32.bool().clone())
+        return Snapshots(self.steps, self.xy, self.ew, b.state_is_f32.bool())  # (a new tensor: uint8 -> bool)
 
     def close(self):
         self.main.wait_stream(self.side)
