@@ -239,8 +239,11 @@ def testing_phase(bmc: BatchedMonteCarlo, test_configs, attempts, interval, samp
         raise IndexError(f"index {attempts * C - 1} is out of bounds for axis 0 with size {cfg.shape[0]}")
     cfg = cfg.to(bmc.device)
     A, n, sf = int(attempts), int(interval), int(sampling_frequency)
-    # (speculate=True asks for it; it still needs a device engine with a flow)
-    speculate = (speculate is None or bool(speculate)) and bmc.device.type == "cuda" and bmc.model is not None
+    # (speculate=True asks for it; it still needs a device engine with a flow, and local moves
+    # between the big moves: the shadow assumes the reject of a big move after local moves,
+    # which re-derives the running energy, monte_carlo.py:299-301)
+    speculate = ((speculate is None or bool(speculate)) and bmc.device.type == "cuda" and bmc.model is not None
+                 and n > 0)
     snaps, acc = [], []
     # the test configurations' energies and log q do not depend on the chain states: one
     # launch per pass over a block of attempts (bit-identical rows), so each attempt's big

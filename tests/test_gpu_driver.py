@@ -156,3 +156,27 @@ def test_speculative_testing_phase_is_bit_identical(temperature):
               "nll_old", "n_accept"):
         assert torch.equal(getattr(b0, k), getattr(b1, k)), k
     assert r0.p_acc_history == r1.p_acc_history
+
+
+@pytest.mark.parametrize("ATT,INT,SF", [(1, 50, 10), (2, 0, 0), (5, 37, 0), (6, 40, 7)])
+def test_speculative_testing_phase_edge_cases(ATT, INT, SF):
+    """Speculation on / off agree for one attempt (no speculation), no local moves, no
+    snapshots and snapshot schedules that do not divide the interval."""
+    runs, N = 10, 3
+    out = []
+    for spec in (False, True):
+        bmc, hb, g = _regime_engine(runs, N, 5.0)
+        cfg = ((torch.rand((ATT * runs, N, 2), generator=g, dtype=torch.float64) * 0.8 + 0.1) * 2 * hb).float()
+        res = A1.testing_phase(bmc, cfg.numpy(), ATT, INT, SF, speculate=spec)
+        torch.cuda.synchronize()
+        out.append((bmc, res))
+    (b0, r0), (b1, r1) = out
+    assert torch.equal(r0.accepts, r1.accepts)
+    assert len(r0.snapshots) == len(r1.snapshots) == ATT
+    for s0, s1 in zip(r0.snapshots, r1.snapshots):
+        assert s0.steps == s1.steps
+        assert s0.xy.shape == s1.xy.shape and torch.equal(s0.xy, s1.xy) and torch.equal(s0.ew, s1.ew)
+        assert torch.equal(s0.is_f32, s1.is_f32)
+    for k in ("state", "state_is_f32", "pcg", "pcg_buf", "max_disp", "attempts", "accepted", "E_old", "W_old",
+              "nll_old", "n_accept"):
+        assert torch.equal(getattr(b0, k), getattr(b1, k)), k
