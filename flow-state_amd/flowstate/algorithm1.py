@@ -148,9 +148,10 @@ class _Speculator:
     (finish), a device byte says whether any chain accepted; only then do
     fs_chains_copy_if / fs_local_moves_if redo the local moves from the real chains, and
     the shadow becomes the real chains either way: the same kernels on the same inputs,
-    so the results are bit-identical, and no step waits for the host.  The reference's
-    acceptance rate in this phase is well under 1 %, so the local moves and the big move,
-    which each fill only a few CUs at this batch size, overlap almost always."""
+    so the results are bit-identical, and no step waits for the host.  The gain is in the
+    attempts that follow a big move no chain accepted (0.2-0.3 % acceptance in the bench's
+    regime: nearly all of them); there the local moves and the big move, which each fill
+    only a few CUs at this batch size, run side by side."""
 
     FIELDS = ("state", "state_is_f32", "pcg", "pcg_buf", "max_disp", "attempts", "accepted", "prev_counts",
               "E_old", "W_old")
