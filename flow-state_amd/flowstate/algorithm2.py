@@ -79,7 +79,12 @@ class Algorithm2:
     # ------------------------------------------------------------------
     def production(self):
         """:399-417 — returns this rank's Snapshots; sets the (gathered) training set."""
-        snap, local = A1.production(self.bmc, self.production_runs, self.sf)
+        snap, _ = A1.production(self.bmc, self.production_runs, self.sf)
+        return self._take(snap)
+
+    def _take(self, snap):
+        """The training set of a production phase's snapshots (A1.production's samples)."""
+        local = snap.xy.reshape(-1, self.bmc.N, 2) - self.bmc.phys.half_width
         self.total_mcmc_steps += self.production_runs * self.bmc.C * self.world
         data = parallel.all_gather_configs(local.contiguous(), group=self.group)
         data = data.to(torch.float32).reshape(data.shape[0], -1)  # get_dataloader: float32 (M, N*dim)
@@ -195,3 +200,36 @@ class Algorithm2:
         loss = self.train()
         acc, p = self.refeed()
         return snap, loss, acc, p
+
+    def run(self, cycles, speculate=None):
+        """`cycles` update cycles in the reference's loop (main_algorithm_2.py:393-570),
+        returning each cycle's (snapshots, loss, accepted, p_acc) as cycle() does.
+        speculate (default: on for a device engine): the next cycle's production runs on a
+        second stream during this cycle's training, from a copy of the runs with what a
+        refeed that every run rejects does to them (one Generator.random() draw, attempts +
+        1, the running energy re-derived; algorithm1._Speculator); after the refeed a device
+        byte says whether any run accepted, and only then does the production run again
+        from the real runs.  The results are those of `cycles` calls of cycle()."""
+        from . import _lib
+
+        bmc, n, sf = self.bmc, self.production_runs, self.sf
+        cycles = int(cycles)
+        spec = None
+        if (speculate is None or bool(speculate)) and bmc.device.type == "cuda" and n > 0 and cycles > 1:
+            spec = A1._Speculator(bmc)
+        out, ahead = [], None
+        with _lib.on_device(bmc.device):
+            try:
+                for c in range(cycles):
+                    snap = self.production() if ahead is None else self._take(ahead)
+                    more = spec is not None and c + 1 < cycles
+                    if more:
+                        spec.begin(n, sf)
+                    loss = self.train()
+                    acc, p = self.refeed()
+                    out.append((snap, loss, acc, p))
+                    ahead = spec.finish(n, sf) if more else None
+            finally:
+                if spec is not None:
+                    spec.close()
+        return out

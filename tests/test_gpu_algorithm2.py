@@ -259,3 +259,47 @@ def test_graphed_epoch_writes_nothing_after_a_nan_step():
     step.step(x)
     assert not bool(step.nan_state())
     assert not torch.equal(step._state_tensors[0], after1[0])
+
+
+def _pipeline_setup(temperature):
+    N, runs = 3, 100
+    m = _cycle_model()
+    B = float(m.flows[0].tail_bound)
+    init = np.array([(initialise_low_left if i % 2 == 0 else initialise_low_right)(N, 0.03, 1.0)[0]
+                     for i in range(runs)])
+    bmc = BatchedMonteCarlo(None, init, Physics(2 * B, temperature=temperature), [42 + i for i in range(runs)],
+                            device="cuda", initial_max_displacement=0.65)
+    bmc.local_moves(500, adjust_every=100)
+    return bmc, Algorithm2(bmc, m, batch_size=256, alpha=1.0, sampling_frequency=10, update_num_samples=1000)
+
+
+def test_run_with_speculative_production_matches_cycles():
+    """Algorithm2.run (the next cycle's production run beside this cycle's training, from
+    a copy of the runs that assumes the refeed rejects every run) against the same number
+    of plain cycle() calls from the same start: every snapshot, training set, loss, refeed
+    decision and the final runs bit-identical.  At T = 1 refeeds that no run accepts keep
+    the speculative production, at T = 50 refeeds with accepts make it run again."""
+    cycles = 3
+    kept = redone = 0
+    for T in (1.0, 50.0):
+        res = []
+        for piped in (False, True):
+            bmc, a = _pipeline_setup(T)
+            torch.manual_seed(0)
+            out = a.run(cycles) if piped else [a.cycle() for _ in range(cycles)]
+            torch.cuda.synchronize()
+            res.append((bmc, a, out))
+        (b0, a0, o0), (b1, a1, o1) = res
+        for (s0, l0, c0, p0), (s1, l1, c1, p1) in zip(o0, o1):
+            assert s0.steps == s1.steps and torch.equal(s0.xy, s1.xy) and torch.equal(s0.ew, s1.ew)
+            assert torch.equal(s0.is_f32, s1.is_f32)
+            assert l0 == l1 and p0 == p1 and torch.equal(c0, c1)
+        assert torch.equal(a0.training_data, a1.training_data)
+        assert a0.total_mcmc_steps == a1.total_mcmc_steps and a0.p_acc_history == a1.p_acc_history
+        for k in ("state", "state_is_f32", "pcg", "pcg_buf", "max_disp", "attempts", "accepted", "E_old", "W_old",
+                  "nll_old", "n_accept"):
+            assert torch.equal(getattr(b0, k), getattr(b1, k)), (T, k)
+        for p in a0.p_acc_history[:-1]:
+            kept += p == 0
+            redone += p > 0
+    assert kept >= 1 and redone >= 1, (kept, redone)
