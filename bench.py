@@ -342,8 +342,9 @@ def algorithm1_regime(attempts=1000, runs=10, N=3, interval=1000, sampling=150, 
                         f"x ({interval} local moves + 1 NF big move) per run, sample() every {sampling}, A1 flow",
             "value": n / dt, "unit": "big-move attempts/s", "local_moves_per_s": n * interval / dt,
             "seconds": dt, "big_move_acceptance": acc / n, "speculated_attempts": res.speculated,
-            "what": "main_algorithm_1.py's testing phase on the device (flowstate.algorithm1.testing_phase, each "
-                    "attempt's local moves run beside the previous big move, bit-identical); "
+            "what": "main_algorithm_1.py's testing phase on the device (flowstate.algorithm1.testing_phase: the "
+                    "local moves back to back on a side stream, each attempt's density pass on its own stream, the "
+                    "big moves on the main stream; stages after an accept run again, bit-identical); "
                     "equilibration and proposal generation untimed"}
 
 

@@ -16,6 +16,9 @@
 // 0..3 (before/after x well 0/1).  Chains are independent: no grid-level sync,
 // each group exits after its n moves.
 #include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -51,6 +54,10 @@ struct LocalArgs {
 };
 
 constexpr int kLocalWaves = 4;
+
+#ifndef FS_LOCAL_DRAW_AHEAD
+#define FS_LOCAL_DRAW_AHEAD 0  // r06: 1 measured no faster (N=3 x 10 chains 2.30 vs 2.27 ms per 1000 moves)
+#endif
 
 // adjust_displacement (monte_carlo.py:375-403) on one chain's registers
 __device__ __forceinline__ void adjust_md(double &md, int64_t att, int64_t acc, int64_t &prev_att, int64_t &prev_acc,
@@ -210,6 +217,12 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
         const double ox = bcast<LPC>(pick<PPL>(xj, pq), pl), oy = bcast<LPC>(pick<PPL>(yj, pq), pl);
         const double d0 = (pcg64_double(rng) - 0.5) * md;
         const double d1 = (pcg64_double(rng) - 0.5) * md;
+#if FS_LOCAL_DRAW_AHEAD
+        // the accept draw, when the move takes one, is the stream's next output: computed here,
+        // beside the energies instead of after them, and committed only if taken
+        uint64_t s_next[4] = {rng.s[0], rng.s[1], rng.s[2], rng.s[3]};
+        const double u_next = (double)(pcg64_next64(s_next) >> 11) * (1.0 / 9007199254740992.0);
+#endif
         double nx, ny;
         if (f32) {  // float32 row += float64 array, then float32 % np.float64 stored back
             nx = (double)(float)np_remainder((double)(float)(ox + d0), P.Lx);
@@ -339,7 +352,15 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
         bool accept;
         if (enn <= eno) accept = true;
         else if (isinf(enn)) accept = false;
-        else accept = pcg64_double(rng) < exp(-P.beta * (enn - eno));
+        else {
+#if FS_LOCAL_DRAW_AHEAD
+            accept = u_next < exp(-P.beta * (enn - eno));
+            rng.s[0] = s_next[0];
+            rng.s[1] = s_next[1];
+#else
+            accept = pcg64_double(rng) < exp(-P.beta * (enn - eno));
+#endif
+        }
         if (accept) {
             acc_n += 1;
             E += enn - eno;
@@ -413,6 +434,21 @@ int64_t fs_local_samples_per_chain(int64_t step0, int64_t n_moves, int32_t sampl
     return (step0 + n_moves) / sample_every - step0 / sample_every;
 }
 
+// the dynamic-LDS limit a launch of `bytes` needs (above the default 64 KiB), raised once
+// per kernel and device (the limit plus the kernel's static LDS must stay within 160 KiB)
+static hipError_t local_dyn_lds_once(const void *kfn, unsigned bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<const void *, int>, unsigned> done;
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+    std::lock_guard<std::mutex> g(mu);
+    unsigned &have = done[{kfn, dev}];
+    if (have >= bytes) return hipSuccess;
+    hipError_t e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) have = bytes;
+    return e;
+}
+
 hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state, const uint8_t *is_f32,
                                double *E, double *W, uint64_t *pcg, uint64_t *pcg_buf, double *max_disp,
                                int64_t *attempts, int64_t *accepted, int64_t *prev, int64_t n_moves, int64_t step0,
@@ -450,10 +486,32 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
     }
     const int64_t chains_per_block = (int64_t)kLocalWaves * (64 / lpc);
     const dim3 grid((unsigned)((C + chains_per_block - 1) / chains_per_block)), block(64 * kLocalWaves);
-#define FS_LCASE(L, Q)                                                                \
-    if (lpc == L && ppl == Q) {                                                       \
-        hipLaunchKernelGGL((local_moves_kernel<L, Q>), grid, block, 0, st, a);        \
-        return hipGetLastError();                                                     \
+    // A launch of a few workgroups (the reference's 10 runs: one) is latency-bound on its
+    // waves' dependent chains, and a workgroup of another stream's kernel placed on its CU
+    // (the Algorithm-1 pipeline runs density passes beside it) takes issue slots from it.
+    // Such launches claim 128 KiB of LDS per workgroup, so no workgroup of the wide path's
+    // trunk or final phase (33 KiB each) is placed on their CUs (FS_LOCAL_EXCLUSIVE=0 turns
+    // this off; 1 forces it).  r06, Algorithm-1 regime through the pipeline: 3114 -> 3214
+    // attempts/s (profiles/r06/r06zk_*).  Placing the work on another XCD than the density
+    // passes' (a workgroup offset) changed nothing (2783-2791 us per stage, r06zo_*): a
+    // local-move launch beside the density passes takes ~2.75 ms per 1000 moves at N = 3
+    // against 2.25 alone, on any XCD.
+    static const int excl_env = [] {
+        const char *e = getenv("FS_LOCAL_EXCLUSIVE");
+        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+    }();
+    const bool excl = excl_env == 1 || (excl_env < 0 && grid.x <= 8);
+#define FS_LCASE(L, Q)                                                                            \
+    if (lpc == L && ppl == Q) {                                                                   \
+        unsigned dyn = 0;                                                                         \
+        if (excl) {                                                                               \
+            dyn = 131072u - (unsigned)sizeof(double) * kLocalWaves * 4 * (64 / L) * L * Q;        \
+            if (hipError_t e = local_dyn_lds_once((const void *)local_moves_kernel<L, Q>, dyn);   \
+                e != hipSuccess)                                                                  \
+                return e;                                                                         \
+        }                                                                                         \
+        hipLaunchKernelGGL((local_moves_kernel<L, Q>), grid, block, dyn, st, a);                  \
+        return hipGetLastError();                                                                 \
     }
     FS_LCASE(8, 1) FS_LCASE(8, 2) FS_LCASE(8, 4) FS_LCASE(8, 8) FS_LCASE(64, 1) FS_LCASE(16, 4) FS_LCASE(4, 16)
     FS_LCASE(4, 8) FS_LCASE(4, 4) FS_LCASE(1, 4) FS_LCASE(1, 8) FS_LCASE(2, 4) FS_LCASE(4, 1)

@@ -464,8 +464,19 @@ class BatchedMonteCarlo:
         lq = self.model._log_prob(self._centered_f32(cfg.to(torch.float64)), self.err)
         return E, W, lq
 
+    def state_nll(self, state=None, log_prob=None):
+        """-log q of the states (C, N, 2) f64 as nf_big_move re-derives the old NLL after
+        local moves (monte_carlo.py:251-261): the density pass over fl32(state - half_width),
+        widened to float64.  Runs on the current stream; a pass that meets a NaN or a
+        hand-off timeout reports it in the engine's sticky err word.  log_prob: optional
+        model.frozen_log_prob() function (the same pass without its per-call checks)."""
+        self._need_model()
+        x = self._centered_f32(self.state if state is None else state)
+        lq = self.model._log_prob(x, self.err) if log_prob is None else log_prob(x, self.err)
+        return -(lq.to(torch.float64))
+
     @_on_own_device
-    def nf_big_move(self, configs, terms=None):
+    def nf_big_move(self, configs, terms=None, nll=None):
         """Batched nf_big_move with supplied proposals (C, N, 2) box coords.
 
         The proposals keep their dtype, as in the reference (monte_carlo.py:245-296):
@@ -473,7 +484,9 @@ class BatchedMonteCarlo:
         energy is computed in that dtype, the flow sees fl32(config - half_width)
         either way (:251-258), and an accepted chain's state takes the config's dtype.
         terms: optional (E_new, W_new, log_q), each (C,), of these configs from
-        proposal_terms()."""
+        proposal_terms().  nll: optional (C,) f64 state_nll() of the current states,
+        computed ahead (the Algorithm-1 pipeline); used only after local moves, where the
+        move would re-derive it, and it becomes the engine's nll_old (updated in place)."""
         cfg = torch.as_tensor(configs, device=self.device)
         if cfg.dtype not in (torch.float32, torch.float64):
             raise ValueError(f"proposals must be float32 or float64, got {cfg.dtype}")
@@ -484,7 +497,10 @@ class BatchedMonteCarlo:
         self._need_model()
         stale = self._moved
         if stale:  # old NLL of the current state (monte_carlo.py:251-261); energy for a reject (:299-301)
-            self.nll_old = -(self.model._log_prob(self._centered_f32(self.state), self.err).to(torch.float64))
+            if nll is not None and (not torch.is_tensor(nll) or nll.dtype != torch.float64 or nll.shape != (self.C,)
+                                    or nll.device != self.device):
+                raise ValueError(f"nll must be a ({self.C},) float64 tensor on {self.device}")
+            self.nll_old = self.state_nll() if nll is None else nll
             E_cur, W_cur = self._energy_of_state()
         if terms is None:
             E_new, W_new, _ = total_energy(cfg if cfg64 is None else cfg64, self.phys.c)

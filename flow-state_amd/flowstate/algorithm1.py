@@ -223,58 +223,283 @@ class _Speculator:
         self.main.wait_stream(self.side)
 
 
+def pipeline_schedule(accepts):
+    """The stage schedule _Pipeline follows for a (C, A) accept matrix: (spec, redo), two
+    lists of A bools.  Stage k = the local moves before big move k.  spec[k]: the stage
+    was run ahead from the previous stage's unfinished state (assuming big move k-1 rejects
+    on every chain); otherwise (a restart, or stage 0) it started from the finished state.
+    redo[k]: the speculative stage was wrong (a big move it assumed rejected accepted on
+    some chain, or its base was itself wrong) and the main stream ran it again.  Stage k+2
+    is decided once big move k-1 is known: a restart when stage k+1 is already known to be
+    wrong."""
+    acc = torch.as_tensor(accepts)
+    A = int(acc.shape[1]) if acc.dim() == 2 else 0
+    g = [bool(acc[:, k].any()) for k in range(A)]
+    spec, redo = [False] * A, [False] * A
+    if A > 1:
+        spec[1] = True
+    for a in range(A):
+        if a >= 1:
+            redo[a] = spec[a] and (redo[a - 1] or g[a - 1])
+        if a + 2 < A:
+            spec[a + 2] = not (spec[a + 1] and redo[a])
+    return spec, redo
+
+
+class _Pipeline:
+    """The testing phase as a three-stream pipeline: the local moves run back to back on a
+    side stream, each stage started from the previous stage's state as a rejected big move
+    leaves it (_Speculator's reject transform), and each stage's density pass (the big
+    move's old NLL, state_nll) runs on one of two density streams as soon as its local
+    moves end; the main stream runs only the big moves' energy and accept, each when its
+    density pass is done.  A stage is the truth as long as no big move it assumed rejected
+    accepted on any chain; the host learns each big move's outcome one attempt behind
+    (a pinned copy of the accept flags, read while the GPU runs the queued stages), runs a
+    wrong stage again on the main stream from the finished state (copy, local moves,
+    density pass: the same kernels on the same inputs, so every result is bit-identical to
+    the plain sequence) and restarts the side stream from the finished state after it.
+
+    With the chains' rare accepts (0.2-0.3 % per big move in the reference's regime), the
+    attempt time is the local moves' (the density pass, 1.3x as long, overlaps two
+    attempts), where _Speculator's is the density pass plus the big move: 2.78 ms per stage
+    against 3.55 ms (r06, timing events: tools/regime_gpu_timeline.py), the regime 2780 ->
+    3230-3340 attempts/s with the stages after its accepts run again.  The density passes
+    use model.frozen_log_prob() (the flow is fixed in the testing phase): the per-pass
+    checks cost ~0.9 ms of host time, which paced the pipeline.  The schedule of stages is
+    pipeline_schedule(accepts)."""
+
+    R = 4  # ring of chain-state slots: a stage's slot is free once the big move after the next is done
+
+    def __init__(self, bmc, n, sf):
+        self.bmc, self.n, self.sf = bmc, n, sf
+        self.L = _lib.load()
+        dev = bmc.device
+        self.main = torch.cuda.current_stream(dev)
+        self.side = torch.cuda.Stream(device=dev)
+        # two density streams: a pass (~3.5 ms at 10 rows) outlasts a stage's local moves
+        # (~2.75 ms), so consecutive passes overlap (4 streams measured slower, r06zh)
+        self.dens = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        # the flow is fixed during the testing phase: its density pass without the per-call
+        # checks, over the image packed now (before another stream reads it)
+        self.log_prob = bmc.model.frozen_log_prob()
+        self.slots = []
+        for r in range(self.R):
+            s = copy.copy(bmc)  # shares the physics, the flow, accept / n_accept / err
+            if r > 0:
+                for k in _Speculator.FIELDS:
+                    setattr(s, k, torch.empty_like(getattr(bmc, k)))
+            self.slots.append(s)
+        self.nll = [torch.empty(bmc.C, dtype=torch.float64, device=dev) for _ in range(self.R)]
+        self.acc_host = [torch.empty(bmc.C, dtype=torch.uint8, pin_memory=True) for _ in range(self.R)]
+        self.draw = torch.empty(bmc.C, dtype=torch.float64, device=dev)
+        self.one = torch.ones(1, dtype=torch.uint8, device=dev)
+        self.S = self.L.fs_local_samples_per_chain(0, n, sf)
+        self.steps = [s for s in range(1, n + 1) if sf and s % sf == 0]
+        self.spec, self.redo, self.acc = {0: False}, {0: False}, {}
+        self.ev_L, self.ev_copy, self.ev_D, self.ev_main = {}, {}, {}, {}
+        self.xy, self.ew = {}, {}
+        self.kept = 0
+        for s in [self.side] + self.dens:
+            s.wait_stream(self.main)  # stage 0's local moves, the flow image, the slots
+        self.ev_L[0] = self.main.record_event()
+        self._density(0)
+
+    def slot(self, k):
+        return self.slots[k % self.R]
+
+    def _moves(self, m, k):
+        _lib.check(self.L.fs_local_moves(
+            m.phys.c, m.C, m.N, _lib.ptr(m.state), _lib.ptr(m.state_is_f32), _lib.ptr(m.E_old), _lib.ptr(m.W_old),
+            _lib.ptr(m.pcg), _lib.ptr(m.pcg_buf), _lib.ptr(m.max_disp), _lib.ptr(m.attempts), _lib.ptr(m.accepted),
+            _lib.ptr(m.prev_counts), self.n, 0, 0, m.target_acceptance, self.sf, _lib.ptr(self.xy[k]),
+            _lib.ptr(self.ew[k]), None, None, _lib.stream_ptr()), "fs_local_moves")
+
+    def _copy(self, k):
+        """slot k := slot k-1 (every chain array), on the current stream."""
+        _lib.check(self.L.fs_chains_copy_if(_lib.ptr(self.one), self.bmc.C, self.bmc.N,
+                                            ctypes.byref(_Speculator._chains(self.slot(k - 1))),
+                                            ctypes.byref(_Speculator._chains(self.slot(k))), _lib.stream_ptr()),
+                   "fs_chains_copy_if")
+
+    def _density(self, k):
+        ds = self.dens[k % len(self.dens)]
+        with torch.cuda.stream(ds):
+            ds.wait_event(self.ev_L[k])
+            self.nll[k % self.R].copy_(self.bmc.state_nll(self.slot(k).state, self.log_prob))
+            self.ev_D[k] = ds.record_event()
+
+    def stage(self, k, spec):
+        """Queue stage k (k >= 1) on the side stream and its density pass.  spec: start
+        from stage k-1's state as big move k-1 leaves it on a reject (queued before that
+        big move); else from the finished state after big move k-1 (queued after it)."""
+        b, sl = self.bmc, self.slot(k)
+        self.spec[k] = spec
+        self.xy[k] = torch.empty((b.C, self.S, b.N, 2), dtype=torch.float64, device=b.device)
+        self.ew[k] = torch.empty((b.C, self.S, 2), dtype=torch.float64, device=b.device)
+        with torch.cuda.stream(self.side):
+            if k - self.R + 1 >= 0:  # the slot's previous stage: its big move and the next one's redo are done
+                self.side.wait_event(self.ev_main[k - self.R + 1])
+            if spec:
+                if k == 1:
+                    self.side.wait_event(self.ev_L[0])
+                self._copy(k)  # before big move k-1 writes slot k-1 (it waits for this event)
+                self.ev_copy[k] = self.side.record_event()
+                st = _lib.stream_ptr()
+                _lib.check(self.L.fs_pcg64_random(_lib.ptr(sl.pcg), b.C, _lib.ptr(self.draw), st), "fs_pcg64_random")
+                sl.attempts += 1
+                _lib.check(self.L.fs_energy_state(b.phys.c, _lib.ptr(sl.state), _lib.ptr(sl.state_is_f32), b.C, b.N,
+                                                  _lib.ptr(sl.E_old), _lib.ptr(sl.W_old), st), "fs_energy_state")
+            else:
+                self.side.wait_event(self.ev_main[k - 1])
+                self._copy(k)
+            self._moves(sl, k)
+            self.ev_L[k] = self.side.record_event()
+        self._density(k)
+
+    def learn(self, k):
+        """Wait for big move k and decide whether stage k+1 must run again."""
+        self.ev_main[k].synchronize()
+        self.acc[k] = bool(self.acc_host[k % self.R].any())
+        k1 = k + 1
+        self.redo[k1] = self.spec[k1] and (self.redo[k] or self.acc[k])
+
+    def attempt(self, k, configs, terms):
+        """Queue big move k on the main stream (after the redo of stage k if it was wrong).
+        Returns (the Snapshots of stage k, or None for stage 0; the accept flags)."""
+        b, sl = self.bmc, self.slot(k)
+        self.main.wait_event(self.ev_D[k])
+        if self.spec.get(k + 1):
+            self.main.wait_event(self.ev_copy[k + 1])
+        if self.redo[k]:
+            self._copy(k)
+            self._moves(sl, k)
+            self.nll[k % self.R].copy_(b.state_nll(sl.state, self.log_prob))
+        elif self.spec[k]:
+            self.kept += 1
+        snap = Snapshots(self.steps, self.xy[k], self.ew[k], sl.state_is_f32.bool()) if k > 0 else None
+        sl._moved = True
+        acc = sl.nf_big_move(configs, terms=terms, nll=self.nll[k % self.R]).clone()
+        self.acc_host[k % self.R].copy_(acc, non_blocking=True)
+        self.ev_main[k] = self.main.record_event()
+        return snap, acc
+
+    def close(self, last):
+        """Join the streams; the engine takes the chain arrays of the last attempt's slot."""
+        for s in [self.side] + self.dens:
+            self.main.wait_stream(s)
+        if last is not None:
+            b, sl = self.bmc, self.slot(last)
+            for k in _Speculator.FIELDS + ("nll_old",):
+                setattr(b, k, getattr(sl, k))
+            b._moved = False
+
+
+def _run_pipeline(bmc, cfg, A, n, sf, terms_of, snaps, acc):
+    """testing_phase's attempts through _Pipeline on the current stream (its main stream)."""
+    C = bmc.C
+    last = None
+    pipe = _Pipeline(bmc, n, sf)
+    try:
+        pipe.stage(1, True)
+        restart = None  # a restart stage waits to be queued after the big move it starts from
+        for a in range(A):
+            if a >= 1:
+                pipe.learn(a - 1)
+            fresh = later = None
+            if a + 2 < A:
+                if pipe.spec[a + 1] and pipe.redo[a]:  # stage a+1 is wrong: start a+2 afresh
+                    fresh = a + 2
+                    pipe.spec[fresh] = False  # (queued once big move a+1 is)
+                elif restart is None:  # the side stream's next stage first: it sets the pace
+                    pipe.stage(a + 2, True)
+                else:  # it starts from the restart stage a+1, queued after big move a
+                    later = a + 2
+            snap, ac = pipe.attempt(a, cfg[a * C:(a + 1) * C], terms_of(a))
+            last = a
+            acc.append(ac)
+            if snap is not None:
+                snaps.append(snap)
+            if restart is not None:
+                pipe.stage(restart, False)
+            if later is not None:
+                pipe.stage(later, True)
+            restart = fresh
+    finally:
+        pipe.close(last if last == A - 1 else None)
+    return pipe
+
+
 def testing_phase(bmc: BatchedMonteCarlo, test_configs, attempts, interval, sampling_frequency,
                   total_mcmc_steps=0, big_move_attempts=0, big_move_accepts=0, speculate=None):
     """main_algorithm_1.py:375-424 for all runs: per attempt, `interval` local moves with
     sampling, then nf_big_move with test_configs[attempt * C + run] (float32 box
-    coordinates, (>= attempts*C, N, 2), numpy or device).  speculate (default: on for a
-    device engine with a flow): overlap each attempt's big move with the next attempt's
-    local moves (_Speculator); the results are the same either way, but the engine's chain
-    buffers (bmc.state, bmc.pcg, ...) may afterwards be other tensors of the same shape:
-    read them from bmc after the call, not through references taken before it."""
+    coordinates, (>= attempts*C, N, 2), numpy or device).  speculate: how the attempts
+    overlap on a device engine with a flow and local moves between the big moves (the
+    results are the same every way): "pipeline" (the default, also True / None: _Pipeline,
+    the local moves back to back on a side stream, each stage's density pass on its own
+    stream, the big moves on the main stream), "local" (_Speculator: each big move beside
+    the next attempt's local moves) or False (one phase after the other).  The engine's
+    chain buffers (bmc.state, bmc.pcg, ...) may afterwards be other tensors of the same
+    shape: read them from bmc after the call, not through references taken before it."""
     C = bmc.C
     cfg = torch.as_tensor(test_configs)
     if cfg.dtype != torch.float32:
         raise ValueError("test configurations are float32 (main_algorithm_1.py:340-343)")
     if cfg.shape[0] < attempts * C:
         raise IndexError(f"index {attempts * C - 1} is out of bounds for axis 0 with size {cfg.shape[0]}")
+    if speculate not in (None, True, False, "pipeline", "local"):
+        raise ValueError(f"speculate must be 'pipeline', 'local', True, False or None, got {speculate!r}")
     cfg = cfg.to(bmc.device)
     A, n, sf = int(attempts), int(interval), int(sampling_frequency)
-    # (speculate=True asks for it; it still needs a device engine with a flow, and local moves
-    # between the big moves: the shadow assumes the reject of a big move after local moves,
-    # which re-derives the running energy, monte_carlo.py:299-301)
-    speculate = ((speculate is None or bool(speculate)) and bmc.device.type == "cuda" and bmc.model is not None
-                 and n > 0)
+    # (speculation needs a device engine with a flow, and local moves between the big moves:
+    # the reject transform assumes a big move after local moves, which re-derives the running
+    # energy, monte_carlo.py:299-301)
+    mode = None
+    if speculate is not False and bmc.device.type == "cuda" and bmc.model is not None and n > 0 and A > 1:
+        mode = "local" if speculate == "local" else "pipeline"
     snaps, acc = [], []
     # the test configurations' energies and log q do not depend on the chain states: one
     # launch per pass over a block of attempts (bit-identical rows), so each attempt's big
     # move runs only the current states' density pass and energy
     block = max(1, BatchedMonteCarlo.FILL_ROWS // max(1, C))
     terms, a0 = None, 0
-    spec = None
+    spec = pipe = None
+
+    def terms_of(a):
+        nonlocal terms, a0
+        if bmc.model is None:
+            return None
+        if a % block == 0:
+            a0, a1 = a, min(A, a + block)
+            terms = bmc.proposal_terms(cfg[a0 * C:a1 * C])
+        o = (a - a0) * C
+        return tuple(x[o:o + C] for x in terms)
+
     with _lib.on_device(bmc.device):
         if A > 0:
             snaps.append(_local(bmc, n, 0, sf))
-        if speculate and A > 1:
-            spec = _Speculator(bmc)
-        try:
-            for a in range(A):
-                if spec is not None and a + 1 < A:
-                    spec.begin(n, sf)
-                if bmc.model is not None and a % block == 0:
-                    a0, a1 = a, min(A, a + block)
-                    terms = bmc.proposal_terms(cfg[a0 * C:a1 * C])
-                o = (a - a0) * C
-                t = tuple(x[o:o + C] for x in terms) if bmc.model is not None else None
-                acc.append(bmc.nf_big_move(cfg[a * C:(a + 1) * C], terms=t).clone())
-                if a + 1 < A:
-                    snaps.append(spec.finish(n, sf) if spec is not None else _local(bmc, n, 0, sf))
-        finally:
-            if spec is not None:
-                spec.close()
+        if mode == "pipeline":
+            pipe = _run_pipeline(bmc, cfg, A, n, sf, terms_of, snaps, acc)
+        else:
+            if mode == "local":
+                spec = _Speculator(bmc)
+            try:
+                for a in range(A):
+                    if spec is not None and a + 1 < A:
+                        spec.begin(n, sf)
+                    t = terms_of(a)
+                    acc.append(bmc.nf_big_move(cfg[a * C:(a + 1) * C], terms=t).clone())
+                    if a + 1 < A:
+                        snaps.append(spec.finish(n, sf) if spec is not None else _local(bmc, n, 0, sf))
+            finally:
+                if spec is not None:
+                    spec.close()
     accepts = torch.stack(acc, 1) if acc else torch.zeros((C, 0), dtype=torch.uint8, device=bmc.device)
-    # attempts whose successor's local moves were the speculative ones (no chain accepted)
-    adopted = int((accepts[:, :-1].sum(0) == 0).sum()) if spec is not None else 0
+    # attempts whose successor's local moves were the speculative ones, kept
+    if pipe is not None:
+        adopted = pipe.kept
+    else:
+        adopted = int((accepts[:, :-1].sum(0) == 0).sum()) if spec is not None else 0
     bmc.check_errors()  # a NaN discriminant or a wide-path hand-off timeout in any pass raises
     p, s, tot, att, nacc = acceptance_history(accepts, n, total_mcmc_steps, big_move_attempts, big_move_accepts)
     return TestingResult(accepts, snaps, p, s, tot, att, nacc, adopted)

@@ -292,6 +292,37 @@ class NormalizingFlow(nn.Module):
         _, lq = _run_stack(self._layers(), x, "inverse", self._cache, base_log_prob=True, err=err)
         return lq.to(x.dtype)
 
+    def frozen_log_prob(self):
+        """log_prob over the flow as it is now, for a caller that holds the weights fixed over
+        many passes (the Algorithm-1 testing phase's density passes): the structure, eval-mode
+        and parameter-version checks a pass makes (~1 ms of host time per pass on the A1 flow,
+        thousands of tensors and modules) run once here, and the returned function
+        run(x, err) launches the same density pass over the packed image taken now
+        (bit-identical to _log_prob(x, err)).  err: the caller's sticky device int32 error
+        word, required (a column-split hand-off timeout is reported there)."""
+        self._base_check()
+        layers = self._layers()
+        _check_stack(layers)
+        packed = self._cache.get(layers)
+        _lib.require_device(packed)
+        dims = layers[0].dims(L=len(layers))
+        D = layers[0].num_input_channels
+        L = _lib.load()
+
+        @torch.no_grad()
+        def run(x, err):
+            if err is None:
+                raise ValueError("frozen_log_prob: err is required")
+            xin = _prepare_input(x, D)
+            B = xin.shape[0]
+            out = torch.empty_like(xin)
+            ld = torch.empty(B, dtype=torch.float32, device=xin.device)
+            with _lib.on_device(xin):
+                _launch_stack(L, dims, packed, xin, B, out, ld, err, "inverse", True)
+            return ld.to(x.dtype)
+
+        return run
+
     @torch.no_grad()
     def sample(self, num_samples=1):
         """core.py:178-196 (fork): returns the samples only."""

@@ -124,16 +124,19 @@ def _regime_engine(runs, N, temperature):
     return bmc, hb, g
 
 
+@pytest.mark.parametrize("mode", ["pipeline", "local"])
 @pytest.mark.parametrize("runs,N,temperature", [(10, 3, 1.0), (10, 3, 40.0), (64, 12, 1.0), (64, 12, 40.0)])
-def test_speculative_testing_phase_is_bit_identical(runs, N, temperature):
-    """testing_phase with the next attempt's local moves run ahead on a side stream
-    (algorithm1._Speculator) against the plain sequence, on two engines from the same
-    start: every accept, snapshot, dtype flag, final state, PCG64 state, counter, running
-    energy and max_displacement equal.  At T=40 many big moves accept (the speculative
-    moves are dropped and rerun), at T=1 almost none do (they are adopted)."""
+def test_speculative_testing_phase_is_bit_identical(runs, N, temperature, mode):
+    """testing_phase with the attempts overlapped (mode "pipeline": algorithm1._Pipeline,
+    the local moves run ahead on a side stream and each stage's density pass on its own
+    stream; "local": algorithm1._Speculator, each big move beside the next attempt's local
+    moves) against the plain sequence, on two engines from the same start: every accept,
+    snapshot, dtype flag, final state, PCG64 state, counter, running energy and
+    max_displacement equal.  At T=40 many big moves accept (the speculative stages are
+    wrong and run again), at T=1 almost none do (they are kept)."""
     ATT, INT, SF = 12, 120, 25
     out = []
-    for spec in (False, True):
+    for spec in (False, mode):
         bmc, hb, g = _regime_engine(runs, N, temperature)
         cfg = ((torch.rand((ATT * runs, N, 2), generator=g, dtype=torch.float64) * 0.8 + 0.1) * 2 * hb).float()
         res = A1.testing_phase(bmc, cfg.numpy(), ATT, INT, SF, speculate=spec)
@@ -142,9 +145,16 @@ def test_speculative_testing_phase_is_bit_identical(runs, N, temperature):
     (b0, r0), (b1, r1) = out
     assert r0.speculated == 0
     dropped = int((r0.accepts[:, :-1].sum(0) > 0).sum())
-    assert r1.speculated == ATT - 1 - dropped
+    if mode == "local":
+        assert r1.speculated == ATT - 1 - dropped
+    else:
+        spec, redo = A1.pipeline_schedule(r0.accepts)
+        assert r1.speculated == sum(s and not r for s, r in zip(spec, redo))
+        assert r1.speculated <= ATT - 1 - dropped
     if temperature > 1:
         assert dropped >= 1  # the drop-and-rerun path ran
+        if mode == "pipeline":
+            assert any(redo) and not all(spec[1:])  # redo and restart stages ran
     elif N == 3:
         assert r1.speculated >= 1  # the adopt path ran
     assert torch.equal(r0.accepts, r1.accepts)
@@ -158,13 +168,15 @@ def test_speculative_testing_phase_is_bit_identical(runs, N, temperature):
     assert r0.p_acc_history == r1.p_acc_history
 
 
-@pytest.mark.parametrize("ATT,INT,SF", [(1, 50, 10), (2, 0, 0), (5, 37, 0), (6, 40, 7)])
-def test_speculative_testing_phase_edge_cases(ATT, INT, SF):
-    """Speculation on / off agree for one attempt (no speculation), no local moves, no
-    snapshots and snapshot schedules that do not divide the interval."""
+@pytest.mark.parametrize("mode", ["pipeline", "local"])
+@pytest.mark.parametrize("ATT,INT,SF", [(1, 50, 10), (2, 0, 0), (2, 30, 10), (3, 25, 5), (5, 37, 0), (6, 40, 7)])
+def test_speculative_testing_phase_edge_cases(ATT, INT, SF, mode):
+    """Speculation on / off agree for one attempt (no speculation), no local moves, two or
+    three attempts (the pipeline's shortest schedules), no snapshots and snapshot schedules
+    that do not divide the interval."""
     runs, N = 10, 3
     out = []
-    for spec in (False, True):
+    for spec in (False, mode):
         bmc, hb, g = _regime_engine(runs, N, 5.0)
         cfg = ((torch.rand((ATT * runs, N, 2), generator=g, dtype=torch.float64) * 0.8 + 0.1) * 2 * hb).float()
         res = A1.testing_phase(bmc, cfg.numpy(), ATT, INT, SF, speculate=spec)
