@@ -87,26 +87,19 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, PairThresh T, co
     // leaves every sum as the full row's.  Evaluating the LJ term inside pass 1 made a wave
     // run the sqrt / reciprocal / pow6 chain on every pair some lane had inside the cutoff
     // (~half of them for 64 lanes).
-    auto sq = [&](int i, int j) -> double {
+    auto sqc = [&](CT xi, CT yi, int j) -> double {
         if (as_f32)
-            return F32 ? sqdist32((float)X[i], (float)Y[i], (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy)
-                       : sqdist_f32((float)X[i], (float)Y[i], (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy);
-        return sqdist_f64(X[i], Y[i], X[j], Y[j], p.Lx, p.Ly, T, iLx, iLy);
+            return F32 ? sqdist32((float)xi, (float)yi, (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy)
+                       : sqdist_f32((float)xi, (float)yi, (float)X[j], (float)Y[j], p.Lx, p.Ly, T, iLx, iLy);
+        return sqdist_f64(xi, yi, X[j], Y[j], p.Lx, p.Ly, T, iLx, iLy);
     };
     auto term = [&](int i, int j, double &e, double &w) {
-        const double s = sq(i, j);
+        const double s = sqc(X[i], Y[i], j);
         lj_pair(as_f32 ? r_of_sq((float)s) : r_of_sq(s), p.r_cut, e_cut, e, w);
     };
-    auto row = [&](int i) {
+    // pass 2 of row i over its in-cutoff mask: the row's energy / virial sums
+    auto row_sums = [&](int i, uint64_t mask) {
         const int n = N - 1 - i;
-        uint64_t mask = 0;  // bit t: pair (i, i + 1 + t) inside the cutoff
-        for (int t = 0; t < n; ++t) {
-            const double s = sq(i, i + 1 + t);
-            const bool core = as_f32 ? (float)s <= T.core32 : s <= T.core64;
-            const bool cut = as_f32 ? (float)s <= T.cut32 : s <= T.cut64;
-            hit |= core;
-            if (cut) mask |= (uint64_t)1 << t;
-        }
         double re = 0.0, rw = 0.0;
         if (n < 8) {
             for (uint64_t b = mask; b; b &= b - 1) {
@@ -147,9 +140,26 @@ __global__ void __launch_bounds__(256) energy_kernel(fs_phys p, PairThresh T, co
         sw[wid][hh][i] = rw;
         if (nbr) nbr[c * N + i] = mask;
     };
+    // pass 1 of both rows of this lane in one loop (r06): rows ra = l and rb = N-2-l have
+    // N-1-l and l+1 pairs, so each lane runs N pairs and the wave N iterations, where one
+    // loop per row ran the longest row of each (N-1 + N/2 iterations)
     const int ra = hl, rb = N - 2 - hl;
-    if (ra <= N - 2) row(ra);
-    if (rb > ra) row(rb);
+    const int na = ra <= N - 2 ? N - 1 - ra : 0, nb = rb > ra ? N - 1 - rb : 0;
+    const CT xa = na ? X[ra] : CT(0), ya = na ? Y[ra] : CT(0), xb = nb ? X[rb] : CT(0), yb = nb ? Y[rb] : CT(0);
+    uint64_t ma = 0, mb = 0;  // bit t: pair (i, i + 1 + t) inside the cutoff
+    for (int k = 0; k < na + nb; ++k) {
+        const bool in_a = k < na;
+        const int t = in_a ? k : k - na;
+        const double s = sqc(in_a ? xa : xb, in_a ? ya : yb, (in_a ? ra : rb) + 1 + t);
+        const bool core = as_f32 ? (float)s <= T.core32 : s <= T.core64;
+        const bool cut = as_f32 ? (float)s <= T.cut32 : s <= T.cut64;
+        hit |= core;
+        const uint64_t bit = cut ? (uint64_t)1 << t : 0;
+        if (in_a) ma |= bit;
+        else mb |= bit;
+    }
+    if (na) row_sums(ra, ma);
+    if (nb) row_sums(rb, mb);
     if (nbr && hl == 0 && N >= 1) nbr[c * N + N - 1] = 0;  // the last row has no j > i
     // external double well per particle (potential.py:89-112)
     for (int q = hl; q < N; q += 32) {

@@ -1,6 +1,7 @@
-"""A/B of the energy kernel builds: the default library vs FS_ENERGY_V1 (the pair loop
-with inline LJ terms), bit-for-bit on sparse (bench-like), clustered and overlapping
-configurations, and per-launch time at the bench shape (65536 chains, N=64, float32)."""
+"""A/B of the energy kernel builds: the default library ("v2") vs another build ("v1": argv[1],
+default the FS_ENERGY_V1 variant, the pair loop with inline LJ terms), bit-for-bit on sparse
+(bench-like), clustered and overlapping configurations, and per-launch time at the bench shape
+(65536 chains, N=64, float32 and float64)."""
 import ctypes
 import json
 import os
@@ -16,7 +17,8 @@ from flowstate import _lib  # noqa: E402
 from flowstate.MCMC.energy_calculator import make_phys  # noqa: E402
 from oracle import physics as OP  # noqa: E402
 
-libs = {"v2": _lib.load(), "v1": _lib.load(os.path.join(REPO, "flow-state_amd/flowstate/lib/variants/ev1/libflowstate.so"))}
+libs = {"v2": _lib.load(), "v1": _lib.load(sys.argv[1] if len(sys.argv) > 1 else
+                                         os.path.join(REPO, "flow-state_amd/flowstate/lib/variants/ev1/libflowstate.so"))}
 N, C = 64, 65536
 L = float(np.sqrt(N / 0.03))
 phys = make_phys(L, L)
