@@ -55,9 +55,6 @@ struct LocalArgs {
 
 constexpr int kLocalWaves = 4;
 
-#ifndef FS_LOCAL_DRAW_AHEAD
-#define FS_LOCAL_DRAW_AHEAD 0  // r06: 1 measured no faster (N=3 x 10 chains 2.30 vs 2.27 ms per 1000 moves)
-#endif
 
 // adjust_displacement (monte_carlo.py:375-403) on one chain's registers
 __device__ __forceinline__ void adjust_md(double &md, int64_t att, int64_t acc, int64_t &prev_att, int64_t &prev_acc,
@@ -217,12 +214,6 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
         const double ox = bcast<LPC>(pick<PPL>(xj, pq), pl), oy = bcast<LPC>(pick<PPL>(yj, pq), pl);
         const double d0 = (pcg64_double(rng) - 0.5) * md;
         const double d1 = (pcg64_double(rng) - 0.5) * md;
-#if FS_LOCAL_DRAW_AHEAD
-        // the accept draw, when the move takes one, is the stream's next output: computed here,
-        // beside the energies instead of after them, and committed only if taken
-        uint64_t s_next[4] = {rng.s[0], rng.s[1], rng.s[2], rng.s[3]};
-        const double u_next = (double)(pcg64_next64(s_next) >> 11) * (1.0 / 9007199254740992.0);
-#endif
         double nx, ny;
         if (f32) {  // float32 row += float64 array, then float32 % np.float64 stored back
             nx = (double)(float)np_remainder((double)(float)(ox + d0), P.Lx);
@@ -352,15 +343,7 @@ __global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_mov
         bool accept;
         if (enn <= eno) accept = true;
         else if (isinf(enn)) accept = false;
-        else {
-#if FS_LOCAL_DRAW_AHEAD
-            accept = u_next < exp(-P.beta * (enn - eno));
-            rng.s[0] = s_next[0];
-            rng.s[1] = s_next[1];
-#else
-            accept = pcg64_double(rng) < exp(-P.beta * (enn - eno));
-#endif
-        }
+        else accept = pcg64_double(rng) < exp(-P.beta * (enn - eno));
         if (accept) {
             acc_n += 1;
             E += enn - eno;
