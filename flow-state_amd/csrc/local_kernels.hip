@@ -162,16 +162,47 @@ __device__ __forceinline__ double pick(const double (&v)[PPL], int q) {
 // one or two lanes, each lane taking RPL of the four sum rows and double-well roles, so a
 // move has no or one shuffle level on its dependent path; the sums are the same
 // additions in the same order, so every layout gives the same bits.
-template <int LPC, int PPL>
-__global__ void __launch_bounds__(64 * kLocalWaves, LPC == 64 ? 4 : 2) local_moves_kernel(LocalArgs a) {
+// position of the k-th set bit of m (k < popcount(m))
+__device__ __forceinline__ int nth_set_bit(uint64_t m, int k) {
+    for (int i = 0; i < k; ++i) m &= m - 1;
+    return __builtin_ctzll(m);
+}
+
+// SORT (small launches, r06): twice the waves per workgroup, the workgroup's float64-state
+// chains packed into its first waves and its float32-state chains from the next wave
+// boundary on, so no wave runs both dtypes' branches (a chain's state turns float32 after an
+// accepted big move, monte_carlo.py:289-292; a wave holding both ran each move's position and
+// distance code twice).  Each chain still runs the same code on its own lanes: the same bits.
+template <int LPC, int PPL, bool SORT = false>
+__global__ void __launch_bounds__(64 * kLocalWaves * (SORT ? 2 : 1), LPC == 64 ? 4 : 2)
+    local_moves_kernel(LocalArgs a) {
     constexpr int G = 64 / LPC;          // chains per wave
     constexpr int SLOTS = LPC * PPL;     // LDS slots per chain and array
-    __shared__ double lds[kLocalWaves][4][G * SLOTS];
+    constexpr int WPB = kLocalWaves * (SORT ? 2 : 1);
+    __shared__ double lds[WPB][4][G * SLOTS];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane / LPC, gl = lane % LPC;
     const int sb = g * SLOTS;            // this chain's slot base
-    const int64_t c = ((int64_t)blockIdx.x * kLocalWaves + wid) * G + g;
-    if (c >= a.C) return;  // whole groups leave; only group-internal shuffles below
+    int64_t c;
+    if constexpr (SORT) {
+        static_assert(kLocalWaves * G <= 64, "a sorted workgroup's chains fit one ballot");
+        constexpr int CPB = kLocalWaves * G;  // chains per workgroup
+        const int64_t cb = (int64_t)blockIdx.x * CPB;
+        const bool v = lane < CPB && cb + lane < a.C;
+        const bool f = v && a.is_f32 && a.is_f32[cb + lane];
+        const uint64_t m32 = __ballot(f), m64 = __ballot(v) & ~m32;
+        const int n64 = __builtin_popcountll(m64), n32 = __builtin_popcountll(m32);
+        const int base32 = (n64 + G - 1) / G * G;
+        const int slot = wid * G + g;
+        int idx = -1;
+        if (slot < n64) idx = nth_set_bit(m64, slot);
+        else if (slot >= base32 && slot - base32 < n32) idx = nth_set_bit(m32, slot - base32);
+        if (idx < 0) return;  // whole groups leave
+        c = cb + idx;
+    } else {
+        c = ((int64_t)blockIdx.x * kLocalWaves + wid) * G + g;
+        if (c >= a.C) return;  // whole groups leave; only group-internal shuffles below
+    }
     if (a.gate && *a.gate == 0) return;  // (launch-uniform)
     const int N = a.N;
     const fs_phys &P = a.p;
@@ -468,7 +499,11 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
         }
     }
     const int64_t chains_per_block = (int64_t)kLocalWaves * (64 / lpc);
-    const dim3 grid((unsigned)((C + chains_per_block - 1) / chains_per_block)), block(64 * kLocalWaves);
+    const dim3 grid((unsigned)((C + chains_per_block - 1) / chains_per_block));
+    // dtype-sorted workgroups for launches of at most 8 workgroups (FS_LOCAL_SORT=0 / 1 turns
+    // them off / on everywhere, for A/B runs and tests)
+    const char *se = getenv("FS_LOCAL_SORT");
+    const bool sort = is_f32 && lpc >= 4 && (se && (se[0] == '0' || se[0] == '1') ? se[0] == '1' : grid.x <= 8);
     // A launch of a few workgroups (the reference's 10 runs: one) is latency-bound on its
     // waves' dependent chains, and a workgroup of another stream's kernel placed on its CU
     // (the Algorithm-1 pipeline runs density passes beside it) takes issue slots from it.
@@ -476,29 +511,40 @@ hipError_t fs_local_moves_impl(const fs_phys *p, int64_t C, int N, double *state
     // trunk or final phase (33 KiB each) is placed on their CUs (FS_LOCAL_EXCLUSIVE=0 turns
     // this off; 1 forces it).  r06, Algorithm-1 regime through the pipeline: 3114 -> 3214
     // attempts/s (profiles/r06/r06zk_*).  Placing the work on another XCD than the density
-    // passes' (a workgroup offset) changed nothing (2783-2791 us per stage, r06zo_*): a
-    // local-move launch beside the density passes takes ~2.75 ms per 1000 moves at N = 3
-    // against 2.25 alone, on any XCD.
+    // passes' (a workgroup offset) changed nothing (r06zo_*), and density passes on one or two
+    // other streams do not slow such a launch (r06zw_*, r06zx_*): what had slowed the regime's
+    // launches (2.71 against 2.3 ms per 1000 moves) was waves holding both float32- and
+    // float64-state chains, which the dtype-sorted workgroups above remove.
     static const int excl_env = [] {
         const char *e = getenv("FS_LOCAL_EXCLUSIVE");
         return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
     }();
     const bool excl = excl_env == 1 || (excl_env < 0 && grid.x <= 8);
-#define FS_LCASE(L, Q)                                                                            \
-    if (lpc == L && ppl == Q) {                                                                   \
+#define FS_LLAUNCH(L, Q, S)                                                                       \
+    {                                                                                             \
         unsigned dyn = 0;                                                                         \
         if (excl) {                                                                               \
-            dyn = 131072u - (unsigned)sizeof(double) * kLocalWaves * 4 * (64 / L) * L * Q;        \
-            if (hipError_t e = local_dyn_lds_once((const void *)local_moves_kernel<L, Q>, dyn);   \
+            dyn = 131072u - (unsigned)sizeof(double) * kLocalWaves * (S ? 2 : 1) * 4 * 64 * Q;    \
+            if (hipError_t e = local_dyn_lds_once((const void *)local_moves_kernel<L, Q, S>, dyn); \
                 e != hipSuccess)                                                                  \
                 return e;                                                                         \
         }                                                                                         \
-        hipLaunchKernelGGL((local_moves_kernel<L, Q>), grid, block, dyn, st, a);                  \
+        hipLaunchKernelGGL((local_moves_kernel<L, Q, S>), grid, dim3(64 * kLocalWaves * (S ? 2 : 1)), dyn, st, \
+                           a);                                                                    \
         return hipGetLastError();                                                                 \
     }
-    FS_LCASE(8, 1) FS_LCASE(8, 2) FS_LCASE(8, 4) FS_LCASE(8, 8) FS_LCASE(64, 1) FS_LCASE(16, 4) FS_LCASE(4, 16)
-    FS_LCASE(4, 8) FS_LCASE(4, 4) FS_LCASE(1, 4) FS_LCASE(1, 8) FS_LCASE(2, 4) FS_LCASE(4, 1)
+#define FS_LCASE(L, Q) \
+    if (lpc == L && ppl == Q) FS_LLAUNCH(L, Q, false)
+#define FS_LCASE_S(L, Q)                    \
+    if (lpc == L && ppl == Q) {             \
+        if (sort) FS_LLAUNCH(L, Q, true)    \
+        FS_LLAUNCH(L, Q, false)             \
+    }
+    FS_LCASE_S(8, 1) FS_LCASE(8, 2) FS_LCASE(8, 4) FS_LCASE_S(8, 8) FS_LCASE(64, 1) FS_LCASE(16, 4) FS_LCASE(4, 16)
+    FS_LCASE(4, 8) FS_LCASE_S(4, 4) FS_LCASE(1, 4) FS_LCASE(1, 8) FS_LCASE(2, 4) FS_LCASE_S(4, 1)
+#undef FS_LCASE_S
 #undef FS_LCASE
+#undef FS_LLAUNCH
     return hipErrorInvalidValue;
 }
 

@@ -212,6 +212,28 @@ def test_every_local_layout_gives_the_same_chains(N, monkeypatch):
     assert ref is not None
 
 
+@pytest.mark.parametrize("N,C", [(3, 10), (3, 64), (16, 40), (64, 32)])
+def test_dtype_sorted_workgroups_give_the_same_chains(N, C, monkeypatch):
+    """Small launches pack each workgroup's float64 and float32 chains into separate waves
+    (FS_LOCAL_SORT, the default at <= 8 workgroups): on a mixed batch the chains, samples
+    and accept logs equal an unsorted launch's bit for bit."""
+    L, init, f32 = _random_batch(N, C, seed=70 + N, spread=0.3)
+    f32[:2] = [True, False]  # both dtypes present
+    state = np.where(f32[:, None, None], init.astype(np.float32).astype(np.float64), init)
+    seeds = np.arange(900, 900 + C, dtype=np.uint64)
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("FS_LOCAL_SORT", mode)
+        b = BatchedMonteCarlo(None, state, Physics(L, L), seeds, initial_max_displacement=0.65)
+        b.state_is_f32.copy_(torch.from_numpy(f32.astype(np.uint8)))
+        b.E_old, b.W_old = b._energy_of_state()
+        xy, ew, log = b.local_moves(200, adjust_every=40, sample_every=50, log_accepts=True)
+        out.append([t.cpu().numpy() for t in (b.state, b.E_old, b.W_old, b.max_disp, b.pcg, b.pcg_buf, b.attempts,
+                                              b.accepted, xy, ew, log)])
+    for a, r in zip(*out):
+        np.testing.assert_array_equal(a, r)
+
+
 def test_local_moves_split_calls_and_samples():
     """n moves in one launch == the same moves over several launches (step0 carries the
     driver's counter); sample() snapshots land at steps divisible by sample_every."""

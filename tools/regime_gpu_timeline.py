@@ -27,7 +27,14 @@ def ev(stream, key):
 
 
 P = A1._Pipeline
-orig_stage, orig_density, orig_attempt = P.stage, P._density, P.attempt
+orig_stage, orig_density, orig_attempt, orig_moves = P.stage, P._density, P.attempt, P._moves
+
+
+def moves(self, m, k):
+    st = torch.cuda.current_stream()
+    ev(st, ("m0", k, st.cuda_stream))
+    orig_moves(self, m, k)
+    ev(st, ("m1", k, st.cuda_stream))
 
 
 def stage(self, k, spec):
@@ -48,11 +55,11 @@ def attempt(self, k, configs, terms):
     return r
 
 
-P.stage, P._density, P.attempt = stage, density, attempt
+P.stage, P._density, P.attempt, P._moves = stage, density, attempt, moves
 r = bench.algorithm1_regime(attempts=att, speculate="pipeline")
 torch.cuda.synchronize()
 # the timed run is the second testing phase: its keys are the last `att` stages
-ks = sorted({k for (_, k) in EV if _ == "M1"})
+ks = sorted({key[1] for key in EV if key[0] == "M1"})
 base = EV[("M1", ks[0])]
 t = lambda key: base.elapsed_time(EV[key]) * 1e3 if key in EV else float("nan")  # noqa: E731
 lo = min(100, max(1, att // 3))
@@ -65,6 +72,9 @@ l_to_d = [t(("D1", k)) - t(("L1", k)) for k in range(lo, att - 5)]
 d_to_m = [t(("M1", k)) - t(("D1", k)) for k in range(lo, att - 5)]
 l_gap = [t(("L1", k + 1)) - t(("L1", k)) for k in range(lo, att - 5)]
 m_to_l0 = [t(("L0", k + 3)) - t(("M1", k)) for k in range(lo, att - 5)]
-print(json.dumps({"median_period_us": st.median(per), "median_L1_to_D1": st.median(l_to_d),
+side = {key[2] for key in EV if key[0] == "m0"}
+lm = [base.elapsed_time(EV[("m1", k, sd)]) * 1e3 - base.elapsed_time(EV[("m0", k, sd)]) * 1e3
+      for k in range(lo, att - 5) for sd in side if ("m0", k, sd) in EV and ("m1", k, sd) in EV]
+print(json.dumps({"median_local_moves_launch_us": st.median(lm), "median_period_us": st.median(per), "median_L1_to_D1": st.median(l_to_d),
                   "median_D1_to_M1": st.median(d_to_m), "median_L1_step": st.median(l_gap),
                   "median_M1k_to_L0k+3": st.median(m_to_l0)}))
