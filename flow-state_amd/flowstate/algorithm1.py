@@ -261,9 +261,9 @@ class _Pipeline:
 
     With the chains' rare accepts (0.2-0.3 % per big move in the reference's regime), the
     attempt time is the local moves' (the density pass, 1.3x as long, overlaps two
-    attempts), where _Speculator's is the density pass plus the big move: 2.78 ms per stage
+    attempts), where _Speculator's is the density pass plus the big move: 2.50 ms per stage
     against 3.55 ms (r06, timing events: tools/regime_gpu_timeline.py), the regime 2780 ->
-    3230-3340 attempts/s with the stages after its accepts run again.  The density passes
+    3508 attempts/s with the stages after its accepts run again.  The density passes
     use model.frozen_log_prob() (the flow is fixed in the testing phase): the per-pass
     checks cost ~0.9 ms of host time, which paced the pipeline.  The schedule of stages is
     pipeline_schedule(accepts)."""
