@@ -21,6 +21,7 @@ asked for.
 """
 import copy
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -134,6 +135,24 @@ def acceptance_history(accepts, interval, total_mcmc_steps=0, big_move_attempts=
     p = [int(c) / int(t) for c, t in zip(cum, att)]  # Python int / int, as the reference
     return (p, [int(s) for s in steps], total_mcmc_steps + interval * n, big_move_attempts + n,
             big_move_accepts + int(acc.sum()))
+
+
+_PIPE_STREAMS = {}
+
+
+def _priority_streams(device):
+    """Three high-priority streams of torch's pool, made once per process (FS_PIPE_STREAMS=
+    priority).  The runtime deals a process's streams over a few hardware queues
+    (GPU_MAX_HW_QUEUES), and two streams that share one run their kernels one after the
+    other, so the pipeline's overlap depends on which pool streams it gets: with fresh
+    normal-priority streams (the default) the same code measured 2137-3546 attempts/s
+    depending on the streams the process had taken before (profiles/r06/r06f5_regime_ab.log;
+    3522-3545 in the bench's own sequence, r06f1, r06f8), with these 3228-3363 in every process
+    measured (r06f7, r06f8)."""
+    key = torch.device(device).index
+    if key not in _PIPE_STREAMS:
+        _PIPE_STREAMS[key] = [torch.cuda.Stream(device=device, priority=-1) for _ in range(3)]
+    return _PIPE_STREAMS[key]
 
 
 class _Speculator:
@@ -275,10 +294,12 @@ class _Pipeline:
         self.L = _lib.load()
         dev = bmc.device
         self.main = torch.cuda.current_stream(dev)
-        self.side = torch.cuda.Stream(device=dev)
-        # two density streams: a pass (~3.5 ms at 10 rows) outlasts a stage's local moves
-        # (~2.75 ms), so consecutive passes overlap (4 streams measured slower, r06zh)
-        self.dens = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        # two density streams: a pass (~3.6 ms at 10 rows) outlasts a stage's local moves
+        # (~2.4 ms), so consecutive passes overlap (4 streams measured slower, r06zh)
+        if os.environ.get("FS_PIPE_STREAMS") == "priority":
+            self.side, *self.dens = _priority_streams(dev)
+        else:
+            self.side, *self.dens = [torch.cuda.Stream(device=dev) for _ in range(3)]
         # the flow is fixed during the testing phase: its density pass without the per-call
         # checks, over the image packed now (before another stream reads it)
         self.log_prob = bmc.model.frozen_log_prob()
