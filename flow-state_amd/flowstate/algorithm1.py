@@ -244,24 +244,16 @@ class _Speculator:
 
 def pipeline_schedule(accepts):
     """The stage schedule _Pipeline follows for a (C, A) accept matrix: (spec, redo), two
-    lists of A bools.  Stage k = the local moves before big move k.  spec[k]: the stage
-    was run ahead from the previous stage's unfinished state (assuming big move k-1 rejects
-    on every chain); otherwise (a restart, or stage 0) it started from the finished state.
-    redo[k]: the speculative stage was wrong (a big move it assumed rejected accepted on
-    some chain, or its base was itself wrong) and the main stream ran it again.  Stage k+2
-    is decided once big move k-1 is known: a restart when stage k+1 is already known to be
-    wrong."""
+    lists of A bools.  Stage k = the local moves before big move k.  spec[k]: the stage ran
+    ahead, from stage k-1's state as a rejected big move k-1 leaves it (every stage but the
+    first).  redo[k]: big move k-1 accepted on some chain, so the main stream ran stage k
+    again from the finished state, and stage k+1 was run ahead again from that redone stage
+    (its first version started from the wrong one): each stage's last version starts from the
+    right state, and only an accept in the big move just before it sends it back."""
     acc = torch.as_tensor(accepts)
     A = int(acc.shape[1]) if acc.dim() == 2 else 0
-    g = [bool(acc[:, k].any()) for k in range(A)]
-    spec, redo = [False] * A, [False] * A
-    if A > 1:
-        spec[1] = True
-    for a in range(A):
-        if a >= 1:
-            redo[a] = spec[a] and (redo[a - 1] or g[a - 1])
-        if a + 2 < A:
-            spec[a + 2] = not (spec[a + 1] and redo[a])
+    spec = [k >= 1 for k in range(A)]
+    redo = [k >= 1 and bool(acc[:, k - 1].any()) for k in range(A)]
     return spec, redo
 
 
@@ -276,13 +268,14 @@ class _Pipeline:
     (a pinned copy of the accept flags, read while the GPU runs the queued stages), runs a
     wrong stage again on the main stream from the finished state (copy, local moves,
     density pass: the same kernels on the same inputs, so every result is bit-identical to
-    the plain sequence) and restarts the side stream from the finished state after it.
+    the plain sequence) and runs the next stage ahead again on the side stream as soon as
+    the redone local moves end.
 
     With the chains' rare accepts (0.2-0.3 % per big move in the reference's regime), the
     attempt time is the local moves' (the density pass, 1.3x as long, overlaps two
     attempts), where _Speculator's is the density pass plus the big move: 2.50 ms per stage
     against 3.55 ms (r06, timing events: tools/regime_gpu_timeline.py), the regime 2780 ->
-    3508 attempts/s with the stages after its accepts run again.  The density passes
+    3737-3777 attempts/s with the stages after its accepts run again.  The density passes
     use model.frozen_log_prob() (the flow is fixed in the testing phase): the per-pass
     checks cost ~0.9 ms of host time, which paced the pipeline.  The schedule of stages is
     pipeline_schedule(accepts)."""
@@ -317,7 +310,7 @@ class _Pipeline:
         self.S = self.L.fs_local_samples_per_chain(0, n, sf)
         self.steps = [s for s in range(1, n + 1) if sf and s % sf == 0]
         self.spec, self.redo, self.acc = {0: False}, {0: False}, {}
-        self.ev_L, self.ev_copy, self.ev_D, self.ev_main = {}, {}, {}, {}
+        self.ev_L, self.ev_copy, self.ev_D, self.ev_main, self.ev_redo = {}, {}, {}, {}, {}
         self.xy, self.ew = {}, {}
         self.kept = 0
         for s in [self.side] + self.dens:
@@ -349,54 +342,60 @@ class _Pipeline:
             self.nll[k % self.R].copy_(self.bmc.state_nll(self.slot(k).state, self.log_prob))
             self.ev_D[k] = ds.record_event()
 
-    def stage(self, k, spec):
-        """Queue stage k (k >= 1) on the side stream and its density pass.  spec: start
-        from stage k-1's state as big move k-1 leaves it on a reject (queued before that
-        big move); else from the finished state after big move k-1 (queued after it)."""
+    def stage(self, k, after_redo=False):
+        """Queue stage k (k >= 1) on the side stream and its density pass: from stage k-1's
+        state as big move k-1 leaves it on a reject — the side stream's stage k-1, or, with
+        after_redo, stage k-1 as the main stream ran it again (queued after that redo's
+        local moves; this version of stage k replaces the one queued before)."""
         b, sl = self.bmc, self.slot(k)
-        self.spec[k] = spec
-        self.xy[k] = torch.empty((b.C, self.S, b.N, 2), dtype=torch.float64, device=b.device)
-        self.ew[k] = torch.empty((b.C, self.S, 2), dtype=torch.float64, device=b.device)
+        self.spec[k] = True
+        if k not in self.xy:  # (a stage run again writes the same snapshot tensors, in stream order)
+            self.xy[k] = torch.empty((b.C, self.S, b.N, 2), dtype=torch.float64, device=b.device)
+            self.ew[k] = torch.empty((b.C, self.S, 2), dtype=torch.float64, device=b.device)
         with torch.cuda.stream(self.side):
             if k - self.R + 1 >= 0:  # the slot's previous stage: its big move and the next one's redo are done
                 self.side.wait_event(self.ev_main[k - self.R + 1])
-            if spec:
-                if k == 1:
-                    self.side.wait_event(self.ev_L[0])
-                self._copy(k)  # before big move k-1 writes slot k-1 (it waits for this event)
-                self.ev_copy[k] = self.side.record_event()
-                st = _lib.stream_ptr()
-                _lib.check(self.L.fs_pcg64_random(_lib.ptr(sl.pcg), b.C, _lib.ptr(self.draw), st), "fs_pcg64_random")
-                sl.attempts += 1
-                _lib.check(self.L.fs_energy_state(b.phys.c, _lib.ptr(sl.state), _lib.ptr(sl.state_is_f32), b.C, b.N,
-                                                  _lib.ptr(sl.E_old), _lib.ptr(sl.W_old), st), "fs_energy_state")
-            else:
-                self.side.wait_event(self.ev_main[k - 1])
-                self._copy(k)
+            if k == 1:
+                self.side.wait_event(self.ev_L[0])
+            if after_redo:
+                self.side.wait_event(self.ev_redo[k - 1])
+            self._copy(k)  # before big move k-1 writes slot k-1 (it waits for this event)
+            self.ev_copy[k] = self.side.record_event()
+            st = _lib.stream_ptr()
+            _lib.check(self.L.fs_pcg64_random(_lib.ptr(sl.pcg), b.C, _lib.ptr(self.draw), st), "fs_pcg64_random")
+            sl.attempts += 1
+            _lib.check(self.L.fs_energy_state(b.phys.c, _lib.ptr(sl.state), _lib.ptr(sl.state_is_f32), b.C, b.N,
+                                              _lib.ptr(sl.E_old), _lib.ptr(sl.W_old), st), "fs_energy_state")
             self._moves(sl, k)
             self.ev_L[k] = self.side.record_event()
         self._density(k)
 
     def learn(self, k):
-        """Wait for big move k and decide whether stage k+1 must run again."""
+        """Wait for big move k; stage k+1 runs again if it accepted on some chain."""
         self.ev_main[k].synchronize()
         self.acc[k] = bool(self.acc_host[k % self.R].any())
-        k1 = k + 1
-        self.redo[k1] = self.spec[k1] and (self.redo[k] or self.acc[k])
+        self.redo[k + 1] = self.acc[k]
+
+    def redo_moves(self, k):
+        """When stage k was wrong: its local moves again on the main stream, from the
+        finished state after big move k-1 (the event marks their end for stage k+1)."""
+        if self.redo[k]:
+            self.main.wait_event(self.ev_D[k])  # (the wrong pass read slot k and writes its NLL)
+            self._copy(k)
+            self._moves(self.slot(k), k)
+            self.ev_redo[k] = self.main.record_event()
 
     def attempt(self, k, configs, terms):
-        """Queue big move k on the main stream (after the redo of stage k if it was wrong).
-        Returns (the Snapshots of stage k, or None for stage 0; the accept flags)."""
+        """Queue big move k on the main stream (after the rest of stage k's redo if it was
+        wrong).  Returns (the Snapshots of stage k, or None for stage 0; the accept flags)."""
         b, sl = self.bmc, self.slot(k)
         self.main.wait_event(self.ev_D[k])
-        if self.spec.get(k + 1):
-            self.main.wait_event(self.ev_copy[k + 1])
         if self.redo[k]:
-            self._copy(k)
-            self._moves(sl, k)
             self.nll[k % self.R].copy_(b.state_nll(sl.state, self.log_prob))
         elif self.spec[k]:
             self.kept += 1
+        if self.spec.get(k + 1):  # stage k+1 copied slot k before this big move writes it
+            self.main.wait_event(self.ev_copy[k + 1])
         snap = Snapshots(self.steps, self.xy[k], self.ew[k], sl.state_is_f32.bool()) if k > 0 else None
         sl._moved = True
         acc = sl.nf_big_move(configs, terms=terms, nll=self.nll[k % self.R]).clone()
@@ -421,30 +420,23 @@ def _run_pipeline(bmc, cfg, A, n, sf, terms_of, snaps, acc):
     last = None
     pipe = _Pipeline(bmc, n, sf)
     try:
-        pipe.stage(1, True)
-        restart = None  # a restart stage waits to be queued after the big move it starts from
+        pipe.stage(1)
         for a in range(A):
             if a >= 1:
                 pipe.learn(a - 1)
-            fresh = later = None
-            if a + 2 < A:
-                if pipe.spec[a + 1] and pipe.redo[a]:  # stage a+1 is wrong: start a+2 afresh
-                    fresh = a + 2
-                    pipe.spec[fresh] = False  # (queued once big move a+1 is)
-                elif restart is None:  # the side stream's next stage first: it sets the pace
-                    pipe.stage(a + 2, True)
-                else:  # it starts from the restart stage a+1, queued after big move a
-                    later = a + 2
+            if a + 2 < A and not pipe.redo[a]:  # the side stream's next stage first: it sets the pace
+                pipe.stage(a + 2)
+            pipe.redo_moves(a)
+            if pipe.redo[a]:  # stage a+1 ran ahead from the wrong stage a: again, from the redone one
+                if a + 1 < A:
+                    pipe.stage(a + 1, after_redo=True)
+                if a + 2 < A:
+                    pipe.stage(a + 2)
             snap, ac = pipe.attempt(a, cfg[a * C:(a + 1) * C], terms_of(a))
             last = a
             acc.append(ac)
             if snap is not None:
                 snaps.append(snap)
-            if restart is not None:
-                pipe.stage(restart, False)
-            if later is not None:
-                pipe.stage(later, True)
-            restart = fresh
     finally:
         pipe.close(last if last == A - 1 else None)
     return pipe

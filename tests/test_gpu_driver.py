@@ -154,7 +154,7 @@ def test_speculative_testing_phase_is_bit_identical(runs, N, temperature, mode):
     if temperature > 1:
         assert dropped >= 1  # the drop-and-rerun path ran
         if mode == "pipeline":
-            assert any(redo) and not all(spec[1:])  # redo and restart stages ran
+            assert any(redo)  # stages ran again on the main stream, the next ones ahead again
     elif N == 3:
         assert r1.speculated >= 1  # the adopt path ran
     assert torch.equal(r0.accepts, r1.accepts)

@@ -256,9 +256,9 @@ def test_column_split_xcd_placement_is_a_bijection():
 
 
 def test_pipeline_schedule():
-    """algorithm1.pipeline_schedule: with no accepts every stage after the first is run
-    ahead and kept; an accept in big move j makes stages j+1 and j+2 run again on the main
-    stream and stage j+3 restart from the finished state, after which the run-ahead resumes."""
+    """algorithm1.pipeline_schedule: every stage after the first runs ahead; an accept in
+    big move j sends stage j+1 back to the main stream (its next stage runs ahead again from
+    the redone one), so the kept stages are those after a big move no chain accepted."""
     from flowstate.algorithm1 import pipeline_schedule
 
     acc = torch.zeros((10, 8), dtype=torch.uint8)
@@ -266,10 +266,10 @@ def test_pipeline_schedule():
     assert spec == [False] + [True] * 7 and redo == [False] * 8
     acc[3, 2] = 1
     spec, redo = pipeline_schedule(acc)
-    assert redo == [False, False, False, True, True, False, False, False]
-    assert spec == [False, True, True, True, True, False, True, True]
-    acc[:, :] = 1  # every big move accepts: every run-ahead stage is wrong
+    assert redo == [False, False, False, True, False, False, False, False]
+    assert spec == [False] + [True] * 7
+    acc[:, :] = 1  # every big move accepts: every stage after the first runs again
     spec, redo = pipeline_schedule(acc)
-    assert all(r for s, r in zip(spec, redo) if s)
+    assert redo == [False] + [True] * 7
     assert pipeline_schedule(torch.zeros((4, 1), dtype=torch.uint8)) == ([False], [False])
     assert pipeline_schedule(torch.zeros((4, 0), dtype=torch.uint8)) == ([], [])

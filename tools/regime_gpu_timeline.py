@@ -37,9 +37,9 @@ def moves(self, m, k):
     ev(st, ("m1", k, st.cuda_stream))
 
 
-def stage(self, k, spec):
+def stage(self, k, *args, **kw):
     ev(self.side, ("L0", k))  # queued on the side stream ahead of the stage's copy (after its waits: below)
-    orig_stage(self, k, spec)
+    orig_stage(self, k, *args, **kw)
     ev(self.side, ("L1", k))
 
 
