@@ -381,6 +381,8 @@ class _Pipeline:
         finished state after big move k-1 (the event marks their end for stage k+1)."""
         if self.redo[k]:
             self.main.wait_event(self.ev_D[k])  # (the wrong pass read slot k and writes its NLL)
+            # (the first version of stage k+1 copied slot k after its local moves, before that
+            # pass started; were it later, only that version, which is replaced, would differ)
             self._copy(k)
             self._moves(self.slot(k), k)
             self.ev_redo[k] = self.main.record_event()
